@@ -1,0 +1,139 @@
+/*
+ * cip.h - C ABI of libcip_hip.so, the MI355X-native invert hot path of
+ * ska_sdp_cip (SKA SDP continuum imaging pipeline).
+ *
+ * Every entry point is `extern "C"`, takes plain pointers and sizes, returns
+ * 0 (CIP_OK) on success or a negative CIP_E* code; the message of the last
+ * failure on the calling thread is returned by cip_last_error(). The library
+ * never frees or retains caller memory. Device pointers are HIP device memory
+ * on the current device (torch tensors' data_ptr() in the Python host code).
+ *
+ * Reference interfaces replaced (see INTEGRATION.md for the bindings):
+ *   cip_ms2dirty       <- ducc0.wgridder.ms2dirty as called at
+ *                         /root/reference/src/ska_sdp_cip/invert.py:170-183
+ *                         (plus the sum of weights of invert.py:184)
+ *   cip_choose_params  <- ducc0's internal parameter choice (grid size,
+ *                         kernel support, w-planes), SURVEY.md 8(a) a4.1/a4.2
+ *   cip_tile_runs      <- create_uvw_tile_mapping_sequential's per-row key and
+ *                         run search, uvw_tiling/tiling_plan.py:29-61,150-181
+ *   cip_stokes_i       <- StokesIGridderInput.from_measurement_set_reader +
+ *                         effective_weights, invert.py:72-116
+ *   cip_release_workspace - frees the per-device workspace cache (no reference
+ *                         counterpart; ducc allocates per call).
+ *   cip_profile_*      <- observability of the hot path (the reference's
+ *                         dask task stream, task_metrics.py:88-135).
+ */
+#ifndef CIP_H
+#define CIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CIP_OK 0
+#define CIP_EINVAL (-1)  /* bad argument (ValueError in Python) */
+#define CIP_ERANGE (-2)  /* uv(w) outside the grid (ValueError) */
+#define CIP_EHIP (-3)    /* HIP / hipFFT runtime failure (RuntimeError) */
+#define CIP_ENOMEM (-4)  /* device allocation failure (MemoryError) */
+
+/* dtype codes for cip_ms2dirty */
+#define CIP_C64 1
+#define CIP_C128 2
+#define CIP_F32 3
+#define CIP_F64 4
+#define CIP_NONE 0 /* wgt == NULL: all weights 1 */
+
+typedef struct cip_gridder_params {
+  int64_t nu, nv;      /* oversampled grid size (cells), even, 2/3/5/7-smooth */
+  int32_t support;     /* kernel support W (even, 4..16) */
+  int32_t degree;      /* polynomial degree of each kernel piece (W + 3) */
+  double beta;         /* ES shape parameter (2.3 W) */
+  double sigma;        /* oversampling factor (2.0) */
+  int32_t do_wstacking;/* 1: w-stacking planes; 0: 2-D (w ignored) */
+  int32_t tile;        /* grid tile edge T (cells) used by the scatter */
+  int64_t nplanes;     /* number of w planes (1 in 2-D mode) */
+  double w0, dw;       /* plane p sits at w = w0 + p dw (wavelengths) */
+  double nmin;         /* min over the field of n - 1 (<= 0) */
+} cip_gridder_params;
+
+/* Grid/kernel/w-plane parameters for an image of npix_x x npix_y pixels of
+ * pixsize (radians, sin-projected). support <= 0 selects W from epsilon.
+ * wmin/wmax: range of w in wavelengths (only used when do_wstacking). */
+int cip_choose_params(int64_t npix_x, int64_t npix_y, double pixsize_x,
+                      double pixsize_y, double epsilon, int support,
+                      int do_wstacking, double wmin, double wmax,
+                      cip_gridder_params* out);
+
+/* Dirty image (drop-in for ms2dirty): uvw (nrow,3) f64 metres, freq (nchan)
+ * f64 Hz, vis (nrow,nchan) complex64/complex128, wgt (nrow,nchan) f32/f64 or
+ * NULL. All pointers are DEVICE pointers. dirty_out: device (npix_x,npix_y)
+ * f64, row-major, axis 0 <-> l <-> u. sum_wgt_out: device f64 scalar, the sum
+ * of wgt (the reference's total_weight, invert.py:184), may be NULL.
+ * Runs on hip_stream (NULL = default stream) and returns when the result is
+ * complete on that stream (synchronous). params_out may be NULL. */
+int cip_ms2dirty(const double* uvw, int64_t nrow, const double* freq,
+                 int64_t nchan, const void* vis, int vis_dtype,
+                 const void* wgt, int wgt_dtype, int64_t npix_x,
+                 int64_t npix_y, double pixsize_x, double pixsize_y,
+                 double epsilon, int support, int do_wstacking,
+                 void* hip_stream, double* dirty_out, double* sum_wgt_out,
+                 cip_gridder_params* params_out);
+
+/* Uniform-grid ("grid only") variant used by the benchmark and the parity
+ * tests: fills grid_out (device, nu x nv complex128, row-major) for w-plane
+ * `plane` (0 in 2-D mode) with the gridded visibilities, using params from
+ * cip_choose_params. Zeroes grid_out first. */
+int cip_grid_plane(const double* uvw, int64_t nrow, const double* freq,
+                   int64_t nchan, const void* vis, int vis_dtype,
+                   const void* wgt, int wgt_dtype,
+                   const cip_gridder_params* params, double pixsize_x,
+                   double pixsize_y, int64_t plane, void* hip_stream,
+                   double* grid_out);
+
+/* Reference-exact UVW tile keys and constant-key channel runs (one run per
+ * maximal range of channels with equal (iu, iv, iw) in a row), rows in
+ * order, runs in channel order: key = floor(f/c * (uvw / tile) + 0.5) in
+ * fp64 without contraction. uvw/freq are DEVICE pointers. Two-phase: call
+ * with runs_* == NULL to get *n_runs, then with buffers of that size (device
+ * pointers): run_key (n_runs,3) int64, run_row (n_runs) int64 (row_offset
+ * added), run_c0/run_c1 (n_runs) int32. */
+int cip_tile_runs(const double* uvw, int64_t nrow, const double* freq,
+                  int64_t nchan, const double* tile_size3, int64_t row_offset,
+                  void* hip_stream, int64_t* n_runs, int64_t* run_key,
+                  int64_t* run_row, int32_t* run_c0, int32_t* run_c1);
+
+/* Stokes-I gridder input from raw (nrow,nchan,4) columns (device pointers):
+ * vis_i = 0.5 (V0 + V3) complex64, flag_i = F0 | F3, wgt_i = 4/(1/w0 + 1/w3)
+ * (0 when either is 0), eff_w = !flag_i * wgt_i (float32). Any output may be
+ * NULL. */
+int cip_stokes_i(const void* vis4, const uint8_t* flags4, const float* wgt4,
+                 int64_t n, void* hip_stream, void* vis_i, uint8_t* flag_i,
+                 float* wgt_i, float* eff_w);
+
+/* Last error message of the calling thread ("" if none). */
+const char* cip_last_error(void);
+
+/* Free the workspace cached for the current device. */
+int cip_release_workspace(void);
+
+/* Per-phase timing of cip_ms2dirty / cip_grid_plane on the calling thread
+ * (no reference counterpart; the reference records dask task streams,
+ * task_metrics.py:88-135). When enabled, hipEvents are recorded on the call's
+ * stream around each phase; cip_profile_last fills
+ *   ms[0..5]     = prep, plan, scatter, fft, correct, total  (milliseconds)
+ *   counts[0..4] = visibilities, runs (row slices), chunks, planes, scatter launches
+ * of the most recent call. */
+#define CIP_PROFILE_PHASES 6
+#define CIP_PROFILE_COUNTS 5
+int cip_profile_enable(int on);
+int cip_profile_last(double* ms, int64_t* counts);
+
+/* Library build identification (architecture, version). */
+const char* cip_build_info(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CIP_H */

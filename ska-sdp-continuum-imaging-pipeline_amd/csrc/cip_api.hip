@@ -1,0 +1,704 @@
+// cip_api.hip - the C ABI of libcip_hip.so (include/cip.h): parameter choice,
+// per-device workspace, the plan -> scatter -> FFT -> correct pipeline of
+// ms2dirty, the reference tiling runs and the Stokes-I conversion.
+#include <hipfft/hipfft.h>
+
+#include <cmath>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "cip_internal.h"
+
+namespace cip {
+
+static thread_local std::string g_last_error;
+
+int set_error(int code, const std::string& msg) {
+  g_last_error = msg;
+  return code;
+}
+
+// ----------------------------------------------------------- profiler ----
+// hipEvents recorded on the call's stream around each phase (cip_profile_*).
+struct Profiler {
+  bool on = false;
+  int device = -1;
+  std::vector<hipEvent_t> pool;
+  size_t used = 0;
+  struct Span {
+    int phase;
+    hipEvent_t a, b;
+  };
+  std::vector<Span> spans;
+  double ms[CIP_PROFILE_PHASES] = {0};
+  int64_t counts[CIP_PROFILE_COUNTS] = {0};
+
+  void reset() {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (dev != device) {  // events belong to a device
+      for (auto e : pool) (void)hipEventDestroy(e);
+      pool.clear();
+      device = dev;
+    }
+    used = 0;
+    spans.clear();
+    for (auto& m : ms) m = 0.0;
+    for (auto& c : counts) c = 0;
+  }
+  hipEvent_t mark(hipStream_t s) {
+    if (!on) return nullptr;
+    if (used == pool.size()) {
+      hipEvent_t e;
+      if (hipEventCreate(&e) != hipSuccess) return nullptr;
+      pool.push_back(e);
+    }
+    hipEvent_t e = pool[used++];
+    if (hipEventRecord(e, s) != hipSuccess) return nullptr;
+    return e;
+  }
+  void span(int phase, hipEvent_t a, hipEvent_t b) {
+    if (on && a && b) spans.push_back({phase, a, b});
+  }
+  void finish() {  // stream already synchronised
+    if (!on) return;
+    for (auto& sp : spans) {
+      float t = 0.f;
+      if (hipEventElapsedTime(&t, sp.a, sp.b) == hipSuccess) ms[sp.phase] += t;
+    }
+  }
+};
+static thread_local Profiler g_prof;
+
+// ------------------------------------------------------------ kernels ----
+// Host copies of the kernel coefficient tables (same data as the device side).
+struct HostKernel {
+  int W, D;
+  double beta;
+  const double* coef;  // [W/2][D+1]
+};
+
+#define CIP_HOST_TABLE(WW)                                                          \
+  static const double host_coef_##WW[WW / 2][CIP_ES_DEGREE_##WW + 1] = CIP_ES_COEFFS_##WW;
+CIP_HOST_TABLE(4)
+CIP_HOST_TABLE(6)
+CIP_HOST_TABLE(8)
+CIP_HOST_TABLE(10)
+CIP_HOST_TABLE(12)
+CIP_HOST_TABLE(14)
+CIP_HOST_TABLE(16)
+#undef CIP_HOST_TABLE
+
+static bool host_kernel(int W, HostKernel* k) {
+  switch (W) {
+#define CASE(WW)                                                              \
+  case WW:                                                                    \
+    *k = {WW, CIP_ES_DEGREE_##WW, CIP_ES_BETA_##WW, &host_coef_##WW[0][0]};  \
+    return true;
+    CASE(4) CASE(6) CASE(8) CASE(10) CASE(12) CASE(14) CASE(16)
+#undef CASE
+    default:
+      return false;
+  }
+}
+
+static double piece_value(const HostKernel& k, int piece, double y) {
+  const int half = k.W / 2;
+  const double* c = (piece < half) ? k.coef + piece * (k.D + 1) : k.coef + (k.W - 1 - piece) * (k.D + 1);
+  const double yy = (piece < half) ? y : -y;
+  double r = c[k.D];
+  for (int d = k.D - 1; d >= 0; --d) r = r * yy + c[d];
+  return r;
+}
+
+// Gauss-Legendre nodes/weights on [-1, 1]
+static void gauss_legendre(int n, std::vector<double>& x, std::vector<double>& w) {
+  x.resize(n);
+  w.resize(n);
+  for (int i = 0; i < n; ++i) {
+    double z = std::cos(M_PI * (i + 0.75) / (n + 0.5));
+    for (int it = 0; it < 100; ++it) {
+      double p0 = 1.0, p1 = z;
+      for (int j = 2; j <= n; ++j) {
+        const double p2 = ((2.0 * j - 1.0) * z * p1 - (j - 1.0) * p0) / j;
+        p0 = p1;
+        p1 = p2;
+      }
+      const double dp = n * (z * p1 - p0) / (z * z - 1.0);
+      const double dz = p1 / dp;
+      z -= dz;
+      if (std::fabs(dz) < 1e-16) break;
+    }
+    double p0 = 1.0, p1 = z;
+    for (int j = 2; j <= n; ++j) {
+      const double p2 = ((2.0 * j - 1.0) * z * p1 - (j - 1.0) * p0) / j;
+      p0 = p1;
+      p1 = p2;
+    }
+    const double dp = n * (z * p1 - p0) / (z * z - 1.0);
+    x[i] = z;
+    w[i] = 2.0 / ((1.0 - z * z) * dp * dp);
+  }
+}
+
+// F(nu) = integral of the piecewise kernel phi(d) cos(2 pi d nu) over its support
+// (d in cells); the grid correction of axis u is 1 / F(p / n_u).
+struct KernelFT {
+  HostKernel k;
+  std::vector<double> gx, gw;
+  explicit KernelFT(const HostKernel& kk) : k(kk) { gauss_legendre(24, gx, gw); }
+  double operator()(double nu) const {
+    double acc = 0.0;
+    for (int piece = 0; piece < k.W; ++piece) {
+      const double a = piece - 0.5 * k.W;  // piece spans d in [a, a + 1]
+      for (size_t i = 0; i < gx.size(); ++i) {
+        const double d = a + 0.5 * (gx[i] + 1.0);
+        const double y = 2.0 * piece + 1.0 - k.W - 2.0 * d;
+        acc += 0.5 * gw[i] * piece_value(k, piece, y) * std::cos(2.0 * M_PI * d * nu);
+      }
+    }
+    return acc;
+  }
+};
+
+// ------------------------------------------------------------- params ----
+static int64_t good_size(int64_t n) {
+  if (n < 16) n = 16;
+  for (int64_t m = n + (n & 1);; m += 2) {
+    int64_t r = m;
+    for (int64_t p : {2, 3, 5, 7})
+      while (r % p == 0) r /= p;
+    if (r == 1) return m;
+  }
+}
+
+static int support_for_epsilon(double eps) {
+  // calibrated against the fp64 direct DFT (DESIGN.md "Accuracy")
+  // max |err| / sum(w) vs the direct DFT measured 2e-3, 2e-5, 3e-7, 4e-9,
+  // 5e-11, 6e-13, 2e-14 for W = 4 .. 16 (tests/test_oracle.py)
+  if (eps >= 2e-3) return 4;
+  if (eps >= 2e-5) return 6;
+  if (eps >= 3e-7) return 8;
+  if (eps >= 4e-9) return 10;
+  if (eps >= 5e-11) return 12;
+  if (eps >= 6e-13) return 14;
+  return 16;
+}
+
+static int choose(int64_t npix_x, int64_t npix_y, double px, double py, double epsilon, int support,
+                  int do_wstacking, double wmin, double wmax, cip_gridder_params* out) {
+  if (npix_x < 2 || npix_y < 2 || (npix_x & 1) || (npix_y & 1))
+    return set_error(CIP_EINVAL, "npix_x and npix_y must be even and >= 2");
+  if (!(px > 0.0) || !(py > 0.0)) return set_error(CIP_EINVAL, "pixel sizes must be positive");
+  if (support > 0) {
+    if ((support & 1) || support < 4 || support > 16)
+      return set_error(CIP_EINVAL, "support must be an even number in [4, 16]");
+  } else {
+    if (!(epsilon > 0.0)) return set_error(CIP_EINVAL, "epsilon must be positive");
+    support = support_for_epsilon(epsilon);
+  }
+  HostKernel hk;
+  host_kernel(support, &hk);
+  cip_gridder_params p;
+  std::memset(&p, 0, sizeof(p));
+  p.sigma = 2.0;
+  p.nu = good_size((int64_t)std::ceil(p.sigma * npix_x));
+  p.nv = good_size((int64_t)std::ceil(p.sigma * npix_y));
+  p.support = support;
+  p.degree = hk.D;
+  p.beta = hk.beta;
+  p.tile = kTile;
+  const double x0 = -0.5 * npix_x * px, y0 = -0.5 * npix_y * py;
+  const double e = x0 * x0 + y0 * y0;
+  if (e >= 1.0) return set_error(CIP_EINVAL, "field of view extends beyond the horizon");
+  p.nmin = -e / (std::sqrt(1.0 - e) + 1.0);
+  p.do_wstacking = do_wstacking ? 1 : 0;
+  if (do_wstacking) {
+    if (!(wmax >= wmin)) return set_error(CIP_EINVAL, "invalid w range");
+    p.dw = 0.5 / p.sigma / std::fabs(p.nmin);
+    p.nplanes = (int64_t)std::ceil((wmax - wmin) / p.dw) + support;
+    p.w0 = 0.5 * (wmin + wmax) - 0.5 * (double)(p.nplanes - 1) * p.dw;
+  } else {
+    p.nplanes = 1;
+    p.w0 = 0.0;
+    p.dw = 1.0;
+  }
+  *out = p;
+  return CIP_OK;
+}
+
+static GridGeometry geometry(const cip_gridder_params& p, double px, double py) {
+  GridGeometry g;
+  g.nu = p.nu;
+  g.nv = p.nv;
+  g.support = p.support;
+  g.scale_u = (double)p.nu * px;
+  g.scale_v = (double)p.nv * py;
+  g.do_wstacking = p.do_wstacking;
+  g.w0 = p.w0;
+  g.dw = p.dw;
+  g.nplanes = p.nplanes;
+  g.tile = p.tile;
+  g.ntx = (p.nu + p.tile - 1) / p.tile;
+  g.nty = (p.nv + p.tile - 1) / p.tile;
+  g.ntw = p.do_wstacking ? (p.nplanes - p.support + 1) : 1;
+  return g;
+}
+
+// ---------------------------------------------------------- workspace ----
+struct DevBuf {
+  void* ptr = nullptr;
+  size_t bytes = 0;
+};
+
+struct FftPlan {
+  hipfftHandle h;
+  int64_t nu, nv;
+};
+
+struct Workspace {
+  std::map<std::string, DevBuf> bufs;
+  std::vector<FftPlan> plans;
+  void* pinned = nullptr;  // small host staging
+  size_t pinned_bytes = 0;
+};
+
+static std::mutex g_ws_mutex;
+static std::map<int, Workspace*> g_ws;
+
+static Workspace* workspace() {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  std::lock_guard<std::mutex> lock(g_ws_mutex);
+  auto it = g_ws.find(dev);
+  if (it != g_ws.end()) return it->second;
+  Workspace* ws = new Workspace();
+  g_ws[dev] = ws;
+  return ws;
+}
+
+// grow-only device buffer; returns nullptr (and sets the error) on failure
+template <typename T>
+static T* buf(Workspace* ws, const char* name, int64_t count) {
+  const size_t bytes = (size_t)(count > 0 ? count : 1) * sizeof(T);
+  DevBuf& b = ws->bufs[name];
+  if (b.bytes < bytes) {
+    if (b.ptr) (void)hipFree(b.ptr);
+    b.ptr = nullptr;
+    b.bytes = 0;
+    // 12.5 % headroom so slowly growing inputs do not reallocate every call
+    const size_t want = bytes + bytes / 8;
+    if (hipMalloc(&b.ptr, want) != hipSuccess) {
+      (void)hipGetLastError();
+      set_error(CIP_ENOMEM, std::string("hipMalloc failed for workspace buffer ") + name);
+      return nullptr;
+    }
+    b.bytes = want;
+  }
+  return (T*)b.ptr;
+}
+
+static void* pinned(Workspace* ws, size_t bytes) {
+  if (ws->pinned_bytes < bytes) {
+    if (ws->pinned) (void)hipHostFree(ws->pinned);
+    ws->pinned = nullptr;
+    ws->pinned_bytes = 0;
+    if (hipHostMalloc(&ws->pinned, bytes) != hipSuccess) return nullptr;
+    ws->pinned_bytes = bytes;
+  }
+  return ws->pinned;
+}
+
+static int fft_plan(Workspace* ws, int64_t nu, int64_t nv, hipStream_t s, hipfftHandle* out) {
+  for (auto& p : ws->plans)
+    if (p.nu == nu && p.nv == nv) {
+      if (hipfftSetStream(p.h, s) != HIPFFT_SUCCESS) return set_error(CIP_EHIP, "hipfftSetStream failed");
+      *out = p.h;
+      return CIP_OK;
+    }
+  hipfftHandle h;
+  if (hipfftPlan2d(&h, (int)nu, (int)nv, HIPFFT_Z2Z) != HIPFFT_SUCCESS)
+    return set_error(CIP_EHIP, "hipfftPlan2d failed");
+  if (hipfftSetStream(h, s) != HIPFFT_SUCCESS) return set_error(CIP_EHIP, "hipfftSetStream failed");
+  ws->plans.push_back({h, nu, nv});
+  *out = h;
+  return CIP_OK;
+}
+
+#define CIP_ALLOC(var, T, name, n)  \
+  T* var = buf<T>(ws, name, (n));   \
+  if (!var) return CIP_ENOMEM;
+
+// ------------------------------------------------------------- planner ----
+struct PlanResult {
+  int64_t nruns = 0, ntiles = 0, nchunks = 0;
+  std::vector<int64_t> plane_chunk_off;  // chunk offset of tile layer iw (ntw + 1)
+  uint64_t* runs = nullptr;
+  int64_t* run_goff = nullptr;
+  int64_t* tile_run_off = nullptr;
+  Chunk* chunks = nullptr;
+};
+
+static int make_plan(Workspace* ws, const double* uvw, int64_t nrow, const double* fx, int64_t nchan,
+                     const GridGeometry& g, hipStream_t s, PlanResult* pr) {
+  const int64_t ntiles = g.ntx * g.nty * g.ntw;
+  pr->ntiles = ntiles;
+  CIP_ALLOC(tile_runs, int64_t, "tile_runs", ntiles + 1)
+  CIP_ALLOC(tile_vis, int64_t, "tile_vis", ntiles + 1)
+  CIP_ALLOC(tile_vis_off, int64_t, "tile_vis_off", ntiles + 1)
+  CIP_ALLOC(tile_cursor, int64_t, "tile_cursor", ntiles + 1)
+  CIP_ALLOC(chunk_off, int64_t, "chunk_off", ntiles + 1)
+  CIP_ALLOC(err, unsigned, "err_flag", 1)
+  CIP_ALLOC(scan_tmp, int64_t, "scan_tmp", scan_tmp_elems(ntiles + 1))
+  CIP_HIP_CHECK(hipMemsetAsync(tile_runs, 0, sizeof(int64_t) * (ntiles + 1), s));
+  CIP_HIP_CHECK(hipMemsetAsync(tile_vis, 0, sizeof(int64_t) * (ntiles + 1), s));
+  CIP_HIP_CHECK(hipMemsetAsync(tile_cursor, 0, sizeof(int64_t) * (ntiles + 1), s));
+  CIP_HIP_CHECK(hipMemsetAsync(err, 0, sizeof(unsigned), s));
+  CIP_HIP_CHECK(launch_plan_count(uvw, nrow, fx, nchan, g, tile_runs, tile_vis, err, s));
+  // tile_runs -> exclusive offsets (entry ntiles = total runs)
+  CIP_HIP_CHECK(exclusive_scan_i64(tile_runs, ntiles + 1, scan_tmp, s));
+  CIP_HIP_CHECK(hipMemcpyAsync(tile_vis_off, tile_vis, sizeof(int64_t) * (ntiles + 1), hipMemcpyDeviceToDevice, s));
+  CIP_HIP_CHECK(exclusive_scan_i64(tile_vis_off, ntiles + 1, scan_tmp, s));
+  int64_t* h = (int64_t*)pinned(ws, 4 * sizeof(int64_t));
+  if (!h) return set_error(CIP_ENOMEM, "hipHostMalloc failed");
+  CIP_HIP_CHECK(hipMemcpyAsync(&h[0], tile_runs + ntiles, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+  CIP_HIP_CHECK(hipMemcpyAsync(&h[1], err, sizeof(unsigned), hipMemcpyDeviceToHost, s));
+  CIP_HIP_CHECK(hipStreamSynchronize(s));
+  const int64_t nruns = h[0];
+  if ((unsigned)h[1] != 0)
+    return set_error(CIP_ERANGE, "some (u, v, w) coordinates fall outside the grid; increase the pixel size "
+                                 "or reduce the image size");
+  pr->nruns = nruns;
+  const int64_t* tile_run_off = tile_runs;
+  CIP_ALLOC(runs, uint64_t, "runs", nruns)
+  CIP_ALLOC(run_goff, int64_t, "run_goff", nruns + 1)
+  CIP_ALLOC(scan_tmp2, int64_t, "scan_tmp2", scan_tmp_elems(nruns + 1))
+  CIP_HIP_CHECK(launch_plan_emit(uvw, nrow, fx, nchan, g, tile_run_off, tile_cursor, runs, s));
+  CIP_HIP_CHECK(launch_run_lengths(runs, nruns, run_goff, s));
+  CIP_HIP_CHECK(exclusive_scan_i64(run_goff, nruns + 1, scan_tmp2, s));
+  CIP_HIP_CHECK(launch_chunk_counts(tile_vis, ntiles, kChunkVis, chunk_off, s));
+  CIP_HIP_CHECK(exclusive_scan_i64(chunk_off, ntiles + 1, scan_tmp, s));
+  // chunk offsets of each w tile layer
+  const int64_t layer = g.ntx * g.nty;
+  CIP_ALLOC(layer_off, int64_t, "layer_off", g.ntw + 1)
+  CIP_HIP_CHECK(launch_gather_i64(chunk_off, layer, g.ntw + 1, layer_off, s));
+  int64_t* hl = (int64_t*)pinned(ws, sizeof(int64_t) * (g.ntw + 1));
+  if (!hl) return set_error(CIP_ENOMEM, "hipHostMalloc failed");
+  CIP_HIP_CHECK(hipMemcpyAsync(hl, layer_off, sizeof(int64_t) * (g.ntw + 1), hipMemcpyDeviceToHost, s));
+  CIP_HIP_CHECK(hipStreamSynchronize(s));
+  pr->plane_chunk_off.assign(hl, hl + g.ntw + 1);
+  pr->nchunks = pr->plane_chunk_off.back();
+  CIP_ALLOC(chunks, Chunk, "chunks", pr->nchunks)
+  CIP_HIP_CHECK(launch_chunk_emit(tile_vis_off, tile_vis, chunk_off, ntiles, kChunkVis, chunks, s));
+  pr->runs = runs;
+  pr->run_goff = run_goff;
+  pr->tile_run_off = tile_runs;
+  pr->chunks = chunks;
+  return CIP_OK;
+}
+
+static bool vis_dtype_ok(int d) { return d == CIP_C64 || d == CIP_C128; }
+static bool wgt_dtype_ok(int d) { return d == CIP_NONE || d == CIP_F32 || d == CIP_F64; }
+
+struct Prepared {
+  cip_gridder_params p;
+  GridGeometry g;
+  double fixed_scale;
+  double* fx;
+  double* red;  // device [sum_w, max|wV|]
+  PlanResult plan;
+};
+
+static int prepare(Workspace* ws, const double* uvw, int64_t nrow, const double* freq, int64_t nchan,
+                   const void* vis, int vis_dtype, const void* wgt, int wgt_dtype, int64_t npix_x, int64_t npix_y,
+                   double px, double py, double epsilon, int support, int do_wstacking,
+                   const cip_gridder_params* given, hipStream_t s, Prepared* out) {
+  if (!vis_dtype_ok(vis_dtype)) return set_error(CIP_EINVAL, "vis dtype must be complex64 or complex128");
+  if (!wgt_dtype_ok(wgt_dtype)) return set_error(CIP_EINVAL, "wgt dtype must be float32, float64 or none");
+  if (wgt == nullptr) wgt_dtype = CIP_NONE;
+  if (nrow < 0 || nchan < 1 || nchan > 65535) return set_error(CIP_EINVAL, "need 1 <= nchan <= 65535, nrow >= 0");
+  if (nrow >= ((int64_t)1 << 32)) return set_error(CIP_EINVAL, "nrow must be < 2^32");
+  CIP_ALLOC(fx, double, "fx", nchan)
+  CIP_ALLOC(partial, double, "prep_partial", 2 * prep_blocks())
+  CIP_ALLOC(red, double, "red", 4)
+  CIP_HIP_CHECK(launch_freq_scale(freq, nchan, fx, s));
+  CIP_HIP_CHECK(launch_prep_reduce(vis, vis_dtype, wgt, wgt_dtype, nrow * nchan, partial, prep_blocks(), red, s));
+  hipEvent_t e_prep = g_prof.mark(s);
+  g_prof.span(0, g_prof.pool.empty() ? nullptr : g_prof.pool[0], e_prep);
+  double* h = (double*)pinned(ws, sizeof(double) * (4 + (size_t)nchan));
+  if (!h) return set_error(CIP_ENOMEM, "hipHostMalloc failed");
+  CIP_HIP_CHECK(hipMemcpyAsync(h, red, 2 * sizeof(double), hipMemcpyDeviceToHost, s));
+  CIP_HIP_CHECK(hipMemcpyAsync(h + 4, fx, sizeof(double) * nchan, hipMemcpyDeviceToHost, s));
+  CIP_HIP_CHECK(hipStreamSynchronize(s));
+  const double maxabs = h[1];
+  double fxmin = h[4], fxmax = h[4];
+  for (int64_t c = 1; c < nchan; ++c) {
+    fxmin = std::fmin(fxmin, h[4 + c]);
+    fxmax = std::fmax(fxmax, h[4 + c]);
+  }
+  if (!(fxmin > 0.0)) return set_error(CIP_EINVAL, "channel frequencies must be positive");
+  if (!std::isfinite(maxabs)) return set_error(CIP_EINVAL, "non-finite visibility or weight");
+  double wmin = 0.0, wmax = 0.0;
+  if (do_wstacking && nrow > 0 && given == nullptr) {
+    const int nb = 256;
+    CIP_ALLOC(wpart, double, "w_partial", 2 * nb)
+    CIP_HIP_CHECK(launch_w_range(uvw, nrow, fxmin, fxmax, wpart, nb, s));
+    double* hw = (double*)pinned(ws, sizeof(double) * 2 * nb);
+    if (!hw) return set_error(CIP_ENOMEM, "hipHostMalloc failed");
+    CIP_HIP_CHECK(hipMemcpyAsync(hw, wpart, sizeof(double) * 2 * nb, hipMemcpyDeviceToHost, s));
+    CIP_HIP_CHECK(hipStreamSynchronize(s));
+    wmin = INFINITY;
+    wmax = -INFINITY;
+    for (int i = 0; i < nb; ++i) {
+      wmin = std::fmin(wmin, hw[2 * i]);
+      wmax = std::fmax(wmax, hw[2 * i + 1]);
+    }
+  }
+  if (given) {
+    out->p = *given;
+  } else {
+    const int rc = choose(npix_x, npix_y, px, py, epsilon, support, do_wstacking, wmin, wmax, &out->p);
+    if (rc != CIP_OK) return rc;
+  }
+  out->g = geometry(out->p, px, py);
+  // fixed point: max contribution <= 2^kFixedBits
+  int e2 = 0;
+  if (maxabs > 0.0) {
+    std::frexp(maxabs, &e2);  // maxabs < 2^e2
+  }
+  out->fixed_scale = std::ldexp(1.0, kFixedBits - e2);
+  out->fx = fx;
+  out->red = red;
+  if (nrow == 0) {
+    out->plan = PlanResult();
+    out->plan.plane_chunk_off.assign(out->g.ntw + 1, 0);
+    return CIP_OK;
+  }
+  const int rc = make_plan(ws, uvw, nrow, fx, nchan, out->g, s, &out->plan);
+  g_prof.span(1, e_prep, g_prof.mark(s));
+  g_prof.counts[0] = nrow * nchan;
+  g_prof.counts[1] = out->plan.nruns;
+  g_prof.counts[2] = out->plan.nchunks;
+  g_prof.counts[3] = out->g.nplanes;
+  return rc;
+}
+
+static int scatter_plane(const Prepared& pp, int64_t plane, const double* uvw, const void* vis, int vis_dtype,
+                         const void* wgt, int wgt_dtype, int64_t nchan, double* grid, hipStream_t s) {
+  const GridGeometry& g = pp.g;
+  CIP_HIP_CHECK(hipMemsetAsync(grid, 0, sizeof(double) * 2 * g.nu * g.nv, s));
+  if (pp.plan.nchunks == 0) return CIP_OK;
+  int64_t lo = 0, hi = 0;  // tile layers feeding this plane
+  if (g.do_wstacking) {
+    lo = plane - g.support + 1;
+    if (lo < 0) lo = 0;
+    hi = plane < g.ntw - 1 ? plane : g.ntw - 1;
+    if (hi < lo) return CIP_OK;
+  }
+  const int64_t cb = pp.plan.plane_chunk_off[lo], ce = pp.plan.plane_chunk_off[hi + 1];
+  if (wgt == nullptr) wgt_dtype = CIP_NONE;
+  hipEvent_t a = g_prof.mark(s);
+  CIP_HIP_CHECK(launch_scatter(g.support, vis_dtype, wgt_dtype, uvw, pp.fx, vis, wgt, nchan, pp.plan.runs,
+                               pp.plan.run_goff, pp.plan.tile_run_off, pp.plan.chunks, cb, ce - cb, g, plane,
+                               pp.fixed_scale, grid, s));
+  g_prof.span(2, a, g_prof.mark(s));
+  if (ce > cb) g_prof.counts[4] += 1;
+  return CIP_OK;
+}
+
+}  // namespace cip
+
+using namespace cip;
+
+extern "C" {
+
+const char* cip_last_error(void) { return g_last_error.c_str(); }
+
+const char* cip_build_info(void) { return "libcip_hip gfx950 (CDNA4) v0.1.0"; }
+
+int cip_choose_params(int64_t npix_x, int64_t npix_y, double pixsize_x, double pixsize_y, double epsilon,
+                      int support, int do_wstacking, double wmin, double wmax, cip_gridder_params* out) {
+  if (!out) return set_error(CIP_EINVAL, "out is NULL");
+  return choose(npix_x, npix_y, pixsize_x, pixsize_y, epsilon, support, do_wstacking, wmin, wmax, out);
+}
+
+int cip_ms2dirty(const double* uvw, int64_t nrow, const double* freq, int64_t nchan, const void* vis, int vis_dtype,
+                 const void* wgt, int wgt_dtype, int64_t npix_x, int64_t npix_y, double pixsize_x,
+                 double pixsize_y, double epsilon, int support, int do_wstacking, void* hip_stream,
+                 double* dirty_out, double* sum_wgt_out, cip_gridder_params* params_out) {
+  g_last_error.clear();
+  if (!dirty_out) return set_error(CIP_EINVAL, "dirty_out is NULL");
+  if (nrow > 0 && (!uvw || !freq || !vis)) return set_error(CIP_EINVAL, "NULL input pointer");
+  hipStream_t s = (hipStream_t)hip_stream;
+  Workspace* ws = workspace();
+  if (!ws) return set_error(CIP_EHIP, "no HIP device");
+  g_prof.reset();
+  hipEvent_t t_start = g_prof.mark(s);
+  Prepared pp;
+  int rc = prepare(ws, uvw, nrow, freq, nchan, vis, vis_dtype, wgt, wgt_dtype, npix_x, npix_y, pixsize_x, pixsize_y,
+                   epsilon, support, do_wstacking, nullptr, s, &pp);
+  if (rc != CIP_OK) return rc;
+  if (params_out) *params_out = pp.p;
+  const GridGeometry& g = pp.g;
+  CIP_ALLOC(grid, double, "grid", 2 * g.nu * g.nv)
+  CIP_ALLOC(cx, double, "cx", npix_x)
+  CIP_ALLOC(cy, double, "cy", npix_y)
+  HostKernel hk;
+  host_kernel(g.support, &hk);
+  KernelFT F(hk);
+  {
+    std::vector<double> hx(npix_x), hy(npix_y);
+    for (int64_t i = 0; i < npix_x; ++i) hx[i] = 1.0 / F((double)(i - npix_x / 2) / (double)g.nu);
+    for (int64_t j = 0; j < npix_y; ++j) hy[j] = 1.0 / F((double)(j - npix_y / 2) / (double)g.nv);
+    CIP_HIP_CHECK(hipMemcpyAsync(cx, hx.data(), sizeof(double) * npix_x, hipMemcpyHostToDevice, s));
+    CIP_HIP_CHECK(hipMemcpyAsync(cy, hy.data(), sizeof(double) * npix_y, hipMemcpyHostToDevice, s));
+    CIP_HIP_CHECK(hipStreamSynchronize(s));  // host vectors go out of scope
+  }
+  hipfftHandle plan;
+  rc = fft_plan(ws, g.nu, g.nv, s, &plan);
+  if (rc != CIP_OK) return rc;
+  for (int64_t p = 0; p < g.nplanes; ++p) {
+    rc = scatter_plane(pp, p, uvw, vis, vis_dtype, wgt, wgt_dtype, nchan, grid, s);
+    if (rc != CIP_OK) return rc;
+    hipEvent_t f0 = g_prof.mark(s);
+    if (hipfftExecZ2Z(plan, (hipfftDoubleComplex*)grid, (hipfftDoubleComplex*)grid, HIPFFT_BACKWARD) !=
+        HIPFFT_SUCCESS)
+      return set_error(CIP_EHIP, "hipfftExecZ2Z failed");
+    hipEvent_t f1 = g_prof.mark(s);
+    g_prof.span(3, f0, f1);
+    if (g.do_wstacking) {
+      CIP_HIP_CHECK(launch_wplane_accumulate(grid, g, npix_x, npix_y, pixsize_x, pixsize_y,
+                                             g.w0 + (double)p * g.dw, p == 0, dirty_out, s));
+    } else {
+      CIP_HIP_CHECK(launch_crop_correct_2d(grid, g, npix_x, npix_y, cx, cy, dirty_out, s));
+    }
+    g_prof.span(4, f1, g_prof.mark(s));
+  }
+  if (g.do_wstacking) {
+    const int64_t fw_n = 4100;
+    const double numax = g.dw * std::fabs(pp.p.nmin);
+    const double dnu = (numax > 0 ? numax : 1e-3) * 1.0001 / 4096.0;
+    std::vector<double> fw(fw_n);
+    for (int64_t k = 0; k < fw_n; ++k) fw[k] = F((double)k * dnu);
+    CIP_ALLOC(fwd, double, "fw_table", fw_n)
+    CIP_HIP_CHECK(hipMemcpyAsync(fwd, fw.data(), sizeof(double) * fw_n, hipMemcpyHostToDevice, s));
+    CIP_HIP_CHECK(
+        launch_wfinal_correct(dirty_out, npix_x, npix_y, pixsize_x, pixsize_y, cx, cy, fwd, fw_n, dnu, g.dw, s));
+    CIP_HIP_CHECK(hipStreamSynchronize(s));
+  }
+  if (sum_wgt_out) CIP_HIP_CHECK(hipMemcpyAsync(sum_wgt_out, pp.red, sizeof(double), hipMemcpyDeviceToDevice, s));
+  g_prof.span(5, t_start, g_prof.mark(s));
+  CIP_HIP_CHECK(hipStreamSynchronize(s));
+  g_prof.finish();
+  return CIP_OK;
+}
+
+int cip_grid_plane(const double* uvw, int64_t nrow, const double* freq, int64_t nchan, const void* vis,
+                   int vis_dtype, const void* wgt, int wgt_dtype, const cip_gridder_params* params,
+                   double pixsize_x, double pixsize_y, int64_t plane, void* hip_stream, double* grid_out) {
+  g_last_error.clear();
+  if (!params || !grid_out) return set_error(CIP_EINVAL, "NULL params or grid_out");
+  if (plane < 0 || plane >= params->nplanes) return set_error(CIP_EINVAL, "plane out of range");
+  hipStream_t s = (hipStream_t)hip_stream;
+  Workspace* ws = workspace();
+  if (!ws) return set_error(CIP_EHIP, "no HIP device");
+  g_prof.reset();
+  hipEvent_t t_start = g_prof.mark(s);
+  Prepared pp;
+  int rc = prepare(ws, uvw, nrow, freq, nchan, vis, vis_dtype, wgt, wgt_dtype, 2, 2, pixsize_x, pixsize_y, 0.0,
+                   params->support, params->do_wstacking, params, s, &pp);
+  if (rc != CIP_OK) return rc;
+  rc = scatter_plane(pp, plane, uvw, vis, vis_dtype, wgt, wgt_dtype, nchan, grid_out, s);
+  if (rc != CIP_OK) return rc;
+  g_prof.span(5, t_start, g_prof.mark(s));
+  CIP_HIP_CHECK(hipStreamSynchronize(s));
+  g_prof.finish();
+  return CIP_OK;
+}
+
+int cip_tile_runs(const double* uvw, int64_t nrow, const double* freq, int64_t nchan, const double* tile_size3,
+                  int64_t row_offset, void* hip_stream, int64_t* n_runs, int64_t* run_key, int64_t* run_row,
+                  int32_t* run_c0, int32_t* run_c1) {
+  g_last_error.clear();
+  if (!tile_size3 || !n_runs) return set_error(CIP_EINVAL, "NULL tile_size or n_runs");
+  if (nrow < 0 || nchan < 1) return set_error(CIP_EINVAL, "need nrow >= 0 and nchan >= 1");
+  hipStream_t s = (hipStream_t)hip_stream;
+  Workspace* ws = workspace();
+  if (!ws) return set_error(CIP_EHIP, "no HIP device");
+  if (nrow == 0) {
+    *n_runs = 0;
+    return CIP_OK;
+  }
+  CIP_ALLOC(winv, double, "winv", nchan)
+  CIP_ALLOC(row_runs, int64_t, "row_runs", nrow + 1)
+  CIP_ALLOC(tmp, int64_t, "scan_tmp_rows", scan_tmp_elems(nrow + 1))
+  CIP_HIP_CHECK(launch_wavelength_inv(freq, nchan, winv, s));
+  CIP_HIP_CHECK(hipMemsetAsync(row_runs + nrow, 0, sizeof(int64_t), s));
+  CIP_HIP_CHECK(launch_tile_run_count(uvw, nrow, winv, nchan, tile_size3[0], tile_size3[1], tile_size3[2], row_runs,
+                                      s));
+  CIP_HIP_CHECK(exclusive_scan_i64(row_runs, nrow + 1, tmp, s));
+  int64_t* h = (int64_t*)pinned(ws, sizeof(int64_t));
+  if (!h) return set_error(CIP_ENOMEM, "hipHostMalloc failed");
+  CIP_HIP_CHECK(hipMemcpyAsync(h, row_runs + nrow, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+  CIP_HIP_CHECK(hipStreamSynchronize(s));
+  const int64_t total = h[0];
+  if (run_key == nullptr) {
+    *n_runs = total;
+    return CIP_OK;
+  }
+  if (*n_runs < total) return set_error(CIP_EINVAL, "output buffers too small (pass *n_runs = capacity)");
+  if (!run_row || !run_c0 || !run_c1) return set_error(CIP_EINVAL, "NULL output buffer");
+  CIP_HIP_CHECK(launch_tile_run_emit(uvw, nrow, winv, nchan, tile_size3[0], tile_size3[1], tile_size3[2],
+                                     row_offset, row_runs, run_key, run_row, run_c0, run_c1, s));
+  CIP_HIP_CHECK(hipStreamSynchronize(s));
+  *n_runs = total;
+  return CIP_OK;
+}
+
+int cip_stokes_i(const void* vis4, const uint8_t* flags4, const float* wgt4, int64_t n, void* hip_stream,
+                 void* vis_i, uint8_t* flag_i, float* wgt_i, float* eff_w) {
+  g_last_error.clear();
+  if (n < 0) return set_error(CIP_EINVAL, "n must be >= 0");
+  if (n == 0) return CIP_OK;
+  if (vis_i && !vis4) return set_error(CIP_EINVAL, "vis_i requested without vis4");
+  if ((wgt_i || eff_w) && !wgt4) return set_error(CIP_EINVAL, "weights requested without wgt4");
+  if ((flag_i || eff_w) && !flags4) return set_error(CIP_EINVAL, "flags requested without flags4");
+  hipStream_t s = (hipStream_t)hip_stream;
+  CIP_HIP_CHECK(launch_stokes_i(vis4, flags4, wgt4, n, vis_i, flag_i, wgt_i, eff_w, s));
+  CIP_HIP_CHECK(hipStreamSynchronize(s));
+  return CIP_OK;
+}
+
+int cip_profile_enable(int on) {
+  g_prof.on = (on != 0);
+  return CIP_OK;
+}
+
+int cip_profile_last(double* ms, int64_t* counts) {
+  if (ms)
+    for (int i = 0; i < CIP_PROFILE_PHASES; ++i) ms[i] = g_prof.ms[i];
+  if (counts)
+    for (int i = 0; i < CIP_PROFILE_COUNTS; ++i) counts[i] = g_prof.counts[i];
+  return CIP_OK;
+}
+
+int cip_release_workspace(void) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return set_error(CIP_EHIP, "no HIP device");
+  std::lock_guard<std::mutex> lock(g_ws_mutex);
+  auto it = g_ws.find(dev);
+  if (it == g_ws.end()) return CIP_OK;
+  Workspace* ws = it->second;
+  for (auto& kv : ws->bufs)
+    if (kv.second.ptr) (void)hipFree(kv.second.ptr);
+  for (auto& p : ws->plans) (void)hipfftDestroy(p.h);
+  if (ws->pinned) (void)hipHostFree(ws->pinned);
+  delete ws;
+  g_ws.erase(it);
+  return CIP_OK;
+}
+
+}  // extern "C"

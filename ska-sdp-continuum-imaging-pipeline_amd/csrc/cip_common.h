@@ -1,0 +1,139 @@
+// cip_common.h - shared device/host definitions of libcip_hip.so (gfx950).
+//
+// Geometry conventions (identical in oracle/cip_oracle.c):
+//   grid cell ix in [0, nu) <-> u = (ix - nu/2) du,  du = 1 / (nu * pixsize_x)
+//   a visibility at u_lambda = u_m * f / c sits at x = u_lambda * nu * pixsize_x + nu/2
+//   footprint ix0 = floor(x - W/2) + 1 .. ix0 + W - 1, kernel piece k at
+//   y = 2 frac(x - W/2) - 1 (pieces k >= W/2 by symmetry: phi_{W-1-k}(y) = phi_k(-y)).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "es_kernels.h"
+
+#define CIP_SPEED_OF_LIGHT 299792458.0
+
+namespace cip {
+
+// Fixed-point accumulation: contributions are scaled by 2^S so the largest
+// |w * V| maps to <= 2^46, rounded to integers by adding 1.5 * 2^52 (one
+// correctly-rounded fma) and accumulated with 64-bit integer LDS atomics
+// (ds_add_u64: 8 CU-cycles/wave-instruction vs 16 for ds_add_f64 measured on
+// gfx950, tools/microbench/lds_ops.hip). Integer sums are exact and
+// order-independent; a chunk holds <= kChunkVis visibilities so a cell sum
+// stays below 2^61.
+constexpr double kMagic = 6755399441055744.0;  // 1.5 * 2^52
+constexpr uint32_t kMagicHi = 0x43380000u;      // high word of kMagic
+constexpr int kFixedBits = 46;
+constexpr int64_t kChunkVis = 32768;
+
+// Tile edge (grid cells) of the scatter work decomposition.
+constexpr int kTile = 32;
+
+__host__ __device__ inline int64_t floor_div(int64_t a, int64_t b) {
+  int64_t q = a / b;
+  return (q * b > a) ? q - 1 : q;
+}
+
+// Horner evaluation of the even/odd halves of piece k at z = y^2.
+template <int W>
+struct EsKernel;
+
+#define CIP_DEFINE_KERNEL(WW)                                                  \
+  template <>                                                                  \
+  struct EsKernel<WW> {                                                        \
+    static constexpr int W = WW;                                               \
+    static constexpr int D = CIP_ES_DEGREE_##WW;                               \
+    __device__ static inline double coef(int k, int d) {                       \
+      constexpr double c[WW / 2][CIP_ES_DEGREE_##WW + 1] = CIP_ES_COEFFS_##WW; \
+      return c[k][d];                                                          \
+    }                                                                          \
+  };
+CIP_DEFINE_KERNEL(4)
+CIP_DEFINE_KERNEL(6)
+CIP_DEFINE_KERNEL(8)
+CIP_DEFINE_KERNEL(10)
+CIP_DEFINE_KERNEL(12)
+CIP_DEFINE_KERNEL(14)
+CIP_DEFINE_KERNEL(16)
+#undef CIP_DEFINE_KERNEL
+
+// All W kernel values at y in [-1, 1): out[k] = phi_k(y).
+template <int W>
+__device__ __forceinline__ void eval_kernel(double y, double* out) {
+  using K = EsKernel<W>;
+  const double z = y * y;
+#pragma unroll
+  for (int k = 0; k < W / 2; ++k) {
+    // even part: sum_m c[2m] z^m ; odd part: sum_m c[2m+1] z^m
+    constexpr int D = K::D;
+    double e = K::coef(k, (D & 1) ? D - 1 : D);
+#pragma unroll
+    for (int d = ((D & 1) ? D - 1 : D) - 2; d >= 0; d -= 2) e = fma(e, z, K::coef(k, d));
+    double o = K::coef(k, (D & 1) ? D : D - 1);
+#pragma unroll
+    for (int d = ((D & 1) ? D : D - 1) - 2; d >= 1; d -= 2) o = fma(o, z, K::coef(k, d));
+    out[k] = fma(y, o, e);
+    out[W - 1 - k] = fma(-y, o, e);
+  }
+}
+
+// A gridding work unit: the flattened visibilities [g0, g1) of tile `tile`
+// (global indices into the tile-sorted visibility stream).
+struct Chunk {
+  int64_t g0, g1;
+  int64_t tile;
+};
+
+// Everything the planner and the scatter need to place a visibility.
+struct GridGeometry {
+  int64_t nu, nv;
+  int support;
+  double scale_u, scale_v;  // nu * pixsize_x, nv * pixsize_y
+  int do_wstacking;
+  double w0, dw;
+  int64_t nplanes;
+  int tile;                 // T
+  int64_t ntx, nty, ntw;    // tiles per axis (ntw = nplanes - W + 1, or 1 in 2-D)
+};
+
+// Grid coordinate -> footprint origin and kernel variable.
+__device__ __forceinline__ void footprint(double x, int half_w, int64_t* i0, double* y) {
+  const double s = x - (double)half_w;
+  const double fl = floor(s);
+  *i0 = (int64_t)fl + 1;
+  *y = 2.0 * (s - fl) - 1.0;
+}
+
+// Place one visibility (metres, fx = f / c) on the grid. Returns false when the
+// footprint leaves the grid (or the w-plane stack). The arithmetic order is
+// pinned (no contraction) so the planner and the scatter agree bit for bit and
+// oracle/cip_oracle.c reproduces it.
+__device__ __forceinline__ bool place_vis(double u_m, double v_m, double w_m, double fx,
+                                          const GridGeometry& g, int64_t* ix0, double* yu,
+                                          int64_t* iy0, double* yv, int64_t* iw0, double* yw) {
+#pragma clang fp contract(off)
+  const int hw = g.support / 2;
+  const double x = (u_m * fx) * g.scale_u + (double)(g.nu / 2);
+  const double y = (v_m * fx) * g.scale_v + (double)(g.nv / 2);
+  footprint(x, hw, ix0, yu);
+  footprint(y, hw, iy0, yv);
+  bool ok = (*ix0 >= 0) && (*ix0 + g.support <= g.nu) && (*iy0 >= 0) && (*iy0 + g.support <= g.nv);
+  if (g.do_wstacking) {
+    const double xw = ((w_m * fx) - g.w0) / g.dw;
+    footprint(xw, hw, iw0, yw);
+    ok = ok && (*iw0 >= 0) && (*iw0 + g.support <= g.nplanes);
+  } else {
+    *iw0 = 0;
+    *yw = 0.0;
+  }
+  // NaN coordinates fail every comparison above except the casts; reject them
+  ok = ok && (x == x) && (y == y);
+  return ok;
+}
+
+__device__ __forceinline__ int64_t tile_key(int64_t ix0, int64_t iy0, int64_t iw0, const GridGeometry& g) {
+  return (iw0 * g.nty + iy0 / g.tile) * g.ntx + ix0 / g.tile;
+}
+
+}  // namespace cip

@@ -1,0 +1,387 @@
+// cip_grid.hip - the convolutional scatter of visibilities onto the uv grid
+// (the hot loop of ducc0.wgridder.ms2dirty) and the
+// post-FFT crop / grid-correction / w-screen kernels (a4.5, a4.6).
+//
+// Scatter design (DESIGN.md "Scatter kernel"): one 256-thread workgroup per
+// chunk (<= kChunkVis visibilities of one T x T grid tile, T = 32). The tile's
+// (T+W-1)^2 sub-grid lives in LDS as 64-bit fixed-point re/im pairs. Each lane
+// owns one visibility at a time (lane-per-visibility), evaluates the 2 x W
+// piecewise-polynomial kernel values, and adds its W x W taps with no-return
+// ds_add_u64. After the chunk the non-zero sub-grid cells are converted back
+// to fp64 and added to the HBM grid with global fp64 atomics. No MFMA: this
+// is a scatter.
+#include "cip_internal.h"
+
+namespace cip {
+
+enum { WK_NONE = 0, WK_F32 = 1, WK_F64 = 2 };
+
+template <int WK>
+__device__ __forceinline__ double load_weight(const void* __restrict__ w, int64_t i) {
+  if constexpr (WK == WK_F32) return (double)((const float*)w)[i];
+  if constexpr (WK == WK_F64) return ((const double*)w)[i];
+  return 1.0;
+}
+
+__device__ __forceinline__ void load_vis(const float2* __restrict__ p, int64_t i, double& re, double& im) {
+  const float2 v = p[i];
+  re = v.x;
+  im = v.y;
+}
+__device__ __forceinline__ void load_vis(const double2* __restrict__ p, int64_t i, double& re, double& im) {
+  const double2 v = p[i];
+  re = v.x;
+  im = v.y;
+}
+
+// ------------------------------------------------------ prep reduction ----
+// Sum of weights (the reference's total_weight, invert.py:184) and max |w V|
+// (sets the fixed-point scale). Deterministic: fixed grid-stride assignment and
+// fixed-order tree reductions.
+constexpr int kPrepBlocks = 1024;
+int prep_blocks() { return kPrepBlocks; }
+
+template <typename VisT, int WK>
+__global__ __launch_bounds__(256) void prep_kernel(const VisT* __restrict__ vis, const void* __restrict__ wgt,
+                                                   int64_t n, double* partial) {
+  double sum = 0.0, mx = 0.0;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const double w = load_weight<WK>(wgt, i);
+    double re, im;
+    load_vis(vis, i, re, im);
+    sum += w;
+    mx = fmax(mx, fabs(w) * fmax(fabs(re), fabs(im)));
+  }
+  for (int d = 32; d > 0; d >>= 1) {
+    sum += __shfl_xor(sum, d, 64);
+    mx = fmax(mx, __shfl_xor(mx, d, 64));
+  }
+  __shared__ double ss[4], sm[4];
+  if ((threadIdx.x & 63) == 0) {
+    ss[threadIdx.x >> 6] = sum;
+    sm[threadIdx.x >> 6] = mx;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    partial[2 * blockIdx.x] = (ss[0] + ss[1]) + (ss[2] + ss[3]);
+    partial[2 * blockIdx.x + 1] = fmax(fmax(sm[0], sm[1]), fmax(sm[2], sm[3]));
+  }
+}
+
+__global__ __launch_bounds__(256) void prep_final_kernel(const double* partial, int nblocks, double* out2) {
+  double sum = 0.0, mx = 0.0;
+  for (int i = threadIdx.x; i < nblocks; i += 256) {
+    sum += partial[2 * i];
+    mx = fmax(mx, partial[2 * i + 1]);
+  }
+  for (int d = 32; d > 0; d >>= 1) {
+    sum += __shfl_xor(sum, d, 64);
+    mx = fmax(mx, __shfl_xor(mx, d, 64));
+  }
+  __shared__ double ss[4], sm[4];
+  if ((threadIdx.x & 63) == 0) {
+    ss[threadIdx.x >> 6] = sum;
+    sm[threadIdx.x >> 6] = mx;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    out2[0] = (ss[0] + ss[1]) + (ss[2] + ss[3]);
+    out2[1] = fmax(fmax(sm[0], sm[1]), fmax(sm[2], sm[3]));
+  }
+}
+
+hipError_t launch_prep_reduce(const void* vis, int vis_dtype, const void* wgt, int wgt_dtype, int64_t n,
+                              double* partial, int nblocks, double* out2, hipStream_t s) {
+#define PREP(VT, WKV) prep_kernel<VT, WKV><<<dim3(nblocks), dim3(256), 0, s>>>((const VT*)vis, wgt, n, partial)
+  if (vis_dtype == CIP_C64) {
+    if (wgt_dtype == CIP_F32) PREP(float2, WK_F32);
+    else if (wgt_dtype == CIP_F64) PREP(float2, WK_F64);
+    else PREP(float2, WK_NONE);
+  } else {
+    if (wgt_dtype == CIP_F32) PREP(double2, WK_F32);
+    else if (wgt_dtype == CIP_F64) PREP(double2, WK_F64);
+    else PREP(double2, WK_NONE);
+  }
+#undef PREP
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  prep_final_kernel<<<dim3(1), dim3(256), 0, s>>>(partial, nblocks, out2);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------ scatter ----
+constexpr int kScatterThreads = 256;
+constexpr int kRunBatch = 256;
+
+template <int W, typename VisT, int WK, bool WSTACK>
+__device__ __forceinline__ void grid_one(const double* __restrict__ uvw, const double* __restrict__ fx,
+                                         const VisT* __restrict__ vis, const void* __restrict__ wgt, int64_t nchan,
+                                         int64_t irow, int64_t c, const GridGeometry& g, int64_t plane,
+                                         int64_t X0, int64_t Y0, double fixed_scale, unsigned long long* sub) {
+  constexpr int T = kTile;
+  constexpr int P = T + W - 1;
+  const int64_t idx = irow * nchan + c;
+  const double wv = load_weight<WK>(wgt, idx);
+  if (wv == 0.0) return;
+  double vr, vi;
+  load_vis(vis, idx, vr, vi);
+  int64_t ix0, iy0, iw0;
+  double yu, yv, yw;
+  if (!place_vis(uvw[3 * irow], uvw[3 * irow + 1], uvw[3 * irow + 2], fx[c], g, &ix0, &yu, &iy0, &yv, &iw0, &yw))
+    return;
+  const int64_t lx = ix0 - X0, ly = iy0 - Y0;
+  if (lx < 0 || lx >= T || ly < 0 || ly >= T) return;  // never for a consistent plan
+  double sc = wv * fixed_scale;
+  if constexpr (WSTACK) {
+    const int64_t kw = plane - iw0;
+    if (kw < 0 || kw >= W) return;
+    double kwv[W];
+    eval_kernel<W>(yw, kwv);
+    double sel = 0.0;
+#pragma unroll
+    for (int k = 0; k < W; ++k) sel = (k == kw) ? kwv[k] : sel;
+    sc *= sel;
+  }
+  vr *= sc;
+  vi *= sc;
+  double ku[W], kv[W];
+  eval_kernel<W>(yu, ku);
+  eval_kernel<W>(yv, kv);
+  double kr[W], ki[W];
+#pragma unroll
+  for (int j = 0; j < W; ++j) {
+    kr[j] = kv[j] * vr;
+    ki[j] = kv[j] * vi;
+  }
+  unsigned long long* base = sub + 2 * (lx * P + ly);
+#pragma unroll
+  for (int i = 0; i < W; ++i) {
+#pragma unroll
+    for (int j = 0; j < W; ++j) {
+      const double qr = fma(ku[i], kr[j], kMagic);
+      const double qi = fma(ku[i], ki[j], kMagic);
+      const unsigned long long br = (unsigned long long)__double_as_longlong(qr) - 0x4338000000000000ull;
+      const unsigned long long bi = (unsigned long long)__double_as_longlong(qi) - 0x4338000000000000ull;
+      atomicAdd(base + 2 * (i * P + j), br);
+      atomicAdd(base + 2 * (i * P + j) + 1, bi);
+    }
+  }
+}
+
+template <int W, typename VisT, int WK, bool WSTACK>
+__global__ __launch_bounds__(kScatterThreads) void scatter_kernel(
+    const double* __restrict__ uvw, const double* __restrict__ fx, const VisT* __restrict__ vis,
+    const void* __restrict__ wgt, int64_t nchan, const uint64_t* __restrict__ runs,
+    const int64_t* __restrict__ run_goff, const int64_t* __restrict__ tile_run_off,
+    const Chunk* __restrict__ chunks, int64_t chunk_begin, GridGeometry g, int64_t plane, double fixed_scale,
+    double inv_scale, double* __restrict__ grid) {
+  constexpr int T = kTile;
+  constexpr int P = T + W - 1;
+  __shared__ unsigned long long sub[P * P * 2];
+  __shared__ int64_t s_voff[kRunBatch + 1];
+  __shared__ uint64_t s_run[kRunBatch];
+  __shared__ int64_t s_first;
+
+  const Chunk ch = chunks[chunk_begin + blockIdx.x];
+  const int64_t t = ch.tile;
+  const int64_t X0 = (t % g.ntx) * T;
+  const int64_t Y0 = ((t / g.ntx) % g.nty) * T;
+  for (int i = threadIdx.x; i < P * P * 2; i += kScatterThreads) sub[i] = 0ull;
+  const int64_t ra = tile_run_off[t], rb = tile_run_off[t + 1];
+  if (threadIdx.x == 0) {
+    int64_t lo = ra, hi = rb - 1;  // first run whose end is beyond g0
+    while (lo < hi) {
+      const int64_t mid = (lo + hi) >> 1;
+      if (run_goff[mid + 1] > ch.g0) hi = mid;
+      else lo = mid + 1;
+    }
+    s_first = lo;
+  }
+  __syncthreads();
+  int64_t r = s_first;
+  int64_t v = ch.g0;
+  while (v < ch.g1 && r < rb) {
+    const int nst = (int)((rb - r) < kRunBatch ? (rb - r) : kRunBatch);
+    __syncthreads();
+    for (int k = threadIdx.x; k <= nst; k += kScatterThreads) {
+      s_voff[k] = run_goff[r + k];
+      if (k < nst) s_run[k] = runs[r + k];
+    }
+    __syncthreads();
+    const int64_t bend = ch.g1 < s_voff[nst] ? ch.g1 : s_voff[nst];
+    for (int64_t q = v + threadIdx.x; q < bend; q += kScatterThreads) {
+      int lo = 0, hi = nst - 1;  // last staged run starting at or before q
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (s_voff[mid] <= q) lo = mid;
+        else hi = mid - 1;
+      }
+      const uint64_t rec = s_run[lo];
+      const int64_t irow = (int64_t)(rec >> 32);
+      const int64_t c = (int64_t)((rec >> 16) & 0xffff) + (q - s_voff[lo]);
+      grid_one<W, VisT, WK, WSTACK>(uvw, fx, vis, wgt, nchan, irow, c, g, plane, X0, Y0, fixed_scale, sub);
+    }
+    v = bend;
+    r += nst;
+  }
+  __syncthreads();
+  // flush the touched cells of the sub-grid to the fp64 HBM grid
+  for (int cell = threadIdx.x; cell < P * P; cell += kScatterThreads) {
+    const long long re = (long long)sub[2 * cell];
+    const long long im = (long long)sub[2 * cell + 1];
+    if ((re | im) != 0) {
+      const int64_t gx = X0 + cell / P, gy = Y0 + cell % P;
+      if (gx < g.nu && gy < g.nv) {
+        double* dst = grid + 2 * (gx * g.nv + gy);
+        unsafeAtomicAdd(dst, (double)re * inv_scale);
+        unsafeAtomicAdd(dst + 1, (double)im * inv_scale);
+      }
+    }
+  }
+}
+
+template <int W, typename VisT, int WK>
+static hipError_t scatter_dispatch_ws(bool ws, dim3 grid_dim, hipStream_t s, const double* uvw, const double* fx,
+                                      const void* vis, const void* wgt, int64_t nchan, const uint64_t* runs,
+                                      const int64_t* run_goff, const int64_t* tile_run_off, const Chunk* chunks,
+                                      int64_t chunk_begin, const GridGeometry& g, int64_t plane, double fs,
+                                      double* grid) {
+  if (ws)
+    scatter_kernel<W, VisT, WK, true><<<grid_dim, dim3(kScatterThreads), 0, s>>>(
+        uvw, fx, (const VisT*)vis, wgt, nchan, runs, run_goff, tile_run_off, chunks, chunk_begin, g, plane, fs,
+        1.0 / fs, grid);
+  else
+    scatter_kernel<W, VisT, WK, false><<<grid_dim, dim3(kScatterThreads), 0, s>>>(
+        uvw, fx, (const VisT*)vis, wgt, nchan, runs, run_goff, tile_run_off, chunks, chunk_begin, g, plane, fs,
+        1.0 / fs, grid);
+  return hipGetLastError();
+}
+
+template <int W>
+static hipError_t scatter_dispatch_w(int vis_dtype, int wgt_dtype, dim3 gd, hipStream_t s, const double* uvw,
+                                     const double* fx, const void* vis, const void* wgt, int64_t nchan,
+                                     const uint64_t* runs, const int64_t* run_goff, const int64_t* tile_run_off,
+                                     const Chunk* chunks, int64_t cb, const GridGeometry& g, int64_t plane,
+                                     double fs, double* grid) {
+  const bool ws = g.do_wstacking != 0;
+#define ARGS ws, gd, s, uvw, fx, vis, wgt, nchan, runs, run_goff, tile_run_off, chunks, cb, g, plane, fs, grid
+  if (vis_dtype == CIP_C64) {
+    if (wgt_dtype == CIP_F32) return scatter_dispatch_ws<W, float2, WK_F32>(ARGS);
+    if (wgt_dtype == CIP_F64) return scatter_dispatch_ws<W, float2, WK_F64>(ARGS);
+    return scatter_dispatch_ws<W, float2, WK_NONE>(ARGS);
+  }
+  if (wgt_dtype == CIP_F32) return scatter_dispatch_ws<W, double2, WK_F32>(ARGS);
+  if (wgt_dtype == CIP_F64) return scatter_dispatch_ws<W, double2, WK_F64>(ARGS);
+  return scatter_dispatch_ws<W, double2, WK_NONE>(ARGS);
+#undef ARGS
+}
+
+hipError_t launch_scatter(int support, int vis_dtype, int wgt_dtype, const double* uvw, const double* fx,
+                          const void* vis, const void* wgt, int64_t nchan, const uint64_t* runs,
+                          const int64_t* run_goff, const int64_t* tile_run_off, const Chunk* chunks,
+                          int64_t chunk_begin, int64_t nchunks, const GridGeometry& g, int64_t plane,
+                          double fixed_scale, double* grid, hipStream_t s) {
+  if (nchunks <= 0) return hipSuccess;
+  const dim3 gd((unsigned)nchunks);
+#define CASE(WW)                                                                                             \
+  case WW:                                                                                                   \
+    return scatter_dispatch_w<WW>(vis_dtype, wgt_dtype, gd, s, uvw, fx, vis, wgt, nchan, runs, run_goff,     \
+                                  tile_run_off, chunks, chunk_begin, g, plane, fixed_scale, grid);
+  switch (support) {
+    CASE(4)
+    CASE(6)
+    CASE(8)
+    CASE(10)
+    CASE(12)
+    CASE(14)
+    CASE(16)
+    default:
+      return hipErrorInvalidValue;
+  }
+#undef CASE
+}
+
+// ---------------------------------------------------- post-FFT kernels ----
+// dirty[i, j] = (-1)^(p+q) Re G^[p mod nu, q mod nv] * cx[i] * cy[j],
+// p = i - npix_x/2, q = j - npix_y/2; cx, cy = 1 / F(p/nu), 1 / F(q/nv).
+__global__ void crop_correct_2d_kernel(const double2* __restrict__ grid, int64_t nu, int64_t nv, int64_t nx,
+                                       int64_t ny, const double* __restrict__ cx, const double* __restrict__ cy,
+                                       double* __restrict__ dirty) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t i = blockIdx.y;
+  if (j >= ny) return;
+  const int64_t p = i - nx / 2, q = j - ny / 2;
+  const int64_t ip = (p + nu) % nu, iq = (q + nv) % nv;
+  const double sgn = ((p + q) & 1) ? -1.0 : 1.0;
+  dirty[i * ny + j] = sgn * grid[ip * nv + iq].x * cx[i] * cy[j];
+}
+
+hipError_t launch_crop_correct_2d(const double* grid, const GridGeometry& g, int64_t npix_x, int64_t npix_y,
+                                  const double* cx, const double* cy, double* dirty, hipStream_t s) {
+  crop_correct_2d_kernel<<<dim3((unsigned)((npix_y + 255) / 256), (unsigned)npix_x), dim3(256), 0, s>>>(
+      (const double2*)grid, g.nu, g.nv, npix_x, npix_y, cx, cy, dirty);
+  return hipGetLastError();
+}
+
+__device__ __forceinline__ double nm1_of(int64_t i, int64_t j, int64_t nx, int64_t ny, double px, double py) {
+  const double l = (double)(i - nx / 2) * px;
+  const double m = (double)(j - ny / 2) * py;
+  const double e = l * l + m * m;
+  return -e / (sqrt(1.0 - e) + 1.0);
+}
+
+// acc[i, j] (+)= (-1)^(p+q) Re(G^_p[..] exp(-2 pi i w_p (n - 1)))
+__global__ void wplane_accumulate_kernel(const double2* __restrict__ grid, int64_t nu, int64_t nv, int64_t nx,
+                                         int64_t ny, double px, double py, double w_plane, int first,
+                                         double* __restrict__ acc) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t i = blockIdx.y;
+  if (j >= ny) return;
+  const int64_t p = i - nx / 2, q = j - ny / 2;
+  const int64_t ip = (p + nu) % nu, iq = (q + nv) % nv;
+  const double sgn = ((p + q) & 1) ? -1.0 : 1.0;
+  const double nm1 = nm1_of(i, j, nx, ny, px, py);
+  double sn, cs;
+  sincospi(-2.0 * w_plane * nm1, &sn, &cs);
+  const double2 gval = grid[ip * nv + iq];
+  const double val = sgn * (gval.x * cs - gval.y * sn);
+  if (first) acc[i * ny + j] = val;
+  else acc[i * ny + j] += val;
+}
+
+hipError_t launch_wplane_accumulate(const double* grid, const GridGeometry& g, int64_t npix_x, int64_t npix_y,
+                                    double pixsize_x, double pixsize_y, double w_plane, int first, double* acc,
+                                    hipStream_t s) {
+  wplane_accumulate_kernel<<<dim3((unsigned)((npix_y + 255) / 256), (unsigned)npix_x), dim3(256), 0, s>>>(
+      (const double2*)grid, g.nu, g.nv, npix_x, npix_y, pixsize_x, pixsize_y, w_plane, first, acc);
+  return hipGetLastError();
+}
+
+// acc *= cx[i] cy[j] / (F(dw |n-1|) n): F from a uniform table (cubic Lagrange).
+__global__ void wfinal_correct_kernel(double* __restrict__ acc, int64_t nx, int64_t ny, double px, double py,
+                                      const double* __restrict__ cx, const double* __restrict__ cy,
+                                      const double* __restrict__ fw, int64_t fw_n, double fw_dnu, double dw) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t i = blockIdx.y;
+  if (j >= ny) return;
+  const double nm1 = nm1_of(i, j, nx, ny, px, py);
+  const double t = fabs(dw * nm1) / fw_dnu;
+  int64_t k = (int64_t)t;
+  if (k < 1) k = 1;
+  if (k > fw_n - 3) k = fw_n - 3;
+  const double x = t - (double)k;  // in [-1, 2]
+  const double f0 = fw[k - 1], f1 = fw[k], f2 = fw[k + 1], f3 = fw[k + 2];
+  const double F = -x * (x - 1.0) * (x - 2.0) / 6.0 * f0 + (x + 1.0) * (x - 1.0) * (x - 2.0) / 2.0 * f1 -
+                   (x + 1.0) * x * (x - 2.0) / 2.0 * f2 + (x + 1.0) * x * (x - 1.0) / 6.0 * f3;
+  acc[i * ny + j] *= cx[i] * cy[j] / (F * (nm1 + 1.0));
+}
+
+hipError_t launch_wfinal_correct(double* acc, int64_t npix_x, int64_t npix_y, double pixsize_x, double pixsize_y,
+                                 const double* cx, const double* cy, const double* fw_table, int64_t fw_n,
+                                 double fw_dnu, double dw, hipStream_t s) {
+  wfinal_correct_kernel<<<dim3((unsigned)((npix_y + 255) / 256), (unsigned)npix_x), dim3(256), 0, s>>>(
+      acc, npix_x, npix_y, pixsize_x, pixsize_y, cx, cy, fw_table, fw_n, fw_dnu, dw);
+  return hipGetLastError();
+}
+
+}  // namespace cip

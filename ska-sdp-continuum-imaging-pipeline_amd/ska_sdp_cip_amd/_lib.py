@@ -1,0 +1,150 @@
+"""
+ctypes binding of libcip_hip.so (C ABI: include/cip.h).
+
+The library is the product: there is no CPU fallback. `lib()` raises when the
+shared object is missing or cannot be loaded, and every call maps a negative
+status to a Python exception carrying `cip_last_error()`:
+CIP_EINVAL / CIP_ERANGE -> ValueError, CIP_EHIP -> RuntimeError,
+CIP_ENOMEM -> MemoryError.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+from pathlib import Path
+
+LIB_PATH = Path(__file__).resolve().parent / "_lib" / "libcip_hip.so"
+
+CIP_OK = 0
+CIP_EINVAL = -1
+CIP_ERANGE = -2
+CIP_EHIP = -3
+CIP_ENOMEM = -4
+
+CIP_NONE = 0
+CIP_C64 = 1
+CIP_C128 = 2
+CIP_F32 = 3
+CIP_F64 = 4
+
+# every symbol declared in include/cip.h
+EXPORTED_SYMBOLS = (
+    "cip_choose_params",
+    "cip_ms2dirty",
+    "cip_grid_plane",
+    "cip_tile_runs",
+    "cip_stokes_i",
+    "cip_last_error",
+    "cip_release_workspace",
+    "cip_profile_enable",
+    "cip_profile_last",
+    "cip_build_info",
+)
+
+PROFILE_PHASES = ("prep", "plan", "scatter", "fft", "correct", "total")
+PROFILE_COUNTS = ("visibilities", "runs", "chunks", "planes", "scatter_launches")
+
+
+class GridderParams(ctypes.Structure):
+    """Mirror of `cip_gridder_params` (include/cip.h)."""
+
+    _fields_ = [
+        ("nu", ctypes.c_int64),
+        ("nv", ctypes.c_int64),
+        ("support", ctypes.c_int32),
+        ("degree", ctypes.c_int32),
+        ("beta", ctypes.c_double),
+        ("sigma", ctypes.c_double),
+        ("do_wstacking", ctypes.c_int32),
+        ("tile", ctypes.c_int32),
+        ("nplanes", ctypes.c_int64),
+        ("w0", ctypes.c_double),
+        ("dw", ctypes.c_double),
+        ("nmin", ctypes.c_double),
+    ]
+
+    def as_dict(self) -> dict:
+        """Plain-dict view (for result files)."""
+        return {name: getattr(self, name) for name, _ in self._fields_}
+
+
+_LIB = None
+
+_vp = ctypes.c_void_p
+_i64 = ctypes.c_int64
+_i32 = ctypes.c_int
+_f64 = ctypes.c_double
+
+
+def lib() -> ctypes.CDLL:
+    """Load (once) and return the HIP library; raises if it is unavailable."""
+    global _LIB  # pylint: disable=global-statement
+    if _LIB is not None:
+        return _LIB
+    path = Path(os.environ.get("CIP_HIP_LIB", LIB_PATH))
+    if not path.exists():
+        raise RuntimeError(
+            f"libcip_hip.so not found at {path}; build it with "
+            "`python -c 'import __graft_entry__ as g; g.build()'` "
+            "(make -C ska-sdp-continuum-imaging-pipeline_amd/csrc)"
+        )
+    so = ctypes.CDLL(str(path))
+    so.cip_choose_params.argtypes = [_i64, _i64, _f64, _f64, _f64, _i32, _i32, _f64, _f64,
+                                     ctypes.POINTER(GridderParams)]
+    so.cip_ms2dirty.argtypes = [_vp, _i64, _vp, _i64, _vp, _i32, _vp, _i32, _i64, _i64, _f64, _f64,
+                                _f64, _i32, _i32, _vp, _vp, _vp, ctypes.POINTER(GridderParams)]
+    so.cip_grid_plane.argtypes = [_vp, _i64, _vp, _i64, _vp, _i32, _vp, _i32,
+                                  ctypes.POINTER(GridderParams), _f64, _f64, _i64, _vp, _vp]
+    so.cip_tile_runs.argtypes = [_vp, _i64, _vp, _i64, ctypes.POINTER(ctypes.c_double), _i64, _vp,
+                                 ctypes.POINTER(ctypes.c_int64), _vp, _vp, _vp, _vp]
+    so.cip_stokes_i.argtypes = [_vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp]
+    so.cip_profile_enable.argtypes = [_i32]
+    so.cip_profile_last.argtypes = [_vp, _vp]
+    so.cip_last_error.restype = ctypes.c_char_p
+    so.cip_build_info.restype = ctypes.c_char_p
+    for name in ("cip_choose_params", "cip_ms2dirty", "cip_grid_plane", "cip_tile_runs",
+                 "cip_stokes_i", "cip_release_workspace", "cip_profile_enable", "cip_profile_last"):
+        getattr(so, name).restype = ctypes.c_int
+    _LIB = so
+    return so
+
+
+def check(rc: int) -> None:
+    """Raise the Python exception matching a CIP status code."""
+    if rc == CIP_OK:
+        return
+    msg = lib().cip_last_error().decode(errors="replace")
+    if rc in (CIP_EINVAL, CIP_ERANGE):
+        raise ValueError(msg)
+    if rc == CIP_ENOMEM:
+        raise MemoryError(msg)
+    raise RuntimeError(f"libcip_hip error {rc}: {msg}")
+
+
+def choose_params(npix_x: int, npix_y: int, pixsize_x: float, pixsize_y: float,
+                  epsilon: float, support: int = 0, do_wstacking: bool = False,
+                  wmin: float = 0.0, wmax: float = 0.0) -> GridderParams:
+    """Host-only parameter choice (no GPU needed)."""
+    out = GridderParams()
+    check(lib().cip_choose_params(int(npix_x), int(npix_y), float(pixsize_x), float(pixsize_y),
+                                  float(epsilon), int(support or 0), int(bool(do_wstacking)),
+                                  float(wmin), float(wmax), ctypes.byref(out)))
+    return out
+
+
+def profile_enable(on: bool = True) -> None:
+    """Record per-phase hipEvents in subsequent calls on this thread."""
+    check(lib().cip_profile_enable(int(bool(on))))
+
+
+def profile_last() -> dict:
+    """Per-phase milliseconds and counters of the last call on this thread."""
+    import numpy as np  # pylint: disable=import-outside-toplevel
+
+    ms = np.zeros(len(PROFILE_PHASES), dtype=np.float64)
+    counts = np.zeros(len(PROFILE_COUNTS), dtype=np.int64)
+    check(lib().cip_profile_last(ms.ctypes.data, counts.ctypes.data))
+    out = {f"{k}_ms": float(v) for k, v in zip(PROFILE_PHASES, ms)}
+    out.update({k: int(v) for k, v in zip(PROFILE_COUNTS, counts)})
+    return out
