@@ -1,0 +1,204 @@
+"""
+CPU-only tests of the product's host side: the reader protocol and its
+partitioning, the tile data format (split / concatenate / rechunk / npz), the
+parameter choice of libcip_hip.so (host-only entry point) against the oracle,
+and the C ABI's exported symbols (no compute calls without a GPU).
+"""
+import ctypes
+import re
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+import oracle
+from ska_sdp_cip_amd import _lib, synthetic as syn
+from ska_sdp_cip_amd.invert import integrate_weighted_images, set_env
+from ska_sdp_cip_amd.measurement_set import (InMemoryMeasurementSet, MeasurementSetReader,
+                                             UnsupportedMeasurementSetLayout, balanced_chunk_bounds,
+                                             balanced_chunk_sizes)
+from ska_sdp_cip_amd.uvw_tiling import Tile, concatenate_tiles, rechunk_tiles_on_disk, split_tile
+
+ROOT = Path(__file__).resolve().parents[1]
+GOLD = ROOT / "tests" / "golden"
+
+
+def _ms(nrow=74214, nchan=4):
+    z = np.zeros
+    return InMemoryMeasurementSet(z((nrow, 3)), z((nrow, nchan, 4), np.complex64), z((nrow, nchan, 4), bool),
+                                  np.ones((nrow, nchan, 4), np.float32),
+                                  np.array([959969726.5625, 960805664.0625, 961641601.5625, 962477539.0625]))
+
+
+def test_partition_matches_reference_golden():
+    g = np.load(GOLD / "partition.npz")
+    ms = _ms()
+    for key in ("1x1", "2x3", "5x1", "7x4", "3x2"):
+        rc, fc = map(int, key.split("x"))
+        got = [(c.row_start, c.row_end, c.channel_start, c.channel_end) for c in ms.partition(rc, fc)]
+        assert got == [tuple(x) for x in g[key].tolist()]
+    ms.set_row_bounds(1000, 5001)
+    ms.set_channel_bounds(1, 4)
+    got = [(c.row_start, c.row_end, c.channel_start, c.channel_end) for c in ms.partition(3, 2)]
+    assert got == [tuple(x) for x in g["sub_3x2"].tolist()]
+
+
+def test_partition_raises_on_excessive_chunks():
+    # reference tests/test_measurement_set_partition_indices.py:87-97
+    ms = _ms()
+    with pytest.raises(ValueError):
+        ms.partition(1_000_000, 1)
+    with pytest.raises(ValueError):
+        ms.partition(1, 1_000_000)
+
+
+def test_bounds_clip_and_chunked_reads_equal_full_read():
+    ms = syn.make_measurement_set(300, 6, n_ant=8, array_radius_m=500.0, seed=2)
+    ms.set_row_bounds(-5, 10_000)
+    ms.set_channel_bounds(-1, 99)
+    assert (ms.row_start, ms.row_end, ms.channel_start, ms.channel_end) == (0, 300, 0, 6)
+    # reference tests/test_measurement_set_chunked_read.py: chunked == slices of full
+    for method in ("visibilities", "flags", "weights", "uvw", "channel_frequencies"):
+        full = getattr(ms, method)()
+        for rc, fc in [(1, 4), (2, 3), (7, 1)]:
+            for chunk in ms.partition(rc, fc):
+                part = getattr(chunk, method)()
+                if method == "uvw":
+                    ref = full[chunk.row_start:chunk.row_end]
+                elif method == "channel_frequencies":
+                    ref = full[chunk.channel_start:chunk.channel_end]
+                else:
+                    ref = full[chunk.row_start:chunk.row_end, chunk.channel_start:chunk.channel_end]
+                assert np.array_equal(part, ref)
+
+
+def test_weight_column_fallback_repeats_over_channels():
+    ms = syn.make_measurement_set(50, 3, n_ant=6, array_radius_m=300.0, weight_spectrum=False)
+    w = ms.weights()
+    assert w.shape == (50, 3, 4) and w.dtype == np.float32
+    assert np.array_equal(w[:, 0], w[:, 2])
+
+
+def test_reader_errors():
+    with pytest.raises(FileNotFoundError):
+        MeasurementSetReader("/nonexistent/path.ms")
+    with pytest.raises(UnsupportedMeasurementSetLayout):
+        InMemoryMeasurementSet(np.zeros((2, 3)), np.zeros((2, 1, 2), np.complex64), np.zeros((2, 1, 4), bool),
+                               np.ones((2, 1, 4), np.float32), np.ones(1))
+    with pytest.raises(ValueError):
+        list(balanced_chunk_sizes(0, 1))
+    with pytest.raises(ValueError):
+        list(balanced_chunk_sizes(3, 4))
+
+
+def test_balanced_bounds_match_golden():
+    g = np.load(GOLD / "partition.npz")
+    for key in g.files:
+        if key.startswith("bounds_"):
+            _, s, e, k = key.split("_")
+            assert list(balanced_chunk_bounds(int(s), int(e), int(k))) == [tuple(x) for x in g[key].tolist()]
+
+
+def _golden_tile():
+    g = np.load(GOLD / "tile_split.npz")
+    return g, Tile((1, -2, 0), g["uvw"], g["visibilities"], g["chan_start"], g["chan_stop"])
+
+
+@pytest.mark.parametrize("mv", [1, 25, 64, 100, 1000, 10_000])
+def test_split_tile_matches_reference(mv):
+    g, tile = _golden_tile()
+    chunks = split_tile(tile, mv)
+    assert [c.num_rows for c in chunks] == g[f"split_{mv}__nrows"].tolist()
+    assert [c.num_visibilities for c in chunks] == g[f"split_{mv}__nvis"].tolist()
+    cat = concatenate_tiles(chunks)
+    assert np.array_equal(cat.visibilities, tile.visibilities) and np.array_equal(cat.uvw, tile.uvw)
+
+
+def test_concatenate_errors():
+    _, tile = _golden_tile()
+    with pytest.raises(ValueError):
+        concatenate_tiles([])
+    other = Tile((0, 0, 0), tile.uvw, tile.visibilities, tile.channel_start_indices, tile.channel_stop_indices)
+    with pytest.raises(ValueError):
+        concatenate_tiles([tile, other])
+
+
+def test_npz_roundtrip_and_rechunk(tmp_path):
+    _, tile = _golden_tile()
+    parts = split_tile(tile, 100)
+    paths = []
+    for i, p in enumerate(parts):
+        path = tmp_path / f"in_{i:02d}.npz"
+        p.save_npz(path)
+        paths.append(path)
+    back = Tile.load_npz(paths[0])
+    assert back.coords == (1, -2, 0) and np.array_equal(back.visibilities, parts[0].visibilities)
+    out = rechunk_tiles_on_disk(paths, tmp_path, "tile_x", max_vis_per_chunk=250)
+    assert [p.name for p in out] == [f"tile_x_chunk{i:03d}.npz" for i in range(len(out))]
+    tiles = [Tile.load_npz(p) for p in out]
+    assert all(t.num_visibilities <= 250 for t in tiles)
+    assert np.array_equal(np.concatenate([t.visibilities for t in tiles]), tile.visibilities)
+
+
+def test_tile_weights_extension_roundtrip(tmp_path):
+    _, tile = _golden_tile()
+    tile.weights = np.arange(tile.num_visibilities, dtype=np.float32)
+    tile.save_npz(tmp_path / "t.npz")
+    back = Tile.load_npz(tmp_path / "t.npz")
+    assert np.array_equal(back.weights, tile.weights)
+    assert all(np.array_equal(c.weights, tile.weights[i:i + c.num_visibilities])
+               for c, i in zip(split_tile(tile, 64), np.cumsum([0] + [c.num_visibilities
+                                                                      for c in split_tile(tile, 64)])))
+
+
+def test_from_jagged_slice_gather():
+    rng = np.random.default_rng(0)
+    vis = (rng.standard_normal((10, 8)) + 1j * rng.standard_normal((10, 8))).astype(np.complex64)
+    uvw = rng.standard_normal((10, 3))
+    slices = [(1, 2, 5), (4, 0, 1), (9, 3, 8)]
+    t = Tile._from_jagged_visibilities_slice(vis, uvw, (0, 1, 2), slices)  # pylint: disable=protected-access
+    assert np.array_equal(t.visibilities, np.concatenate([vis[1, 2:5], vis[4, 0:1], vis[9, 3:8]]))
+    assert np.array_equal(t.uvw, uvw[[1, 4, 9]])
+
+
+def test_params_match_oracle():
+    for npix, px, eps, sup, ws, wr in [(4096, 1e-5, 1e-4, 8, False, (0, 0)), (128, 8e-5, 1e-4, None, True, (-900.0, 1400.0)),
+                                       (1000, 3e-5, 1e-7, None, True, (-50.0, 20000.0)), (250, 1e-4, 1e-3, 4, False, (0, 0))]:
+        p = _lib.choose_params(npix, npix, px, px, eps, sup or 0, ws, *wr)
+        o = oracle.choose_params(npix, npix, px, px, eps, sup, ws, *wr)
+        assert (p.nu, p.nv, p.support, p.nplanes) == (o["nu"], o["nv"], o["support"], o["nplanes"])
+        assert p.w0 == pytest.approx(o["w0"], rel=1e-15, abs=1e-12) and p.dw == pytest.approx(o["dw"], rel=1e-15)
+    with pytest.raises(ValueError):
+        _lib.choose_params(63, 64, 1e-5, 1e-5, 1e-4)
+    with pytest.raises(ValueError):
+        _lib.choose_params(64, 64, 1e-5, 1e-5, 1e-4, support=18)
+    with pytest.raises(ValueError):
+        _lib.choose_params(64, 64, 0.1, 0.1, 1e-4, do_wstacking=True)  # beyond the horizon
+
+
+def test_library_exports_every_declared_symbol():
+    header = (ROOT / "include" / "cip.h").read_text()
+    declared = set(re.findall(r"^(?:int|const char\*)\s+(cip_\w+)\(", header, flags=re.M))
+    assert declared == set(_lib.EXPORTED_SYMBOLS)
+    so = ctypes.CDLL(str(_lib.LIB_PATH))
+    for name in declared:
+        assert hasattr(so, name), name
+    assert b"gfx950" in _lib.lib().cip_build_info()
+
+
+def test_integrate_and_set_env(monkeypatch):
+    imgs = [(np.ones((2, 2)), 2.0), (3 * np.ones((2, 2)), 6.0)]
+    assert np.allclose(integrate_weighted_images(imgs), 0.5)
+    monkeypatch.delenv("CIP_TEST_VAR", raising=False)
+    with set_env("CIP_TEST_VAR", 3):
+        import os
+
+        assert os.environ["CIP_TEST_VAR"] == "3"
+    assert "CIP_TEST_VAR" not in os.environ
+
+
+def test_synthetic_ms_shapes():
+    ms = syn.make_measurement_set(500, 4, n_ant=8, array_radius_m=500.0)
+    assert ms.visibilities().dtype == np.complex64 and ms.visibilities().shape == (500, 4, 4)
+    assert ms.flags().dtype == bool and ms.weights().dtype == np.float32
+    assert ms.uvw().shape == (500, 3) and ms.uvw().dtype == np.float64
