@@ -264,6 +264,8 @@ struct Workspace {
   std::vector<FftPlan> plans;
   void* pinned = nullptr;  // small host staging
   size_t pinned_bytes = 0;
+  std::vector<int64_t> corr_key;  // (npix_x, npix_y, nu, nv, W) of the cached cx / cy
+  std::vector<double> fw_key;     // (W, dw |nmin|) of the cached w-correction table
 };
 
 static std::mutex g_ws_mutex;
@@ -354,14 +356,11 @@ static int make_plan(Workspace* ws, const double* uvw, int64_t nrow, const doubl
   CIP_ALLOC(err, unsigned, "err_flag", 1)
   CIP_ALLOC(scan_tmp, int64_t, "scan_tmp", scan_tmp_elems(ntiles + 1))
   CIP_HIP_CHECK(hipMemsetAsync(tile_runs, 0, sizeof(int64_t) * (ntiles + 1), s));
-  CIP_HIP_CHECK(hipMemsetAsync(tile_vis, 0, sizeof(int64_t) * (ntiles + 1), s));
   CIP_HIP_CHECK(hipMemsetAsync(tile_cursor, 0, sizeof(int64_t) * (ntiles + 1), s));
   CIP_HIP_CHECK(hipMemsetAsync(err, 0, sizeof(unsigned), s));
-  CIP_HIP_CHECK(launch_plan_count(uvw, nrow, fx, nchan, g, tile_runs, tile_vis, err, s));
+  CIP_HIP_CHECK(launch_plan_count(uvw, nrow, fx, nchan, g, tile_runs, nullptr, err, s));
   // tile_runs -> exclusive offsets (entry ntiles = total runs)
   CIP_HIP_CHECK(exclusive_scan_i64(tile_runs, ntiles + 1, scan_tmp, s));
-  CIP_HIP_CHECK(hipMemcpyAsync(tile_vis_off, tile_vis, sizeof(int64_t) * (ntiles + 1), hipMemcpyDeviceToDevice, s));
-  CIP_HIP_CHECK(exclusive_scan_i64(tile_vis_off, ntiles + 1, scan_tmp, s));
   int64_t* h = (int64_t*)pinned(ws, 4 * sizeof(int64_t));
   if (!h) return set_error(CIP_ENOMEM, "hipHostMalloc failed");
   CIP_HIP_CHECK(hipMemcpyAsync(&h[0], tile_runs + ntiles, sizeof(int64_t), hipMemcpyDeviceToHost, s));
@@ -369,8 +368,7 @@ static int make_plan(Workspace* ws, const double* uvw, int64_t nrow, const doubl
   CIP_HIP_CHECK(hipStreamSynchronize(s));
   const int64_t nruns = h[0];
   if ((unsigned)h[1] != 0)
-    return set_error(CIP_ERANGE, "some (u, v, w) coordinates fall outside the grid; increase the pixel size "
-                                 "or reduce the image size");
+    return set_error(CIP_ERANGE, "non-finite (u, v, w) coordinates, or w outside the w-plane stack");
   pr->nruns = nruns;
   const int64_t* tile_run_off = tile_runs;
   CIP_ALLOC(runs, uint64_t, "runs", nruns)
@@ -379,6 +377,7 @@ static int make_plan(Workspace* ws, const double* uvw, int64_t nrow, const doubl
   CIP_HIP_CHECK(launch_plan_emit(uvw, nrow, fx, nchan, g, tile_run_off, tile_cursor, runs, s));
   CIP_HIP_CHECK(launch_run_lengths(runs, nruns, run_goff, s));
   CIP_HIP_CHECK(exclusive_scan_i64(run_goff, nruns + 1, scan_tmp2, s));
+  CIP_HIP_CHECK(launch_tile_vis(run_goff, tile_run_off, ntiles, tile_vis_off, tile_vis, s));
   CIP_HIP_CHECK(launch_chunk_counts(tile_vis, ntiles, kChunkVis, chunk_off, s));
   CIP_HIP_CHECK(exclusive_scan_i64(chunk_off, ntiles + 1, scan_tmp, s));
   // chunk offsets of each w tile layer
@@ -549,13 +548,17 @@ int cip_ms2dirty(const double* uvw, int64_t nrow, const double* freq, int64_t nc
   HostKernel hk;
   host_kernel(g.support, &hk);
   KernelFT F(hk);
-  {
+  // the correction vectors depend only on (npix, grid, W): cache them per device
+  const std::vector<int64_t> corr_key = {npix_x, npix_y, g.nu, g.nv, g.support};
+  if (ws->corr_key != corr_key) {
+    ws->corr_key.clear();
     std::vector<double> hx(npix_x), hy(npix_y);
     for (int64_t i = 0; i < npix_x; ++i) hx[i] = 1.0 / F((double)(i - npix_x / 2) / (double)g.nu);
     for (int64_t j = 0; j < npix_y; ++j) hy[j] = 1.0 / F((double)(j - npix_y / 2) / (double)g.nv);
     CIP_HIP_CHECK(hipMemcpyAsync(cx, hx.data(), sizeof(double) * npix_x, hipMemcpyHostToDevice, s));
     CIP_HIP_CHECK(hipMemcpyAsync(cy, hy.data(), sizeof(double) * npix_y, hipMemcpyHostToDevice, s));
     CIP_HIP_CHECK(hipStreamSynchronize(s));  // host vectors go out of scope
+    ws->corr_key = corr_key;
   }
   hipfftHandle plan;
   rc = fft_plan(ws, g.nu, g.nv, s, &plan);
@@ -581,10 +584,16 @@ int cip_ms2dirty(const double* uvw, int64_t nrow, const double* freq, int64_t nc
     const int64_t fw_n = 4100;
     const double numax = g.dw * std::fabs(pp.p.nmin);
     const double dnu = (numax > 0 ? numax : 1e-3) * 1.0001 / 4096.0;
-    std::vector<double> fw(fw_n);
-    for (int64_t k = 0; k < fw_n; ++k) fw[k] = F((double)k * dnu);
     CIP_ALLOC(fwd, double, "fw_table", fw_n)
-    CIP_HIP_CHECK(hipMemcpyAsync(fwd, fw.data(), sizeof(double) * fw_n, hipMemcpyHostToDevice, s));
+    const std::vector<double> fw_key = {(double)g.support, numax};
+    if (ws->fw_key != fw_key) {
+      ws->fw_key.clear();
+      std::vector<double> fw(fw_n);
+      for (int64_t k = 0; k < fw_n; ++k) fw[k] = F((double)k * dnu);
+      CIP_HIP_CHECK(hipMemcpyAsync(fwd, fw.data(), sizeof(double) * fw_n, hipMemcpyHostToDevice, s));
+      CIP_HIP_CHECK(hipStreamSynchronize(s));
+      ws->fw_key = fw_key;
+    }
     CIP_HIP_CHECK(
         launch_wfinal_correct(dirty_out, npix_x, npix_y, pixsize_x, pixsize_y, cx, cy, fwd, fw_n, dnu, g.dw, s));
     CIP_HIP_CHECK(hipStreamSynchronize(s));

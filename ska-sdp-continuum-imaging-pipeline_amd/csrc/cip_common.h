@@ -118,7 +118,12 @@ __device__ __forceinline__ bool place_vis(double u_m, double v_m, double w_m, do
   const double y = (v_m * fx) * g.scale_v + (double)(g.nv / 2);
   footprint(x, hw, ix0, yu);
   footprint(y, hw, iy0, yv);
-  bool ok = (*ix0 >= 0) && (*ix0 + g.support <= g.nu) && (*iy0 >= 0) && (*iy0 + g.support <= g.nv);
+  // The dirty image is sampled at l = k * pixsize, so it is periodic in u with
+  // period 1 / pixsize = the grid extent: coordinates beyond the grid wrap
+  // (exactly, as ducc0 does), and the footprint origin is taken modulo nu.
+  *ix0 = ((*ix0 % g.nu) + g.nu) % g.nu;
+  *iy0 = ((*iy0 % g.nv) + g.nv) % g.nv;
+  bool ok = true;
   if (g.do_wstacking) {
     const double xw = ((w_m * fx) - g.w0) / g.dw;
     footprint(xw, hw, iw0, yw);
@@ -127,8 +132,8 @@ __device__ __forceinline__ bool place_vis(double u_m, double v_m, double w_m, do
     *iw0 = 0;
     *yw = 0.0;
   }
-  // NaN coordinates fail every comparison above except the casts; reject them
-  ok = ok && (x == x) && (y == y);
+  // non-finite coordinates are an error (the planner raises)
+  ok = ok && isfinite(x) && isfinite(y) && fabs(x) < 9.0e15 && fabs(y) < 9.0e15;
   return ok;
 }
 

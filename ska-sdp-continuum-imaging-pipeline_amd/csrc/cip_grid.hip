@@ -153,7 +153,10 @@ __device__ __forceinline__ void grid_one(const double* __restrict__ uvw, const d
     kr[j] = kv[j] * vr;
     ki[j] = kv[j] * vi;
   }
-  unsigned long long* base = sub + 2 * (lx * P + ly);
+  // separate re / im planes: a lane-scattered 8-byte add touches 2 of the 64
+  // LDS banks, so 8-byte cells spread a wave over twice the bank pairs that
+  // interleaved 16-byte (re, im) cells would
+  unsigned long long* base = sub + (lx * P + ly);
 #pragma unroll
   for (int i = 0; i < W; ++i) {
 #pragma unroll
@@ -162,8 +165,8 @@ __device__ __forceinline__ void grid_one(const double* __restrict__ uvw, const d
       const double qi = fma(ku[i], ki[j], kMagic);
       const unsigned long long br = (unsigned long long)__double_as_longlong(qr) - 0x4338000000000000ull;
       const unsigned long long bi = (unsigned long long)__double_as_longlong(qi) - 0x4338000000000000ull;
-      atomicAdd(base + 2 * (i * P + j), br);
-      atomicAdd(base + 2 * (i * P + j) + 1, bi);
+      atomicAdd(base + (i * P + j), br);
+      atomicAdd(base + P * P + (i * P + j), bi);
     }
   }
 }
@@ -227,15 +230,16 @@ __global__ __launch_bounds__(kScatterThreads) void scatter_kernel(
   __syncthreads();
   // flush the touched cells of the sub-grid to the fp64 HBM grid
   for (int cell = threadIdx.x; cell < P * P; cell += kScatterThreads) {
-    const long long re = (long long)sub[2 * cell];
-    const long long im = (long long)sub[2 * cell + 1];
+    const long long re = (long long)sub[cell];
+    const long long im = (long long)sub[P * P + cell];
     if ((re | im) != 0) {
-      const int64_t gx = X0 + cell / P, gy = Y0 + cell % P;
-      if (gx < g.nu && gy < g.nv) {
-        double* dst = grid + 2 * (gx * g.nv + gy);
-        unsafeAtomicAdd(dst, (double)re * inv_scale);
-        unsafeAtomicAdd(dst + 1, (double)im * inv_scale);
-      }
+      // the sub-grid of an edge tile wraps around the periodic grid
+      int64_t gx = X0 + cell / P, gy = Y0 + cell % P;
+      gx -= (gx >= g.nu) ? g.nu : 0;
+      gy -= (gy >= g.nv) ? g.nv : 0;
+      double* dst = grid + 2 * (gx * g.nv + gy);
+      unsafeAtomicAdd(dst, (double)re * inv_scale);
+      unsafeAtomicAdd(dst + 1, (double)im * inv_scale);
     }
   }
 }

@@ -37,6 +37,8 @@ hipError_t launch_plan_count(const double* uvw, int64_t nrow, const double* fx, 
 hipError_t launch_plan_emit(const double* uvw, int64_t nrow, const double* fx, int64_t nchan,
                             const GridGeometry& g, const int64_t* tile_run_off, int64_t* tile_cursor,
                             uint64_t* runs, hipStream_t s);
+hipError_t launch_tile_vis(const int64_t* run_goff, const int64_t* tile_run_off, int64_t ntiles,
+                           int64_t* tile_vis_off, int64_t* tile_vis, hipStream_t s);
 hipError_t launch_run_lengths(const uint64_t* runs, int64_t nruns, int64_t* out, hipStream_t s);
 hipError_t launch_chunk_counts(const int64_t* tile_vis, int64_t ntiles, int64_t chunk_vis,
                                int64_t* out, hipStream_t s);

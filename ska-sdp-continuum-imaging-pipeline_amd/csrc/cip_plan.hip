@@ -157,8 +157,9 @@ __global__ __launch_bounds__(256) void plan_kernel(const double* __restrict__ uv
           const int64_t pos = tile_run_off[prev] + atomicAdd((unsigned long long*)&tile_cursor[prev], 1ull);
           runs[pos] = ((uint64_t)r << 32) | ((uint64_t)start << 16) | (uint64_t)c;
         } else {
+          // one atomic per run; per-tile visibility counts come later from
+          // the scanned run lengths (tile_vis_kernel)
           atomicAdd((unsigned long long*)&tile_runs[prev], 1ull);
-          atomicAdd((unsigned long long*)&tile_vis[prev], (unsigned long long)(c - start));
         }
       }
       prev = key;
@@ -195,6 +196,23 @@ __global__ void run_lengths_kernel(const uint64_t* runs, int64_t nruns, int64_t*
 
 hipError_t launch_run_lengths(const uint64_t* runs, int64_t nruns, int64_t* out, hipStream_t s) {
   run_lengths_kernel<<<dim3((unsigned)((nruns + 256) / 256)), dim3(256), 0, s>>>(runs, nruns, out);
+  return hipGetLastError();
+}
+
+// tile_vis_off[t] = run_goff[tile_run_off[t]], tile_vis[t] = its difference
+__global__ void tile_vis_kernel(const int64_t* run_goff, const int64_t* tile_run_off, int64_t ntiles,
+                                int64_t* tile_vis_off, int64_t* tile_vis) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t > ntiles) return;
+  const int64_t a = run_goff[tile_run_off[t]];
+  tile_vis_off[t] = a;
+  if (t < ntiles) tile_vis[t] = run_goff[tile_run_off[t + 1]] - a;
+}
+
+hipError_t launch_tile_vis(const int64_t* run_goff, const int64_t* tile_run_off, int64_t ntiles,
+                           int64_t* tile_vis_off, int64_t* tile_vis, hipStream_t s) {
+  tile_vis_kernel<<<dim3((unsigned)((ntiles + 256) / 256)), dim3(256), 0, s>>>(run_goff, tile_run_off, ntiles,
+                                                                               tile_vis_off, tile_vis);
   return hipGetLastError();
 }
 

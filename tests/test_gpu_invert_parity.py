@@ -129,9 +129,28 @@ def test_point_source_at_centre_and_off_centre(gpu_device):
         assert abs(img[i, j] - 1.0 / n) < 1e-8
 
 
-def test_uv_outside_grid_raises(gpu_device):
-    uvw, f, vis, w = _case(1_000, 1)
-    px = syn.pixel_size_for_grid(uvw, f, 64) * 3.0  # grid far too small
+@pytest.mark.parametrize("wstack", [False, True])
+def test_uv_beyond_grid_wraps_like_the_dft(gpu_device, wstack):
+    # the image is sampled at l = k * pixsize, so u is periodic with period
+    # 1 / pixsize (the grid extent): baselines longer than the grid wrap exactly
+    # (the reference's own test set-up, 2048 px at 5", wraps MeerKAT baselines)
+    uvw, f, vis, w = _case(3_000, 2, fov=0.02, seed=1)
+    npix = 64
+    px = syn.pixel_size_for_grid(uvw, f, npix) * 3.0
+    gpu = gridder.ms2dirty(uvw, f, vis.astype(np.complex128), w.astype(np.float64), npix, npix, px, px,
+                           support=12, do_wstacking=wstack)
+    dft = oracle.dft_dirty(uvw, f, vis, w, npix, npix, px, px, apply_w=wstack)
+    ref = oracle.ms2dirty(uvw, f, vis, w, npix, npix, px, px, support=12, do_wstacking=wstack)
+    sumw = float(w.astype(np.float64).sum())
+    assert _norm_err(gpu, ref, sumw) < TIGHT
+    assert _norm_err(gpu, dft, sumw) < 1e-9
+
+
+def test_non_finite_uvw_raises(gpu_device):
+    uvw, f, vis, w = _case(500, 1)
+    uvw = uvw.copy()
+    uvw[17, 0] = np.nan
+    px = syn.pixel_size_for_grid(uvw[:10], f, 64)
     with pytest.raises(ValueError):
         gridder.ms2dirty(uvw, f, vis, w, 64, 64, px, px, support=8, do_wstacking=False)
 

@@ -32,3 +32,18 @@ def test_oracle_vs_dft(case, support, wstack):
     err = np.abs(img - dft[wstack]).max() / w.astype(np.float64).sum()
     assert err < EXPECTED[support], err
     assert oracle.support_for_epsilon(EXPECTED[support] * 0.99) >= support
+
+
+@pytest.mark.parametrize("wstack", [False, True])
+def test_oracle_wraps_periodic_uv_exactly(wstack):
+    # pixel 3x too coarse: most baselines lie beyond the grid and wrap; the DFT
+    # on the pixel grid is periodic in u with period 1 / pixsize, so the
+    # wrapped gridder must still reproduce it
+    ms = syn.make_measurement_set(3_000, 2, n_ant=16, array_radius_m=1000.0, fov_l=0.02, seed=1)
+    vis, _, _, w = oracle.stokes_i(ms.visibilities(), ms.flags(), ms.weights())
+    uvw, f = ms.uvw(), ms.channel_frequencies()
+    npix = 64
+    px = syn.pixel_size_for_grid(uvw, f, npix) * 3.0
+    dft = oracle.dft_dirty(uvw, f, vis, w, npix, npix, px, px, apply_w=wstack)
+    img = oracle.ms2dirty(uvw, f, vis, w, npix, npix, px, px, support=12, do_wstacking=wstack)
+    assert np.abs(img - dft).max() / w.astype(np.float64).sum() < 1e-10
