@@ -142,6 +142,7 @@ def main():
     import torch.distributed as dist
 
     from ska_sdp_cip_amd import _lib, gridder
+    from ska_sdp_cip_amd.distributed import reduce_images
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -161,11 +162,8 @@ def main():
     def step():
         gridder.device_ms2dirty(uvw_d, freq_d, vis_d, wgt_d, npix, npix, px, px, support=args.support,
                                 do_wstacking=args.wstacking, out=dirty, sum_weights=sumw)
-        if world > 1:
-            dist.reduce(dirty, 0)
-            dist.reduce(sumw, 0)
-        if rank == 0:
-            dirty.div_(sumw)
+        # RCCL reduce of the partial images + weights to rank 0, normalise there
+        reduce_images(dirty, sumw, dst=0)
 
     log(f"[bench] rank {rank}/{world} config {args.config}: {nvis:,} vis/GPU, {npix}^2 image, "
         f"pixsize {px:.3e} rad, support {args.support}, wstacking={args.wstacking}")
