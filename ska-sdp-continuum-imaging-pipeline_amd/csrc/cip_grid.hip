@@ -171,7 +171,24 @@ __device__ __forceinline__ void grid_one(const double* __restrict__ uvw, const d
   }
 }
 
-template <int W, typename VisT, int WK, bool WSTACK>
+// last staged run starting at or before flattened visibility q
+__device__ __forceinline__ void locate_vis(int64_t q, const int64_t* s_voff, const uint64_t* s_run, int nst,
+                                           int64_t* irow, int64_t* c) {
+  int lo = 0, hi = nst - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (s_voff[mid] <= q) lo = mid;
+    else hi = mid - 1;
+  }
+  const uint64_t rec = s_run[lo];
+  *irow = (int64_t)(rec >> 32);
+  *c = (int64_t)((rec >> 16) & 0xffff) + (q - s_voff[lo]);
+}
+
+constexpr int kSortPer = 4;
+constexpr int kSortBatch = kScatterThreads * kSortPer;
+
+template <int W, typename VisT, int WK, bool WSTACK, bool ORDER>
 __global__ __launch_bounds__(kScatterThreads) void scatter_kernel(
     const double* __restrict__ uvw, const double* __restrict__ fx, const VisT* __restrict__ vis,
     const void* __restrict__ wgt, int64_t nchan, const uint64_t* __restrict__ runs,
@@ -184,6 +201,8 @@ __global__ __launch_bounds__(kScatterThreads) void scatter_kernel(
   __shared__ int64_t s_voff[kRunBatch + 1];
   __shared__ uint64_t s_run[kRunBatch];
   __shared__ int64_t s_first;
+  __shared__ __attribute__((aligned(16))) unsigned s_cnt[32];
+  __shared__ uint64_t s_order[ORDER ? kSortBatch : 1];
 
   const Chunk ch = chunks[chunk_begin + blockIdx.x];
   const int64_t t = ch.tile;
@@ -212,17 +231,70 @@ __global__ __launch_bounds__(kScatterThreads) void scatter_kernel(
     }
     __syncthreads();
     const int64_t bend = ch.g1 < s_voff[nst] ? ch.g1 : s_voff[nst];
-    for (int64_t q = v + threadIdx.x; q < bend; q += kScatterThreads) {
-      int lo = 0, hi = nst - 1;  // last staged run starting at or before q
-      while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (s_voff[mid] <= q) lo = mid;
-        else hi = mid - 1;
+    if constexpr (!ORDER) {
+      for (int64_t q = v + threadIdx.x; q < bend; q += kScatterThreads) {
+        int64_t irow, c;
+        locate_vis(q, s_voff, s_run, nst, &irow, &c);
+        grid_one<W, VisT, WK, WSTACK>(uvw, fx, vis, wgt, nchan, irow, c, g, plane, X0, Y0, fixed_scale, sub);
       }
-      const uint64_t rec = s_run[lo];
-      const int64_t irow = (int64_t)(rec >> 32);
-      const int64_t c = (int64_t)((rec >> 16) & 0xffff) + (q - s_voff[lo]);
-      grid_one<W, VisT, WK, WSTACK>(uvw, fx, vis, wgt, nchan, irow, c, g, plane, X0, Y0, fixed_scale, sub);
+    } else {
+      // Bank-class interleave: a lane-scattered 8-byte LDS atomic hits bank
+      // pair (cell mod 32). Order each sub-batch level-major by that class
+      // (position = rank-within-class major, class minor, compacted), so the
+      // lanes of a wave-instruction add into distinct bank pairs.
+      for (int64_t sb = v; sb < bend; sb += kSortBatch) {
+        const int nsb = (int)((bend - sb) < kSortBatch ? (bend - sb) : kSortBatch);
+        if (threadIdx.x < 32) s_cnt[threadIdx.x] = 0u;
+        __syncthreads();
+        uint64_t packed[kSortPer];
+        int cls[kSortPer];
+        unsigned rk[kSortPer];
+#pragma unroll
+        for (int k = 0; k < kSortPer; ++k) {
+          const int qi = threadIdx.x + k * kScatterThreads;
+          cls[k] = -1;
+          if (qi < nsb) {
+            int64_t irow, c;
+            locate_vis(sb + qi, s_voff, s_run, nst, &irow, &c);
+            packed[k] = ((uint64_t)irow << 16) | (uint64_t)c;
+            int64_t ix0, iy0, iw0;
+            double yu, yv, yw;
+            place_vis(uvw[3 * irow], uvw[3 * irow + 1], uvw[3 * irow + 2], fx[c], g, &ix0, &yu, &iy0, &yv, &iw0,
+                      &yw);
+            cls[k] = (int)(((ix0 - X0) * P + (iy0 - Y0)) & 31);
+            rk[k] = atomicAdd(&s_cnt[cls[k]], 1u);
+          }
+        }
+        __syncthreads();
+        unsigned cnt[32];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const uint4 c4 = reinterpret_cast<const uint4*>(s_cnt)[i];
+          cnt[4 * i] = c4.x;
+          cnt[4 * i + 1] = c4.y;
+          cnt[4 * i + 2] = c4.z;
+          cnt[4 * i + 3] = c4.w;
+        }
+#pragma unroll
+        for (int k = 0; k < kSortPer; ++k) {
+          if (cls[k] >= 0) {
+            unsigned pos = 0;
+#pragma unroll
+            for (int c2 = 0; c2 < 32; ++c2) {
+              pos += cnt[c2] < rk[k] ? cnt[c2] : rk[k];
+              pos += (c2 < cls[k] && cnt[c2] > rk[k]) ? 1u : 0u;
+            }
+            s_order[pos] = packed[k];
+          }
+        }
+        __syncthreads();
+        for (int pi = threadIdx.x; pi < nsb; pi += kScatterThreads) {
+          const uint64_t pk = s_order[pi];
+          grid_one<W, VisT, WK, WSTACK>(uvw, fx, vis, wgt, nchan, (int64_t)(pk >> 16), (int64_t)(pk & 0xffff), g,
+                                        plane, X0, Y0, fixed_scale, sub);
+        }
+        __syncthreads();
+      }
     }
     v = bend;
     r += nst;
@@ -244,20 +316,34 @@ __global__ __launch_bounds__(kScatterThreads) void scatter_kernel(
   }
 }
 
+static int scatter_order_mode() {
+  static int mode = -1;
+  if (mode < 0) {
+    const char* e = getenv("CIP_SCATTER_ORDER");
+    mode = (e && e[0] == '0') ? 0 : 1;
+  }
+  return mode;
+}
+
 template <int W, typename VisT, int WK>
 static hipError_t scatter_dispatch_ws(bool ws, dim3 grid_dim, hipStream_t s, const double* uvw, const double* fx,
                                       const void* vis, const void* wgt, int64_t nchan, const uint64_t* runs,
                                       const int64_t* run_goff, const int64_t* tile_run_off, const Chunk* chunks,
                                       int64_t chunk_begin, const GridGeometry& g, int64_t plane, double fs,
                                       double* grid) {
-  if (ws)
-    scatter_kernel<W, VisT, WK, true><<<grid_dim, dim3(kScatterThreads), 0, s>>>(
-        uvw, fx, (const VisT*)vis, wgt, nchan, runs, run_goff, tile_run_off, chunks, chunk_begin, g, plane, fs,
-        1.0 / fs, grid);
-  else
-    scatter_kernel<W, VisT, WK, false><<<grid_dim, dim3(kScatterThreads), 0, s>>>(
-        uvw, fx, (const VisT*)vis, wgt, nchan, runs, run_goff, tile_run_off, chunks, chunk_begin, g, plane, fs,
-        1.0 / fs, grid);
+#define LAUNCH(WSV, ORD)                                                                                     \
+  scatter_kernel<W, VisT, WK, WSV, ORD><<<grid_dim, dim3(kScatterThreads), 0, s>>>(                          \
+      uvw, fx, (const VisT*)vis, wgt, nchan, runs, run_goff, tile_run_off, chunks, chunk_begin, g, plane, fs, \
+      1.0 / fs, grid)
+  const bool ord = scatter_order_mode() != 0;
+  if (ws) {
+    if (ord) LAUNCH(true, true);
+    else LAUNCH(true, false);
+  } else {
+    if (ord) LAUNCH(false, true);
+    else LAUNCH(false, false);
+  }
+#undef LAUNCH
   return hipGetLastError();
 }
 

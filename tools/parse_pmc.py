@@ -1,0 +1,62 @@
+"""
+Summarise rocprofv3 --pmc runs (one counter per pass) into per-kernel
+averages and write profiles/traffic_<config>.json for bench.py's
+roofline.traffic. gfx950 corrections (MI355X_MICROARCH.md, HBM section):
+FETCH_SIZE (KB) counts exactly half the bytes of wide coalesced reads -> x2;
+WRITE_SIZE (KB) reads the bytes exactly for 16-B stores and float atomics.
+Usage: python tools/parse_pmc.py <round> <config> <dir>...
+"""
+import csv
+import json
+import sys
+from collections import defaultdict
+from pathlib import Path
+
+
+def short(name: str) -> str:
+    name = name.split("(")[0]
+    for key in ("scatter_kernel", "plan_kernel<true>", "plan_kernel<false>", "prep_kernel", "fft_rtc",
+                "transpose_rtc", "crop_correct", "scan_local", "scan_add", "run_lengths", "tile_vis",
+                "chunk_emit", "chunk_counts", "fillBuffer"):
+        if key in name:
+            return key
+    return name[-60:]
+
+
+def main():
+    rnd, config, dirs = sys.argv[1], sys.argv[2], sys.argv[3:]
+    vals = defaultdict(lambda: defaultdict(list))
+    for d in dirs:
+        for f in Path(d).glob("*counter_collection.csv"):
+            for row in csv.DictReader(open(f)):
+                vals[short(row["Kernel_Name"])][row["Counter_Name"]].append(float(row["Counter_Value"]))
+    out = {}
+    lines = [f"# PMC summary {rnd} ({config}); per-dispatch averages", "",
+             "| kernel | dispatches | FETCH_SIZE KB (raw) | HBM read bytes (x2) | WRITE_SIZE KB | TCC_EA0_ATOMIC |",
+             "|---|---|---|---|---|---|"]
+    for k, cs in sorted(vals.items(), key=lambda kv: -sum(kv[1].get("FETCH_SIZE", [0]))):
+        avg = {c: sum(v) / len(v) for c, v in cs.items()}
+        n = max(len(v) for v in cs.values())
+        rd = 2 * avg.get("FETCH_SIZE", 0.0) * 1024
+        wr = avg.get("WRITE_SIZE", 0.0) * 1024
+        out[k] = {"dispatches": n, "fetch_kb_raw": avg.get("FETCH_SIZE"), "hbm_read_bytes": rd,
+                  "write_kb": avg.get("WRITE_SIZE"), "hbm_write_bytes": wr,
+                  "atomic_requests": avg.get("TCC_EA0_ATOMIC_sum")}
+        lines.append(f"| {k} | {n} | {avg.get('FETCH_SIZE', 0):.0f} | {rd:.3e} | {avg.get('WRITE_SIZE', 0):.0f} | "
+                     f"{avg.get('TCC_EA0_ATOMIC_sum', 0):.3e} |")
+    sc = out.get("scatter_kernel")
+    if sc:
+        traffic = {"kernel": "cip::scatter_kernel", "round": rnd,
+                   "hbm_bytes_per_launch": int(sc["hbm_read_bytes"] + sc["hbm_write_bytes"]),
+                   "hbm_read_bytes_per_launch": int(sc["hbm_read_bytes"]),
+                   "hbm_write_bytes_per_launch": int(sc["hbm_write_bytes"]),
+                   "correction": "FETCH_SIZE x2 (gfx950 half-count of wide reads); WRITE_SIZE as reported",
+                   "source": f"profiles/{rnd}_pmc_summary.md"}
+        Path("profiles").mkdir(exist_ok=True)
+        Path(f"profiles/traffic_{config}.json").write_text(json.dumps(traffic, indent=1))
+    Path(f"profiles/{rnd}_pmc_summary.md").write_text("\n".join(lines) + "\n")
+    print("\n".join(lines))
+
+
+if __name__ == "__main__":
+    main()
