@@ -335,6 +335,18 @@ static int fft_plan(Workspace* ws, int64_t nu, int64_t nv, hipStream_t s, hipfft
   if (!var) return CIP_ENOMEM;
 
 // ------------------------------------------------------------- planner ----
+// Visibilities per scatter work unit (<= kChunkVis, the fixed-point bound);
+// CIP_CHUNK_VIS overrides it for tuning.
+static int64_t chunk_vis() {
+  static int64_t cv = -1;
+  if (cv < 0) {
+    const char* e = getenv("CIP_CHUNK_VIS");
+    cv = e ? atoll(e) : kChunkVis;
+    if (cv < 256 || cv > kChunkVis) cv = kChunkVis;
+  }
+  return cv;
+}
+
 struct PlanResult {
   int64_t nruns = 0, ntiles = 0, nchunks = 0;
   std::vector<int64_t> plane_chunk_off;  // chunk offset of tile layer iw (ntw + 1)
@@ -378,7 +390,7 @@ static int make_plan(Workspace* ws, const double* uvw, int64_t nrow, const doubl
   CIP_HIP_CHECK(launch_run_lengths(runs, nruns, run_goff, s));
   CIP_HIP_CHECK(exclusive_scan_i64(run_goff, nruns + 1, scan_tmp2, s));
   CIP_HIP_CHECK(launch_tile_vis(run_goff, tile_run_off, ntiles, tile_vis_off, tile_vis, s));
-  CIP_HIP_CHECK(launch_chunk_counts(tile_vis, ntiles, kChunkVis, chunk_off, s));
+  CIP_HIP_CHECK(launch_chunk_counts(tile_vis, ntiles, chunk_vis(), chunk_off, s));
   CIP_HIP_CHECK(exclusive_scan_i64(chunk_off, ntiles + 1, scan_tmp, s));
   // chunk offsets of each w tile layer
   const int64_t layer = g.ntx * g.nty;
@@ -391,7 +403,8 @@ static int make_plan(Workspace* ws, const double* uvw, int64_t nrow, const doubl
   pr->plane_chunk_off.assign(hl, hl + g.ntw + 1);
   pr->nchunks = pr->plane_chunk_off.back();
   CIP_ALLOC(chunks, Chunk, "chunks", pr->nchunks)
-  CIP_HIP_CHECK(launch_chunk_emit(tile_vis_off, tile_vis, chunk_off, ntiles, kChunkVis, chunks, s));
+  CIP_HIP_CHECK(launch_chunk_emit(tile_vis_off, tile_vis, chunk_off, run_goff, tile_runs, ntiles, chunk_vis(), chunks,
+                                  s));
   pr->runs = runs;
   pr->run_goff = run_goff;
   pr->tile_run_off = tile_runs;

@@ -58,6 +58,16 @@ CIP_DEFINE_KERNEL(14)
 CIP_DEFINE_KERNEL(16)
 #undef CIP_DEFINE_KERNEL
 
+// A kernel coefficient materialised in an SGPR pair at its point of use. The
+// empty volatile asm stops the compiler from hoisting all (W/2)(D+1)
+// coefficients out of the scatter loop, which needs more than the 102 SGPRs
+// and spills them to VGPR lanes (v_readlane per use); two s_mov_b32 per use
+// issue on the scalar pipe beside the VALU instead.
+__device__ __forceinline__ double sgpr_const(double c) {
+  asm volatile("" : "+s"(c));
+  return c;
+}
+
 // All W kernel values at y in [-1, 1): out[k] = phi_k(y).
 template <int W>
 __device__ __forceinline__ void eval_kernel(double y, double* out) {
@@ -67,12 +77,12 @@ __device__ __forceinline__ void eval_kernel(double y, double* out) {
   for (int k = 0; k < W / 2; ++k) {
     // even part: sum_m c[2m] z^m ; odd part: sum_m c[2m+1] z^m
     constexpr int D = K::D;
-    double e = K::coef(k, (D & 1) ? D - 1 : D);
+    double e = sgpr_const(K::coef(k, (D & 1) ? D - 1 : D));
 #pragma unroll
-    for (int d = ((D & 1) ? D - 1 : D) - 2; d >= 0; d -= 2) e = fma(e, z, K::coef(k, d));
-    double o = K::coef(k, (D & 1) ? D : D - 1);
+    for (int d = ((D & 1) ? D - 1 : D) - 2; d >= 0; d -= 2) e = fma(e, z, sgpr_const(K::coef(k, d)));
+    double o = sgpr_const(K::coef(k, (D & 1) ? D : D - 1));
 #pragma unroll
-    for (int d = ((D & 1) ? D : D - 1) - 2; d >= 1; d -= 2) o = fma(o, z, K::coef(k, d));
+    for (int d = ((D & 1) ? D : D - 1) - 2; d >= 1; d -= 2) o = fma(o, z, sgpr_const(K::coef(k, d)));
     out[k] = fma(y, o, e);
     out[W - 1 - k] = fma(-y, o, e);
   }
@@ -83,6 +93,7 @@ __device__ __forceinline__ void eval_kernel(double y, double* out) {
 struct Chunk {
   int64_t g0, g1;
   int64_t tile;
+  int64_t first_run;  // first row slice of the tile overlapping [g0, g1)
 };
 
 // Everything the planner and the scatter need to place a visibility.

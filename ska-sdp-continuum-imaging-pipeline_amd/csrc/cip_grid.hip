@@ -113,25 +113,67 @@ hipError_t launch_prep_reduce(const void* vis, int vis_dtype, const void* wgt, i
 constexpr int kScatterThreads = 256;
 constexpr int kRunBatch = 256;
 
-template <int W, typename VisT, int WK, bool WSTACK>
-__device__ __forceinline__ void grid_one(const double* __restrict__ uvw, const double* __restrict__ fx,
-                                         const VisT* __restrict__ vis, const void* __restrict__ wgt, int64_t nchan,
-                                         int64_t irow, int64_t c, const GridGeometry& g, int64_t plane,
-                                         int64_t X0, int64_t Y0, double fixed_scale, unsigned long long* sub) {
+// Everything one visibility needs, loaded one iteration ahead of its use so
+// the global-memory latency overlaps the previous visibility's taps.
+struct VisFetch {
+  double u, v, w, fx, vr, vi, wt;
+};
+
+// last staged run starting at or before flattened visibility q
+__device__ __forceinline__ void locate_vis(int64_t q, const int64_t* s_voff, const uint64_t* s_run, int nst,
+                                           int64_t* irow, int64_t* c) {
+  int lo = 0, hi = nst - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (s_voff[mid] <= q) lo = mid;
+    else hi = mid - 1;
+  }
+  const uint64_t rec = s_run[lo];
+  *irow = (int64_t)(rec >> 32);
+  *c = (int64_t)((rec >> 16) & 0xffff) + (q - s_voff[lo]);
+}
+
+template <typename VisT, int WK>
+__device__ __forceinline__ void fetch_at(int64_t irow, int64_t c, const double* __restrict__ uvw,
+                                         const double* __restrict__ fx, const VisT* __restrict__ vis,
+                                         const void* __restrict__ wgt, int64_t nchan, VisFetch& f) {
+  const int64_t idx = irow * nchan + c;
+  f.u = uvw[3 * irow];
+  f.v = uvw[3 * irow + 1];
+  f.w = uvw[3 * irow + 2];
+  f.fx = fx[c];
+  load_vis(vis, idx, f.vr, f.vi);
+  f.wt = load_weight<WK>(wgt, idx);
+}
+
+template <typename VisT, int WK>
+__device__ __forceinline__ void fetch_vis(int64_t q, const int64_t* s_voff, const uint64_t* s_run, int nst,
+                                          const double* __restrict__ uvw, const double* __restrict__ fx,
+                                          const VisT* __restrict__ vis, const void* __restrict__ wgt,
+                                          int64_t nchan, VisFetch& f) {
+  int64_t irow, c;
+  locate_vis(q, s_voff, s_run, nst, &irow, &c);
+  const int64_t idx = irow * nchan + c;
+  f.u = uvw[3 * irow];
+  f.v = uvw[3 * irow + 1];
+  f.w = uvw[3 * irow + 2];
+  f.fx = fx[c];
+  load_vis(vis, idx, f.vr, f.vi);
+  f.wt = load_weight<WK>(wgt, idx);
+}
+
+template <int W, bool WSTACK>
+__device__ __forceinline__ void grid_fetched(const VisFetch& f, const GridGeometry& g, int64_t plane, int64_t X0,
+                                             int64_t Y0, double fixed_scale, unsigned long long* sub) {
   constexpr int T = kTile;
   constexpr int P = T + W - 1;
-  const int64_t idx = irow * nchan + c;
-  const double wv = load_weight<WK>(wgt, idx);
-  if (wv == 0.0) return;
-  double vr, vi;
-  load_vis(vis, idx, vr, vi);
+  if (f.wt == 0.0) return;
   int64_t ix0, iy0, iw0;
   double yu, yv, yw;
-  if (!place_vis(uvw[3 * irow], uvw[3 * irow + 1], uvw[3 * irow + 2], fx[c], g, &ix0, &yu, &iy0, &yv, &iw0, &yw))
-    return;
+  if (!place_vis(f.u, f.v, f.w, f.fx, g, &ix0, &yu, &iy0, &yv, &iw0, &yw)) return;
   const int64_t lx = ix0 - X0, ly = iy0 - Y0;
   if (lx < 0 || lx >= T || ly < 0 || ly >= T) return;  // never for a consistent plan
-  double sc = wv * fixed_scale;
+  double sc = f.wt * fixed_scale;
   if constexpr (WSTACK) {
     const int64_t kw = plane - iw0;
     if (kw < 0 || kw >= W) return;
@@ -142,8 +184,7 @@ __device__ __forceinline__ void grid_one(const double* __restrict__ uvw, const d
     for (int k = 0; k < W; ++k) sel = (k == kw) ? kwv[k] : sel;
     sc *= sel;
   }
-  vr *= sc;
-  vi *= sc;
+  const double vr = f.vr * sc, vi = f.vi * sc;
   double ku[W], kv[W];
   eval_kernel<W>(yu, ku);
   eval_kernel<W>(yv, kv);
@@ -163,30 +204,99 @@ __device__ __forceinline__ void grid_one(const double* __restrict__ uvw, const d
     for (int j = 0; j < W; ++j) {
       const double qr = fma(ku[i], kr[j], kMagic);
       const double qi = fma(ku[i], ki[j], kMagic);
-      const unsigned long long br = (unsigned long long)__double_as_longlong(qr) - 0x4338000000000000ull;
-      const unsigned long long bi = (unsigned long long)__double_as_longlong(qi) - 0x4338000000000000ull;
-      atomicAdd(base + (i * P + j), br);
-      atomicAdd(base + P * P + (i * P + j), bi);
+      atomicAdd(base + (i * P + j), (unsigned long long)__double_as_longlong(qr) - 0x4338000000000000ull);
+      atomicAdd(base + P * P + (i * P + j), (unsigned long long)__double_as_longlong(qi) - 0x4338000000000000ull);
     }
   }
 }
 
-// last staged run starting at or before flattened visibility q
-__device__ __forceinline__ void locate_vis(int64_t q, const int64_t* s_voff, const uint64_t* s_run, int nst,
-                                           int64_t* irow, int64_t* c) {
-  int lo = 0, hi = nst - 1;
-  while (lo < hi) {
-    const int mid = (lo + hi + 1) >> 1;
-    if (s_voff[mid] <= q) lo = mid;
-    else hi = mid - 1;
-  }
-  const uint64_t rec = s_run[lo];
-  *irow = (int64_t)(rec >> 32);
-  *c = (int64_t)((rec >> 16) & 0xffff) + (q - s_voff[lo]);
-}
-
-constexpr int kSortPer = 4;
+// Bank-class ordering (ORDER): a lane-scattered 8-byte LDS atomic hits bank
+// pair (cell mod 32), so 32 lanes with random footprints collide (measured
+// 27 CU-cycles per visibility, tools/microbench/lds_scatter.hip) while 32
+// lanes with distinct classes run at 14. Each sub-batch of kSortBatch
+// visibilities is counting-sorted by class into level-major order (position =
+// visibilities of lower rank in every class + lower classes of equal rank), so
+// every run of up to 32 consecutive positions within a level has distinct
+// classes. Level tables: S[r] = sum_c min(cnt[c], r), M[r] = {c : cnt[c] > r}.
+constexpr int kSortPer = 2;
 constexpr int kSortBatch = kScatterThreads * kSortPer;
+
+template <int W, typename VisT, int WK, bool WSTACK>
+__device__ __forceinline__ void scatter_sorted_batch(
+    int64_t sb, int nsb, const int64_t* s_voff, const uint64_t* s_run, int nst, unsigned* s_cnt, unsigned* s_S,
+    unsigned* s_M, uint64_t* s_order, const double* __restrict__ uvw, const double* __restrict__ fx,
+    const VisT* __restrict__ vis, const void* __restrict__ wgt, int64_t nchan, const GridGeometry& g, int64_t plane,
+    int64_t X0, int64_t Y0, double fixed_scale, unsigned long long* sub) {
+  constexpr int P = kTile + W - 1;
+  if (threadIdx.x < 32) s_cnt[threadIdx.x] = 0u;
+  __syncthreads();
+  uint64_t packed[kSortPer];
+  unsigned cls[kSortPer], rk[kSortPer];
+#pragma unroll
+  for (int k = 0; k < kSortPer; ++k) {
+    const int qi = threadIdx.x + k * kScatterThreads;
+    cls[k] = 32u;
+    if (qi < nsb) {
+      int64_t irow, c;
+      locate_vis(sb + qi, s_voff, s_run, nst, &irow, &c);
+      packed[k] = ((uint64_t)irow << 16) | (uint64_t)c;
+      int64_t ix0, iy0, iw0;
+      double yu, yv, yw;
+      place_vis(uvw[3 * irow], uvw[3 * irow + 1], uvw[3 * irow + 2], fx[c], g, &ix0, &yu, &iy0, &yv, &iw0, &yw);
+      cls[k] = (unsigned)(((ix0 - X0) * P + (iy0 - Y0)) & 31);
+      rk[k] = atomicAdd(&s_cnt[cls[k]], 1u);
+    }
+  }
+  __syncthreads();
+  unsigned cnt[32], maxcnt = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const uint4 c4 = reinterpret_cast<const uint4*>(s_cnt)[i];
+    cnt[4 * i] = c4.x;
+    cnt[4 * i + 1] = c4.y;
+    cnt[4 * i + 2] = c4.z;
+    cnt[4 * i + 3] = c4.w;
+  }
+#pragma unroll
+  for (int i = 0; i < 32; ++i) maxcnt = cnt[i] > maxcnt ? cnt[i] : maxcnt;
+  for (unsigned r = threadIdx.x; r < maxcnt; r += kScatterThreads) {
+    unsigned S = 0, M = 0;
+#pragma unroll
+    for (int c2 = 0; c2 < 32; ++c2) {
+      S += cnt[c2] < r ? cnt[c2] : r;
+      M |= (cnt[c2] > r ? 1u : 0u) << c2;
+    }
+    s_S[r] = S;
+    s_M[r] = M;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < kSortPer; ++k)
+    if (cls[k] < 32u) s_order[s_S[rk[k]] + __popc(s_M[rk[k]] & ((1u << cls[k]) - 1u))] = packed[k];
+  __syncthreads();
+  // grid in sorted order, fetching one visibility ahead
+  int pi = threadIdx.x;
+  bool have = pi < nsb;
+  VisFetch cur;
+  if (have) {
+    const uint64_t pk = s_order[pi];
+    fetch_at<VisT, WK>((int64_t)(pk >> 16), (int64_t)(pk & 0xffff), uvw, fx, vis, wgt, nchan, cur);
+  }
+  while (have) {
+    const int pn = pi + kScatterThreads;
+    const bool hn = pn < nsb;
+    VisFetch nxt;
+    if (hn) {
+      const uint64_t pk = s_order[pn];
+      fetch_at<VisT, WK>((int64_t)(pk >> 16), (int64_t)(pk & 0xffff), uvw, fx, vis, wgt, nchan, nxt);
+    }
+    grid_fetched<W, WSTACK>(cur, g, plane, X0, Y0, fixed_scale, sub);
+    cur = nxt;
+    pi = pn;
+    have = hn;
+  }
+  __syncthreads();
+}
 
 template <int W, typename VisT, int WK, bool WSTACK, bool ORDER>
 __global__ __launch_bounds__(kScatterThreads) void scatter_kernel(
@@ -200,8 +310,8 @@ __global__ __launch_bounds__(kScatterThreads) void scatter_kernel(
   __shared__ unsigned long long sub[P * P * 2];
   __shared__ int64_t s_voff[kRunBatch + 1];
   __shared__ uint64_t s_run[kRunBatch];
-  __shared__ int64_t s_first;
   __shared__ __attribute__((aligned(16))) unsigned s_cnt[32];
+  __shared__ unsigned s_S[ORDER ? kSortBatch : 1], s_M[ORDER ? kSortBatch : 1];
   __shared__ uint64_t s_order[ORDER ? kSortBatch : 1];
 
   const Chunk ch = chunks[chunk_begin + blockIdx.x];
@@ -209,18 +319,8 @@ __global__ __launch_bounds__(kScatterThreads) void scatter_kernel(
   const int64_t X0 = (t % g.ntx) * T;
   const int64_t Y0 = ((t / g.ntx) % g.nty) * T;
   for (int i = threadIdx.x; i < P * P * 2; i += kScatterThreads) sub[i] = 0ull;
-  const int64_t ra = tile_run_off[t], rb = tile_run_off[t + 1];
-  if (threadIdx.x == 0) {
-    int64_t lo = ra, hi = rb - 1;  // first run whose end is beyond g0
-    while (lo < hi) {
-      const int64_t mid = (lo + hi) >> 1;
-      if (run_goff[mid + 1] > ch.g0) hi = mid;
-      else lo = mid + 1;
-    }
-    s_first = lo;
-  }
-  __syncthreads();
-  int64_t r = s_first;
+  const int64_t rb = tile_run_off[t + 1];
+  int64_t r = ch.first_run;
   int64_t v = ch.g0;
   while (v < ch.g1 && r < rb) {
     const int nst = (int)((rb - r) < kRunBatch ? (rb - r) : kRunBatch);
@@ -231,69 +331,27 @@ __global__ __launch_bounds__(kScatterThreads) void scatter_kernel(
     }
     __syncthreads();
     const int64_t bend = ch.g1 < s_voff[nst] ? ch.g1 : s_voff[nst];
-    if constexpr (!ORDER) {
-      for (int64_t q = v + threadIdx.x; q < bend; q += kScatterThreads) {
-        int64_t irow, c;
-        locate_vis(q, s_voff, s_run, nst, &irow, &c);
-        grid_one<W, VisT, WK, WSTACK>(uvw, fx, vis, wgt, nchan, irow, c, g, plane, X0, Y0, fixed_scale, sub);
-      }
-    } else {
-      // Bank-class interleave: a lane-scattered 8-byte LDS atomic hits bank
-      // pair (cell mod 32). Order each sub-batch level-major by that class
-      // (position = rank-within-class major, class minor, compacted), so the
-      // lanes of a wave-instruction add into distinct bank pairs.
+    if constexpr (ORDER) {
       for (int64_t sb = v; sb < bend; sb += kSortBatch) {
         const int nsb = (int)((bend - sb) < kSortBatch ? (bend - sb) : kSortBatch);
-        if (threadIdx.x < 32) s_cnt[threadIdx.x] = 0u;
-        __syncthreads();
-        uint64_t packed[kSortPer];
-        int cls[kSortPer];
-        unsigned rk[kSortPer];
-#pragma unroll
-        for (int k = 0; k < kSortPer; ++k) {
-          const int qi = threadIdx.x + k * kScatterThreads;
-          cls[k] = -1;
-          if (qi < nsb) {
-            int64_t irow, c;
-            locate_vis(sb + qi, s_voff, s_run, nst, &irow, &c);
-            packed[k] = ((uint64_t)irow << 16) | (uint64_t)c;
-            int64_t ix0, iy0, iw0;
-            double yu, yv, yw;
-            place_vis(uvw[3 * irow], uvw[3 * irow + 1], uvw[3 * irow + 2], fx[c], g, &ix0, &yu, &iy0, &yv, &iw0,
-                      &yw);
-            cls[k] = (int)(((ix0 - X0) * P + (iy0 - Y0)) & 31);
-            rk[k] = atomicAdd(&s_cnt[cls[k]], 1u);
-          }
-        }
-        __syncthreads();
-        unsigned cnt[32];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const uint4 c4 = reinterpret_cast<const uint4*>(s_cnt)[i];
-          cnt[4 * i] = c4.x;
-          cnt[4 * i + 1] = c4.y;
-          cnt[4 * i + 2] = c4.z;
-          cnt[4 * i + 3] = c4.w;
-        }
-#pragma unroll
-        for (int k = 0; k < kSortPer; ++k) {
-          if (cls[k] >= 0) {
-            unsigned pos = 0;
-#pragma unroll
-            for (int c2 = 0; c2 < 32; ++c2) {
-              pos += cnt[c2] < rk[k] ? cnt[c2] : rk[k];
-              pos += (c2 < cls[k] && cnt[c2] > rk[k]) ? 1u : 0u;
-            }
-            s_order[pos] = packed[k];
-          }
-        }
-        __syncthreads();
-        for (int pi = threadIdx.x; pi < nsb; pi += kScatterThreads) {
-          const uint64_t pk = s_order[pi];
-          grid_one<W, VisT, WK, WSTACK>(uvw, fx, vis, wgt, nchan, (int64_t)(pk >> 16), (int64_t)(pk & 0xffff), g,
-                                        plane, X0, Y0, fixed_scale, sub);
-        }
-        __syncthreads();
+        scatter_sorted_batch<W, VisT, WK, WSTACK>(sb, nsb, s_voff, s_run, nst, s_cnt, s_S, s_M, s_order, uvw, fx,
+                                                  vis, wgt, nchan, g, plane, X0, Y0, fixed_scale, sub);
+      }
+    } else {
+      // software pipeline: fetch visibility q + 256 while gridding q
+      int64_t q = v + threadIdx.x;
+      bool have = q < bend;
+      VisFetch cur;
+      if (have) fetch_vis<VisT, WK>(q, s_voff, s_run, nst, uvw, fx, vis, wgt, nchan, cur);
+      while (have) {
+        const int64_t qn = q + kScatterThreads;
+        const bool hn = qn < bend;
+        VisFetch nxt;
+        if (hn) fetch_vis<VisT, WK>(qn, s_voff, s_run, nst, uvw, fx, vis, wgt, nchan, nxt);
+        grid_fetched<W, WSTACK>(cur, g, plane, X0, Y0, fixed_scale, sub);
+        cur = nxt;
+        q = qn;
+        have = hn;
       }
     }
     v = bend;
@@ -316,15 +374,6 @@ __global__ __launch_bounds__(kScatterThreads) void scatter_kernel(
   }
 }
 
-static int scatter_order_mode() {
-  static int mode = -1;
-  if (mode < 0) {
-    const char* e = getenv("CIP_SCATTER_ORDER");
-    mode = (e && e[0] == '0') ? 0 : 1;
-  }
-  return mode;
-}
-
 template <int W, typename VisT, int WK>
 static hipError_t scatter_dispatch_ws(bool ws, dim3 grid_dim, hipStream_t s, const double* uvw, const double* fx,
                                       const void* vis, const void* wgt, int64_t nchan, const uint64_t* runs,
@@ -335,12 +384,15 @@ static hipError_t scatter_dispatch_ws(bool ws, dim3 grid_dim, hipStream_t s, con
   scatter_kernel<W, VisT, WK, WSV, ORD><<<grid_dim, dim3(kScatterThreads), 0, s>>>(                          \
       uvw, fx, (const VisT*)vis, wgt, nchan, runs, run_goff, tile_run_off, chunks, chunk_begin, g, plane, fs, \
       1.0 / fs, grid)
-  const bool ord = scatter_order_mode() != 0;
+  static const bool order = [] {  // CIP_SCATTER_ORDER=0 selects the unsorted variant (A/B)
+    const char* e = getenv("CIP_SCATTER_ORDER");
+    return !(e && e[0] == '0');
+  }();
   if (ws) {
-    if (ord) LAUNCH(true, true);
+    if (order) LAUNCH(true, true);
     else LAUNCH(true, false);
   } else {
-    if (ord) LAUNCH(false, true);
+    if (order) LAUNCH(false, true);
     else LAUNCH(false, false);
   }
 #undef LAUNCH

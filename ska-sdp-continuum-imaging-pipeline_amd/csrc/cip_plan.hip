@@ -230,26 +230,37 @@ hipError_t launch_chunk_counts(const int64_t* tile_vis, int64_t ntiles, int64_t 
 }
 
 __global__ void chunk_emit_kernel(const int64_t* tile_vis_off, const int64_t* tile_vis, const int64_t* chunk_off,
-                                  int64_t ntiles, int64_t cv, Chunk* chunks) {
+                                  const int64_t* run_goff, const int64_t* tile_run_off, int64_t ntiles, int64_t cv,
+                                  Chunk* chunks) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= ntiles) return;
   const int64_t nv = tile_vis[t];
   const int64_t b = chunk_off[t];
   const int64_t g = tile_vis_off[t];
+  int64_t lo = tile_run_off[t];
+  const int64_t rend = tile_run_off[t + 1];
   for (int64_t k = 0; k * cv < nv; ++k) {
     Chunk ch;
     ch.g0 = g + k * cv;
     ch.g1 = g + ((k + 1) * cv < nv ? (k + 1) * cv : nv);
     ch.tile = t;
+    // first run whose end lies beyond g0 (runs of a tile are consecutive)
+    int64_t hi = rend - 1;
+    while (lo < hi) {
+      const int64_t mid = (lo + hi) >> 1;
+      if (run_goff[mid + 1] > ch.g0) hi = mid;
+      else lo = mid + 1;
+    }
+    ch.first_run = lo;
     chunks[b + k] = ch;
   }
 }
 
 hipError_t launch_chunk_emit(const int64_t* tile_vis_off, const int64_t* tile_vis, const int64_t* chunk_off,
-                             int64_t ntiles, int64_t chunk_vis, Chunk* chunks, hipStream_t s) {
-  chunk_emit_kernel<<<dim3((unsigned)((ntiles + 255) / 256)), dim3(256), 0, s>>>(tile_vis_off, tile_vis,
-                                                                                 chunk_off, ntiles, chunk_vis,
-                                                                                 chunks);
+                             const int64_t* run_goff, const int64_t* tile_run_off, int64_t ntiles,
+                             int64_t chunk_vis, Chunk* chunks, hipStream_t s) {
+  chunk_emit_kernel<<<dim3((unsigned)((ntiles + 255) / 256)), dim3(256), 0, s>>>(
+      tile_vis_off, tile_vis, chunk_off, run_goff, tile_run_off, ntiles, chunk_vis, chunks);
   return hipGetLastError();
 }
 
