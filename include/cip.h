@@ -45,6 +45,15 @@ extern "C" {
 #define CIP_F64 4
 #define CIP_NONE 0 /* wgt == NULL: all weights 1 */
 
+/* flags of cip_ms2dirty / cip_grid_plane */
+#define CIP_WSTACKING 1  /* w-stacking planes (cip_ms2dirty only; else 2-D) */
+#define CIP_ACC_SINGLE 2 /* complex64 only: single-precision accumulation
+                          * class, the reference's ducc0 float gridding (re/im
+                          * packed in one 64-bit fixed-point LDS cell, W^2
+                          * instead of 2 W^2 atomics per visibility). Without
+                          * it every input accumulates in 64-bit fixed point
+                          * (2^-46 of max|w V|, fp64 class). */
+
 typedef struct cip_gridder_params {
   int64_t nu, nv;      /* oversampled grid size (cells), even, 2/3/5/7-smooth */
   int32_t support;     /* kernel support W (even, 4..16) */
@@ -77,7 +86,7 @@ int cip_ms2dirty(const double* uvw, int64_t nrow, const double* freq,
                  int64_t nchan, const void* vis, int vis_dtype,
                  const void* wgt, int wgt_dtype, int64_t npix_x,
                  int64_t npix_y, double pixsize_x, double pixsize_y,
-                 double epsilon, int support, int do_wstacking,
+                 double epsilon, int support, int flags,
                  void* hip_stream, double* dirty_out, double* sum_wgt_out,
                  cip_gridder_params* params_out);
 
@@ -89,8 +98,8 @@ int cip_grid_plane(const double* uvw, int64_t nrow, const double* freq,
                    int64_t nchan, const void* vis, int vis_dtype,
                    const void* wgt, int wgt_dtype,
                    const cip_gridder_params* params, double pixsize_x,
-                   double pixsize_y, int64_t plane, void* hip_stream,
-                   double* grid_out);
+                   double pixsize_y, int64_t plane, int flags,
+                   void* hip_stream, double* grid_out);
 
 /* Reference-exact UVW tile keys and constant-key channel runs (one run per
  * maximal range of channels with equal (iu, iv, iw) in a row), rows in

@@ -335,16 +335,17 @@ static int fft_plan(Workspace* ws, int64_t nu, int64_t nv, hipStream_t s, hipfft
   if (!var) return CIP_ENOMEM;
 
 // ------------------------------------------------------------- planner ----
-// Visibilities per scatter work unit (<= kChunkVis, the fixed-point bound);
-// CIP_CHUNK_VIS overrides it for tuning.
-static int64_t chunk_vis() {
-  static int64_t cv = -1;
-  if (cv < 0) {
+// Visibilities per scatter work unit: <= kChunkVis (64-bit fixed point) or
+// kChunkVisPacked (packed class, complex64 input); CIP_CHUNK_VIS lowers it for
+// tuning.
+static int64_t chunk_vis(bool packed) {
+  static int64_t env = -2;
+  if (env == -2) {
     const char* e = getenv("CIP_CHUNK_VIS");
-    cv = e ? atoll(e) : kChunkVis;
-    if (cv < 256 || cv > kChunkVis) cv = kChunkVis;
+    env = e ? atoll(e) : -1;
   }
-  return cv;
+  const int64_t cap = packed ? kChunkVisPacked : kChunkVis;
+  return (env >= 256 && env < cap) ? env : cap;
 }
 
 struct PlanResult {
@@ -354,10 +355,20 @@ struct PlanResult {
   int64_t* run_goff = nullptr;
   int64_t* tile_run_off = nullptr;
   Chunk* chunks = nullptr;
+  uint64_t* perm = nullptr;  // bank-class ordered visibility stream, or NULL
 };
 
+// CIP_SCATTER_ORDER=0 skips the bank-class order (A/B experiments)
+static bool scatter_order() {
+  static const bool on = [] {
+    const char* e = getenv("CIP_SCATTER_ORDER");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 static int make_plan(Workspace* ws, const double* uvw, int64_t nrow, const double* fx, int64_t nchan,
-                     const GridGeometry& g, hipStream_t s, PlanResult* pr) {
+                     const GridGeometry& g, int64_t cv, hipStream_t s, PlanResult* pr) {
   const int64_t ntiles = g.ntx * g.nty * g.ntw;
   pr->ntiles = ntiles;
   CIP_ALLOC(tile_runs, int64_t, "tile_runs", ntiles + 1)
@@ -370,7 +381,13 @@ static int make_plan(Workspace* ws, const double* uvw, int64_t nrow, const doubl
   CIP_HIP_CHECK(hipMemsetAsync(tile_runs, 0, sizeof(int64_t) * (ntiles + 1), s));
   CIP_HIP_CHECK(hipMemsetAsync(tile_cursor, 0, sizeof(int64_t) * (ntiles + 1), s));
   CIP_HIP_CHECK(hipMemsetAsync(err, 0, sizeof(unsigned), s));
-  CIP_HIP_CHECK(launch_plan_count(uvw, nrow, fx, nchan, g, tile_runs, nullptr, err, s));
+  const int64_t nvis = nrow * nchan, nseg = (nvis + 63) / 64;
+  CIP_ALLOC(vis_class, uint8_t, "vis_class", nvis)
+  CIP_ALLOC(seg_nruns, uint8_t, "seg_nruns", nseg)
+  CIP_ALLOC(park_key, int64_t, "park_key", nseg * 64)
+  CIP_ALLOC(park_run, uint64_t, "park_run", nseg * 64)
+  CIP_HIP_CHECK(launch_plan_place(uvw, nrow, fx, nchan, g, tile_runs, err, vis_class, seg_nruns, park_key, park_run,
+                                  s));
   // tile_runs -> exclusive offsets (entry ntiles = total runs)
   CIP_HIP_CHECK(exclusive_scan_i64(tile_runs, ntiles + 1, scan_tmp, s));
   int64_t* h = (int64_t*)pinned(ws, 4 * sizeof(int64_t));
@@ -386,11 +403,11 @@ static int make_plan(Workspace* ws, const double* uvw, int64_t nrow, const doubl
   CIP_ALLOC(runs, uint64_t, "runs", nruns)
   CIP_ALLOC(run_goff, int64_t, "run_goff", nruns + 1)
   CIP_ALLOC(scan_tmp2, int64_t, "scan_tmp2", scan_tmp_elems(nruns + 1))
-  CIP_HIP_CHECK(launch_plan_emit(uvw, nrow, fx, nchan, g, tile_run_off, tile_cursor, runs, s));
+  CIP_HIP_CHECK(launch_plan_distribute(nvis, seg_nruns, park_key, park_run, tile_run_off, tile_cursor, runs, s));
   CIP_HIP_CHECK(launch_run_lengths(runs, nruns, run_goff, s));
   CIP_HIP_CHECK(exclusive_scan_i64(run_goff, nruns + 1, scan_tmp2, s));
   CIP_HIP_CHECK(launch_tile_vis(run_goff, tile_run_off, ntiles, tile_vis_off, tile_vis, s));
-  CIP_HIP_CHECK(launch_chunk_counts(tile_vis, ntiles, chunk_vis(), chunk_off, s));
+  CIP_HIP_CHECK(launch_chunk_counts(tile_vis, ntiles, cv, chunk_off, s));
   CIP_HIP_CHECK(exclusive_scan_i64(chunk_off, ntiles + 1, scan_tmp, s));
   // chunk offsets of each w tile layer
   const int64_t layer = g.ntx * g.nty;
@@ -403,12 +420,17 @@ static int make_plan(Workspace* ws, const double* uvw, int64_t nrow, const doubl
   pr->plane_chunk_off.assign(hl, hl + g.ntw + 1);
   pr->nchunks = pr->plane_chunk_off.back();
   CIP_ALLOC(chunks, Chunk, "chunks", pr->nchunks)
-  CIP_HIP_CHECK(launch_chunk_emit(tile_vis_off, tile_vis, chunk_off, run_goff, tile_runs, ntiles, chunk_vis(), chunks,
+  CIP_HIP_CHECK(launch_chunk_emit(tile_vis_off, tile_vis, chunk_off, run_goff, tile_runs, ntiles, cv, chunks,
                                   s));
   pr->runs = runs;
   pr->run_goff = run_goff;
   pr->tile_run_off = tile_runs;
   pr->chunks = chunks;
+  if (scatter_order() && pr->nchunks > 0) {
+    CIP_ALLOC(perm, uint64_t, "perm", nrow * nchan)
+    CIP_HIP_CHECK(launch_order(vis_class, nchan, runs, run_goff, tile_runs, chunks, pr->nchunks, perm, s));
+    pr->perm = perm;
+  }
   return CIP_OK;
 }
 
@@ -419,6 +441,7 @@ struct Prepared {
   cip_gridder_params p;
   GridGeometry g;
   double fixed_scale;
+  bool packed;  // single-precision class (CIP_ACC_SINGLE)
   double* fx;
   double* red;  // device [sum_w, max|wV|]
   PlanResult plan;
@@ -426,7 +449,7 @@ struct Prepared {
 
 static int prepare(Workspace* ws, const double* uvw, int64_t nrow, const double* freq, int64_t nchan,
                    const void* vis, int vis_dtype, const void* wgt, int wgt_dtype, int64_t npix_x, int64_t npix_y,
-                   double px, double py, double epsilon, int support, int do_wstacking,
+                   double px, double py, double epsilon, int support, int do_wstacking, bool packed,
                    const cip_gridder_params* given, hipStream_t s, Prepared* out) {
   if (!vis_dtype_ok(vis_dtype)) return set_error(CIP_EINVAL, "vis dtype must be complex64 or complex128");
   if (!wgt_dtype_ok(wgt_dtype)) return set_error(CIP_EINVAL, "wgt dtype must be float32, float64 or none");
@@ -476,12 +499,16 @@ static int prepare(Workspace* ws, const double* uvw, int64_t nrow, const double*
     if (rc != CIP_OK) return rc;
   }
   out->g = geometry(out->p, px, py);
-  // fixed point: max contribution <= 2^kFixedBits
+  // fixed point: max contribution <= 2^kFixedBits, or 2^kPackedBits for a
+  // full packed chunk (the scatter raises it for shorter chunks)
+  if (packed && vis_dtype != CIP_C64)
+    return set_error(CIP_EINVAL, "single-precision accumulation needs complex64 visibilities");
+  out->packed = packed;
   int e2 = 0;
   if (maxabs > 0.0) {
     std::frexp(maxabs, &e2);  // maxabs < 2^e2
   }
-  out->fixed_scale = std::ldexp(1.0, kFixedBits - e2);
+  out->fixed_scale = std::ldexp(1.0, (packed ? kPackedBits : kFixedBits) - e2);
   out->fx = fx;
   out->red = red;
   if (nrow == 0) {
@@ -489,7 +516,7 @@ static int prepare(Workspace* ws, const double* uvw, int64_t nrow, const double*
     out->plan.plane_chunk_off.assign(out->g.ntw + 1, 0);
     return CIP_OK;
   }
-  const int rc = make_plan(ws, uvw, nrow, fx, nchan, out->g, s, &out->plan);
+  const int rc = make_plan(ws, uvw, nrow, fx, nchan, out->g, chunk_vis(packed), s, &out->plan);
   g_prof.span(1, e_prep, g_prof.mark(s));
   g_prof.counts[0] = nrow * nchan;
   g_prof.counts[1] = out->plan.nruns;
@@ -513,8 +540,9 @@ static int scatter_plane(const Prepared& pp, int64_t plane, const double* uvw, c
   const int64_t cb = pp.plan.plane_chunk_off[lo], ce = pp.plan.plane_chunk_off[hi + 1];
   if (wgt == nullptr) wgt_dtype = CIP_NONE;
   hipEvent_t a = g_prof.mark(s);
-  CIP_HIP_CHECK(launch_scatter(g.support, vis_dtype, wgt_dtype, uvw, pp.fx, vis, wgt, nchan, pp.plan.runs,
-                               pp.plan.run_goff, pp.plan.tile_run_off, pp.plan.chunks, cb, ce - cb, g, plane,
+  CIP_HIP_CHECK(launch_scatter(g.support, vis_dtype, wgt_dtype, pp.packed, uvw, pp.fx, vis, wgt, nchan, pp.plan.runs,
+                               pp.plan.run_goff, pp.plan.tile_run_off, pp.plan.perm, pp.plan.chunks, cb, ce - cb,
+                               g, plane,
                                pp.fixed_scale, grid, s));
   g_prof.span(2, a, g_prof.mark(s));
   if (ce > cb) g_prof.counts[4] += 1;
@@ -539,9 +567,12 @@ int cip_choose_params(int64_t npix_x, int64_t npix_y, double pixsize_x, double p
 
 int cip_ms2dirty(const double* uvw, int64_t nrow, const double* freq, int64_t nchan, const void* vis, int vis_dtype,
                  const void* wgt, int wgt_dtype, int64_t npix_x, int64_t npix_y, double pixsize_x,
-                 double pixsize_y, double epsilon, int support, int do_wstacking, void* hip_stream,
+                 double pixsize_y, double epsilon, int support, int flags, void* hip_stream,
                  double* dirty_out, double* sum_wgt_out, cip_gridder_params* params_out) {
   g_last_error.clear();
+  if (flags & ~(CIP_WSTACKING | CIP_ACC_SINGLE)) return set_error(CIP_EINVAL, "unknown flags");
+  const int do_wstacking = (flags & CIP_WSTACKING) ? 1 : 0;
+  const bool packed = (flags & CIP_ACC_SINGLE) != 0;
   if (!dirty_out) return set_error(CIP_EINVAL, "dirty_out is NULL");
   if (nrow > 0 && (!uvw || !freq || !vis)) return set_error(CIP_EINVAL, "NULL input pointer");
   hipStream_t s = (hipStream_t)hip_stream;
@@ -551,7 +582,7 @@ int cip_ms2dirty(const double* uvw, int64_t nrow, const double* freq, int64_t nc
   hipEvent_t t_start = g_prof.mark(s);
   Prepared pp;
   int rc = prepare(ws, uvw, nrow, freq, nchan, vis, vis_dtype, wgt, wgt_dtype, npix_x, npix_y, pixsize_x, pixsize_y,
-                   epsilon, support, do_wstacking, nullptr, s, &pp);
+                   epsilon, support, do_wstacking, packed, nullptr, s, &pp);
   if (rc != CIP_OK) return rc;
   if (params_out) *params_out = pp.p;
   const GridGeometry& g = pp.g;
@@ -620,8 +651,10 @@ int cip_ms2dirty(const double* uvw, int64_t nrow, const double* freq, int64_t nc
 
 int cip_grid_plane(const double* uvw, int64_t nrow, const double* freq, int64_t nchan, const void* vis,
                    int vis_dtype, const void* wgt, int wgt_dtype, const cip_gridder_params* params,
-                   double pixsize_x, double pixsize_y, int64_t plane, void* hip_stream, double* grid_out) {
+                   double pixsize_x, double pixsize_y, int64_t plane, int flags, void* hip_stream,
+                   double* grid_out) {
   g_last_error.clear();
+  if (flags & ~CIP_ACC_SINGLE) return set_error(CIP_EINVAL, "unknown flags");
   if (!params || !grid_out) return set_error(CIP_EINVAL, "NULL params or grid_out");
   if (plane < 0 || plane >= params->nplanes) return set_error(CIP_EINVAL, "plane out of range");
   hipStream_t s = (hipStream_t)hip_stream;
@@ -631,7 +664,7 @@ int cip_grid_plane(const double* uvw, int64_t nrow, const double* freq, int64_t 
   hipEvent_t t_start = g_prof.mark(s);
   Prepared pp;
   int rc = prepare(ws, uvw, nrow, freq, nchan, vis, vis_dtype, wgt, wgt_dtype, 2, 2, pixsize_x, pixsize_y, 0.0,
-                   params->support, params->do_wstacking, params, s, &pp);
+                   params->support, params->do_wstacking, (flags & CIP_ACC_SINGLE) != 0, params, s, &pp);
   if (rc != CIP_OK) return rc;
   rc = scatter_plane(pp, plane, uvw, vis, vis_dtype, wgt, wgt_dtype, nchan, grid_out, s);
   if (rc != CIP_OK) return rc;

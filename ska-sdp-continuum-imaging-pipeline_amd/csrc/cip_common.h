@@ -27,6 +27,17 @@ constexpr uint32_t kMagicHi = 0x43380000u;      // high word of kMagic
 constexpr int kFixedBits = 46;
 constexpr int64_t kChunkVis = 32768;
 
+// Packed single-precision class (complex64 input, ducc0's float gridding):
+// (re, im) of a cell share ONE 64-bit integer, re * 2^32 + im, so a
+// visibility costs W^2 LDS atomics instead of 2 W^2. Both halves must stay
+// within +-2^31 per chunk: a chunk of n <= kChunkVisPacked visibilities is
+// scaled so its largest contribution maps to 2^(kPackedBits + lg(kChunkVisPacked)
+// - ceil(lg n)) (<= 2^30 / n). Quantisation is <= 2^-19 of max|wV| per
+// contribution, finer than the float32 grid of the reference's gridder.
+constexpr int kPackedBits = 18;
+constexpr int64_t kChunkVisPacked = 4096;
+constexpr int kChunkVisPackedLog2 = 12;
+
 // Tile edge (grid cells) of the scatter work decomposition.
 constexpr int kTile = 32;
 
@@ -88,6 +99,14 @@ __device__ __forceinline__ void eval_kernel(double y, double* out) {
   }
 }
 
+// Scale of a packed chunk of n visibilities relative to the launch's base
+// scale (which assumes n = kChunkVisPacked): 2^(12 - ceil(lg n)), exact.
+__host__ __device__ inline double packed_chunk_gain(int64_t n) {
+  int lg = 0;
+  while (((int64_t)1 << lg) < n) ++lg;
+  return (double)((int64_t)1 << (kChunkVisPackedLog2 - (lg < kChunkVisPackedLog2 ? lg : kChunkVisPackedLog2)));
+}
+
 // A gridding work unit: the flattened visibilities [g0, g1) of tile `tile`
 // (global indices into the tile-sorted visibility stream).
 struct Chunk {
@@ -116,6 +135,19 @@ __device__ __forceinline__ void footprint(double x, int half_w, int64_t* i0, dou
   *y = 2.0 * (s - fl) - 1.0;
 }
 
+// i mod n in [0, n): one compare-and-add for |i| < 2n (all but absurd
+// coordinates), the 64-bit remainder only beyond that.
+__device__ __forceinline__ int64_t wrap_index(int64_t i, int64_t n) {
+  if (i >= n) {
+    i -= n;
+    if (i >= n) i %= n;
+  } else if (i < 0) {
+    i += n;
+    if (i < 0) i = ((i % n) + n) % n;
+  }
+  return i;
+}
+
 // Place one visibility (metres, fx = f / c) on the grid. Returns false when the
 // footprint leaves the grid (or the w-plane stack). The arithmetic order is
 // pinned (no contraction) so the planner and the scatter agree bit for bit and
@@ -132,8 +164,8 @@ __device__ __forceinline__ bool place_vis(double u_m, double v_m, double w_m, do
   // The dirty image is sampled at l = k * pixsize, so it is periodic in u with
   // period 1 / pixsize = the grid extent: coordinates beyond the grid wrap
   // (exactly, as ducc0 does), and the footprint origin is taken modulo nu.
-  *ix0 = ((*ix0 % g.nu) + g.nu) % g.nu;
-  *iy0 = ((*iy0 % g.nv) + g.nv) % g.nv;
+  *ix0 = wrap_index(*ix0, g.nu);
+  *iy0 = wrap_index(*iy0, g.nv);
   bool ok = true;
   if (g.do_wstacking) {
     const double xw = ((w_m * fx) - g.w0) / g.dw;
@@ -149,7 +181,7 @@ __device__ __forceinline__ bool place_vis(double u_m, double v_m, double w_m, do
 }
 
 __device__ __forceinline__ int64_t tile_key(int64_t ix0, int64_t iy0, int64_t iw0, const GridGeometry& g) {
-  return (iw0 * g.nty + iy0 / g.tile) * g.ntx + ix0 / g.tile;
+  return (iw0 * g.nty + iy0 / kTile) * g.ntx + ix0 / kTile;  // g.tile == kTile
 }
 
 }  // namespace cip

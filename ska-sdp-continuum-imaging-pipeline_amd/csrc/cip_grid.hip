@@ -11,6 +11,13 @@
 // to fp64 and added to the HBM grid with global fp64 atomics. No MFMA: this
 // is a scatter.
 #include "cip_internal.h"
+#include <type_traits>
+
+// Experiment-only builds (tools/build_variant.sh): 1 = conflict-free LDS
+// addresses, 2 = no LDS atomics, 3 = no kernel evaluation. 0 in the library.
+#ifndef CIP_ABLATE
+#define CIP_ABLATE 0
+#endif
 
 namespace cip {
 
@@ -162,7 +169,7 @@ __device__ __forceinline__ void fetch_vis(int64_t q, const int64_t* s_voff, cons
   f.wt = load_weight<WK>(wgt, idx);
 }
 
-template <int W, bool WSTACK>
+template <int W, bool WSTACK, bool PACK>
 __device__ __forceinline__ void grid_fetched(const VisFetch& f, const GridGeometry& g, int64_t plane, int64_t X0,
                                              int64_t Y0, double fixed_scale, unsigned long long* sub) {
   constexpr int T = kTile;
@@ -186,8 +193,16 @@ __device__ __forceinline__ void grid_fetched(const VisFetch& f, const GridGeomet
   }
   const double vr = f.vr * sc, vi = f.vi * sc;
   double ku[W], kv[W];
+#if CIP_ABLATE == 3
+#pragma unroll
+  for (int k = 0; k < W; ++k) {
+    ku[k] = yu + (double)k;
+    kv[k] = yv - (double)k;
+  }
+#else
   eval_kernel<W>(yu, ku);
   eval_kernel<W>(yv, kv);
+#endif
   double kr[W], ki[W];
 #pragma unroll
   for (int j = 0; j < W; ++j) {
@@ -197,147 +212,212 @@ __device__ __forceinline__ void grid_fetched(const VisFetch& f, const GridGeomet
   // separate re / im planes: a lane-scattered 8-byte add touches 2 of the 64
   // LDS banks, so 8-byte cells spread a wave over twice the bank pairs that
   // interleaved 16-byte (re, im) cells would
+#if CIP_ABLATE == 1
+  unsigned long long* base = sub + ((threadIdx.x & 31) + ((threadIdx.x & 32) ? 8 * P : 0));
+#else
   unsigned long long* base = sub + (lx * P + ly);
+#endif
+#if CIP_ABLATE == 2
+  unsigned long long acc = 0;
+#define atomicAdd(p, v) (acc += (v) ^ (unsigned long long)(p))
+#endif
 #pragma unroll
   for (int i = 0; i < W; ++i) {
 #pragma unroll
     for (int j = 0; j < W; ++j) {
       const double qr = fma(ku[i], kr[j], kMagic);
       const double qi = fma(ku[i], ki[j], kMagic);
-      atomicAdd(base + (i * P + j), (unsigned long long)__double_as_longlong(qr) - 0x4338000000000000ull);
-      atomicAdd(base + P * P + (i * P + j), (unsigned long long)__double_as_longlong(qi) - 0x4338000000000000ull);
+      const unsigned long long br = (unsigned long long)__double_as_longlong(qr);
+      const unsigned long long bi = (unsigned long long)__double_as_longlong(qi);
+      if constexpr (PACK) {
+        // bits(kMagic + k) = 0x43380000'00000000 + k (two's complement), so
+        // re * 2^32 + im = {lo32(br) + hi32(bi) - 0x43380000, lo32(bi)}
+        unsigned hi;  // one v_add3_u32 (the compiler otherwise widens it to 64-bit adds)
+#if CIP_ABLATE == 2
+        hi = (unsigned)br + (unsigned)(bi >> 32) + (0u - kMagicHi);
+#else
+        asm("v_add3_u32 %0, %1, %2, %3" : "=v"(hi) : "v"((unsigned)br), "v"((unsigned)(bi >> 32)),
+            "s"(0u - kMagicHi));
+#endif
+        atomicAdd(base + (i * P + j), __builtin_bit_cast(unsigned long long, make_uint2((unsigned)bi, hi)));
+      } else {
+        atomicAdd(base + (i * P + j), br - 0x4338000000000000ull);
+        atomicAdd(base + P * P + (i * P + j), bi - 0x4338000000000000ull);
+      }
     }
+  }
+#if CIP_ABLATE == 2
+#undef atomicAdd
+  if (acc == 0x123456789ull) sub[0] = acc;
+#endif
+}
+
+// ------------------------------------------ bank-class visibility order ----
+// A lane-scattered 8-byte LDS atomic hits bank pair (cell mod 32): 32 lanes
+// whose footprints start on equal classes serialise (tools/microbench:
+// 27 CU-cycles per visibility at random classes, 14 at distinct ones; the
+// scatter with conflict-free addresses runs 1.7x faster, profiles/). The
+// planner therefore stores, per chunk, the tile-order visibilities of each
+// aligned window of kOrderBatch positions counting-sorted by class into
+// level-major order (position = visibilities of lower rank in every class +
+// lower classes of equal rank), so any 32 consecutive positions of a level
+// have distinct classes and the scatter's waves (64 consecutive positions)
+// issue conflict-free atomics. Level tables: S[r] = sum_c min(cnt[c], r),
+// M[r] = {c : cnt[c] > r}. perm[g] = (row << 16) | channel. Atomic ranks make
+// the order within a class run-to-run variable; the integer sums are not.
+constexpr int kOrderThreads = 256;
+constexpr int kOrderPer = 4;
+constexpr int kOrderBatch = kOrderThreads * kOrderPer;
+
+__global__ __launch_bounds__(kOrderThreads) void order_kernel(const uint8_t* __restrict__ vis_class, int64_t nchan,
+                                                              const uint64_t* __restrict__ runs,
+                                                              const int64_t* __restrict__ run_goff,
+                                                              const int64_t* __restrict__ tile_run_off,
+                                                              const Chunk* __restrict__ chunks,
+                                                              uint64_t* __restrict__ perm) {
+  __shared__ __attribute__((aligned(16))) unsigned s_cnt[32];
+  __shared__ unsigned s_S[kOrderBatch], s_M[kOrderBatch];
+  // the row slices overlapping the current window (a window of kOrderBatch
+  // positions meets at most kOrderBatch of them)
+  __shared__ int64_t s_voff[kOrderBatch + 1];
+  __shared__ uint64_t s_run[kOrderBatch];
+  __shared__ uint64_t s_vis[kOrderBatch];  // window position -> (row << 16) | channel
+  __shared__ int s_next;
+  const Chunk ch = chunks[blockIdx.x];
+  const int64_t r1 = tile_run_off[ch.tile + 1];
+  int64_t r = ch.first_run;  // first slice overlapping the window
+  for (int64_t sb = ch.g0; sb < ch.g1; sb += kOrderBatch) {
+    const int nsb = (int)((ch.g1 - sb) < kOrderBatch ? (ch.g1 - sb) : kOrderBatch);
+    const int nst = (int)((r1 - r) < kOrderBatch ? (r1 - r) : kOrderBatch);
+    __syncthreads();
+    for (int k = threadIdx.x; k <= nst; k += kOrderThreads) {
+      s_voff[k] = run_goff[r + k];
+      if (k < nst) s_run[k] = runs[r + k];
+    }
+    if (threadIdx.x < 32) s_cnt[threadIdx.x] = 0u;
+    if (threadIdx.x == 0) s_next = nst;
+    __syncthreads();
+    // expand the staged slices over the window; the next window starts in
+    // the slice holding position sb + nsb
+    for (int k = threadIdx.x; k < nst; k += kOrderThreads) {
+      const int64_t a = s_voff[k], b = s_voff[k + 1];
+      if (a <= sb + nsb && b > sb + nsb) s_next = k;
+      const int64_t lo = a > sb ? a : sb, hi = b < sb + nsb ? b : sb + nsb;
+      const uint64_t rec = s_run[k];
+      const uint64_t base = ((rec >> 32) << 16) + ((rec >> 16) & 0xffff) - (uint64_t)a;
+      for (int64_t q = lo; q < hi; ++q) s_vis[q - sb] = base + (uint64_t)q;
+    }
+    __syncthreads();
+    uint64_t packed[kOrderPer];
+    unsigned cls[kOrderPer], rk[kOrderPer];
+#pragma unroll
+    for (int k = 0; k < kOrderPer; ++k) {
+      const int qi = threadIdx.x + k * kOrderThreads;
+      cls[k] = 32u;
+      if (qi < nsb) {
+        packed[k] = s_vis[qi];
+        cls[k] = vis_class[(int64_t)(packed[k] >> 16) * nchan + (int64_t)(packed[k] & 0xffff)];
+        rk[k] = atomicAdd(&s_cnt[cls[k]], 1u);
+      }
+    }
+    __syncthreads();
+    unsigned cnt[32], maxcnt = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const uint4 c4 = reinterpret_cast<const uint4*>(s_cnt)[i];
+      cnt[4 * i] = c4.x;
+      cnt[4 * i + 1] = c4.y;
+      cnt[4 * i + 2] = c4.z;
+      cnt[4 * i + 3] = c4.w;
+    }
+#pragma unroll
+    for (int i = 0; i < 32; ++i) maxcnt = cnt[i] > maxcnt ? cnt[i] : maxcnt;
+    for (unsigned r = threadIdx.x; r < maxcnt; r += kOrderThreads) {
+      unsigned S = 0, M = 0;
+#pragma unroll
+      for (int c2 = 0; c2 < 32; ++c2) {
+        S += cnt[c2] < r ? cnt[c2] : r;
+        M |= (cnt[c2] > r ? 1u : 0u) << c2;
+      }
+      s_S[r] = S;
+      s_M[r] = M;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kOrderPer; ++k)
+      if (cls[k] < 32u) perm[sb + s_S[rk[k]] + __popc(s_M[rk[k]] & ((1u << cls[k]) - 1u))] = packed[k];
+    r += s_next;
   }
 }
 
-// Bank-class ordering (ORDER): a lane-scattered 8-byte LDS atomic hits bank
-// pair (cell mod 32), so 32 lanes with random footprints collide (measured
-// 27 CU-cycles per visibility, tools/microbench/lds_scatter.hip) while 32
-// lanes with distinct classes run at 14. Each sub-batch of kSortBatch
-// visibilities is counting-sorted by class into level-major order (position =
-// visibilities of lower rank in every class + lower classes of equal rank), so
-// every run of up to 32 consecutive positions within a level has distinct
-// classes. Level tables: S[r] = sum_c min(cnt[c], r), M[r] = {c : cnt[c] > r}.
-constexpr int kSortPer = 2;
-constexpr int kSortBatch = kScatterThreads * kSortPer;
-
-template <int W, typename VisT, int WK, bool WSTACK>
-__device__ __forceinline__ void scatter_sorted_batch(
-    int64_t sb, int nsb, const int64_t* s_voff, const uint64_t* s_run, int nst, unsigned* s_cnt, unsigned* s_S,
-    unsigned* s_M, uint64_t* s_order, const double* __restrict__ uvw, const double* __restrict__ fx,
-    const VisT* __restrict__ vis, const void* __restrict__ wgt, int64_t nchan, const GridGeometry& g, int64_t plane,
-    int64_t X0, int64_t Y0, double fixed_scale, unsigned long long* sub) {
-  constexpr int P = kTile + W - 1;
-  if (threadIdx.x < 32) s_cnt[threadIdx.x] = 0u;
-  __syncthreads();
-  uint64_t packed[kSortPer];
-  unsigned cls[kSortPer], rk[kSortPer];
-#pragma unroll
-  for (int k = 0; k < kSortPer; ++k) {
-    const int qi = threadIdx.x + k * kScatterThreads;
-    cls[k] = 32u;
-    if (qi < nsb) {
-      int64_t irow, c;
-      locate_vis(sb + qi, s_voff, s_run, nst, &irow, &c);
-      packed[k] = ((uint64_t)irow << 16) | (uint64_t)c;
-      int64_t ix0, iy0, iw0;
-      double yu, yv, yw;
-      place_vis(uvw[3 * irow], uvw[3 * irow + 1], uvw[3 * irow + 2], fx[c], g, &ix0, &yu, &iy0, &yv, &iw0, &yw);
-      cls[k] = (unsigned)(((ix0 - X0) * P + (iy0 - Y0)) & 31);
-      rk[k] = atomicAdd(&s_cnt[cls[k]], 1u);
-    }
-  }
-  __syncthreads();
-  unsigned cnt[32], maxcnt = 0;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const uint4 c4 = reinterpret_cast<const uint4*>(s_cnt)[i];
-    cnt[4 * i] = c4.x;
-    cnt[4 * i + 1] = c4.y;
-    cnt[4 * i + 2] = c4.z;
-    cnt[4 * i + 3] = c4.w;
-  }
-#pragma unroll
-  for (int i = 0; i < 32; ++i) maxcnt = cnt[i] > maxcnt ? cnt[i] : maxcnt;
-  for (unsigned r = threadIdx.x; r < maxcnt; r += kScatterThreads) {
-    unsigned S = 0, M = 0;
-#pragma unroll
-    for (int c2 = 0; c2 < 32; ++c2) {
-      S += cnt[c2] < r ? cnt[c2] : r;
-      M |= (cnt[c2] > r ? 1u : 0u) << c2;
-    }
-    s_S[r] = S;
-    s_M[r] = M;
-  }
-  __syncthreads();
-#pragma unroll
-  for (int k = 0; k < kSortPer; ++k)
-    if (cls[k] < 32u) s_order[s_S[rk[k]] + __popc(s_M[rk[k]] & ((1u << cls[k]) - 1u))] = packed[k];
-  __syncthreads();
-  // grid in sorted order, fetching one visibility ahead
-  int pi = threadIdx.x;
-  bool have = pi < nsb;
-  VisFetch cur;
-  if (have) {
-    const uint64_t pk = s_order[pi];
-    fetch_at<VisT, WK>((int64_t)(pk >> 16), (int64_t)(pk & 0xffff), uvw, fx, vis, wgt, nchan, cur);
-  }
-  while (have) {
-    const int pn = pi + kScatterThreads;
-    const bool hn = pn < nsb;
-    VisFetch nxt;
-    if (hn) {
-      const uint64_t pk = s_order[pn];
-      fetch_at<VisT, WK>((int64_t)(pk >> 16), (int64_t)(pk & 0xffff), uvw, fx, vis, wgt, nchan, nxt);
-    }
-    grid_fetched<W, WSTACK>(cur, g, plane, X0, Y0, fixed_scale, sub);
-    cur = nxt;
-    pi = pn;
-    have = hn;
-  }
-  __syncthreads();
+hipError_t launch_order(const uint8_t* vis_class, int64_t nchan, const uint64_t* runs, const int64_t* run_goff,
+                        const int64_t* tile_run_off, const Chunk* chunks, int64_t nchunks, uint64_t* perm,
+                        hipStream_t s) {
+  if (nchunks <= 0) return hipSuccess;
+  order_kernel<<<dim3((unsigned)nchunks), dim3(kOrderThreads), 0, s>>>(vis_class, nchan, runs, run_goff, tile_run_off,
+                                                                      chunks, perm);
+  return hipGetLastError();
 }
 
-template <int W, typename VisT, int WK, bool WSTACK, bool ORDER>
+template <int W, typename VisT, int WK, bool WSTACK, bool PERM, bool PACK>
 __global__ __launch_bounds__(kScatterThreads) void scatter_kernel(
     const double* __restrict__ uvw, const double* __restrict__ fx, const VisT* __restrict__ vis,
     const void* __restrict__ wgt, int64_t nchan, const uint64_t* __restrict__ runs,
     const int64_t* __restrict__ run_goff, const int64_t* __restrict__ tile_run_off,
-    const Chunk* __restrict__ chunks, int64_t chunk_begin, GridGeometry g, int64_t plane, double fixed_scale,
-    double inv_scale, double* __restrict__ grid) {
+    const uint64_t* __restrict__ perm, const Chunk* __restrict__ chunks, int64_t chunk_begin, GridGeometry g,
+    int64_t plane, double fixed_scale, double inv_scale, double* __restrict__ grid) {
   constexpr int T = kTile;
   constexpr int P = T + W - 1;
-  __shared__ unsigned long long sub[P * P * 2];
-  __shared__ int64_t s_voff[kRunBatch + 1];
-  __shared__ uint64_t s_run[kRunBatch];
-  __shared__ __attribute__((aligned(16))) unsigned s_cnt[32];
-  __shared__ unsigned s_S[ORDER ? kSortBatch : 1], s_M[ORDER ? kSortBatch : 1];
-  __shared__ uint64_t s_order[ORDER ? kSortBatch : 1];
+  __shared__ unsigned long long sub[P * P * (PACK ? 1 : 2)];
+  __shared__ int64_t s_voff[PERM ? 1 : kRunBatch + 1];
+  __shared__ uint64_t s_run[PERM ? 1 : kRunBatch];
 
   const Chunk ch = chunks[chunk_begin + blockIdx.x];
   const int64_t t = ch.tile;
   const int64_t X0 = (t % g.ntx) * T;
   const int64_t Y0 = ((t / g.ntx) % g.nty) * T;
-  for (int i = threadIdx.x; i < P * P * 2; i += kScatterThreads) sub[i] = 0ull;
-  const int64_t rb = tile_run_off[t + 1];
-  int64_t r = ch.first_run;
-  int64_t v = ch.g0;
-  while (v < ch.g1 && r < rb) {
-    const int nst = (int)((rb - r) < kRunBatch ? (rb - r) : kRunBatch);
+  for (int i = threadIdx.x; i < P * P * (PACK ? 1 : 2); i += kScatterThreads) sub[i] = 0ull;
+  if constexpr (PACK) {
+    fixed_scale *= packed_chunk_gain(ch.g1 - ch.g0);
+    inv_scale = 1.0 / fixed_scale;
+  }
+  if constexpr (PERM) {
+    // bank-class ordered stream (order_kernel); software pipeline: fetch
+    // position q + 256 while gridding q
     __syncthreads();
-    for (int k = threadIdx.x; k <= nst; k += kScatterThreads) {
-      s_voff[k] = run_goff[r + k];
-      if (k < nst) s_run[k] = runs[r + k];
+    int64_t q = ch.g0 + threadIdx.x;
+    bool have = q < ch.g1;
+    VisFetch cur;
+    if (have) {
+      const uint64_t pk = perm[q];
+      fetch_at<VisT, WK>((int64_t)(pk >> 16), (int64_t)(pk & 0xffff), uvw, fx, vis, wgt, nchan, cur);
     }
-    __syncthreads();
-    const int64_t bend = ch.g1 < s_voff[nst] ? ch.g1 : s_voff[nst];
-    if constexpr (ORDER) {
-      for (int64_t sb = v; sb < bend; sb += kSortBatch) {
-        const int nsb = (int)((bend - sb) < kSortBatch ? (bend - sb) : kSortBatch);
-        scatter_sorted_batch<W, VisT, WK, WSTACK>(sb, nsb, s_voff, s_run, nst, s_cnt, s_S, s_M, s_order, uvw, fx,
-                                                  vis, wgt, nchan, g, plane, X0, Y0, fixed_scale, sub);
+    while (have) {
+      const int64_t qn = q + kScatterThreads;
+      const bool hn = qn < ch.g1;
+      VisFetch nxt;
+      if (hn) {
+        const uint64_t pk = perm[qn];
+        fetch_at<VisT, WK>((int64_t)(pk >> 16), (int64_t)(pk & 0xffff), uvw, fx, vis, wgt, nchan, nxt);
       }
-    } else {
+      grid_fetched<W, WSTACK, PACK>(cur, g, plane, X0, Y0, fixed_scale, sub);
+      cur = nxt;
+      q = qn;
+      have = hn;
+    }
+  } else {
+    const int64_t rb = tile_run_off[t + 1];
+    int64_t r = ch.first_run;
+    int64_t v = ch.g0;
+    while (v < ch.g1 && r < rb) {
+      const int nst = (int)((rb - r) < kRunBatch ? (rb - r) : kRunBatch);
+      __syncthreads();
+      for (int k = threadIdx.x; k <= nst; k += kScatterThreads) {
+        s_voff[k] = run_goff[r + k];
+        if (k < nst) s_run[k] = runs[r + k];
+      }
+      __syncthreads();
+      const int64_t bend = ch.g1 < s_voff[nst] ? ch.g1 : s_voff[nst];
       // software pipeline: fetch visibility q + 256 while gridding q
       int64_t q = v + threadIdx.x;
       bool have = q < bend;
@@ -348,20 +428,27 @@ __global__ __launch_bounds__(kScatterThreads) void scatter_kernel(
         const bool hn = qn < bend;
         VisFetch nxt;
         if (hn) fetch_vis<VisT, WK>(qn, s_voff, s_run, nst, uvw, fx, vis, wgt, nchan, nxt);
-        grid_fetched<W, WSTACK>(cur, g, plane, X0, Y0, fixed_scale, sub);
+        grid_fetched<W, WSTACK, PACK>(cur, g, plane, X0, Y0, fixed_scale, sub);
         cur = nxt;
         q = qn;
         have = hn;
       }
+      v = bend;
+      r += nst;
     }
-    v = bend;
-    r += nst;
   }
   __syncthreads();
   // flush the touched cells of the sub-grid to the fp64 HBM grid
   for (int cell = threadIdx.x; cell < P * P; cell += kScatterThreads) {
-    const long long re = (long long)sub[cell];
-    const long long im = (long long)sub[P * P + cell];
+    long long re, im;
+    if constexpr (PACK) {
+      const unsigned long long s = sub[cell];
+      im = (long long)(int)(unsigned)s;
+      re = (long long)(int)(unsigned)((s - (unsigned long long)im) >> 32);
+    } else {
+      re = (long long)sub[cell];
+      im = (long long)sub[P * P + cell];
+    }
     if ((re | im) != 0) {
       // the sub-grid of an edge tile wraps around the periodic grid
       int64_t gx = X0 + cell / P, gy = Y0 + cell % P;
@@ -375,38 +462,52 @@ __global__ __launch_bounds__(kScatterThreads) void scatter_kernel(
 }
 
 template <int W, typename VisT, int WK>
-static hipError_t scatter_dispatch_ws(bool ws, dim3 grid_dim, hipStream_t s, const double* uvw, const double* fx,
-                                      const void* vis, const void* wgt, int64_t nchan, const uint64_t* runs,
-                                      const int64_t* run_goff, const int64_t* tile_run_off, const Chunk* chunks,
-                                      int64_t chunk_begin, const GridGeometry& g, int64_t plane, double fs,
-                                      double* grid) {
-#define LAUNCH(WSV, ORD)                                                                                     \
-  scatter_kernel<W, VisT, WK, WSV, ORD><<<grid_dim, dim3(kScatterThreads), 0, s>>>(                          \
-      uvw, fx, (const VisT*)vis, wgt, nchan, runs, run_goff, tile_run_off, chunks, chunk_begin, g, plane, fs, \
-      1.0 / fs, grid)
-  static const bool order = [] {  // CIP_SCATTER_ORDER=0 selects the unsorted variant (A/B)
-    const char* e = getenv("CIP_SCATTER_ORDER");
-    return !(e && e[0] == '0');
-  }();
-  if (ws) {
-    if (order) LAUNCH(true, true);
-    else LAUNCH(true, false);
-  } else {
-    if (order) LAUNCH(false, true);
-    else LAUNCH(false, false);
+static hipError_t scatter_dispatch_ws(bool ws, bool pack, dim3 grid_dim, hipStream_t s, const double* uvw,
+                                      const double* fx, const void* vis, const void* wgt, int64_t nchan,
+                                      const uint64_t* runs, const int64_t* run_goff, const int64_t* tile_run_off,
+                                      const uint64_t* perm, const Chunk* chunks, int64_t chunk_begin,
+                                      const GridGeometry& g, int64_t plane, double fs, double* grid) {
+#define LAUNCH(WSV, PRM, PK)                                                                                   \
+  scatter_kernel<W, VisT, WK, WSV, PRM, PK><<<grid_dim, dim3(kScatterThreads), 0, s>>>(                        \
+      uvw, fx, (const VisT*)vis, wgt, nchan, runs, run_goff, tile_run_off, perm, chunks, chunk_begin, g, plane, \
+      fs, 1.0 / fs, grid)
+#define LAUNCH_WS(PRM, PK)      \
+  if (ws) LAUNCH(true, PRM, PK); \
+  else LAUNCH(false, PRM, PK);
+  // the packed single-precision class exists for complex64 input only (the
+  // reference's configuration)
+  bool done = false;
+  if constexpr (std::is_same<VisT, float2>::value) {
+    if (pack) {
+      if (perm) {
+        LAUNCH_WS(true, true)
+      } else {
+        LAUNCH_WS(false, true)
+      }
+      done = true;
+    }
   }
+  if (!done) {
+    if (perm) {
+      LAUNCH_WS(true, false)
+    } else {
+      LAUNCH_WS(false, false)
+    }
+  }
+#undef LAUNCH_WS
 #undef LAUNCH
   return hipGetLastError();
 }
 
 template <int W>
-static hipError_t scatter_dispatch_w(int vis_dtype, int wgt_dtype, dim3 gd, hipStream_t s, const double* uvw,
-                                     const double* fx, const void* vis, const void* wgt, int64_t nchan,
-                                     const uint64_t* runs, const int64_t* run_goff, const int64_t* tile_run_off,
-                                     const Chunk* chunks, int64_t cb, const GridGeometry& g, int64_t plane,
-                                     double fs, double* grid) {
+static hipError_t scatter_dispatch_w(int vis_dtype, int wgt_dtype, bool pack, dim3 gd, hipStream_t s,
+                                     const double* uvw, const double* fx, const void* vis, const void* wgt,
+                                     int64_t nchan, const uint64_t* runs, const int64_t* run_goff,
+                                     const int64_t* tile_run_off, const uint64_t* perm, const Chunk* chunks,
+                                     int64_t cb, const GridGeometry& g, int64_t plane, double fs, double* grid) {
   const bool ws = g.do_wstacking != 0;
-#define ARGS ws, gd, s, uvw, fx, vis, wgt, nchan, runs, run_goff, tile_run_off, chunks, cb, g, plane, fs, grid
+#define ARGS \
+  ws, pack, gd, s, uvw, fx, vis, wgt, nchan, runs, run_goff, tile_run_off, perm, chunks, cb, g, plane, fs, grid
   if (vis_dtype == CIP_C64) {
     if (wgt_dtype == CIP_F32) return scatter_dispatch_ws<W, float2, WK_F32>(ARGS);
     if (wgt_dtype == CIP_F64) return scatter_dispatch_ws<W, float2, WK_F64>(ARGS);
@@ -418,17 +519,18 @@ static hipError_t scatter_dispatch_w(int vis_dtype, int wgt_dtype, dim3 gd, hipS
 #undef ARGS
 }
 
-hipError_t launch_scatter(int support, int vis_dtype, int wgt_dtype, const double* uvw, const double* fx,
-                          const void* vis, const void* wgt, int64_t nchan, const uint64_t* runs,
-                          const int64_t* run_goff, const int64_t* tile_run_off, const Chunk* chunks,
-                          int64_t chunk_begin, int64_t nchunks, const GridGeometry& g, int64_t plane,
-                          double fixed_scale, double* grid, hipStream_t s) {
+hipError_t launch_scatter(int support, int vis_dtype, int wgt_dtype, bool packed, const double* uvw,
+                          const double* fx, const void* vis, const void* wgt, int64_t nchan, const uint64_t* runs,
+                          const int64_t* run_goff, const int64_t* tile_run_off, const uint64_t* perm,
+                          const Chunk* chunks, int64_t chunk_begin, int64_t nchunks, const GridGeometry& g,
+                          int64_t plane, double fixed_scale, double* grid, hipStream_t s) {
   if (nchunks <= 0) return hipSuccess;
+  if (packed && vis_dtype != CIP_C64) return hipErrorInvalidValue;
   const dim3 gd((unsigned)nchunks);
 #define CASE(WW)                                                                                             \
   case WW:                                                                                                   \
-    return scatter_dispatch_w<WW>(vis_dtype, wgt_dtype, gd, s, uvw, fx, vis, wgt, nchan, runs, run_goff,     \
-                                  tile_run_off, chunks, chunk_begin, g, plane, fixed_scale, grid);
+    return scatter_dispatch_w<WW>(vis_dtype, wgt_dtype, packed, gd, s, uvw, fx, vis, wgt, nchan, runs,       \
+                                  run_goff, tile_run_off, perm, chunks, chunk_begin, g, plane, fixed_scale, grid);
   switch (support) {
     CASE(4)
     CASE(6)

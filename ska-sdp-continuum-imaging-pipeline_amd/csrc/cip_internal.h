@@ -31,12 +31,14 @@ hipError_t launch_freq_scale(const double* freq, int64_t nchan, double* fx, hipS
 // per-row w range over channels (only f min/max matter): out[0]=min, out[1]=max
 hipError_t launch_w_range(const double* uvw, int64_t nrow, double fxmin, double fxmax, double* partial,
                           int nblocks, hipStream_t s);
-hipError_t launch_plan_count(const double* uvw, int64_t nrow, const double* fx, int64_t nchan,
-                             const GridGeometry& g, int64_t* tile_runs, int64_t* tile_vis,
-                             unsigned* err_flag, hipStream_t s);
-hipError_t launch_plan_emit(const double* uvw, int64_t nrow, const double* fx, int64_t nchan,
-                            const GridGeometry& g, const int64_t* tile_run_off, int64_t* tile_cursor,
-                            uint64_t* runs, hipStream_t s);
+// place pass: runs per tile (atomics), per-visibility bank class, parked runs
+// (park_* hold 64 slots per 64-visibility segment, seg_nruns the used ones)
+hipError_t launch_plan_place(const double* uvw, int64_t nrow, const double* fx, int64_t nchan,
+                             const GridGeometry& g, int64_t* tile_runs, unsigned* err_flag, uint8_t* vis_class,
+                             uint8_t* seg_nruns, int64_t* park_key, uint64_t* park_run, hipStream_t s);
+hipError_t launch_plan_distribute(int64_t nvis, const uint8_t* seg_nruns, const int64_t* park_key,
+                                  const uint64_t* park_run, const int64_t* tile_run_off, int64_t* tile_cursor,
+                                  uint64_t* runs, hipStream_t s);
 hipError_t launch_tile_vis(const int64_t* run_goff, const int64_t* tile_run_off, int64_t ntiles,
                            int64_t* tile_vis_off, int64_t* tile_vis, hipStream_t s);
 hipError_t launch_run_lengths(const uint64_t* runs, int64_t nruns, int64_t* out, hipStream_t s);
@@ -53,11 +55,18 @@ hipError_t launch_gather_i64(const int64_t* src, int64_t stride, int64_t count, 
 hipError_t launch_prep_reduce(const void* vis, int vis_dtype, const void* wgt, int wgt_dtype, int64_t n,
                               double* partial, int nblocks, double* out2, hipStream_t s);
 int prep_blocks();
-hipError_t launch_scatter(int support, int vis_dtype, int wgt_dtype, const double* uvw, const double* fx,
-                          const void* vis, const void* wgt, int64_t nchan, const uint64_t* runs,
-                          const int64_t* run_goff, const int64_t* tile_run_off, const Chunk* chunks,
-                          int64_t chunk_begin, int64_t nchunks, const GridGeometry& g, int64_t plane,
-                          double fixed_scale, double* grid, hipStream_t s);
+// packed: single-precision class (re/im packed in one 64-bit integer), complex64
+// only. perm: bank-class ordered stream from launch_order, or NULL (visibilities
+// located through the tile's row slices in tile order).
+hipError_t launch_scatter(int support, int vis_dtype, int wgt_dtype, bool packed, const double* uvw,
+                          const double* fx, const void* vis, const void* wgt, int64_t nchan, const uint64_t* runs,
+                          const int64_t* run_goff, const int64_t* tile_run_off, const uint64_t* perm,
+                          const Chunk* chunks, int64_t chunk_begin, int64_t nchunks, const GridGeometry& g,
+                          int64_t plane, double fixed_scale, double* grid, hipStream_t s);
+// perm[g] for every tile-order position g of every chunk (cip_grid.hip)
+hipError_t launch_order(const uint8_t* vis_class, int64_t nchan, const uint64_t* runs, const int64_t* run_goff,
+                        const int64_t* tile_run_off, const Chunk* chunks, int64_t nchunks, uint64_t* perm,
+                        hipStream_t s);
 hipError_t launch_crop_correct_2d(const double* grid, const GridGeometry& g, int64_t npix_x, int64_t npix_y,
                                   const double* cx, const double* cy, double* dirty, hipStream_t s);
 hipError_t launch_wplane_accumulate(const double* grid, const GridGeometry& g, int64_t npix_x, int64_t npix_y,

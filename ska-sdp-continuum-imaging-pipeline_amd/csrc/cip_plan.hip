@@ -125,62 +125,110 @@ hipError_t launch_w_range(const double* uvw, int64_t nrow, double fxmin, double 
 }
 
 // ---------------------------------------------------------- planner ----
-// One thread per row walks its channels; a run is a maximal channel range of
-// constant tile key (keys are monotone in frequency along a row's radial
-// track, so a row visits each tile at most once - cf. tiling_plan.py:150-181).
-template <bool EMIT>
-__global__ __launch_bounds__(256) void plan_kernel(const double* __restrict__ uvw, int64_t nrow,
-                                                   const double* __restrict__ fx, int64_t nchan, GridGeometry g,
-                                                   int64_t* tile_runs, int64_t* tile_vis, unsigned* err_flag,
-                                                   const int64_t* __restrict__ tile_run_off, int64_t* tile_cursor,
-                                                   uint64_t* runs) {
-  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= nrow) return;
-  const double u = uvw[3 * r], v = uvw[3 * r + 1], w = uvw[3 * r + 2];
-  int64_t prev = -1, start = 0;
-  for (int64_t c = 0; c <= nchan; ++c) {
-    int64_t key = -2;  // sentinel closes the last run
-    if (c < nchan) {
+// A run is a maximal range of consecutive channels of one row with constant
+// tile key (cf. the reference's row slices, tiling_plan.py:150-181). Each
+// wave takes 64 consecutive flattened (row, channel) visibilities, one per
+// lane: a lane starts a run when its key differs from the previous channel's
+// (or at a row start or the wave's first lane), and the run ends at the next
+// start in the wave (ballot), so runs are split at 64-visibility segment
+// boundaries. The place pass is the only one that places visibilities: it
+// counts runs per tile (one global atomic per run), parks each run in its
+// segment's slots of a scratch array and records every visibility's LDS bank
+// class for the order pass; the distribute pass moves the parked runs into
+// their tile buckets.
+__global__ __launch_bounds__(256) void plan_place_kernel(const double* __restrict__ uvw, int64_t nrow,
+                                                         const double* __restrict__ fx, int64_t nchan,
+                                                         GridGeometry g, int64_t* tile_runs, unsigned* err_flag,
+                                                         uint8_t* __restrict__ vis_class,
+                                                         uint8_t* __restrict__ seg_nruns,
+                                                         int64_t* __restrict__ park_key,
+                                                         uint64_t* __restrict__ park_run) {
+  const int lane = threadIdx.x & 63;
+  const int64_t nvis = nrow * nchan;
+  const int64_t nseg = (nvis + 63) / 64;
+  const int P = kTile + g.support - 1;
+  for (int64_t seg = ((int64_t)blockIdx.x * 256 + threadIdx.x) / 64; seg < nseg;
+       seg += (int64_t)gridDim.x * 4) {
+    const int64_t i = seg * 64 + lane;
+    const bool valid = i < nvis;
+    int64_t key = -1, r = 0, c = 0;
+    bool bad = false;
+    if (valid) {
+      // i / nchan through fp64 (exact after one correction for i < 2^52)
+      r = (int64_t)((double)i / (double)nchan);
+      c = i - r * nchan;
+      if (c < 0) {
+        --r;
+        c += nchan;
+      } else if (c >= nchan) {
+        ++r;
+        c -= nchan;
+      }
       int64_t ix0, iy0, iw0;
       double yu, yv, yw;
-      const bool ok = place_vis(u, v, w, fx[c], g, &ix0, &yu, &iy0, &yv, &iw0, &yw);
-      if (ok) {
+      if (place_vis(uvw[3 * r], uvw[3 * r + 1], uvw[3 * r + 2], fx[c], g, &ix0, &yu, &iy0, &yv, &iw0, &yw)) {
         key = tile_key(ix0, iy0, iw0, g);
+        vis_class[i] = (uint8_t)((((int)(ix0 % kTile)) * P + (int)(iy0 % kTile)) & 31);
       } else {
-        key = -1;
-        if (!EMIT) atomicOr(err_flag, 1u);
+        bad = true;
+        vis_class[i] = 0;
       }
     }
-    if (key != prev) {
-      if (prev >= 0) {
-        if (EMIT) {
-          const int64_t pos = tile_run_off[prev] + atomicAdd((unsigned long long*)&tile_cursor[prev], 1ull);
-          runs[pos] = ((uint64_t)r << 32) | ((uint64_t)start << 16) | (uint64_t)c;
-        } else {
-          // one atomic per run; per-tile visibility counts come later from
-          // the scanned run lengths (tile_vis_kernel)
-          atomicAdd((unsigned long long*)&tile_runs[prev], 1ull);
-        }
-      }
-      prev = key;
-      start = c;
+    if (__ballot(bad) != 0ull && lane == 0) atomicOr(err_flag, 1u);
+    const int64_t prev = __shfl_up(key, 1, 64);
+    const bool start = valid && (lane == 0 || c == 0 || key != prev);
+    const unsigned long long starts = __ballot(start);
+    const bool emit = start && key >= 0;
+    const unsigned long long emits = __ballot(emit);
+    const int nvalid = __popcll(__ballot(valid));  // wave-uniform: outside the branch
+    if (lane == 0) seg_nruns[seg] = (uint8_t)__popcll(emits);
+    if (emit) {
+      const unsigned long long above = starts & ~((2ull << lane) - 1ull);  // lane 63: 2 << 63 == 0
+      const int next = above ? (__ffsll((long long)above) - 1) : nvalid;
+      const int slot = __popcll(emits & ((1ull << lane) - 1ull));
+      park_key[seg * 64 + slot] = key;
+      park_run[seg * 64 + slot] = ((uint64_t)r << 32) | ((uint64_t)c << 16) | (uint64_t)(c + (next - lane));
+      atomicAdd((unsigned long long*)&tile_runs[key], 1ull);
     }
   }
 }
 
-hipError_t launch_plan_count(const double* uvw, int64_t nrow, const double* fx, int64_t nchan,
-                             const GridGeometry& g, int64_t* tile_runs, int64_t* tile_vis, unsigned* err_flag,
-                             hipStream_t s) {
-  plan_kernel<false><<<dim3((unsigned)((nrow + 255) / 256)), dim3(256), 0, s>>>(
-      uvw, nrow, fx, nchan, g, tile_runs, tile_vis, err_flag, nullptr, nullptr, nullptr);
+__global__ __launch_bounds__(256) void plan_distribute_kernel(int64_t nseg, const uint8_t* __restrict__ seg_nruns,
+                                                              const int64_t* __restrict__ park_key,
+                                                              const uint64_t* __restrict__ park_run,
+                                                              const int64_t* __restrict__ tile_run_off,
+                                                              int64_t* tile_cursor, uint64_t* __restrict__ runs) {
+  const int lane = threadIdx.x & 63;
+  for (int64_t seg = ((int64_t)blockIdx.x * 256 + threadIdx.x) / 64; seg < nseg;
+       seg += (int64_t)gridDim.x * 4) {
+    if (lane < (int)seg_nruns[seg]) {
+      const int64_t key = park_key[seg * 64 + lane];
+      const int64_t pos = tile_run_off[key] + atomicAdd((unsigned long long*)&tile_cursor[key], 1ull);
+      runs[pos] = park_run[seg * 64 + lane];
+    }
+  }
+}
+
+static unsigned plan_blocks(int64_t nvis) {
+  const int64_t segs = (nvis + 63) / 64;
+  const int64_t b = (segs + 3) / 4;
+  return (unsigned)(b < 16384 ? (b > 0 ? b : 1) : 16384);
+}
+
+hipError_t launch_plan_place(const double* uvw, int64_t nrow, const double* fx, int64_t nchan,
+                             const GridGeometry& g, int64_t* tile_runs, unsigned* err_flag, uint8_t* vis_class,
+                             uint8_t* seg_nruns, int64_t* park_key, uint64_t* park_run, hipStream_t s) {
+  plan_place_kernel<<<dim3(plan_blocks(nrow * nchan)), dim3(256), 0, s>>>(uvw, nrow, fx, nchan, g, tile_runs, err_flag,
+                                                                         vis_class, seg_nruns, park_key, park_run);
   return hipGetLastError();
 }
 
-hipError_t launch_plan_emit(const double* uvw, int64_t nrow, const double* fx, int64_t nchan,
-                            const GridGeometry& g, const int64_t* tile_run_off, int64_t* tile_cursor,
-                            uint64_t* runs, hipStream_t s) {
-  plan_kernel<true><<<dim3((unsigned)((nrow + 255) / 256)), dim3(256), 0, s>>>(
-      uvw, nrow, fx, nchan, g, nullptr, nullptr, nullptr, tile_run_off, tile_cursor, runs);
+hipError_t launch_plan_distribute(int64_t nvis, const uint8_t* seg_nruns, const int64_t* park_key,
+                                  const uint64_t* park_run, const int64_t* tile_run_off, int64_t* tile_cursor,
+                                  uint64_t* runs, hipStream_t s) {
+  const int64_t nseg = (nvis + 63) / 64;
+  plan_distribute_kernel<<<dim3(plan_blocks(nvis)), dim3(256), 0, s>>>(nseg, seg_nruns, park_key, park_run,
+                                                                      tile_run_off, tile_cursor, runs);
   return hipGetLastError();
 }
 

@@ -27,6 +27,8 @@ CIP_C64 = 1
 CIP_C128 = 2
 CIP_F32 = 3
 CIP_F64 = 4
+CIP_WSTACKING = 1
+CIP_ACC_SINGLE = 2
 
 # every symbol declared in include/cip.h
 EXPORTED_SYMBOLS = (
@@ -95,7 +97,7 @@ def lib() -> ctypes.CDLL:
     so.cip_ms2dirty.argtypes = [_vp, _i64, _vp, _i64, _vp, _i32, _vp, _i32, _i64, _i64, _f64, _f64,
                                 _f64, _i32, _i32, _vp, _vp, _vp, ctypes.POINTER(GridderParams)]
     so.cip_grid_plane.argtypes = [_vp, _i64, _vp, _i64, _vp, _i32, _vp, _i32,
-                                  ctypes.POINTER(GridderParams), _f64, _f64, _i64, _vp, _vp]
+                                  ctypes.POINTER(GridderParams), _f64, _f64, _i64, _i32, _vp, _vp]
     so.cip_tile_runs.argtypes = [_vp, _i64, _vp, _i64, ctypes.POINTER(ctypes.c_double), _i64, _vp,
                                  ctypes.POINTER(ctypes.c_int64), _vp, _vp, _vp, _vp]
     so.cip_stokes_i.argtypes = [_vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp]

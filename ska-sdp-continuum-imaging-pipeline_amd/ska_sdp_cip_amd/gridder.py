@@ -68,11 +68,16 @@ def device_ms2dirty(
     do_wstacking: bool = False,
     out: Optional["torch.Tensor"] = None,
     sum_weights: Optional["torch.Tensor"] = None,
+    single_precision_accumulation: bool = False,
 ) -> tuple["torch.Tensor", _lib.GridderParams]:
     """
     Device-resident ms2dirty: all tensors already in HBM on the current device.
     Returns (dirty fp64 tensor (npix_x, npix_y), params). `sum_weights`
     (fp64, 1 element) receives the sum of `wgt` when given.
+    `single_precision_accumulation` (complex64 `vis` only) selects the packed
+    single-precision class (CIP_ACC_SINGLE, include/cip.h): quantisation
+    2^-19 of max|w V| per contribution, like ducc0's float gridding; the
+    default accumulates every input in 64-bit fixed point (fp64 class).
     """
     vis_codes, wgt_codes = _codes()
     if vis.dtype not in vis_codes:
@@ -99,7 +104,10 @@ def device_ms2dirty(
         wgt.data_ptr() if wgt is not None else None,
         wgt_codes[wgt.dtype] if wgt is not None else _lib.CIP_NONE,
         int(npix_x), int(npix_y), float(pixsize_x), float(pixsize_y), float(epsilon),
-        int(support or 0), int(bool(do_wstacking)), stream, out.data_ptr(),
+        int(support or 0),
+        (_lib.CIP_WSTACKING if do_wstacking else 0)
+        | (_lib.CIP_ACC_SINGLE if single_precision_accumulation else 0),
+        stream, out.data_ptr(),
         sum_weights.data_ptr() if sum_weights is not None else None, params)
     _lib.check(rc)
     return out, params
@@ -121,7 +129,7 @@ def ms2dirty(  # pylint: disable=too-many-arguments,unused-argument
     nthreads: int = 1,
     verbosity: int = 0,
     mask=None,
-    double_precision_accumulation: bool = False,
+    double_precision_accumulation: Optional[bool] = None,
     *,
     support: Optional[int] = None,
     device=None,
@@ -129,11 +137,14 @@ def ms2dirty(  # pylint: disable=too-many-arguments,unused-argument
 ):
     """
     Drop-in for `ducc0.wgridder.ms2dirty` (same positional order as the call
-    at reference invert.py:170-183). `nu`, `nv`, `nthreads`, `verbosity` and
-    `double_precision_accumulation` are accepted for signature compatibility
-    and ignored (the grid is chosen from epsilon / `support`; accumulation is
-    always 64-bit). `mask` (uint8, shape of ms) zeroes the weights where 0.
-    Output dtype follows ducc: float32 for complex64 `ms`, else float64.
+    at reference invert.py:170-183). `nu`, `nv`, `nthreads` and `verbosity`
+    are accepted for signature compatibility and ignored (the grid is chosen
+    from epsilon / `support`). Accumulation is 64-bit fixed point unless
+    `double_precision_accumulation=False` is passed explicitly with complex64
+    `ms` (ducc0's float gridding class, CIP_ACC_SINGLE); left at None it is the
+    fp64 class, at least as accurate as ducc0 in every mode. `mask` (uint8,
+    shape of ms) zeroes the weights where 0. Output dtype follows ducc:
+    float32 for complex64 `ms`, else float64.
     """
     _require_gpu()
     if npix_x is None or npix_y is None or pixsize_x is None or pixsize_y is None:
@@ -159,7 +170,8 @@ def ms2dirty(  # pylint: disable=too-many-arguments,unused-argument
                 wgt_d = wgt_d * m.to(wgt_d.dtype)
         dirty, params = device_ms2dirty(
             uvw_d, freq_d, vis_d, wgt_d, int(npix_x), int(npix_y), float(pixsize_x),
-            float(pixsize_y), epsilon=epsilon, support=support, do_wstacking=do_wstacking)
+            float(pixsize_y), epsilon=epsilon, support=support, do_wstacking=do_wstacking,
+            single_precision_accumulation=single and double_precision_accumulation is False)
         dirty = dirty.to(torch.float32) if single else dirty
         result = dirty.cpu().numpy() if numpy_in else dirty
     if return_params:

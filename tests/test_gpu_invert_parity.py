@@ -103,12 +103,48 @@ def test_grid_plane_matches_oracle_grid(gpu_device):
     tu, tf, tv, tw = (torch.from_numpy(np.ascontiguousarray(a)).cuda() for a in (uvw, f, vis, w))
     _lib.check(_lib.lib().cip_grid_plane(
         tu.data_ptr(), uvw.shape[0], tf.data_ptr(), f.size, tv.data_ptr(), _lib.CIP_C64,
-        tw.data_ptr(), _lib.CIP_F32, prm, px, px, 0, None, grid.data_ptr()))
+        tw.data_ptr(), _lib.CIP_F32, prm, px, px, 0, 0, None, grid.data_ptr()))
     torch.cuda.synchronize()
     oprm = oracle.choose_params(npix, npix, px, px, support=8)
     ref = oracle.grid_plane(uvw, f, vis, w, oprm, px, px, 0)
     scale = np.abs(ref).max()
     assert np.abs(grid.cpu().numpy() - ref).max() / scale < 1e-13
+    # single-precision class: each contribution quantised to <= 2^-20 of
+    # max|w V| (chunks here hold < 2^11 visibilities)
+    _lib.check(_lib.lib().cip_grid_plane(
+        tu.data_ptr(), uvw.shape[0], tf.data_ptr(), f.size, tv.data_ptr(), _lib.CIP_C64,
+        tw.data_ptr(), _lib.CIP_F32, prm, px, px, 0, _lib.CIP_ACC_SINGLE, None, grid.data_ptr()))
+    torch.cuda.synchronize()
+    maxwv = float(np.abs(w.astype(np.float64) * vis).max())
+    per_cell = np.abs(grid.cpu().numpy() - ref).max() / maxwv
+    assert 0 < per_cell < 2e-3  # random walk of <= 0.5-unit roundings over a cell's contributions
+
+
+@pytest.mark.parametrize("wstack", [False, True])
+def test_single_precision_class_vs_oracle(gpu_device, wstack):
+    # CIP_ACC_SINGLE (ducc0's float class; the reference calls ducc0 with
+    # epsilon=1e-4): normalised error well below epsilon, and the default path
+    # on the same complex64 input stays at the fp64 class
+    import torch
+
+    uvw, f, vis, w = _case(4_000, 16, n_ant=24, radius=2000.0, fov=0.05)
+    npix = 192
+    px = syn.pixel_size_for_grid(uvw, f, npix, fill=0.3 if wstack else 0.5)
+    args = [torch.from_numpy(a).cuda() for a in (uvw, f, vis, w)]
+    single, _ = gridder.device_ms2dirty(*args, npix, npix, px, px, support=8, do_wstacking=wstack,
+                                        single_precision_accumulation=True)
+    double, _ = gridder.device_ms2dirty(*args, npix, npix, px, px, support=8, do_wstacking=wstack)
+    ref = oracle.ms2dirty(uvw, f, vis, w, npix, npix, px, px, support=8, do_wstacking=wstack)
+    sumw = float(w.astype(np.float64).sum())
+    assert _norm_err(double.cpu().numpy(), ref, sumw) < TIGHT
+    assert _norm_err(single.cpu().numpy(), ref, sumw) < 1e-5
+    np_single = gridder.ms2dirty(uvw, f, vis, w, npix, npix, px, px, do_wstacking=wstack,
+                                 double_precision_accumulation=False, support=8)
+    assert np_single.dtype == np.float32
+    assert np.abs(np_single - single.cpu().numpy()).max() / sumw < 1e-6
+    with pytest.raises(ValueError):  # complex128 has no single class
+        gridder.device_ms2dirty(args[0], args[1], args[2].to(torch.complex128), args[3], npix, npix, px, px,
+                                support=8, single_precision_accumulation=True)
 
 
 def test_point_source_at_centre_and_off_centre(gpu_device):
