@@ -257,6 +257,7 @@ struct DevBuf {
 struct FftPlan {
   hipfftHandle h;
   int64_t nu, nv;
+  int64_t cols;  // 0: 2-D nu x nv plan; > 0: batch of `cols` strided column FFTs of length nu
 };
 
 struct Workspace {
@@ -266,6 +267,7 @@ struct Workspace {
   size_t pinned_bytes = 0;
   std::vector<int64_t> corr_key;  // (npix_x, npix_y, nu, nv, W) of the cached cx / cy
   std::vector<double> fw_key;     // (W, dw |nmin|) of the cached w-correction table
+  int64_t tw_n = 0;               // length of the cached row-FFT twiddle table
 };
 
 static std::mutex g_ws_mutex;
@@ -316,7 +318,7 @@ static void* pinned(Workspace* ws, size_t bytes) {
 
 static int fft_plan(Workspace* ws, int64_t nu, int64_t nv, hipStream_t s, hipfftHandle* out) {
   for (auto& p : ws->plans)
-    if (p.nu == nu && p.nv == nv) {
+    if (p.cols == 0 && p.nu == nu && p.nv == nv) {
       if (hipfftSetStream(p.h, s) != HIPFFT_SUCCESS) return set_error(CIP_EHIP, "hipfftSetStream failed");
       *out = p.h;
       return CIP_OK;
@@ -325,8 +327,51 @@ static int fft_plan(Workspace* ws, int64_t nu, int64_t nv, hipStream_t s, hipfft
   if (hipfftPlan2d(&h, (int)nu, (int)nv, HIPFFT_Z2Z) != HIPFFT_SUCCESS)
     return set_error(CIP_EHIP, "hipfftPlan2d failed");
   if (hipfftSetStream(h, s) != HIPFFT_SUCCESS) return set_error(CIP_EHIP, "hipfftSetStream failed");
-  ws->plans.push_back({h, nu, nv});
+  ws->plans.push_back({h, nu, nv, 0});
   *out = h;
+  return CIP_OK;
+}
+
+#define CIP_ALLOC_RET(var, T, name, n) \
+  T* var = buf<T>(ws, name, (n));      \
+  if (!var) return CIP_ENOMEM;
+
+// Column pass of the pruned 2-D FFT: `cols` transforms of length nu over a
+// (nu, cols) row-major array (stride cols, distance 1), in place.
+static int fft_col_plan(Workspace* ws, int64_t nu, int64_t cols, hipStream_t s, hipfftHandle* out) {
+  for (auto& p : ws->plans)
+    if (p.cols == cols && p.nu == nu) {
+      if (hipfftSetStream(p.h, s) != HIPFFT_SUCCESS) return set_error(CIP_EHIP, "hipfftSetStream failed");
+      *out = p.h;
+      return CIP_OK;
+    }
+  hipfftHandle h;
+  int n[1] = {(int)nu};
+  int emb[1] = {(int)nu};
+  if (hipfftPlanMany(&h, 1, n, emb, (int)cols, 1, emb, (int)cols, 1, HIPFFT_Z2Z, (int)cols) != HIPFFT_SUCCESS)
+    return set_error(CIP_EHIP, "hipfftPlanMany failed");
+  if (hipfftSetStream(h, s) != HIPFFT_SUCCESS) return set_error(CIP_EHIP, "hipfftSetStream failed");
+  ws->plans.push_back({h, nu, 0, cols});
+  *out = h;
+  return CIP_OK;
+}
+
+// exp(+2 pi i m / n), m < n, for the row FFT (cached per workspace)
+static int row_fft_twiddles(Workspace* ws, int64_t n, hipStream_t s, double** out) {
+  CIP_ALLOC_RET(tw, double, "fft_twiddle", 2 * n)
+  if (ws->tw_n != n) {
+    std::vector<double> h(2 * n);
+    for (int64_t m = 0; m < n; ++m) {
+      // long double arguments: each entry correctly rounded (to within an ulp)
+      const long double a = 2.0L * 3.14159265358979323846264338327950288L * (long double)m / (long double)n;
+      h[2 * m] = (double)cosl(a);
+      h[2 * m + 1] = (double)sinl(a);
+    }
+    CIP_HIP_CHECK(hipMemcpyAsync(tw, h.data(), sizeof(double) * 2 * n, hipMemcpyHostToDevice, s));
+    CIP_HIP_CHECK(hipStreamSynchronize(s));
+    ws->tw_n = n;
+  }
+  *out = tw;
   return CIP_OK;
 }
 
@@ -345,7 +390,8 @@ static int64_t chunk_vis(bool packed) {
     env = e ? atoll(e) : -1;
   }
   const int64_t cap = packed ? kChunkVisPacked : kChunkVis;
-  return (env >= 256 && env < cap) ? env : cap;
+  // a multiple of kOrderWindow, so ordering windows never straddle chunks
+  return (env >= kOrderWindow && env < cap) ? env / kOrderWindow * kOrderWindow : cap;
 }
 
 struct PlanResult {
@@ -358,6 +404,15 @@ struct PlanResult {
   uint64_t* perm = nullptr;  // bank-class ordered visibility stream, or NULL
 };
 
+// CIP_FFT_PRUNED=0 selects the full 2-D hipFFT transform (A/B experiments)
+static bool fft_pruned() {
+  static const bool on = [] {
+    const char* e = getenv("CIP_FFT_PRUNED");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 // CIP_SCATTER_ORDER=0 skips the bank-class order (A/B experiments)
 static bool scatter_order() {
   static const bool on = [] {
@@ -367,43 +422,72 @@ static bool scatter_order() {
   return on;
 }
 
+// Also reduces {sum w, max |w V|} into red (device) and returns max |w V| in
+// *maxabs (the place pass reads the visibilities anyway).
 static int make_plan(Workspace* ws, const double* uvw, int64_t nrow, const double* fx, int64_t nchan,
-                     const GridGeometry& g, int64_t cv, hipStream_t s, PlanResult* pr) {
+                     const void* vis, int vis_dtype, const void* wgt, int wgt_dtype, double* red,
+                     const GridGeometry& g, int64_t cv, hipStream_t s, PlanResult* pr, double* maxabs) {
   const int64_t ntiles = g.ntx * g.nty * g.ntw;
   pr->ntiles = ntiles;
   CIP_ALLOC(tile_runs, int64_t, "tile_runs", ntiles + 1)
   CIP_ALLOC(tile_vis, int64_t, "tile_vis", ntiles + 1)
   CIP_ALLOC(tile_vis_off, int64_t, "tile_vis_off", ntiles + 1)
-  CIP_ALLOC(tile_cursor, int64_t, "tile_cursor", ntiles + 1)
   CIP_ALLOC(chunk_off, int64_t, "chunk_off", ntiles + 1)
   CIP_ALLOC(err, unsigned, "err_flag", 1)
   CIP_ALLOC(scan_tmp, int64_t, "scan_tmp", scan_tmp_elems(ntiles + 1))
-  CIP_HIP_CHECK(hipMemsetAsync(tile_runs, 0, sizeof(int64_t) * (ntiles + 1), s));
-  CIP_HIP_CHECK(hipMemsetAsync(tile_cursor, 0, sizeof(int64_t) * (ntiles + 1), s));
   CIP_HIP_CHECK(hipMemsetAsync(err, 0, sizeof(unsigned), s));
   const int64_t nvis = nrow * nchan, nseg = (nvis + 63) / 64;
   CIP_ALLOC(vis_class, uint8_t, "vis_class", nvis)
-  CIP_ALLOC(seg_nruns, uint8_t, "seg_nruns", nseg)
-  CIP_ALLOC(park_key, int64_t, "park_key", nseg * 64)
+  CIP_ALLOC(seg_off, int64_t, "seg_off", nseg + 1)
+  CIP_ALLOC(scan_seg, int64_t, "scan_seg", scan_tmp_elems(nseg + 1))
+  CIP_ALLOC(park_key, uint32_t, "park_key", nseg * 64)
   CIP_ALLOC(park_run, uint64_t, "park_run", nseg * 64)
-  CIP_HIP_CHECK(launch_plan_place(uvw, nrow, fx, nchan, g, tile_runs, err, vis_class, seg_nruns, park_key, park_run,
-                                  s));
-  // tile_runs -> exclusive offsets (entry ntiles = total runs)
-  CIP_HIP_CHECK(exclusive_scan_i64(tile_runs, ntiles + 1, scan_tmp, s));
+  const int nblk = plan_place_blocks(nvis);
+  CIP_ALLOC(partial, double, "prep_partial", 2 * nblk)
+  CIP_HIP_CHECK(hipMemsetAsync(seg_off + nseg, 0, sizeof(int64_t), s));
+  CIP_HIP_CHECK(launch_plan_place(uvw, nrow, fx, nchan, vis, vis_dtype, wgt, wgt_dtype, g, err, vis_class, seg_off,
+                                  park_key, park_run, partial, s));
+  CIP_HIP_CHECK(launch_prep_final(partial, nblk, red, s));
+  CIP_HIP_CHECK(exclusive_scan_i64(seg_off, nseg + 1, scan_seg, s));  // entry nseg = total runs
   int64_t* h = (int64_t*)pinned(ws, 4 * sizeof(int64_t));
   if (!h) return set_error(CIP_ENOMEM, "hipHostMalloc failed");
-  CIP_HIP_CHECK(hipMemcpyAsync(&h[0], tile_runs + ntiles, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+  CIP_HIP_CHECK(hipMemcpyAsync(&h[0], seg_off + nseg, sizeof(int64_t), hipMemcpyDeviceToHost, s));
   CIP_HIP_CHECK(hipMemcpyAsync(&h[1], err, sizeof(unsigned), hipMemcpyDeviceToHost, s));
+  CIP_HIP_CHECK(hipMemcpyAsync(&h[2], red + 1, sizeof(double), hipMemcpyDeviceToHost, s));
   CIP_HIP_CHECK(hipStreamSynchronize(s));
   const int64_t nruns = h[0];
-  if ((unsigned)h[1] != 0)
+  const unsigned errbits = (unsigned)h[1];
+  std::memcpy(maxabs, &h[2], sizeof(double));
+  if (errbits & 2u) return set_error(CIP_EINVAL, "non-finite visibility or weight");
+  if (errbits & 1u)
     return set_error(CIP_ERANGE, "non-finite (u, v, w) coordinates, or w outside the w-plane stack");
   pr->nruns = nruns;
+  // bucket the runs by tile: compact, then a stable LSD radix sort
+  int key_bits = 1;
+  while (key_bits < 32 && ((int64_t)1 << key_bits) < ntiles) ++key_bits;
+  const int npass = (key_bits + 7) / 8;
+  CIP_ALLOC(key_a, uint32_t, "sort_key_a", nruns)
+  CIP_ALLOC(key_b, uint32_t, "sort_key_b", nruns)
+  CIP_ALLOC(run_a, uint64_t, "sort_run_a", nruns)
+  CIP_ALLOC(run_b, uint64_t, "sort_run_b", nruns)
+  const int64_t nbd = radix_blocks(nruns);
+  CIP_ALLOC(hist, int64_t, "radix_hist", 256 * nbd + 1)
+  CIP_ALLOC(scan_h, int64_t, "scan_hist", scan_tmp_elems(256 * nbd + 1))
+  CIP_HIP_CHECK(launch_compact_runs(nseg, seg_off, park_key, park_run, key_a, run_a, s));
+  uint32_t *kin = key_a, *kout = key_b;
+  uint64_t *rin = run_a, *rout = run_b;
+  for (int p = 0; p < npass; ++p) {
+    CIP_HIP_CHECK(launch_radix_hist(kin, nruns, 8 * p, hist, s));
+    CIP_HIP_CHECK(exclusive_scan_i64(hist, 256 * nbd + 1, scan_h, s));
+    CIP_HIP_CHECK(launch_radix_scatter(kin, rin, nruns, 8 * p, hist, kout, rout, s));
+    std::swap(kin, kout);
+    std::swap(rin, rout);
+  }
+  uint64_t* runs = rin;
+  CIP_HIP_CHECK(launch_tile_offsets(kin, nruns, ntiles, tile_runs, s));
   const int64_t* tile_run_off = tile_runs;
-  CIP_ALLOC(runs, uint64_t, "runs", nruns)
   CIP_ALLOC(run_goff, int64_t, "run_goff", nruns + 1)
   CIP_ALLOC(scan_tmp2, int64_t, "scan_tmp2", scan_tmp_elems(nruns + 1))
-  CIP_HIP_CHECK(launch_plan_distribute(nvis, seg_nruns, park_key, park_run, tile_run_off, tile_cursor, runs, s));
   CIP_HIP_CHECK(launch_run_lengths(runs, nruns, run_goff, s));
   CIP_HIP_CHECK(exclusive_scan_i64(run_goff, nruns + 1, scan_tmp2, s));
   CIP_HIP_CHECK(launch_tile_vis(run_goff, tile_run_off, ntiles, tile_vis_off, tile_vis, s));
@@ -413,11 +497,20 @@ static int make_plan(Workspace* ws, const double* uvw, int64_t nrow, const doubl
   const int64_t layer = g.ntx * g.nty;
   CIP_ALLOC(layer_off, int64_t, "layer_off", g.ntw + 1)
   CIP_HIP_CHECK(launch_gather_i64(chunk_off, layer, g.ntw + 1, layer_off, s));
-  int64_t* hl = (int64_t*)pinned(ws, sizeof(int64_t) * (g.ntw + 1));
+  // bank-class ordering windows: the same split with kOrderWindow
+  const bool order = scatter_order();
+  CIP_ALLOC(win_off, int64_t, "win_off", ntiles + 1)
+  if (order) {
+    CIP_HIP_CHECK(launch_chunk_counts(tile_vis, ntiles, kOrderWindow, win_off, s));
+    CIP_HIP_CHECK(exclusive_scan_i64(win_off, ntiles + 1, scan_tmp, s));
+  }
+  int64_t* hl = (int64_t*)pinned(ws, sizeof(int64_t) * (g.ntw + 2));
   if (!hl) return set_error(CIP_ENOMEM, "hipHostMalloc failed");
   CIP_HIP_CHECK(hipMemcpyAsync(hl, layer_off, sizeof(int64_t) * (g.ntw + 1), hipMemcpyDeviceToHost, s));
+  if (order) CIP_HIP_CHECK(hipMemcpyAsync(hl + g.ntw + 1, win_off + ntiles, sizeof(int64_t), hipMemcpyDeviceToHost, s));
   CIP_HIP_CHECK(hipStreamSynchronize(s));
   pr->plane_chunk_off.assign(hl, hl + g.ntw + 1);
+  const int64_t nwin = order ? hl[g.ntw + 1] : 0;
   pr->nchunks = pr->plane_chunk_off.back();
   CIP_ALLOC(chunks, Chunk, "chunks", pr->nchunks)
   CIP_HIP_CHECK(launch_chunk_emit(tile_vis_off, tile_vis, chunk_off, run_goff, tile_runs, ntiles, cv, chunks,
@@ -426,9 +519,12 @@ static int make_plan(Workspace* ws, const double* uvw, int64_t nrow, const doubl
   pr->run_goff = run_goff;
   pr->tile_run_off = tile_runs;
   pr->chunks = chunks;
-  if (scatter_order() && pr->nchunks > 0) {
+  if (order && nwin > 0) {
+    CIP_ALLOC(windows, Chunk, "windows", nwin)
+    CIP_HIP_CHECK(launch_chunk_emit(tile_vis_off, tile_vis, win_off, run_goff, tile_runs, ntiles, kOrderWindow, windows,
+                                    s));
     CIP_ALLOC(perm, uint64_t, "perm", nrow * nchan)
-    CIP_HIP_CHECK(launch_order(vis_class, nchan, runs, run_goff, tile_runs, chunks, pr->nchunks, perm, s));
+    CIP_HIP_CHECK(launch_order(vis_class, nchan, runs, run_goff, nruns, windows, nwin, perm, s));
     pr->perm = perm;
   }
   return CIP_OK;
@@ -457,25 +553,18 @@ static int prepare(Workspace* ws, const double* uvw, int64_t nrow, const double*
   if (nrow < 0 || nchan < 1 || nchan > 65535) return set_error(CIP_EINVAL, "need 1 <= nchan <= 65535, nrow >= 0");
   if (nrow >= ((int64_t)1 << 32)) return set_error(CIP_EINVAL, "nrow must be < 2^32");
   CIP_ALLOC(fx, double, "fx", nchan)
-  CIP_ALLOC(partial, double, "prep_partial", 2 * prep_blocks())
   CIP_ALLOC(red, double, "red", 4)
   CIP_HIP_CHECK(launch_freq_scale(freq, nchan, fx, s));
-  CIP_HIP_CHECK(launch_prep_reduce(vis, vis_dtype, wgt, wgt_dtype, nrow * nchan, partial, prep_blocks(), red, s));
-  hipEvent_t e_prep = g_prof.mark(s);
-  g_prof.span(0, g_prof.pool.empty() ? nullptr : g_prof.pool[0], e_prep);
   double* h = (double*)pinned(ws, sizeof(double) * (4 + (size_t)nchan));
   if (!h) return set_error(CIP_ENOMEM, "hipHostMalloc failed");
-  CIP_HIP_CHECK(hipMemcpyAsync(h, red, 2 * sizeof(double), hipMemcpyDeviceToHost, s));
   CIP_HIP_CHECK(hipMemcpyAsync(h + 4, fx, sizeof(double) * nchan, hipMemcpyDeviceToHost, s));
   CIP_HIP_CHECK(hipStreamSynchronize(s));
-  const double maxabs = h[1];
   double fxmin = h[4], fxmax = h[4];
   for (int64_t c = 1; c < nchan; ++c) {
     fxmin = std::fmin(fxmin, h[4 + c]);
     fxmax = std::fmax(fxmax, h[4 + c]);
   }
   if (!(fxmin > 0.0)) return set_error(CIP_EINVAL, "channel frequencies must be positive");
-  if (!std::isfinite(maxabs)) return set_error(CIP_EINVAL, "non-finite visibility or weight");
   double wmin = 0.0, wmax = 0.0;
   if (do_wstacking && nrow > 0 && given == nullptr) {
     const int nb = 256;
@@ -499,25 +588,31 @@ static int prepare(Workspace* ws, const double* uvw, int64_t nrow, const double*
     if (rc != CIP_OK) return rc;
   }
   out->g = geometry(out->p, px, py);
-  // fixed point: max contribution <= 2^kFixedBits, or 2^kPackedBits for a
-  // full packed chunk (the scatter raises it for shorter chunks)
   if (packed && vis_dtype != CIP_C64)
     return set_error(CIP_EINVAL, "single-precision accumulation needs complex64 visibilities");
   out->packed = packed;
-  int e2 = 0;
-  if (maxabs > 0.0) {
-    std::frexp(maxabs, &e2);  // maxabs < 2^e2
-  }
-  out->fixed_scale = std::ldexp(1.0, (packed ? kPackedBits : kFixedBits) - e2);
+  out->fixed_scale = 1.0;
   out->fx = fx;
   out->red = red;
+  hipEvent_t e_prep = g_prof.mark(s);
+  g_prof.span(0, g_prof.pool.empty() ? nullptr : g_prof.pool[0], e_prep);
   if (nrow == 0) {
+    CIP_HIP_CHECK(hipMemsetAsync(red, 0, 2 * sizeof(double), s));
     out->plan = PlanResult();
     out->plan.plane_chunk_off.assign(out->g.ntw + 1, 0);
     return CIP_OK;
   }
-  const int rc = make_plan(ws, uvw, nrow, fx, nchan, out->g, chunk_vis(packed), s, &out->plan);
+  double maxabs = 0.0;
+  const int rc = make_plan(ws, uvw, nrow, fx, nchan, vis, vis_dtype, wgt, wgt_dtype, red, out->g, chunk_vis(packed),
+                           s, &out->plan, &maxabs);
   g_prof.span(1, e_prep, g_prof.mark(s));
+  if (rc != CIP_OK) return rc;
+  if (!std::isfinite(maxabs)) return set_error(CIP_EINVAL, "non-finite visibility or weight");
+  // fixed point: max contribution <= 2^kFixedBits, or 2^kPackedBits for a
+  // full packed chunk (the scatter raises it for shorter chunks)
+  int e2 = 0;
+  if (maxabs > 0.0) std::frexp(maxabs, &e2);  // maxabs < 2^e2
+  out->fixed_scale = std::ldexp(1.0, (packed ? kPackedBits : kFixedBits) - e2);
   g_prof.counts[0] = nrow * nchan;
   g_prof.counts[1] = out->plan.nruns;
   g_prof.counts[2] = out->plan.nchunks;
@@ -604,23 +699,38 @@ int cip_ms2dirty(const double* uvw, int64_t nrow, const double* freq, int64_t nc
     CIP_HIP_CHECK(hipStreamSynchronize(s));  // host vectors go out of scope
     ws->corr_key = corr_key;
   }
+  // pruned FFT: hand-written row pass keeping the image's npix_y columns,
+  // then hipFFT's column pass on that half (CIP_FFT_PRUNED=0: full 2-D hipFFT)
+  const bool pruned = fft_pruned() && row_fft_supported(g.nv, npix_y);
   hipfftHandle plan;
-  rc = fft_plan(ws, g.nu, g.nv, s, &plan);
-  if (rc != CIP_OK) return rc;
+  double* fft_out = grid;
+  double* tw = nullptr;
+  if (pruned) {
+    rc = fft_col_plan(ws, g.nu, npix_y, s, &plan);
+    if (rc != CIP_OK) return rc;
+    rc = row_fft_twiddles(ws, g.nv, s, &tw);
+    if (rc != CIP_OK) return rc;
+    fft_out = buf<double>(ws, "fft_rows", 2 * g.nu * npix_y);
+    if (!fft_out) return CIP_ENOMEM;
+  } else {
+    rc = fft_plan(ws, g.nu, g.nv, s, &plan);
+    if (rc != CIP_OK) return rc;
+  }
   for (int64_t p = 0; p < g.nplanes; ++p) {
     rc = scatter_plane(pp, p, uvw, vis, vis_dtype, wgt, wgt_dtype, nchan, grid, s);
     if (rc != CIP_OK) return rc;
     hipEvent_t f0 = g_prof.mark(s);
-    if (hipfftExecZ2Z(plan, (hipfftDoubleComplex*)grid, (hipfftDoubleComplex*)grid, HIPFFT_BACKWARD) !=
+    if (pruned) CIP_HIP_CHECK(launch_row_fft(grid, g.nu, g.nv, npix_y, tw, fft_out, s));
+    if (hipfftExecZ2Z(plan, (hipfftDoubleComplex*)fft_out, (hipfftDoubleComplex*)fft_out, HIPFFT_BACKWARD) !=
         HIPFFT_SUCCESS)
       return set_error(CIP_EHIP, "hipfftExecZ2Z failed");
     hipEvent_t f1 = g_prof.mark(s);
     g_prof.span(3, f0, f1);
     if (g.do_wstacking) {
-      CIP_HIP_CHECK(launch_wplane_accumulate(grid, g, npix_x, npix_y, pixsize_x, pixsize_y,
-                                             g.w0 + (double)p * g.dw, p == 0, dirty_out, s));
+      CIP_HIP_CHECK(launch_wplane_accumulate(fft_out, g, npix_x, npix_y, pixsize_x, pixsize_y,
+                                             g.w0 + (double)p * g.dw, p == 0, pruned ? 1 : 0, dirty_out, s));
     } else {
-      CIP_HIP_CHECK(launch_crop_correct_2d(grid, g, npix_x, npix_y, cx, cy, dirty_out, s));
+      CIP_HIP_CHECK(launch_crop_correct_2d(fft_out, g, npix_x, npix_y, cx, cy, pruned ? 1 : 0, dirty_out, s));
     }
     g_prof.span(4, f1, g_prof.mark(s));
   }

@@ -38,8 +38,16 @@ constexpr int kPackedBits = 18;
 constexpr int64_t kChunkVisPacked = 4096;
 constexpr int kChunkVisPackedLog2 = 12;
 
-// Tile edge (grid cells) of the scatter work decomposition.
-constexpr int kTile = 32;
+// Tile edge (grid cells) of the scatter work decomposition (CIP_TILE
+// overrides it in experiment builds, tools/build_variant_full.sh).
+#ifndef CIP_TILE
+#define CIP_TILE 32
+#endif
+constexpr int kTile = CIP_TILE;
+
+// Visibilities per bank-class ordering window (cip_grid.hip order_kernel);
+// divides kChunkVis and kChunkVisPacked so windows never straddle chunks.
+constexpr int kOrderWindow = 1024;
 
 __host__ __device__ inline int64_t floor_div(int64_t a, int64_t b) {
   int64_t q = a / b;
@@ -182,6 +190,27 @@ __device__ __forceinline__ bool place_vis(double u_m, double v_m, double w_m, do
 
 __device__ __forceinline__ int64_t tile_key(int64_t ix0, int64_t iy0, int64_t iw0, const GridGeometry& g) {
   return (iw0 * g.nty + iy0 / kTile) * g.ntx + ix0 / kTile;  // g.tile == kTile
+}
+
+// visibility / weight loads by dtype (CIP_C64 -> float2, CIP_C128 -> double2)
+enum { WK_NONE = 0, WK_F32 = 1, WK_F64 = 2 };
+
+template <int WK>
+__device__ __forceinline__ double load_weight(const void* __restrict__ w, int64_t i) {
+  if constexpr (WK == WK_F32) return (double)((const float*)w)[i];
+  if constexpr (WK == WK_F64) return ((const double*)w)[i];
+  return 1.0;
+}
+
+__device__ __forceinline__ void load_vis(const float2* __restrict__ p, int64_t i, double& re, double& im) {
+  const float2 v = p[i];
+  re = v.x;
+  im = v.y;
+}
+__device__ __forceinline__ void load_vis(const double2* __restrict__ p, int64_t i, double& re, double& im) {
+  const double2 v = p[i];
+  re = v.x;
+  im = v.y;
 }
 
 }  // namespace cip

@@ -21,59 +21,10 @@
 
 namespace cip {
 
-enum { WK_NONE = 0, WK_F32 = 1, WK_F64 = 2 };
-
-template <int WK>
-__device__ __forceinline__ double load_weight(const void* __restrict__ w, int64_t i) {
-  if constexpr (WK == WK_F32) return (double)((const float*)w)[i];
-  if constexpr (WK == WK_F64) return ((const double*)w)[i];
-  return 1.0;
-}
-
-__device__ __forceinline__ void load_vis(const float2* __restrict__ p, int64_t i, double& re, double& im) {
-  const float2 v = p[i];
-  re = v.x;
-  im = v.y;
-}
-__device__ __forceinline__ void load_vis(const double2* __restrict__ p, int64_t i, double& re, double& im) {
-  const double2 v = p[i];
-  re = v.x;
-  im = v.y;
-}
-
 // ------------------------------------------------------ prep reduction ----
 // Sum of weights (the reference's total_weight, invert.py:184) and max |w V|
-// (sets the fixed-point scale). Deterministic: fixed grid-stride assignment and
-// fixed-order tree reductions.
-constexpr int kPrepBlocks = 1024;
-int prep_blocks() { return kPrepBlocks; }
-
-template <typename VisT, int WK>
-__global__ __launch_bounds__(256) void prep_kernel(const VisT* __restrict__ vis, const void* __restrict__ wgt,
-                                                   int64_t n, double* partial) {
-  double sum = 0.0, mx = 0.0;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
-    const double w = load_weight<WK>(wgt, i);
-    double re, im;
-    load_vis(vis, i, re, im);
-    sum += w;
-    mx = fmax(mx, fabs(w) * fmax(fabs(re), fabs(im)));
-  }
-  for (int d = 32; d > 0; d >>= 1) {
-    sum += __shfl_xor(sum, d, 64);
-    mx = fmax(mx, __shfl_xor(mx, d, 64));
-  }
-  __shared__ double ss[4], sm[4];
-  if ((threadIdx.x & 63) == 0) {
-    ss[threadIdx.x >> 6] = sum;
-    sm[threadIdx.x >> 6] = mx;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    partial[2 * blockIdx.x] = (ss[0] + ss[1]) + (ss[2] + ss[3]);
-    partial[2 * blockIdx.x + 1] = fmax(fmax(sm[0], sm[1]), fmax(sm[2], sm[3]));
-  }
-}
+// (sets the fixed-point scale): per-block partials come from the planner's
+// place pass (cip_plan.hip); this reduces them in a fixed order.
 
 __global__ __launch_bounds__(256) void prep_final_kernel(const double* partial, int nblocks, double* out2) {
   double sum = 0.0, mx = 0.0;
@@ -97,21 +48,7 @@ __global__ __launch_bounds__(256) void prep_final_kernel(const double* partial, 
   }
 }
 
-hipError_t launch_prep_reduce(const void* vis, int vis_dtype, const void* wgt, int wgt_dtype, int64_t n,
-                              double* partial, int nblocks, double* out2, hipStream_t s) {
-#define PREP(VT, WKV) prep_kernel<VT, WKV><<<dim3(nblocks), dim3(256), 0, s>>>((const VT*)vis, wgt, n, partial)
-  if (vis_dtype == CIP_C64) {
-    if (wgt_dtype == CIP_F32) PREP(float2, WK_F32);
-    else if (wgt_dtype == CIP_F64) PREP(float2, WK_F64);
-    else PREP(float2, WK_NONE);
-  } else {
-    if (wgt_dtype == CIP_F32) PREP(double2, WK_F32);
-    else if (wgt_dtype == CIP_F64) PREP(double2, WK_F64);
-    else PREP(double2, WK_NONE);
-  }
-#undef PREP
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return e;
+hipError_t launch_prep_final(const double* partial, int nblocks, double* out2, hipStream_t s) {
   prep_final_kernel<<<dim3(1), dim3(256), 0, s>>>(partial, nblocks, out2);
   return hipGetLastError();
 }
@@ -268,94 +205,111 @@ __device__ __forceinline__ void grid_fetched(const VisFetch& f, const GridGeomet
 constexpr int kOrderThreads = 256;
 constexpr int kOrderPer = 4;
 constexpr int kOrderBatch = kOrderThreads * kOrderPer;
+static_assert(kOrderBatch == kOrderWindow, "one order block per window");
 
-__global__ __launch_bounds__(kOrderThreads) void order_kernel(const uint8_t* __restrict__ vis_class, int64_t nchan,
-                                                              const uint64_t* __restrict__ runs,
-                                                              const int64_t* __restrict__ run_goff,
-                                                              const int64_t* __restrict__ tile_run_off,
-                                                              const Chunk* __restrict__ chunks,
-                                                              uint64_t* __restrict__ perm) {
-  __shared__ __attribute__((aligned(16))) unsigned s_cnt[32];
-  __shared__ unsigned s_S[kOrderBatch], s_M[kOrderBatch];
-  // the row slices overlapping the current window (a window of kOrderBatch
-  // positions meets at most kOrderBatch of them)
-  __shared__ int64_t s_voff[kOrderBatch + 1];
-  __shared__ uint64_t s_run[kOrderBatch];
-  __shared__ uint64_t s_vis[kOrderBatch];  // window position -> (row << 16) | channel
-  __shared__ int s_next;
-  const Chunk ch = chunks[blockIdx.x];
-  const int64_t r1 = tile_run_off[ch.tile + 1];
-  int64_t r = ch.first_run;  // first slice overlapping the window
-  for (int64_t sb = ch.g0; sb < ch.g1; sb += kOrderBatch) {
-    const int nsb = (int)((ch.g1 - sb) < kOrderBatch ? (ch.g1 - sb) : kOrderBatch);
-    const int nst = (int)((r1 - r) < kOrderBatch ? (r1 - r) : kOrderBatch);
-    __syncthreads();
-    for (int k = threadIdx.x; k <= nst; k += kOrderThreads) {
-      s_voff[k] = run_goff[r + k];
-      if (k < nst) s_run[k] = runs[r + k];
+// Expansion: each wave takes 64 consecutive row slices (tile order, so their
+// visibilities are one contiguous range of the list), parks them in LDS and
+// writes that range with coalesced stores, each lane finding its slice by a
+// 6-step binary search: records (class << 48) | (row << 16) | channel.
+__global__ __launch_bounds__(256) void expand_kernel(const uint8_t* __restrict__ vis_class, int64_t nchan,
+                                                     const uint64_t* __restrict__ runs,
+                                                     const int64_t* __restrict__ run_goff, int64_t nruns,
+                                                     uint64_t* __restrict__ list) {
+  __shared__ int64_t s_g0[4][64];
+  __shared__ uint64_t s_rec[4][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t ngroups = (nruns + 63) / 64;
+  for (int64_t grp = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6; grp < ngroups;
+       grp += ((int64_t)gridDim.x * 256) >> 6) {
+    const int64_t r0 = grp * 64;
+    const int n = (int)((nruns - r0) < 64 ? (nruns - r0) : 64);
+    if (lane < n) {
+      s_g0[wave][lane] = run_goff[r0 + lane];
+      s_rec[wave][lane] = runs[r0 + lane];
     }
-    if (threadIdx.x < 32) s_cnt[threadIdx.x] = 0u;
-    if (threadIdx.x == 0) s_next = nst;
-    __syncthreads();
-    // expand the staged slices over the window; the next window starts in
-    // the slice holding position sb + nsb
-    for (int k = threadIdx.x; k < nst; k += kOrderThreads) {
-      const int64_t a = s_voff[k], b = s_voff[k + 1];
-      if (a <= sb + nsb && b > sb + nsb) s_next = k;
-      const int64_t lo = a > sb ? a : sb, hi = b < sb + nsb ? b : sb + nsb;
-      const uint64_t rec = s_run[k];
-      const uint64_t base = ((rec >> 32) << 16) + ((rec >> 16) & 0xffff) - (uint64_t)a;
-      for (int64_t q = lo; q < hi; ++q) s_vis[q - sb] = base + (uint64_t)q;
-    }
-    __syncthreads();
-    uint64_t packed[kOrderPer];
-    unsigned cls[kOrderPer], rk[kOrderPer];
-#pragma unroll
-    for (int k = 0; k < kOrderPer; ++k) {
-      const int qi = threadIdx.x + k * kOrderThreads;
-      cls[k] = 32u;
-      if (qi < nsb) {
-        packed[k] = s_vis[qi];
-        cls[k] = vis_class[(int64_t)(packed[k] >> 16) * nchan + (int64_t)(packed[k] & 0xffff)];
-        rk[k] = atomicAdd(&s_cnt[cls[k]], 1u);
+    const int64_t G0 = run_goff[r0], G1 = run_goff[r0 + n];
+    __builtin_amdgcn_wave_barrier();
+    for (int64_t q = G0 + lane; q < G1; q += 64) {
+      int lo = 0, hi = n - 1;
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (s_g0[wave][mid] <= q) lo = mid;
+        else hi = mid - 1;
       }
+      const uint64_t rec = s_rec[wave][lo];
+      const int64_t row = (int64_t)(rec >> 32);
+      const int64_t c = (int64_t)((rec >> 16) & 0xffff) + (q - s_g0[wave][lo]);
+      list[q] = ((uint64_t)vis_class[row * nchan + c] << 48) | ((uint64_t)row << 16) | (uint64_t)c;
     }
-    __syncthreads();
-    unsigned cnt[32], maxcnt = 0;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const uint4 c4 = reinterpret_cast<const uint4*>(s_cnt)[i];
-      cnt[4 * i] = c4.x;
-      cnt[4 * i + 1] = c4.y;
-      cnt[4 * i + 2] = c4.z;
-      cnt[4 * i + 3] = c4.w;
-    }
-#pragma unroll
-    for (int i = 0; i < 32; ++i) maxcnt = cnt[i] > maxcnt ? cnt[i] : maxcnt;
-    for (unsigned r = threadIdx.x; r < maxcnt; r += kOrderThreads) {
-      unsigned S = 0, M = 0;
-#pragma unroll
-      for (int c2 = 0; c2 < 32; ++c2) {
-        S += cnt[c2] < r ? cnt[c2] : r;
-        M |= (cnt[c2] > r ? 1u : 0u) << c2;
-      }
-      s_S[r] = S;
-      s_M[r] = M;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < kOrderPer; ++k)
-      if (cls[k] < 32u) perm[sb + s_S[rk[k]] + __popc(s_M[rk[k]] & ((1u << cls[k]) - 1u))] = packed[k];
-    r += s_next;
+    __builtin_amdgcn_wave_barrier();
   }
 }
 
+// Window sort, in place: one block per window of <= kOrderWindow list
+// positions; the perm records keep (row << 16) | channel.
+__global__ __launch_bounds__(kOrderThreads) void order_kernel(const Chunk* __restrict__ windows,
+                                                              uint64_t* __restrict__ list) {
+  __shared__ __attribute__((aligned(16))) unsigned s_cnt[32];
+  __shared__ unsigned s_S[kOrderBatch], s_M[kOrderBatch];
+  const Chunk ch = windows[blockIdx.x];
+  const int64_t sb = ch.g0;
+  const int nsb = (int)(ch.g1 - ch.g0);
+  if (threadIdx.x < 32) s_cnt[threadIdx.x] = 0u;
+  uint64_t packed[kOrderPer];
+#pragma unroll
+  for (int k = 0; k < kOrderPer; ++k) {
+    const int qi = threadIdx.x + k * kOrderThreads;
+    packed[k] = qi < nsb ? list[sb + qi] : 0ull;
+  }
+  __syncthreads();
+  unsigned cls[kOrderPer], rk[kOrderPer];
+#pragma unroll
+  for (int k = 0; k < kOrderPer; ++k) {
+    const int qi = threadIdx.x + k * kOrderThreads;
+    cls[k] = 32u;
+    if (qi < nsb) {
+      cls[k] = (unsigned)(packed[k] >> 48) & 31u;
+      rk[k] = atomicAdd(&s_cnt[cls[k]], 1u);
+    }
+  }
+  __syncthreads();
+  unsigned cnt[32], maxcnt = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const uint4 c4 = reinterpret_cast<const uint4*>(s_cnt)[i];
+    cnt[4 * i] = c4.x;
+    cnt[4 * i + 1] = c4.y;
+    cnt[4 * i + 2] = c4.z;
+    cnt[4 * i + 3] = c4.w;
+  }
+#pragma unroll
+  for (int i = 0; i < 32; ++i) maxcnt = cnt[i] > maxcnt ? cnt[i] : maxcnt;
+  for (unsigned r = threadIdx.x; r < maxcnt; r += kOrderThreads) {
+    unsigned S = 0, M = 0;
+#pragma unroll
+    for (int c2 = 0; c2 < 32; ++c2) {
+      S += cnt[c2] < r ? cnt[c2] : r;
+      M |= (cnt[c2] > r ? 1u : 0u) << c2;
+    }
+    s_S[r] = S;
+    s_M[r] = M;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < kOrderPer; ++k)
+    if (cls[k] < 32u)
+      list[sb + s_S[rk[k]] + __popc(s_M[rk[k]] & ((1u << cls[k]) - 1u))] = packed[k] & 0xffffffffffffull;
+}
+
 hipError_t launch_order(const uint8_t* vis_class, int64_t nchan, const uint64_t* runs, const int64_t* run_goff,
-                        const int64_t* tile_run_off, const Chunk* chunks, int64_t nchunks, uint64_t* perm,
-                        hipStream_t s) {
-  if (nchunks <= 0) return hipSuccess;
-  order_kernel<<<dim3((unsigned)nchunks), dim3(kOrderThreads), 0, s>>>(vis_class, nchan, runs, run_goff, tile_run_off,
-                                                                      chunks, perm);
+                        int64_t nruns, const Chunk* windows, int64_t nwindows, uint64_t* perm, hipStream_t s) {
+  if (nwindows <= 0) return hipSuccess;
+  int64_t nb = (nruns + 255) / 256;
+  if (nb > 16384) nb = 16384;
+  expand_kernel<<<dim3((unsigned)nb), dim3(256), 0, s>>>(vis_class, nchan, runs, run_goff, nruns, perm);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  order_kernel<<<dim3((unsigned)nwindows), dim3(kOrderThreads), 0, s>>>(windows, perm);
   return hipGetLastError();
 }
 
@@ -548,22 +502,28 @@ hipError_t launch_scatter(int support, int vis_dtype, int wgt_dtype, bool packed
 // ---------------------------------------------------- post-FFT kernels ----
 // dirty[i, j] = (-1)^(p+q) Re G^[p mod nu, q mod nv] * cx[i] * cy[j],
 // p = i - npix_x/2, q = j - npix_y/2; cx, cy = 1 / F(p/nu), 1 / F(q/nv).
+// pruned: the FFT output holds only the image's columns, (nu, ny) row-major
+// with column j <-> q (cip_fft.hip); else the full (nu, nv) transform
+__device__ __forceinline__ int64_t fft_index(int64_t ip, int64_t iq, int64_t j, int64_t nv, int64_t ny, int pruned) {
+  return pruned ? ip * ny + j : ip * nv + iq;
+}
+
 __global__ void crop_correct_2d_kernel(const double2* __restrict__ grid, int64_t nu, int64_t nv, int64_t nx,
                                        int64_t ny, const double* __restrict__ cx, const double* __restrict__ cy,
-                                       double* __restrict__ dirty) {
+                                       int pruned, double* __restrict__ dirty) {
   const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t i = blockIdx.y;
   if (j >= ny) return;
   const int64_t p = i - nx / 2, q = j - ny / 2;
   const int64_t ip = (p + nu) % nu, iq = (q + nv) % nv;
   const double sgn = ((p + q) & 1) ? -1.0 : 1.0;
-  dirty[i * ny + j] = sgn * grid[ip * nv + iq].x * cx[i] * cy[j];
+  dirty[i * ny + j] = sgn * grid[fft_index(ip, iq, j, nv, ny, pruned)].x * cx[i] * cy[j];
 }
 
 hipError_t launch_crop_correct_2d(const double* grid, const GridGeometry& g, int64_t npix_x, int64_t npix_y,
-                                  const double* cx, const double* cy, double* dirty, hipStream_t s) {
+                                  const double* cx, const double* cy, int pruned, double* dirty, hipStream_t s) {
   crop_correct_2d_kernel<<<dim3((unsigned)((npix_y + 255) / 256), (unsigned)npix_x), dim3(256), 0, s>>>(
-      (const double2*)grid, g.nu, g.nv, npix_x, npix_y, cx, cy, dirty);
+      (const double2*)grid, g.nu, g.nv, npix_x, npix_y, cx, cy, pruned, dirty);
   return hipGetLastError();
 }
 
@@ -576,7 +536,7 @@ __device__ __forceinline__ double nm1_of(int64_t i, int64_t j, int64_t nx, int64
 
 // acc[i, j] (+)= (-1)^(p+q) Re(G^_p[..] exp(-2 pi i w_p (n - 1)))
 __global__ void wplane_accumulate_kernel(const double2* __restrict__ grid, int64_t nu, int64_t nv, int64_t nx,
-                                         int64_t ny, double px, double py, double w_plane, int first,
+                                         int64_t ny, double px, double py, double w_plane, int first, int pruned,
                                          double* __restrict__ acc) {
   const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t i = blockIdx.y;
@@ -587,17 +547,17 @@ __global__ void wplane_accumulate_kernel(const double2* __restrict__ grid, int64
   const double nm1 = nm1_of(i, j, nx, ny, px, py);
   double sn, cs;
   sincospi(-2.0 * w_plane * nm1, &sn, &cs);
-  const double2 gval = grid[ip * nv + iq];
+  const double2 gval = grid[fft_index(ip, iq, j, nv, ny, pruned)];
   const double val = sgn * (gval.x * cs - gval.y * sn);
   if (first) acc[i * ny + j] = val;
   else acc[i * ny + j] += val;
 }
 
 hipError_t launch_wplane_accumulate(const double* grid, const GridGeometry& g, int64_t npix_x, int64_t npix_y,
-                                    double pixsize_x, double pixsize_y, double w_plane, int first, double* acc,
-                                    hipStream_t s) {
+                                    double pixsize_x, double pixsize_y, double w_plane, int first, int pruned,
+                                    double* acc, hipStream_t s) {
   wplane_accumulate_kernel<<<dim3((unsigned)((npix_y + 255) / 256), (unsigned)npix_x), dim3(256), 0, s>>>(
-      (const double2*)grid, g.nu, g.nv, npix_x, npix_y, pixsize_x, pixsize_y, w_plane, first, acc);
+      (const double2*)grid, g.nu, g.nv, npix_x, npix_y, pixsize_x, pixsize_y, w_plane, first, pruned, acc);
   return hipGetLastError();
 }
 

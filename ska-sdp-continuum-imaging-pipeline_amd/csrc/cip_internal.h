@@ -31,14 +31,26 @@ hipError_t launch_freq_scale(const double* freq, int64_t nchan, double* fx, hipS
 // per-row w range over channels (only f min/max matter): out[0]=min, out[1]=max
 hipError_t launch_w_range(const double* uvw, int64_t nrow, double fxmin, double fxmax, double* partial,
                           int nblocks, hipStream_t s);
-// place pass: runs per tile (atomics), per-visibility bank class, parked runs
-// (park_* hold 64 slots per 64-visibility segment, seg_nruns the used ones)
+// place pass: per-visibility bank class, runs parked with their tile keys
+// (park_* hold 64 slots per 64-visibility segment, seg_nruns[seg] the used
+// ones), and per-block {sum w, max |w V|} partials (2 * plan_place_blocks(n)).
+// err_flag: bit 0 non-finite uvw / w off the stack, bit 1 non-finite vis or weight.
+int plan_place_blocks(int64_t nvis);
 hipError_t launch_plan_place(const double* uvw, int64_t nrow, const double* fx, int64_t nchan,
-                             const GridGeometry& g, int64_t* tile_runs, unsigned* err_flag, uint8_t* vis_class,
-                             uint8_t* seg_nruns, int64_t* park_key, uint64_t* park_run, hipStream_t s);
-hipError_t launch_plan_distribute(int64_t nvis, const uint8_t* seg_nruns, const int64_t* park_key,
-                                  const uint64_t* park_run, const int64_t* tile_run_off, int64_t* tile_cursor,
-                                  uint64_t* runs, hipStream_t s);
+                             const void* vis, int vis_dtype, const void* wgt, int wgt_dtype, const GridGeometry& g,
+                             unsigned* err_flag, uint8_t* vis_class, int64_t* seg_nruns, uint32_t* park_key,
+                             uint64_t* park_run, double* partial, hipStream_t s);
+// parked runs -> dense (seg_off: exclusive scan of seg_nruns, nseg + 1 entries)
+hipError_t launch_compact_runs(int64_t nseg, const int64_t* seg_off, const uint32_t* park_key,
+                               const uint64_t* park_run, uint32_t* key_out, uint64_t* run_out, hipStream_t s);
+// one stable LSD radix sort pass on digit (key >> shift) & 255. hist holds
+// 256 * radix_blocks(n) + 1 entries, exclusive-scanned between the two calls.
+int64_t radix_blocks(int64_t n);
+hipError_t launch_radix_hist(const uint32_t* keys, int64_t n, int shift, int64_t* hist, hipStream_t s);
+hipError_t launch_radix_scatter(const uint32_t* keys, const uint64_t* vals, int64_t n, int shift,
+                                const int64_t* hist, uint32_t* keys_out, uint64_t* vals_out, hipStream_t s);
+hipError_t launch_tile_offsets(const uint32_t* keys, int64_t nruns, int64_t ntiles, int64_t* tile_run_off,
+                               hipStream_t s);
 hipError_t launch_tile_vis(const int64_t* run_goff, const int64_t* tile_run_off, int64_t ntiles,
                            int64_t* tile_vis_off, int64_t* tile_vis, hipStream_t s);
 hipError_t launch_run_lengths(const uint64_t* runs, int64_t nruns, int64_t* out, hipStream_t s);
@@ -51,10 +63,8 @@ hipError_t launch_gather_i64(const int64_t* src, int64_t stride, int64_t count, 
                              hipStream_t s);
 
 // ---- gridding (cip_grid.hip) -----------------------------------------------
-// vis_dtype/wgt_dtype: CIP_* codes. partial needs 2 * nblocks doubles.
-hipError_t launch_prep_reduce(const void* vis, int vis_dtype, const void* wgt, int wgt_dtype, int64_t n,
-                              double* partial, int nblocks, double* out2, hipStream_t s);
-int prep_blocks();
+// out2 = {sum, max} of the place pass's 2 * nblocks partials
+hipError_t launch_prep_final(const double* partial, int nblocks, double* out2, hipStream_t s);
 // packed: single-precision class (re/im packed in one 64-bit integer), complex64
 // only. perm: bank-class ordered stream from launch_order, or NULL (visibilities
 // located through the tile's row slices in tile order).
@@ -64,17 +74,28 @@ hipError_t launch_scatter(int support, int vis_dtype, int wgt_dtype, bool packed
                           const Chunk* chunks, int64_t chunk_begin, int64_t nchunks, const GridGeometry& g,
                           int64_t plane, double fixed_scale, double* grid, hipStream_t s);
 // perm[g] for every tile-order position g of every chunk (cip_grid.hip)
+// perm (nvis records): the tile-order visibilities as (row << 16) | channel,
+// bank-class sorted within each window (the tiles split into <= kOrderWindow
+// pieces by chunk_emit with cv = kOrderWindow)
 hipError_t launch_order(const uint8_t* vis_class, int64_t nchan, const uint64_t* runs, const int64_t* run_goff,
-                        const int64_t* tile_run_off, const Chunk* chunks, int64_t nchunks, uint64_t* perm,
-                        hipStream_t s);
+                        int64_t nruns, const Chunk* windows, int64_t nwindows, uint64_t* perm, hipStream_t s);
+// pruned != 0: grid is the (nu, npix_y) output of the pruned FFT (launch_row_fft
+// + column pass), else the full (nu, nv) transform
 hipError_t launch_crop_correct_2d(const double* grid, const GridGeometry& g, int64_t npix_x, int64_t npix_y,
-                                  const double* cx, const double* cy, double* dirty, hipStream_t s);
+                                  const double* cx, const double* cy, int pruned, double* dirty, hipStream_t s);
 hipError_t launch_wplane_accumulate(const double* grid, const GridGeometry& g, int64_t npix_x, int64_t npix_y,
-                                    double pixsize_x, double pixsize_y, double w_plane, int first,
+                                    double pixsize_x, double pixsize_y, double w_plane, int first, int pruned,
                                     double* acc, hipStream_t s);
 hipError_t launch_wfinal_correct(double* acc, int64_t npix_x, int64_t npix_y, double pixsize_x, double pixsize_y,
                                  const double* cx, const double* cy, const double* fw_table, int64_t fw_n,
                                  double fw_dnu, double dw, hipStream_t s);
+
+// ---- pruned row FFT (cip_fft.hip) ------------------------------------------
+// out[x, j] = sum_y grid[x, y] exp(+2 pi i y (j - ny/2) / nv) for j < ny;
+// twiddles: exp(+2 pi i m / nv), m < nv (interleaved re, im).
+bool row_fft_supported(int64_t nv, int64_t ny);
+hipError_t launch_row_fft(const double* grid, int64_t nu, int64_t nv, int64_t ny, const double* twiddles,
+                          double* out, hipStream_t s);
 
 // ---- reference tiling + Stokes I (cip_tiling.hip) --------------------------
 hipError_t launch_tile_run_count(const double* uvw, int64_t nrow, const double* winv, int64_t nchan,

@@ -132,18 +132,25 @@ hipError_t launch_w_range(const double* uvw, int64_t nrow, double fxmin, double 
 // (or at a row start or the wave's first lane), and the run ends at the next
 // start in the wave (ballot), so runs are split at 64-visibility segment
 // boundaries. The place pass is the only one that places visibilities: it
-// counts runs per tile (one global atomic per run), parks each run in its
-// segment's slots of a scratch array and records every visibility's LDS bank
-// class for the order pass; the distribute pass moves the parked runs into
-// their tile buckets.
+// parks each run with its tile key in its segment's slots of a scratch array
+// and records every visibility's LDS bank class for the order pass. The runs
+// are then bucketed by tile with a stable LSD radix sort (8-bit digits, no
+// global atomics: scattered device-scope atomics execute at the memory side
+// at ~10-25 G/s on MI355X, which made an atomic counting sort of the 13 M
+// runs of C3 cost more than 1 ms).
+template <typename VisT, int WK>
 __global__ __launch_bounds__(256) void plan_place_kernel(const double* __restrict__ uvw, int64_t nrow,
                                                          const double* __restrict__ fx, int64_t nchan,
-                                                         GridGeometry g, int64_t* tile_runs, unsigned* err_flag,
+                                                         const VisT* __restrict__ vis, const void* __restrict__ wgt,
+                                                         GridGeometry g, unsigned* err_flag,
                                                          uint8_t* __restrict__ vis_class,
-                                                         uint8_t* __restrict__ seg_nruns,
-                                                         int64_t* __restrict__ park_key,
-                                                         uint64_t* __restrict__ park_run) {
+                                                         int64_t* __restrict__ seg_nruns,
+                                                         uint32_t* __restrict__ park_key,
+                                                         uint64_t* __restrict__ park_run, double* partial) {
   const int lane = threadIdx.x & 63;
+  // fused prep reduction (sum of weights, max |w V|), fixed order
+  double wsum = 0.0, wvmax = 0.0;
+  bool nonfinite = false;
   const int64_t nvis = nrow * nchan;
   const int64_t nseg = (nvis + 63) / 64;
   const int P = kTile + g.support - 1;
@@ -154,6 +161,14 @@ __global__ __launch_bounds__(256) void plan_place_kernel(const double* __restric
     int64_t key = -1, r = 0, c = 0;
     bool bad = false;
     if (valid) {
+      const double wt = load_weight<WK>(wgt, i);
+      double vr, vi;
+      load_vis(vis, i, vr, vi);
+      // zero-weight visibilities are skipped by the scatter, whatever they hold
+      const double a = wt == 0.0 ? 0.0 : fabs(wt) * fmax(fabs(vr), fabs(vi));
+      nonfinite = nonfinite || (wt != 0.0 && !(isfinite(wt) && isfinite(vr) && isfinite(vi)));
+      wsum += wt;
+      wvmax = fmax(wvmax, a);
       // i / nchan through fp64 (exact after one correction for i < 2^52)
       r = (int64_t)((double)i / (double)nchan);
       c = i - r * nchan;
@@ -181,31 +196,29 @@ __global__ __launch_bounds__(256) void plan_place_kernel(const double* __restric
     const bool emit = start && key >= 0;
     const unsigned long long emits = __ballot(emit);
     const int nvalid = __popcll(__ballot(valid));  // wave-uniform: outside the branch
-    if (lane == 0) seg_nruns[seg] = (uint8_t)__popcll(emits);
+    if (lane == 0) seg_nruns[seg] = __popcll(emits);
     if (emit) {
       const unsigned long long above = starts & ~((2ull << lane) - 1ull);  // lane 63: 2 << 63 == 0
       const int next = above ? (__ffsll((long long)above) - 1) : nvalid;
       const int slot = __popcll(emits & ((1ull << lane) - 1ull));
-      park_key[seg * 64 + slot] = key;
+      park_key[seg * 64 + slot] = (uint32_t)key;
       park_run[seg * 64 + slot] = ((uint64_t)r << 32) | ((uint64_t)c << 16) | (uint64_t)(c + (next - lane));
-      atomicAdd((unsigned long long*)&tile_runs[key], 1ull);
     }
   }
-}
-
-__global__ __launch_bounds__(256) void plan_distribute_kernel(int64_t nseg, const uint8_t* __restrict__ seg_nruns,
-                                                              const int64_t* __restrict__ park_key,
-                                                              const uint64_t* __restrict__ park_run,
-                                                              const int64_t* __restrict__ tile_run_off,
-                                                              int64_t* tile_cursor, uint64_t* __restrict__ runs) {
-  const int lane = threadIdx.x & 63;
-  for (int64_t seg = ((int64_t)blockIdx.x * 256 + threadIdx.x) / 64; seg < nseg;
-       seg += (int64_t)gridDim.x * 4) {
-    if (lane < (int)seg_nruns[seg]) {
-      const int64_t key = park_key[seg * 64 + lane];
-      const int64_t pos = tile_run_off[key] + atomicAdd((unsigned long long*)&tile_cursor[key], 1ull);
-      runs[pos] = park_run[seg * 64 + lane];
-    }
+  if (nonfinite) atomicOr(err_flag, 2u);
+  for (int d = 32; d > 0; d >>= 1) {
+    wsum += __shfl_xor(wsum, d, 64);
+    wvmax = fmax(wvmax, __shfl_xor(wvmax, d, 64));
+  }
+  __shared__ double ss[4], sm[4];
+  if (lane == 0) {
+    ss[threadIdx.x >> 6] = wsum;
+    sm[threadIdx.x >> 6] = wvmax;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    partial[2 * blockIdx.x] = (ss[0] + ss[1]) + (ss[2] + ss[3]);
+    partial[2 * blockIdx.x + 1] = fmax(fmax(sm[0], sm[1]), fmax(sm[2], sm[3]));
   }
 }
 
@@ -215,20 +228,185 @@ static unsigned plan_blocks(int64_t nvis) {
   return (unsigned)(b < 16384 ? (b > 0 ? b : 1) : 16384);
 }
 
+int plan_place_blocks(int64_t nvis) { return (int)plan_blocks(nvis); }
+
 hipError_t launch_plan_place(const double* uvw, int64_t nrow, const double* fx, int64_t nchan,
-                             const GridGeometry& g, int64_t* tile_runs, unsigned* err_flag, uint8_t* vis_class,
-                             uint8_t* seg_nruns, int64_t* park_key, uint64_t* park_run, hipStream_t s) {
-  plan_place_kernel<<<dim3(plan_blocks(nrow * nchan)), dim3(256), 0, s>>>(uvw, nrow, fx, nchan, g, tile_runs, err_flag,
-                                                                         vis_class, seg_nruns, park_key, park_run);
+                             const void* vis, int vis_dtype, const void* wgt, int wgt_dtype, const GridGeometry& g,
+                             unsigned* err_flag, uint8_t* vis_class, int64_t* seg_nruns, uint32_t* park_key,
+                             uint64_t* park_run, double* partial, hipStream_t s) {
+  const dim3 gd(plan_blocks(nrow * nchan));
+#define PLACE(VT, WKV)                                                                                           \
+  plan_place_kernel<VT, WKV><<<gd, dim3(256), 0, s>>>(uvw, nrow, fx, nchan, (const VT*)vis, wgt, g, err_flag,  \
+                                                      vis_class, seg_nruns, park_key, park_run, partial)
+  if (vis_dtype == CIP_C64) {
+    if (wgt_dtype == CIP_F32) PLACE(float2, WK_F32);
+    else if (wgt_dtype == CIP_F64) PLACE(float2, WK_F64);
+    else PLACE(float2, WK_NONE);
+  } else {
+    if (wgt_dtype == CIP_F32) PLACE(double2, WK_F32);
+    else if (wgt_dtype == CIP_F64) PLACE(double2, WK_F64);
+    else PLACE(double2, WK_NONE);
+  }
+#undef PLACE
   return hipGetLastError();
 }
 
-hipError_t launch_plan_distribute(int64_t nvis, const uint8_t* seg_nruns, const int64_t* park_key,
-                                  const uint64_t* park_run, const int64_t* tile_run_off, int64_t* tile_cursor,
-                                  uint64_t* runs, hipStream_t s) {
-  const int64_t nseg = (nvis + 63) / 64;
-  plan_distribute_kernel<<<dim3(plan_blocks(nvis)), dim3(256), 0, s>>>(nseg, seg_nruns, park_key, park_run,
-                                                                      tile_run_off, tile_cursor, runs);
+// ---------------------------------------------------------- radix sort ----
+// Stable LSD radix sort of (uint32 key, uint64 run) pairs, 8-bit digits.
+// A block ranks 4096 items (16 per thread, striped: item k * 256 + tid, all
+// loaded up front), so item order within a block is (k, tid) = input order.
+// Per k each wave ranks its 64 items by digit with 8 ballots (peer mask), the
+// waves' digit counts meet in LDS, and a running per-digit offset carries
+// across k. Global bases come from the exclusive scan of the digit-major
+// histogram hist[d * nblocks + b] (plus one trailing entry: after the scan it
+// holds the item count).
+constexpr int kRadixThreads = 256;
+constexpr int kRadixPer = 16;
+constexpr int64_t kRadixBlock = (int64_t)kRadixThreads * kRadixPer;
+
+__global__ __launch_bounds__(kRadixThreads) void radix_hist_kernel(const uint32_t* __restrict__ keys, int64_t n,
+                                                                   int shift, int64_t nblocks,
+                                                                   int64_t* __restrict__ hist) {
+  __shared__ unsigned cnt[256];
+  cnt[threadIdx.x] = 0u;
+  __syncthreads();
+  const int64_t i0 = (int64_t)blockIdx.x * kRadixBlock + threadIdx.x;
+#pragma unroll
+  for (int k = 0; k < kRadixPer; ++k) {
+    const int64_t i = i0 + (int64_t)k * kRadixThreads;
+    if (i < n) atomicAdd(&cnt[(keys[i] >> shift) & 255u], 1u);
+  }
+  __syncthreads();
+  hist[(int64_t)threadIdx.x * nblocks + blockIdx.x] = cnt[threadIdx.x];
+  if (blockIdx.x == 0 && threadIdx.x == 0) hist[256 * nblocks] = 0;
+}
+
+__global__ __launch_bounds__(kRadixThreads) void radix_scatter_kernel(
+    const uint32_t* __restrict__ keys, const uint64_t* __restrict__ vals, int64_t n, int shift, int64_t nblocks,
+    const int64_t* __restrict__ hist, uint32_t* __restrict__ keys_out, uint64_t* __restrict__ vals_out) {
+  __shared__ unsigned wcnt[4][256];  // per-wave digit counts of the current k
+  __shared__ int64_t base[256];      // global base + running offset per digit
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t i0 = (int64_t)blockIdx.x * kRadixBlock + threadIdx.x;
+  uint32_t key[kRadixPer];
+  uint64_t val[kRadixPer];
+#pragma unroll
+  for (int k = 0; k < kRadixPer; ++k) {
+    const int64_t i = i0 + (int64_t)k * kRadixThreads;
+    key[k] = i < n ? keys[i] : 0u;
+    val[k] = i < n ? vals[i] : 0ull;
+  }
+  base[threadIdx.x] = hist[(int64_t)threadIdx.x * nblocks + blockIdx.x];
+#pragma unroll
+  for (int k = 0; k < kRadixPer; ++k) {
+    const bool valid = i0 + (int64_t)k * kRadixThreads < n;
+    const unsigned d = (key[k] >> shift) & 255u;
+    unsigned long long peers = __ballot(valid);
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+      const bool bit = (d >> b) & 1u;
+      const unsigned long long m = __ballot(bit);
+      peers &= bit ? m : ~m;
+    }
+    const unsigned rank = (unsigned)__popcll(peers & ((1ull << lane) - 1ull));
+    wcnt[0][threadIdx.x] = 0u;
+    wcnt[1][threadIdx.x] = 0u;
+    wcnt[2][threadIdx.x] = 0u;
+    wcnt[3][threadIdx.x] = 0u;
+    __syncthreads();
+    if (valid && rank == 0) wcnt[wave][d] = (unsigned)__popcll(peers);
+    __syncthreads();
+    // wave prefix per digit; the running base advances by the k-step total
+    const unsigned c0 = wcnt[0][threadIdx.x], c1 = wcnt[1][threadIdx.x], c2 = wcnt[2][threadIdx.x],
+                   c3 = wcnt[3][threadIdx.x];
+    wcnt[0][threadIdx.x] = 0u;
+    wcnt[1][threadIdx.x] = c0;
+    wcnt[2][threadIdx.x] = c0 + c1;
+    wcnt[3][threadIdx.x] = c0 + c1 + c2;
+    const int64_t b0 = base[threadIdx.x];
+    __syncthreads();
+    if (valid) {
+      const int64_t pos = base[d] + wcnt[wave][d] + rank;
+      keys_out[pos] = key[k];
+      vals_out[pos] = val[k];
+    }
+    __syncthreads();
+    base[threadIdx.x] = b0 + c0 + c1 + c2 + c3;
+  }
+}
+
+// the parked runs of each segment -> dense arrays at the scanned offsets
+__global__ void compact_runs_kernel(int64_t nseg, const int64_t* __restrict__ seg_off,
+                                    const uint32_t* __restrict__ park_key, const uint64_t* __restrict__ park_run,
+                                    uint32_t* __restrict__ key_out, uint64_t* __restrict__ run_out) {
+  // one wave per 4 segments (loads of all four issued together), grid-stride
+  const int j = threadIdx.x & 63;
+  for (int64_t seg0 = (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6) * 4; seg0 < nseg;
+       seg0 += (((int64_t)gridDim.x * blockDim.x) >> 6) * 4) {
+    int64_t o[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) o[k] = seg_off[seg0 + k < nseg ? seg0 + k : nseg];
+    uint32_t kk[4];
+    uint64_t rr[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const bool v = j < o[k + 1] - o[k];
+      kk[k] = v ? park_key[(seg0 + k) * 64 + j] : 0u;
+      rr[k] = v ? park_run[(seg0 + k) * 64 + j] : 0ull;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (j < o[k + 1] - o[k]) {
+        key_out[o[k] + j] = kk[k];
+        run_out[o[k] + j] = rr[k];
+      }
+  }
+}
+
+// tile_run_off[t] = first sorted run with key >= t (t in [0, ntiles])
+__global__ void tile_offsets_kernel(const uint32_t* __restrict__ keys, int64_t nruns, int64_t ntiles,
+                                    int64_t* __restrict__ tile_run_off) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t > ntiles) return;
+  int64_t lo = 0, hi = nruns;
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if ((int64_t)keys[mid] < t) lo = mid + 1;
+    else hi = mid;
+  }
+  tile_run_off[t] = lo;
+}
+
+int64_t radix_blocks(int64_t n) { return (n + kRadixBlock - 1) / kRadixBlock; }
+
+hipError_t launch_radix_hist(const uint32_t* keys, int64_t n, int shift, int64_t* hist, hipStream_t s) {
+  const int64_t nb = radix_blocks(n);
+  if (nb == 0) return hipSuccess;
+  radix_hist_kernel<<<dim3((unsigned)nb), dim3(kRadixThreads), 0, s>>>(keys, n, shift, nb, hist);
+  return hipGetLastError();
+}
+
+hipError_t launch_radix_scatter(const uint32_t* keys, const uint64_t* vals, int64_t n, int shift,
+                                const int64_t* hist, uint32_t* keys_out, uint64_t* vals_out, hipStream_t s) {
+  const int64_t nb = radix_blocks(n);
+  if (nb == 0) return hipSuccess;
+  radix_scatter_kernel<<<dim3((unsigned)nb), dim3(kRadixThreads), 0, s>>>(keys, vals, n, shift, nb, hist, keys_out,
+                                                                          vals_out);
+  return hipGetLastError();
+}
+
+hipError_t launch_compact_runs(int64_t nseg, const int64_t* seg_off, const uint32_t* park_key,
+                               const uint64_t* park_run, uint32_t* key_out, uint64_t* run_out, hipStream_t s) {
+  if (nseg == 0) return hipSuccess;
+  const int64_t nb = (nseg + 15) / 16;
+  compact_runs_kernel<<<dim3((unsigned)(nb < 16384 ? nb : 16384)), dim3(256), 0, s>>>(nseg, seg_off, park_key,
+                                                                                      park_run, key_out, run_out);
+  return hipGetLastError();
+}
+
+hipError_t launch_tile_offsets(const uint32_t* keys, int64_t nruns, int64_t ntiles, int64_t* tile_run_off,
+                               hipStream_t s) {
+  tile_offsets_kernel<<<dim3((unsigned)((ntiles + 256) / 256)), dim3(256), 0, s>>>(keys, nruns, ntiles, tile_run_off);
   return hipGetLastError();
 }
 

@@ -191,6 +191,19 @@ def test_non_finite_uvw_raises(gpu_device):
         gridder.ms2dirty(uvw, f, vis, w, 64, 64, px, px, support=8, do_wstacking=False)
 
 
+def test_non_finite_visibility(gpu_device):
+    uvw, f, vis, w = _case(500, 4)
+    vis, w = vis.copy(), w.copy()
+    px = syn.pixel_size_for_grid(uvw, f, 64)
+    vis[3, 1] = np.nan
+    w[3, 1] = 0.0  # a zero-weight sample is skipped whatever it holds
+    img = gridder.ms2dirty(uvw, f, vis, w, 64, 64, px, px, support=8)
+    assert np.isfinite(img).all()
+    w[3, 1] = 1.0
+    with pytest.raises(ValueError):
+        gridder.ms2dirty(uvw, f, vis, w, 64, 64, px, px, support=8)
+
+
 def test_bad_arguments_raise(gpu_device):
     uvw, f, vis, w = _case(100, 1)
     px = syn.pixel_size_for_grid(uvw, f, 64)
