@@ -3,6 +3,7 @@
 // ms2dirty, the reference tiling runs and the Stokes-I conversion.
 #include <hipfft/hipfft.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 #include <map>
@@ -245,6 +246,7 @@ static GridGeometry geometry(const cip_gridder_params& p, double px, double py) 
   g.ntx = (p.nu + p.tile - 1) / p.tile;
   g.nty = (p.nv + p.tile - 1) / p.tile;
   g.ntw = p.do_wstacking ? (p.nplanes - p.support + 1) : 1;
+  g.transposed = 0;
   return g;
 }
 
@@ -257,7 +259,6 @@ struct DevBuf {
 struct FftPlan {
   hipfftHandle h;
   int64_t nu, nv;
-  int64_t cols;  // 0: 2-D nu x nv plan; > 0: batch of `cols` strided column FFTs of length nu
 };
 
 struct Workspace {
@@ -267,7 +268,7 @@ struct Workspace {
   size_t pinned_bytes = 0;
   std::vector<int64_t> corr_key;  // (npix_x, npix_y, nu, nv, W) of the cached cx / cy
   std::vector<double> fw_key;     // (W, dw |nmin|) of the cached w-correction table
-  int64_t tw_n = 0;               // length of the cached row-FFT twiddle table
+  std::vector<int64_t> tw_ready;  // lengths whose FFT twiddle tables are on the device
 };
 
 static std::mutex g_ws_mutex;
@@ -318,7 +319,7 @@ static void* pinned(Workspace* ws, size_t bytes) {
 
 static int fft_plan(Workspace* ws, int64_t nu, int64_t nv, hipStream_t s, hipfftHandle* out) {
   for (auto& p : ws->plans)
-    if (p.cols == 0 && p.nu == nu && p.nv == nv) {
+    if (p.nu == nu && p.nv == nv) {
       if (hipfftSetStream(p.h, s) != HIPFFT_SUCCESS) return set_error(CIP_EHIP, "hipfftSetStream failed");
       *out = p.h;
       return CIP_OK;
@@ -327,39 +328,17 @@ static int fft_plan(Workspace* ws, int64_t nu, int64_t nv, hipStream_t s, hipfft
   if (hipfftPlan2d(&h, (int)nu, (int)nv, HIPFFT_Z2Z) != HIPFFT_SUCCESS)
     return set_error(CIP_EHIP, "hipfftPlan2d failed");
   if (hipfftSetStream(h, s) != HIPFFT_SUCCESS) return set_error(CIP_EHIP, "hipfftSetStream failed");
-  ws->plans.push_back({h, nu, nv, 0});
+  ws->plans.push_back({h, nu, nv});
   *out = h;
   return CIP_OK;
 }
 
-#define CIP_ALLOC_RET(var, T, name, n) \
-  T* var = buf<T>(ws, name, (n));      \
-  if (!var) return CIP_ENOMEM;
-
-// Column pass of the pruned 2-D FFT: `cols` transforms of length nu over a
-// (nu, cols) row-major array (stride cols, distance 1), in place.
-static int fft_col_plan(Workspace* ws, int64_t nu, int64_t cols, hipStream_t s, hipfftHandle* out) {
-  for (auto& p : ws->plans)
-    if (p.cols == cols && p.nu == nu) {
-      if (hipfftSetStream(p.h, s) != HIPFFT_SUCCESS) return set_error(CIP_EHIP, "hipfftSetStream failed");
-      *out = p.h;
-      return CIP_OK;
-    }
-  hipfftHandle h;
-  int n[1] = {(int)nu};
-  int emb[1] = {(int)nu};
-  if (hipfftPlanMany(&h, 1, n, emb, (int)cols, 1, emb, (int)cols, 1, HIPFFT_Z2Z, (int)cols) != HIPFFT_SUCCESS)
-    return set_error(CIP_EHIP, "hipfftPlanMany failed");
-  if (hipfftSetStream(h, s) != HIPFFT_SUCCESS) return set_error(CIP_EHIP, "hipfftSetStream failed");
-  ws->plans.push_back({h, nu, 0, cols});
-  *out = h;
-  return CIP_OK;
-}
-
-// exp(+2 pi i m / n), m < n, for the row FFT (cached per workspace)
-static int row_fft_twiddles(Workspace* ws, int64_t n, hipStream_t s, double** out) {
-  CIP_ALLOC_RET(tw, double, "fft_twiddle", 2 * n)
-  if (ws->tw_n != n) {
+// exp(+2 pi i m / n), m < n, for the pruned FFT passes (cached per length)
+static int fft_twiddles(Workspace* ws, int64_t n, hipStream_t s, double** out) {
+  const std::string name = "fft_twiddle_" + std::to_string(n);
+  double* tw = buf<double>(ws, name.c_str(), 2 * n);
+  if (!tw) return CIP_ENOMEM;
+  if (std::find(ws->tw_ready.begin(), ws->tw_ready.end(), n) == ws->tw_ready.end()) {
     std::vector<double> h(2 * n);
     for (int64_t m = 0; m < n; ++m) {
       // long double arguments: each entry correctly rounded (to within an ulp)
@@ -369,7 +348,7 @@ static int row_fft_twiddles(Workspace* ws, int64_t n, hipStream_t s, double** ou
     }
     CIP_HIP_CHECK(hipMemcpyAsync(tw, h.data(), sizeof(double) * 2 * n, hipMemcpyHostToDevice, s));
     CIP_HIP_CHECK(hipStreamSynchronize(s));
-    ws->tw_n = n;
+    ws->tw_ready.push_back(n);
   }
   *out = tw;
   return CIP_OK;
@@ -620,9 +599,12 @@ static int prepare(Workspace* ws, const double* uvw, int64_t nrow, const double*
   return rc;
 }
 
+// transposed: store the grid as gT[y, x] (input layout of the pruned FFT)
 static int scatter_plane(const Prepared& pp, int64_t plane, const double* uvw, const void* vis, int vis_dtype,
-                         const void* wgt, int wgt_dtype, int64_t nchan, double* grid, hipStream_t s) {
-  const GridGeometry& g = pp.g;
+                         const void* wgt, int wgt_dtype, int64_t nchan, bool transposed, double* grid,
+                         hipStream_t s) {
+  GridGeometry g = pp.g;
+  g.transposed = transposed ? 1 : 0;
   CIP_HIP_CHECK(hipMemsetAsync(grid, 0, sizeof(double) * 2 * g.nu * g.nv, s));
   if (pp.plan.nchunks == 0) return CIP_OK;
   int64_t lo = 0, hi = 0;  // tile layers feeding this plane
@@ -699,38 +681,45 @@ int cip_ms2dirty(const double* uvw, int64_t nrow, const double* freq, int64_t nc
     CIP_HIP_CHECK(hipStreamSynchronize(s));  // host vectors go out of scope
     ws->corr_key = corr_key;
   }
-  // pruned FFT: hand-written row pass keeping the image's npix_y columns,
-  // then hipFFT's column pass on that half (CIP_FFT_PRUNED=0: full 2-D hipFFT)
-  const bool pruned = fft_pruned() && row_fft_supported(g.nv, npix_y);
-  hipfftHandle plan;
-  double* fft_out = grid;
-  double* tw = nullptr;
-  if (pruned) {
-    rc = fft_col_plan(ws, g.nu, npix_y, s, &plan);
+  // pruned FFT (cip_fft.hip) for power-of-two grids; hipFFT 2-D otherwise
+  // (CIP_FFT_PRUNED=0 forces the latter)
+  const bool fast = fft_pruned() && fast_fft_supported(g.nu, g.nv, npix_x, npix_y);
+  hipfftHandle plan = nullptr;
+  double *tw_u = nullptr, *tw_v = nullptr, *fft_h = nullptr;
+  if (fast) {
+    rc = fft_twiddles(ws, g.nu, s, &tw_u);
     if (rc != CIP_OK) return rc;
-    rc = row_fft_twiddles(ws, g.nv, s, &tw);
+    rc = fft_twiddles(ws, g.nv, s, &tw_v);
     if (rc != CIP_OK) return rc;
-    fft_out = buf<double>(ws, "fft_rows", 2 * g.nu * npix_y);
-    if (!fft_out) return CIP_ENOMEM;
+    fft_h = buf<double>(ws, "fft_pass_a", 2 * npix_x * g.nv);
+    if (!fft_h) return CIP_ENOMEM;
   } else {
     rc = fft_plan(ws, g.nu, g.nv, s, &plan);
     if (rc != CIP_OK) return rc;
   }
   for (int64_t p = 0; p < g.nplanes; ++p) {
-    rc = scatter_plane(pp, p, uvw, vis, vis_dtype, wgt, wgt_dtype, nchan, grid, s);
+    rc = scatter_plane(pp, p, uvw, vis, vis_dtype, wgt, wgt_dtype, nchan, fast, grid, s);
     if (rc != CIP_OK) return rc;
     hipEvent_t f0 = g_prof.mark(s);
-    if (pruned) CIP_HIP_CHECK(launch_row_fft(grid, g.nu, g.nv, npix_y, tw, fft_out, s));
-    if (hipfftExecZ2Z(plan, (hipfftDoubleComplex*)fft_out, (hipfftDoubleComplex*)fft_out, HIPFFT_BACKWARD) !=
-        HIPFFT_SUCCESS)
+    if (fast) {
+      CIP_HIP_CHECK(launch_fft_rows(grid, g.nu, g.nv, npix_x, tw_u, fft_h, s));
+    } else if (hipfftExecZ2Z(plan, (hipfftDoubleComplex*)grid, (hipfftDoubleComplex*)grid, HIPFFT_BACKWARD) !=
+               HIPFFT_SUCCESS) {
       return set_error(CIP_EHIP, "hipfftExecZ2Z failed");
+    }
+    const double w_plane = g.w0 + (double)p * g.dw;
+    // pass B carries the crop epilogue: it is booked under "fft"
+    if (fast)
+      CIP_HIP_CHECK(launch_fft_cols(fft_h, g.nv, npix_x, npix_y, tw_v, g.do_wstacking ? 1 : 0, dirty_out, cx, cy,
+                                    pixsize_x, pixsize_y, w_plane, p == 0, s));
     hipEvent_t f1 = g_prof.mark(s);
     g_prof.span(3, f0, f1);
-    if (g.do_wstacking) {
-      CIP_HIP_CHECK(launch_wplane_accumulate(fft_out, g, npix_x, npix_y, pixsize_x, pixsize_y,
-                                             g.w0 + (double)p * g.dw, p == 0, pruned ? 1 : 0, dirty_out, s));
+    if (fast) {
+    } else if (g.do_wstacking) {
+      CIP_HIP_CHECK(launch_wplane_accumulate(grid, g, npix_x, npix_y, pixsize_x, pixsize_y, w_plane, p == 0,
+                                             dirty_out, s));
     } else {
-      CIP_HIP_CHECK(launch_crop_correct_2d(fft_out, g, npix_x, npix_y, cx, cy, pruned ? 1 : 0, dirty_out, s));
+      CIP_HIP_CHECK(launch_crop_correct_2d(grid, g, npix_x, npix_y, cx, cy, dirty_out, s));
     }
     g_prof.span(4, f1, g_prof.mark(s));
   }
@@ -776,7 +765,7 @@ int cip_grid_plane(const double* uvw, int64_t nrow, const double* freq, int64_t 
   int rc = prepare(ws, uvw, nrow, freq, nchan, vis, vis_dtype, wgt, wgt_dtype, 2, 2, pixsize_x, pixsize_y, 0.0,
                    params->support, params->do_wstacking, (flags & CIP_ACC_SINGLE) != 0, params, s, &pp);
   if (rc != CIP_OK) return rc;
-  rc = scatter_plane(pp, plane, uvw, vis, vis_dtype, wgt, wgt_dtype, nchan, grid_out, s);
+  rc = scatter_plane(pp, plane, uvw, vis, vis_dtype, wgt, wgt_dtype, nchan, false, grid_out, s);
   if (rc != CIP_OK) return rc;
   g_prof.span(5, t_start, g_prof.mark(s));
   CIP_HIP_CHECK(hipStreamSynchronize(s));

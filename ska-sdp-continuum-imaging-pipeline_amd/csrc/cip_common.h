@@ -133,6 +133,7 @@ struct GridGeometry {
   int64_t nplanes;
   int tile;                 // T
   int64_t ntx, nty, ntw;    // tiles per axis (ntw = nplanes - W + 1, or 1 in 2-D)
+  int transposed;           // HBM grid stored as gT[y, x] (pruned FFT), else g[x, y]
 };
 
 // Grid coordinate -> footprint origin and kernel variable.

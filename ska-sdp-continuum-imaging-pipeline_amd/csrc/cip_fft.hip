@@ -1,18 +1,18 @@
-// cip_fft.hip - the dirty image's first FFT axis as a hand-written row FFT
-// with a pruned output.
+// cip_fft.hip - the dirty image's 2-D FFT as two hand-written pruned passes
+// (SURVEY.md 8(a) a4.5), for power-of-two grids of 1024..8192 cells per axis.
 //
-// The image only needs the npix_y frequencies q in [-npix_y/2, npix_y/2) of
-// each grid row, i.e. half of them for sigma = 2. row_fft_kernel transforms
-// one grid row (length N = nv, a power of two from 1024 to 8192) per
-// workgroup of N/16 threads, each holding 16 complex values in registers:
-// radix-16 (and a last radix-2/4/8) Stockham passes, exchanged through a
-// "half" LDS array (real parts, then imaginary parts: 17/16 N doubles = 68 KiB
-// at N = 8192, two workgroups per CU), and writes only the kept columns,
-// H[x, j] = sum_y G[x, y] exp(+2 pi i y (j - npix_y/2) / nv), as a
-// (nu, npix_y) row-major array. The column FFT (along x) then runs on half
-// the data (hipFFT, strided batch) and the crop kernels read H directly.
-// HBM traffic of this pass: 16 nu nv bytes read + 16 nu npix_y written,
-// against 32 nu nv for a full c2c pass of hipFFT's row transform.
+// The image keeps only nx x ny of the nu x nv frequencies (a quarter for
+// sigma = 2). The scatter writes the grid transposed (gT[y, x]); pass A
+// transforms each row of gT along u and keeps the nx frequencies i, written
+// in 8-column blocks; pass B transforms each kept column i along v and writes
+// image row i directly through the crop epilogue (grid correction, or the
+// w-plane screen and accumulation). Each workgroup holds one N-point
+// transform: N/16 threads x 16 complex values in registers, radix-16 (and a
+// last radix-2/4/8) Stockham passes exchanged through a "half" LDS array
+// (real parts, then imaginary parts; 17/16 N doubles = 68 KiB at N = 8192,
+// two workgroups per CU). HBM bytes per plane: pass A 16 nu nv read +
+// 16 nx nv written, pass B 16 nx nv read + 8 nx ny written (against 64 nu nv
+// for hipFFT's in-place 2-D c2c plus the crop pass).
 #include "cip_internal.h"
 
 namespace cip {
@@ -37,22 +37,6 @@ __device__ __constant__ const double kW16c[16] = {1.0,
 
 __device__ __forceinline__ double2 cmul(double2 a, double2 b) {
   return make_double2(fma(a.x, b.x, -a.y * b.y), fma(a.x, b.y, a.y * b.x));
-}
-
-// v * exp(+2 pi i k / M) for compile-time k, M (exact special cases)
-template <int K, int M>
-__device__ __forceinline__ double2 twc(double2 v) {
-  constexpr int k = ((K % M) + M) % M;
-  if constexpr (k == 0) return v;
-  else if constexpr (4 * k == M) return make_double2(-v.y, v.x);          // * i
-  else if constexpr (2 * k == M) return make_double2(-v.x, -v.y);         // * -1
-  else if constexpr (4 * k == 3 * M) return make_double2(v.y, -v.x);      // * -i
-  else {
-    static_assert(16 % M == 0, "twiddle table covers M | 16");
-    constexpr int idx = k * (16 / M);
-    const double c = kW16c[idx], s = kW16c[(idx + 12) & 15];  // sin(t) = cos(t - pi/2)
-    return make_double2(fma(v.x, c, -v.y * s), fma(v.x, s, v.y * c));
-  }
 }
 
 // In-register DFT of size R (R | 16), natural order in and out, sign +.
@@ -157,63 +141,162 @@ __device__ __forceinline__ void exchange(double2* v, int t, int ns, double* lds)
   }
 }
 
-// log2 N = 4 P + B: P radix-16 passes then one radix-2^B pass (B = 0: none)
+// All passes of an N-point transform (log2 N = 4 P + B: P radix-16 passes,
+// then one radix-2^B pass). On return v[m * RF + r] holds frequency
+// out_pos<N, RF>(t, m, r, N / RF).
 template <int N>
-__global__ __launch_bounds__(N / 16) void row_fft_kernel(const double2* __restrict__ grid, int64_t ny,
-                                                         const double2* __restrict__ tw, double2* __restrict__ out) {
-  constexpr int T = N / 16;
-  constexpr int L = __builtin_ctz(N);
-  constexpr int P = L / 4, B = L % 4, RL = 1 << B;
-  __shared__ double lds[N + N / 16];
-  const int t = threadIdx.x;
-  const int64_t x = blockIdx.x;
-  const double2* row = grid + x * N;
-  double2 v[16];
-#pragma unroll
-  for (int r = 0; r < 16; ++r) v[r] = row[t + r * T];
+struct FftShape {
+  static constexpr int T = N / 16;
+  static constexpr int L = __builtin_ctz(N);
+  static constexpr int P = L / 4, B = L % 4;
+  static constexpr int RF = B ? (1 << B) : 16;  // radix of the final pass
+};
+
+template <int N>
+__device__ __forceinline__ void fft_core(double2* v, int t, double* lds, const double2* __restrict__ tw) {
+  using S = FftShape<N>;
   int ns = 1;
   stockham_pass<N, 16>(v, t, ns, tw);
 #pragma unroll
-  for (int p = 1; p < P; ++p) {
+  for (int p = 1; p < S::P; ++p) {
     exchange<N, 16, 16>(v, t, ns, lds);
     ns *= 16;
     stockham_pass<N, 16>(v, t, ns, tw);
   }
-  constexpr int RF = B ? RL : 16;  // radix of the final pass
-  if constexpr (B != 0) {
-    exchange<N, 16, RL>(v, t, ns, lds);
+  if constexpr (S::B != 0) {
+    exchange<N, 16, S::RF>(v, t, ns, lds);
     ns *= 16;
-    stockham_pass<N, RL>(v, t, ns, tw);
+    stockham_pass<N, S::RF>(v, t, ns, tw);
   }
-  // final outputs: frequency k = out_pos (< N); keep j = (k + ny/2) mod N < ny
-  double2* orow = out + x * ny;
+}
+
+// Pass A, along u: row y of the transposed grid gT (nv rows of nu = N cells)
+// -> the nx kept frequencies, i = (k + nx/2) mod N < nx, stored in blocks of
+// 8 columns: H[((i / 8) nv + y) 8 + i % 8] (128-byte rows per block, so pass
+// B's 8 columns of a block read whole lines between them).
+template <int N>
+__global__ __launch_bounds__(N / 16) void fft_rows_kernel(const double2* __restrict__ gT, int64_t nv, int64_t nx,
+                                                          const double2* __restrict__ tw, double2* __restrict__ H) {
+  using S = FftShape<N>;
+  __shared__ double lds[N + N / 16];
+  const int t = threadIdx.x;
+  const int64_t y = blockIdx.x;
+  const double2* row = gT + y * N;
+  double2 v[16];
 #pragma unroll
-  for (int m = 0; m < 16 / RF; ++m)
+  for (int r = 0; r < 16; ++r) v[r] = row[t + r * S::T];
+  fft_core<N>(v, t, lds, tw);
 #pragma unroll
-    for (int r = 0; r < RF; ++r) {
-      const int k = out_pos<N, RF>(t, m, r, ns);
-      const int64_t j = (int64_t)((k + (int)(ny / 2)) & (N - 1));
-      if (j < ny) orow[j] = v[m * RF + r];
+  for (int m = 0; m < 16 / S::RF; ++m)
+#pragma unroll
+    for (int r = 0; r < S::RF; ++r) {
+      const int k = out_pos<N, S::RF>(t, m, r, N / S::RF);
+      const int64_t i = (int64_t)((k + (int)(nx / 2)) & (N - 1));
+      if (i < nx) H[((i >> 3) * nv + y) * 8 + (i & 7)] = v[m * S::RF + r];
     }
 }
 
-bool row_fft_supported(int64_t nv, int64_t ny) {
-  return (nv == 1024 || nv == 2048 || nv == 4096 || nv == 8192) && ny <= nv && ny > 0 && (ny % 2) == 0;
+// Pass B, along v, for image row i: column i of H (N = nv points) -> the ny
+// kept frequencies j = (k + ny/2) mod N < ny, written straight into image row
+// i with the crop epilogue:
+//   MODE 0 (2-D):      dirty[i, j]  = (-1)^(p+q) Re(.) cx[i] cy[j]
+//   MODE 1 (w plane):  acc[i, j] (+)= (-1)^(p+q) Re(. exp(-2 pi i w (n-1)))
+// p = i - nx/2, q = j - ny/2. Blocks b, b+8, ... share an XCD (round-robin
+// dispatch), so the 8 columns of one H block go to one XCD's L2 together.
+struct ColEpilogue {
+  double* out;
+  const double* cx;
+  const double* cy;
+  double px, py, w_plane;
+  int first;
+};
+
+template <int N, int MODE>
+__global__ __launch_bounds__(N / 16) void fft_cols_kernel(const double2* __restrict__ H, int64_t nx, int64_t ny,
+                                                          const double2* __restrict__ tw, ColEpilogue ep) {
+  using S = FftShape<N>;
+  __shared__ double lds[N + N / 16];
+  const int t = threadIdx.x;
+  const int64_t b = blockIdx.x;
+  int64_t i = b;
+  if (nx % 64 == 0) i = (b & ~63ll) + ((b & 7) << 3) + ((b >> 3) & 7);
+  const double2* col = H + ((i >> 3) * N) * 8 + (i & 7);
+  double2 v[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) v[r] = col[(int64_t)(t + r * S::T) * 8];
+  fft_core<N>(v, t, lds, tw);
+  const int64_t p = i - nx / 2;
+  double* orow = ep.out + i * ny;
+#pragma unroll
+  for (int m = 0; m < 16 / S::RF; ++m)
+#pragma unroll
+    for (int r = 0; r < S::RF; ++r) {
+      const int k = out_pos<N, S::RF>(t, m, r, N / S::RF);
+      const int64_t j = (int64_t)((k + (int)(ny / 2)) & (N - 1));
+      if (j < ny) {
+        const int64_t q = j - ny / 2;
+        const double sgn = ((p + q) & 1) ? -1.0 : 1.0;
+        const double2 g = v[m * S::RF + r];
+        if constexpr (MODE == 0) {
+          orow[j] = sgn * g.x * ep.cx[i] * ep.cy[j];
+        } else {
+          const double l = (double)p * ep.px, mm = (double)q * ep.py;
+          const double e = l * l + mm * mm;
+          const double nm1 = -e / (sqrt(1.0 - e) + 1.0);
+          double sn, cs;
+          sincospi(-2.0 * ep.w_plane * nm1, &sn, &cs);
+          const double val = sgn * (g.x * cs - g.y * sn);
+          if (ep.first) orow[j] = val;
+          else orow[j] += val;
+        }
+      }
+    }
 }
 
-hipError_t launch_row_fft(const double* grid, int64_t nu, int64_t nv, int64_t ny, const double* twiddles,
-                          double* out, hipStream_t s) {
-  const dim3 gd((unsigned)nu);
-  const double2* g = (const double2*)grid;
-  const double2* tw = (const double2*)twiddles;
-  double2* o = (double2*)out;
-  switch (nv) {
-    case 1024: row_fft_kernel<1024><<<gd, dim3(64), 0, s>>>(g, ny, tw, o); break;
-    case 2048: row_fft_kernel<2048><<<gd, dim3(128), 0, s>>>(g, ny, tw, o); break;
-    case 4096: row_fft_kernel<4096><<<gd, dim3(256), 0, s>>>(g, ny, tw, o); break;
-    case 8192: row_fft_kernel<8192><<<gd, dim3(512), 0, s>>>(g, ny, tw, o); break;
+static bool fft_len_ok(int64_t n) { return n == 1024 || n == 2048 || n == 4096 || n == 8192; }
+
+bool fast_fft_supported(int64_t nu, int64_t nv, int64_t nx, int64_t ny) {
+  return fft_len_ok(nu) && fft_len_ok(nv) && nx > 0 && ny > 0 && nx <= nu && ny <= nv && nx % 8 == 0 &&
+         ny % 2 == 0;
+}
+
+hipError_t launch_fft_rows(const double* gT, int64_t nu, int64_t nv, int64_t nx, const double* tw_u, double* H,
+                           hipStream_t s) {
+  const dim3 gd((unsigned)nv);
+  const double2* g = (const double2*)gT;
+  const double2* tw = (const double2*)tw_u;
+  double2* h = (double2*)H;
+  switch (nu) {
+    case 1024: fft_rows_kernel<1024><<<gd, dim3(64), 0, s>>>(g, nv, nx, tw, h); break;
+    case 2048: fft_rows_kernel<2048><<<gd, dim3(128), 0, s>>>(g, nv, nx, tw, h); break;
+    case 4096: fft_rows_kernel<4096><<<gd, dim3(256), 0, s>>>(g, nv, nx, tw, h); break;
+    case 8192: fft_rows_kernel<8192><<<gd, dim3(512), 0, s>>>(g, nv, nx, tw, h); break;
     default: return hipErrorInvalidValue;
   }
+  return hipGetLastError();
+}
+
+hipError_t launch_fft_cols(const double* H, int64_t nv, int64_t nx, int64_t ny, const double* tw_v, int mode,
+                           double* out, const double* cx, const double* cy, double px, double py, double w_plane,
+                           int first, hipStream_t s) {
+  const dim3 gd((unsigned)nx);
+  const double2* h = (const double2*)H;
+  const double2* tw = (const double2*)tw_v;
+  const ColEpilogue ep{out, cx, cy, px, py, w_plane, first};
+#define COLS(NN)                                                                    \
+  case NN:                                                                          \
+    if (mode == 0) fft_cols_kernel<NN, 0><<<gd, dim3(NN / 16), 0, s>>>(h, nx, ny, tw, ep); \
+    else fft_cols_kernel<NN, 1><<<gd, dim3(NN / 16), 0, s>>>(h, nx, ny, tw, ep);          \
+    break;
+  switch (nv) {
+    COLS(1024)
+    COLS(2048)
+    COLS(4096)
+    COLS(8192)
+    default:
+      return hipErrorInvalidValue;
+  }
+#undef COLS
   return hipGetLastError();
 }
 

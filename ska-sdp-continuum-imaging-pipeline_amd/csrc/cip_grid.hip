@@ -393,22 +393,25 @@ __global__ __launch_bounds__(kScatterThreads) void scatter_kernel(
   }
   __syncthreads();
   // flush the touched cells of the sub-grid to the fp64 HBM grid
+  // (lanes walk the HBM grid's contiguous axis: y, or x when it is stored
+  // transposed for the pruned FFT)
   for (int cell = threadIdx.x; cell < P * P; cell += kScatterThreads) {
+    const int lcell = g.transposed ? (cell % P) * P + cell / P : cell;  // lx * P + ly
     long long re, im;
     if constexpr (PACK) {
-      const unsigned long long s = sub[cell];
+      const unsigned long long s = sub[lcell];
       im = (long long)(int)(unsigned)s;
       re = (long long)(int)(unsigned)((s - (unsigned long long)im) >> 32);
     } else {
-      re = (long long)sub[cell];
-      im = (long long)sub[P * P + cell];
+      re = (long long)sub[lcell];
+      im = (long long)sub[P * P + lcell];
     }
     if ((re | im) != 0) {
       // the sub-grid of an edge tile wraps around the periodic grid
-      int64_t gx = X0 + cell / P, gy = Y0 + cell % P;
+      int64_t gx = X0 + lcell / P, gy = Y0 + lcell % P;
       gx -= (gx >= g.nu) ? g.nu : 0;
       gy -= (gy >= g.nv) ? g.nv : 0;
-      double* dst = grid + 2 * (gx * g.nv + gy);
+      double* dst = grid + 2 * (g.transposed ? gy * g.nu + gx : gx * g.nv + gy);
       unsafeAtomicAdd(dst, (double)re * inv_scale);
       unsafeAtomicAdd(dst + 1, (double)im * inv_scale);
     }
@@ -502,28 +505,22 @@ hipError_t launch_scatter(int support, int vis_dtype, int wgt_dtype, bool packed
 // ---------------------------------------------------- post-FFT kernels ----
 // dirty[i, j] = (-1)^(p+q) Re G^[p mod nu, q mod nv] * cx[i] * cy[j],
 // p = i - npix_x/2, q = j - npix_y/2; cx, cy = 1 / F(p/nu), 1 / F(q/nv).
-// pruned: the FFT output holds only the image's columns, (nu, ny) row-major
-// with column j <-> q (cip_fft.hip); else the full (nu, nv) transform
-__device__ __forceinline__ int64_t fft_index(int64_t ip, int64_t iq, int64_t j, int64_t nv, int64_t ny, int pruned) {
-  return pruned ? ip * ny + j : ip * nv + iq;
-}
-
 __global__ void crop_correct_2d_kernel(const double2* __restrict__ grid, int64_t nu, int64_t nv, int64_t nx,
                                        int64_t ny, const double* __restrict__ cx, const double* __restrict__ cy,
-                                       int pruned, double* __restrict__ dirty) {
+                                       double* __restrict__ dirty) {
   const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t i = blockIdx.y;
   if (j >= ny) return;
   const int64_t p = i - nx / 2, q = j - ny / 2;
   const int64_t ip = (p + nu) % nu, iq = (q + nv) % nv;
   const double sgn = ((p + q) & 1) ? -1.0 : 1.0;
-  dirty[i * ny + j] = sgn * grid[fft_index(ip, iq, j, nv, ny, pruned)].x * cx[i] * cy[j];
+  dirty[i * ny + j] = sgn * grid[ip * nv + iq].x * cx[i] * cy[j];
 }
 
 hipError_t launch_crop_correct_2d(const double* grid, const GridGeometry& g, int64_t npix_x, int64_t npix_y,
-                                  const double* cx, const double* cy, int pruned, double* dirty, hipStream_t s) {
+                                  const double* cx, const double* cy, double* dirty, hipStream_t s) {
   crop_correct_2d_kernel<<<dim3((unsigned)((npix_y + 255) / 256), (unsigned)npix_x), dim3(256), 0, s>>>(
-      (const double2*)grid, g.nu, g.nv, npix_x, npix_y, cx, cy, pruned, dirty);
+      (const double2*)grid, g.nu, g.nv, npix_x, npix_y, cx, cy, dirty);
   return hipGetLastError();
 }
 
@@ -536,7 +533,7 @@ __device__ __forceinline__ double nm1_of(int64_t i, int64_t j, int64_t nx, int64
 
 // acc[i, j] (+)= (-1)^(p+q) Re(G^_p[..] exp(-2 pi i w_p (n - 1)))
 __global__ void wplane_accumulate_kernel(const double2* __restrict__ grid, int64_t nu, int64_t nv, int64_t nx,
-                                         int64_t ny, double px, double py, double w_plane, int first, int pruned,
+                                         int64_t ny, double px, double py, double w_plane, int first,
                                          double* __restrict__ acc) {
   const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t i = blockIdx.y;
@@ -547,17 +544,17 @@ __global__ void wplane_accumulate_kernel(const double2* __restrict__ grid, int64
   const double nm1 = nm1_of(i, j, nx, ny, px, py);
   double sn, cs;
   sincospi(-2.0 * w_plane * nm1, &sn, &cs);
-  const double2 gval = grid[fft_index(ip, iq, j, nv, ny, pruned)];
+  const double2 gval = grid[ip * nv + iq];
   const double val = sgn * (gval.x * cs - gval.y * sn);
   if (first) acc[i * ny + j] = val;
   else acc[i * ny + j] += val;
 }
 
 hipError_t launch_wplane_accumulate(const double* grid, const GridGeometry& g, int64_t npix_x, int64_t npix_y,
-                                    double pixsize_x, double pixsize_y, double w_plane, int first, int pruned,
-                                    double* acc, hipStream_t s) {
+                                    double pixsize_x, double pixsize_y, double w_plane, int first, double* acc,
+                                    hipStream_t s) {
   wplane_accumulate_kernel<<<dim3((unsigned)((npix_y + 255) / 256), (unsigned)npix_x), dim3(256), 0, s>>>(
-      (const double2*)grid, g.nu, g.nv, npix_x, npix_y, pixsize_x, pixsize_y, w_plane, first, pruned, acc);
+      (const double2*)grid, g.nu, g.nv, npix_x, npix_y, pixsize_x, pixsize_y, w_plane, first, acc);
   return hipGetLastError();
 }
 

@@ -79,23 +79,25 @@ hipError_t launch_scatter(int support, int vis_dtype, int wgt_dtype, bool packed
 // pieces by chunk_emit with cv = kOrderWindow)
 hipError_t launch_order(const uint8_t* vis_class, int64_t nchan, const uint64_t* runs, const int64_t* run_goff,
                         int64_t nruns, const Chunk* windows, int64_t nwindows, uint64_t* perm, hipStream_t s);
-// pruned != 0: grid is the (nu, npix_y) output of the pruned FFT (launch_row_fft
-// + column pass), else the full (nu, nv) transform
 hipError_t launch_crop_correct_2d(const double* grid, const GridGeometry& g, int64_t npix_x, int64_t npix_y,
-                                  const double* cx, const double* cy, int pruned, double* dirty, hipStream_t s);
+                                  const double* cx, const double* cy, double* dirty, hipStream_t s);
 hipError_t launch_wplane_accumulate(const double* grid, const GridGeometry& g, int64_t npix_x, int64_t npix_y,
-                                    double pixsize_x, double pixsize_y, double w_plane, int first, int pruned,
+                                    double pixsize_x, double pixsize_y, double w_plane, int first,
                                     double* acc, hipStream_t s);
 hipError_t launch_wfinal_correct(double* acc, int64_t npix_x, int64_t npix_y, double pixsize_x, double pixsize_y,
                                  const double* cx, const double* cy, const double* fw_table, int64_t fw_n,
                                  double fw_dnu, double dw, hipStream_t s);
 
-// ---- pruned row FFT (cip_fft.hip) ------------------------------------------
-// out[x, j] = sum_y grid[x, y] exp(+2 pi i y (j - ny/2) / nv) for j < ny;
-// twiddles: exp(+2 pi i m / nv), m < nv (interleaved re, im).
-bool row_fft_supported(int64_t nv, int64_t ny);
-hipError_t launch_row_fft(const double* grid, int64_t nu, int64_t nv, int64_t ny, const double* twiddles,
-                          double* out, hipStream_t s);
+// ---- pruned 2-D FFT (cip_fft.hip) -----------------------------------------
+// gT: the grid transposed (nv rows of nu cells); H: (nx / 8) x nv x 8 complex;
+// tw_u / tw_v: exp(+2 pi i m / n), m < n (interleaved re, im).
+// mode 0: out = dirty (crop + cx cy); mode 1: out = w-plane accumulator.
+bool fast_fft_supported(int64_t nu, int64_t nv, int64_t nx, int64_t ny);
+hipError_t launch_fft_rows(const double* gT, int64_t nu, int64_t nv, int64_t nx, const double* tw_u, double* H,
+                           hipStream_t s);
+hipError_t launch_fft_cols(const double* H, int64_t nv, int64_t nx, int64_t ny, const double* tw_v, int mode,
+                           double* out, const double* cx, const double* cy, double px, double py, double w_plane,
+                           int first, hipStream_t s);
 
 // ---- reference tiling + Stokes I (cip_tiling.hip) --------------------------
 hipError_t launch_tile_run_count(const double* uvw, int64_t nrow, const double* winv, int64_t nchan,
