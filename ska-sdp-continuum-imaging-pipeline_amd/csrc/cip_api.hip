@@ -415,22 +415,27 @@ static int make_plan(Workspace* ws, const double* uvw, int64_t nrow, const doubl
   CIP_ALLOC(err, unsigned, "err_flag", 1)
   CIP_ALLOC(scan_tmp, int64_t, "scan_tmp", scan_tmp_elems(ntiles + 1))
   CIP_HIP_CHECK(hipMemsetAsync(err, 0, sizeof(unsigned), s));
-  const int64_t nvis = nrow * nchan, nseg = (nvis + 63) / 64;
-  CIP_ALLOC(vis_class, uint8_t, "vis_class", nvis)
-  CIP_ALLOC(seg_off, int64_t, "seg_off", nseg + 1)
-  CIP_ALLOC(scan_seg, int64_t, "scan_seg", scan_tmp_elems(nseg + 1))
-  CIP_ALLOC(park_key, uint32_t, "park_key", nseg * 64)
-  CIP_ALLOC(park_run, uint64_t, "park_run", nseg * 64)
+  const int64_t nvis = nrow * nchan;
   const int nblk = plan_place_blocks(nvis);
+  CIP_ALLOC(vis_class, uint8_t, "vis_class", nvis)
+  CIP_ALLOC(blk_cnt, int64_t, "blk_cnt", nblk)
+  CIP_ALLOC(park_key, uint32_t, "park_key", (int64_t)nblk * 4096)
+  CIP_ALLOC(park_run, uint64_t, "park_run", (int64_t)nblk * 4096)
   CIP_ALLOC(partial, double, "prep_partial", 2 * nblk)
-  CIP_HIP_CHECK(hipMemsetAsync(seg_off + nseg, 0, sizeof(int64_t), s));
-  CIP_HIP_CHECK(launch_plan_place(uvw, nrow, fx, nchan, vis, vis_dtype, wgt, wgt_dtype, g, err, vis_class, seg_off,
+  CIP_HIP_CHECK(launch_plan_place(uvw, nrow, fx, nchan, vis, vis_dtype, wgt, wgt_dtype, g, err, vis_class, blk_cnt,
                                   park_key, park_run, partial, s));
   CIP_HIP_CHECK(launch_prep_final(partial, nblk, red, s));
-  CIP_HIP_CHECK(exclusive_scan_i64(seg_off, nseg + 1, scan_seg, s));  // entry nseg = total runs
+  // radix pass 0 histogram over the parked runs; its scan's last entry = runs
+  int key_bits = 1;
+  while (key_bits < 32 && ((int64_t)1 << key_bits) < ntiles) ++key_bits;
+  const int npass = (key_bits + 7) / 8;
+  CIP_ALLOC(hist0, int64_t, "radix_hist0", 256 * (int64_t)nblk + 1)
+  CIP_ALLOC(scan_h0, int64_t, "scan_hist0", scan_tmp_elems(256 * (int64_t)nblk + 1))
+  CIP_HIP_CHECK(launch_radix_hist(park_key, 0, blk_cnt, nblk, 0, hist0, s));
+  CIP_HIP_CHECK(exclusive_scan_i64(hist0, 256 * (int64_t)nblk + 1, scan_h0, s));
   int64_t* h = (int64_t*)pinned(ws, 4 * sizeof(int64_t));
   if (!h) return set_error(CIP_ENOMEM, "hipHostMalloc failed");
-  CIP_HIP_CHECK(hipMemcpyAsync(&h[0], seg_off + nseg, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+  CIP_HIP_CHECK(hipMemcpyAsync(&h[0], hist0 + 256 * (int64_t)nblk, sizeof(int64_t), hipMemcpyDeviceToHost, s));
   CIP_HIP_CHECK(hipMemcpyAsync(&h[1], err, sizeof(unsigned), hipMemcpyDeviceToHost, s));
   CIP_HIP_CHECK(hipMemcpyAsync(&h[2], red + 1, sizeof(double), hipMemcpyDeviceToHost, s));
   CIP_HIP_CHECK(hipStreamSynchronize(s));
@@ -441,10 +446,7 @@ static int make_plan(Workspace* ws, const double* uvw, int64_t nrow, const doubl
   if (errbits & 1u)
     return set_error(CIP_ERANGE, "non-finite (u, v, w) coordinates, or w outside the w-plane stack");
   pr->nruns = nruns;
-  // bucket the runs by tile: compact, then a stable LSD radix sort
-  int key_bits = 1;
-  while (key_bits < 32 && ((int64_t)1 << key_bits) < ntiles) ++key_bits;
-  const int npass = (key_bits + 7) / 8;
+  // bucket the runs by tile: stable LSD radix sort, pass 0 from the parked runs
   CIP_ALLOC(key_a, uint32_t, "sort_key_a", nruns)
   CIP_ALLOC(key_b, uint32_t, "sort_key_b", nruns)
   CIP_ALLOC(run_a, uint64_t, "sort_run_a", nruns)
@@ -452,13 +454,13 @@ static int make_plan(Workspace* ws, const double* uvw, int64_t nrow, const doubl
   const int64_t nbd = radix_blocks(nruns);
   CIP_ALLOC(hist, int64_t, "radix_hist", 256 * nbd + 1)
   CIP_ALLOC(scan_h, int64_t, "scan_hist", scan_tmp_elems(256 * nbd + 1))
-  CIP_HIP_CHECK(launch_compact_runs(nseg, seg_off, park_key, park_run, key_a, run_a, s));
+  CIP_HIP_CHECK(launch_radix_scatter(park_key, park_run, 0, blk_cnt, nblk, 0, hist0, key_a, run_a, s));
   uint32_t *kin = key_a, *kout = key_b;
   uint64_t *rin = run_a, *rout = run_b;
-  for (int p = 0; p < npass; ++p) {
-    CIP_HIP_CHECK(launch_radix_hist(kin, nruns, 8 * p, hist, s));
+  for (int p = 1; p < npass; ++p) {
+    CIP_HIP_CHECK(launch_radix_hist(kin, nruns, nullptr, nbd, 8 * p, hist, s));
     CIP_HIP_CHECK(exclusive_scan_i64(hist, 256 * nbd + 1, scan_h, s));
-    CIP_HIP_CHECK(launch_radix_scatter(kin, rin, nruns, 8 * p, hist, kout, rout, s));
+    CIP_HIP_CHECK(launch_radix_scatter(kin, rin, nruns, nullptr, nbd, 8 * p, hist, kout, rout, s));
     std::swap(kin, kout);
     std::swap(rin, rout);
   }
@@ -503,7 +505,7 @@ static int make_plan(Workspace* ws, const double* uvw, int64_t nrow, const doubl
     CIP_HIP_CHECK(launch_chunk_emit(tile_vis_off, tile_vis, win_off, run_goff, tile_runs, ntiles, kOrderWindow, windows,
                                     s));
     CIP_ALLOC(perm, uint64_t, "perm", nrow * nchan)
-    CIP_HIP_CHECK(launch_order(vis_class, nchan, runs, run_goff, nruns, windows, nwin, perm, s));
+    CIP_HIP_CHECK(launch_order(vis_class, nchan, runs, run_goff, tile_runs, windows, nwin, perm, s));
     pr->perm = perm;
   }
   return CIP_OK;

@@ -207,71 +207,61 @@ constexpr int kOrderPer = 4;
 constexpr int kOrderBatch = kOrderThreads * kOrderPer;
 static_assert(kOrderBatch == kOrderWindow, "one order block per window");
 
-// Expansion: each wave takes 64 consecutive row slices (tile order, so their
-// visibilities are one contiguous range of the list), parks them in LDS and
-// writes that range with coalesced stores, each lane finding its slice by a
-// 6-step binary search: records (class << 48) | (row << 16) | channel.
-__global__ __launch_bounds__(256) void expand_kernel(const uint8_t* __restrict__ vis_class, int64_t nchan,
-                                                     const uint64_t* __restrict__ runs,
-                                                     const int64_t* __restrict__ run_goff, int64_t nruns,
-                                                     uint64_t* __restrict__ list) {
-  __shared__ int64_t s_g0[4][64];
-  __shared__ uint64_t s_rec[4][64];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int64_t ngroups = (nruns + 63) / 64;
-  for (int64_t grp = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6; grp < ngroups;
-       grp += ((int64_t)gridDim.x * 256) >> 6) {
-    const int64_t r0 = grp * 64;
-    const int n = (int)((nruns - r0) < 64 ? (nruns - r0) : 64);
-    if (lane < n) {
-      s_g0[wave][lane] = run_goff[r0 + lane];
-      s_rec[wave][lane] = runs[r0 + lane];
-    }
-    const int64_t G0 = run_goff[r0], G1 = run_goff[r0 + n];
-    __builtin_amdgcn_wave_barrier();
-    for (int64_t q = G0 + lane; q < G1; q += 64) {
-      int lo = 0, hi = n - 1;
-      while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (s_g0[wave][mid] <= q) lo = mid;
-        else hi = mid - 1;
-      }
-      const uint64_t rec = s_rec[wave][lo];
-      const int64_t row = (int64_t)(rec >> 32);
-      const int64_t c = (int64_t)((rec >> 16) & 0xffff) + (q - s_g0[wave][lo]);
-      list[q] = ((uint64_t)vis_class[row * nchan + c] << 48) | ((uint64_t)row << 16) | (uint64_t)c;
-    }
-    __builtin_amdgcn_wave_barrier();
-  }
-}
-
-// Window sort, in place: one block per window of <= kOrderWindow list
-// positions; the perm records keep (row << 16) | channel.
-__global__ __launch_bounds__(kOrderThreads) void order_kernel(const Chunk* __restrict__ windows,
-                                                              uint64_t* __restrict__ list) {
+// One block per window (<= kOrderWindow consecutive tile-order positions).
+// The window's row slices are staged in LDS (positions relative to the
+// window start; the next window of the tile starts in its last slice), each
+// thread finds the slice of its 4 positions by binary search, gathers the
+// bank class recorded by the place pass and the window is counting-sorted
+// into level-major order: perm[g] = (row << 16) | channel.
+__global__ __launch_bounds__(kOrderThreads) void order_kernel(const uint8_t* __restrict__ vis_class, int64_t nchan,
+                                                              const uint64_t* __restrict__ runs,
+                                                              const int64_t* __restrict__ run_goff,
+                                                              const int64_t* __restrict__ tile_run_off,
+                                                              const Chunk* __restrict__ windows, int64_t nwindows,
+                                                              uint64_t* __restrict__ perm) {
   __shared__ __attribute__((aligned(16))) unsigned s_cnt[32];
   __shared__ unsigned s_S[kOrderBatch], s_M[kOrderBatch];
+  __shared__ int s_off[kOrderBatch + 1];  // slice starts relative to the window start
+  __shared__ uint64_t s_rec[kOrderBatch];
   const Chunk ch = windows[blockIdx.x];
   const int64_t sb = ch.g0;
   const int nsb = (int)(ch.g1 - ch.g0);
-  if (threadIdx.x < 32) s_cnt[threadIdx.x] = 0u;
-  uint64_t packed[kOrderPer];
-#pragma unroll
-  for (int k = 0; k < kOrderPer; ++k) {
-    const int qi = threadIdx.x + k * kOrderThreads;
-    packed[k] = qi < nsb ? list[sb + qi] : 0ull;
+  // slices [first_run, last]: the next window of this tile starts in `last`
+  int64_t last = tile_run_off[ch.tile + 1] - 1;
+  if (blockIdx.x + 1 < nwindows) {
+    const Chunk nx = windows[blockIdx.x + 1];
+    if (nx.tile == ch.tile) last = nx.first_run;
   }
+  const int nst = (int)(last - ch.first_run + 1);
+  for (int k = threadIdx.x; k < nst; k += kOrderThreads) {
+    s_off[k] = (int)(run_goff[ch.first_run + k] - sb);
+    s_rec[k] = runs[ch.first_run + k];
+  }
+  if (threadIdx.x < 32) s_cnt[threadIdx.x] = 0u;
   __syncthreads();
+  uint64_t packed[kOrderPer];
   unsigned cls[kOrderPer], rk[kOrderPer];
 #pragma unroll
   for (int k = 0; k < kOrderPer; ++k) {
     const int qi = threadIdx.x + k * kOrderThreads;
     cls[k] = 32u;
     if (qi < nsb) {
-      cls[k] = (unsigned)(packed[k] >> 48) & 31u;
-      rk[k] = atomicAdd(&s_cnt[cls[k]], 1u);
+      int lo = 0, hi = nst - 1;
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (s_off[mid] <= qi) lo = mid;
+        else hi = mid - 1;
+      }
+      const uint64_t rec = s_rec[lo];
+      const int64_t row = (int64_t)(rec >> 32);
+      const int64_t c = (int64_t)((rec >> 16) & 0xffff) + (qi - s_off[lo]);
+      packed[k] = ((uint64_t)row << 16) | (uint64_t)c;
+      cls[k] = vis_class[row * nchan + c];
     }
   }
+#pragma unroll
+  for (int k = 0; k < kOrderPer; ++k)
+    if (cls[k] < 32u) rk[k] = atomicAdd(&s_cnt[cls[k]], 1u);
   __syncthreads();
   unsigned cnt[32], maxcnt = 0;
 #pragma unroll
@@ -297,19 +287,15 @@ __global__ __launch_bounds__(kOrderThreads) void order_kernel(const Chunk* __res
   __syncthreads();
 #pragma unroll
   for (int k = 0; k < kOrderPer; ++k)
-    if (cls[k] < 32u)
-      list[sb + s_S[rk[k]] + __popc(s_M[rk[k]] & ((1u << cls[k]) - 1u))] = packed[k] & 0xffffffffffffull;
+    if (cls[k] < 32u) perm[sb + s_S[rk[k]] + __popc(s_M[rk[k]] & ((1u << cls[k]) - 1u))] = packed[k];
 }
 
 hipError_t launch_order(const uint8_t* vis_class, int64_t nchan, const uint64_t* runs, const int64_t* run_goff,
-                        int64_t nruns, const Chunk* windows, int64_t nwindows, uint64_t* perm, hipStream_t s) {
+                        const int64_t* tile_run_off, const Chunk* windows, int64_t nwindows, uint64_t* perm,
+                        hipStream_t s) {
   if (nwindows <= 0) return hipSuccess;
-  int64_t nb = (nruns + 255) / 256;
-  if (nb > 16384) nb = 16384;
-  expand_kernel<<<dim3((unsigned)nb), dim3(256), 0, s>>>(vis_class, nchan, runs, run_goff, nruns, perm);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return e;
-  order_kernel<<<dim3((unsigned)nwindows), dim3(kOrderThreads), 0, s>>>(windows, perm);
+  order_kernel<<<dim3((unsigned)nwindows), dim3(kOrderThreads), 0, s>>>(vis_class, nchan, runs, run_goff, tile_run_off,
+                                                                        windows, nwindows, perm);
   return hipGetLastError();
 }
 

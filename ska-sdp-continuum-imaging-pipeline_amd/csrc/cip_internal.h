@@ -31,24 +31,25 @@ hipError_t launch_freq_scale(const double* freq, int64_t nchan, double* fx, hipS
 // per-row w range over channels (only f min/max matter): out[0]=min, out[1]=max
 hipError_t launch_w_range(const double* uvw, int64_t nrow, double fxmin, double fxmax, double* partial,
                           int nblocks, hipStream_t s);
-// place pass: per-visibility bank class, runs parked with their tile keys
-// (park_* hold 64 slots per 64-visibility segment, seg_nruns[seg] the used
-// ones), and per-block {sum w, max |w V|} partials (2 * plan_place_blocks(n)).
+// place pass: per-visibility bank class, the runs of place block b (4096
+// visibilities) parked with their tile keys at slots [4096 b, 4096 b +
+// blk_cnt[b]), and per-block {sum w, max |w V|} partials (2 * plan_place_blocks).
 // err_flag: bit 0 non-finite uvw / w off the stack, bit 1 non-finite vis or weight.
 int plan_place_blocks(int64_t nvis);
 hipError_t launch_plan_place(const double* uvw, int64_t nrow, const double* fx, int64_t nchan,
                              const void* vis, int vis_dtype, const void* wgt, int wgt_dtype, const GridGeometry& g,
-                             unsigned* err_flag, uint8_t* vis_class, int64_t* seg_nruns, uint32_t* park_key,
+                             unsigned* err_flag, uint8_t* vis_class, int64_t* blk_cnt, uint32_t* park_key,
                              uint64_t* park_run, double* partial, hipStream_t s);
-// parked runs -> dense (seg_off: exclusive scan of seg_nruns, nseg + 1 entries)
-hipError_t launch_compact_runs(int64_t nseg, const int64_t* seg_off, const uint32_t* park_key,
-                               const uint64_t* park_run, uint32_t* key_out, uint64_t* run_out, hipStream_t s);
-// one stable LSD radix sort pass on digit (key >> shift) & 255. hist holds
-// 256 * radix_blocks(n) + 1 entries, exclusive-scanned between the two calls.
+// one stable LSD radix sort pass on digit (key >> shift) & 255 over nblocks
+// blocks of 4096 slots: dense (blk_cnt NULL, n items) or the place pass's
+// parked runs (blk_cnt). hist: 256 * nblocks + 1 entries, exclusive-scanned
+// between the two calls (its last entry then holds the item count).
 int64_t radix_blocks(int64_t n);
-hipError_t launch_radix_hist(const uint32_t* keys, int64_t n, int shift, int64_t* hist, hipStream_t s);
-hipError_t launch_radix_scatter(const uint32_t* keys, const uint64_t* vals, int64_t n, int shift,
-                                const int64_t* hist, uint32_t* keys_out, uint64_t* vals_out, hipStream_t s);
+hipError_t launch_radix_hist(const uint32_t* keys, int64_t n, const int64_t* blk_cnt, int64_t nblocks, int shift,
+                             int64_t* hist, hipStream_t s);
+hipError_t launch_radix_scatter(const uint32_t* keys, const uint64_t* vals, int64_t n, const int64_t* blk_cnt,
+                                int64_t nblocks, int shift, const int64_t* hist, uint32_t* keys_out,
+                                uint64_t* vals_out, hipStream_t s);
 hipError_t launch_tile_offsets(const uint32_t* keys, int64_t nruns, int64_t ntiles, int64_t* tile_run_off,
                                hipStream_t s);
 hipError_t launch_tile_vis(const int64_t* run_goff, const int64_t* tile_run_off, int64_t ntiles,
@@ -78,7 +79,8 @@ hipError_t launch_scatter(int support, int vis_dtype, int wgt_dtype, bool packed
 // bank-class sorted within each window (the tiles split into <= kOrderWindow
 // pieces by chunk_emit with cv = kOrderWindow)
 hipError_t launch_order(const uint8_t* vis_class, int64_t nchan, const uint64_t* runs, const int64_t* run_goff,
-                        int64_t nruns, const Chunk* windows, int64_t nwindows, uint64_t* perm, hipStream_t s);
+                        const int64_t* tile_run_off, const Chunk* windows, int64_t nwindows, uint64_t* perm,
+                        hipStream_t s);
 hipError_t launch_crop_correct_2d(const double* grid, const GridGeometry& g, int64_t npix_x, int64_t npix_y,
                                   const double* cx, const double* cy, double* dirty, hipStream_t s);
 hipError_t launch_wplane_accumulate(const double* grid, const GridGeometry& g, int64_t npix_x, int64_t npix_y,

@@ -138,24 +138,30 @@ hipError_t launch_w_range(const double* uvw, int64_t nrow, double fxmin, double 
 // global atomics: scattered device-scope atomics execute at the memory side
 // at ~10-25 G/s on MI355X, which made an atomic counting sort of the 13 M
 // runs of C3 cost more than 1 ms).
+constexpr int kPlaceSegs = 64;  // 64-visibility segments per place block (4096 visibilities)
+
 template <typename VisT, int WK>
 __global__ __launch_bounds__(256) void plan_place_kernel(const double* __restrict__ uvw, int64_t nrow,
                                                          const double* __restrict__ fx, int64_t nchan,
                                                          const VisT* __restrict__ vis, const void* __restrict__ wgt,
                                                          GridGeometry g, unsigned* err_flag,
                                                          uint8_t* __restrict__ vis_class,
-                                                         int64_t* __restrict__ seg_nruns,
+                                                         int64_t* __restrict__ blk_cnt,
                                                          uint32_t* __restrict__ park_key,
                                                          uint64_t* __restrict__ park_run, double* partial) {
-  const int lane = threadIdx.x & 63;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  __shared__ unsigned s_nruns;
+  if (threadIdx.x == 0) s_nruns = 0u;
+  __syncthreads();
   // fused prep reduction (sum of weights, max |w V|), fixed order
   double wsum = 0.0, wvmax = 0.0;
   bool nonfinite = false;
   const int64_t nvis = nrow * nchan;
   const int64_t nseg = (nvis + 63) / 64;
   const int P = kTile + g.support - 1;
-  for (int64_t seg = ((int64_t)blockIdx.x * 256 + threadIdx.x) / 64; seg < nseg;
-       seg += (int64_t)gridDim.x * 4) {
+  // block b owns segments [64 b, 64 b + 64): wave w takes every 4th
+  for (int64_t seg = (int64_t)blockIdx.x * kPlaceSegs + wave; seg < nseg && seg < ((int64_t)blockIdx.x + 1) * kPlaceSegs;
+       seg += 4) {
     const int64_t i = seg * 64 + lane;
     const bool valid = i < nvis;
     int64_t key = -1, r = 0, c = 0;
@@ -196,13 +202,16 @@ __global__ __launch_bounds__(256) void plan_place_kernel(const double* __restric
     const bool emit = start && key >= 0;
     const unsigned long long emits = __ballot(emit);
     const int nvalid = __popcll(__ballot(valid));  // wave-uniform: outside the branch
-    if (lane == 0) seg_nruns[seg] = __popcll(emits);
+    // the block's runs are parked densely from slot 64 * kPlaceSegs * b on
+    unsigned wbase = 0;
+    if (lane == 0 && emits) wbase = atomicAdd(&s_nruns, (unsigned)__popcll(emits));
+    wbase = __shfl(wbase, 0, 64);
     if (emit) {
       const unsigned long long above = starts & ~((2ull << lane) - 1ull);  // lane 63: 2 << 63 == 0
       const int next = above ? (__ffsll((long long)above) - 1) : nvalid;
-      const int slot = __popcll(emits & ((1ull << lane) - 1ull));
-      park_key[seg * 64 + slot] = (uint32_t)key;
-      park_run[seg * 64 + slot] = ((uint64_t)r << 32) | ((uint64_t)c << 16) | (uint64_t)(c + (next - lane));
+      const int64_t slot = (int64_t)blockIdx.x * kPlaceSegs * 64 + wbase + __popcll(emits & ((1ull << lane) - 1ull));
+      park_key[slot] = (uint32_t)key;
+      park_run[slot] = ((uint64_t)r << 32) | ((uint64_t)c << 16) | (uint64_t)(c + (next - lane));
     }
   }
   if (nonfinite) atomicOr(err_flag, 2u);
@@ -219,25 +228,26 @@ __global__ __launch_bounds__(256) void plan_place_kernel(const double* __restric
   if (threadIdx.x == 0) {
     partial[2 * blockIdx.x] = (ss[0] + ss[1]) + (ss[2] + ss[3]);
     partial[2 * blockIdx.x + 1] = fmax(fmax(sm[0], sm[1]), fmax(sm[2], sm[3]));
+    blk_cnt[blockIdx.x] = s_nruns;
   }
 }
 
 static unsigned plan_blocks(int64_t nvis) {
   const int64_t segs = (nvis + 63) / 64;
-  const int64_t b = (segs + 3) / 4;
-  return (unsigned)(b < 16384 ? (b > 0 ? b : 1) : 16384);
+  const int64_t b = (segs + kPlaceSegs - 1) / kPlaceSegs;
+  return (unsigned)(b > 0 ? b : 1);
 }
 
 int plan_place_blocks(int64_t nvis) { return (int)plan_blocks(nvis); }
 
 hipError_t launch_plan_place(const double* uvw, int64_t nrow, const double* fx, int64_t nchan,
                              const void* vis, int vis_dtype, const void* wgt, int wgt_dtype, const GridGeometry& g,
-                             unsigned* err_flag, uint8_t* vis_class, int64_t* seg_nruns, uint32_t* park_key,
+                             unsigned* err_flag, uint8_t* vis_class, int64_t* blk_cnt, uint32_t* park_key,
                              uint64_t* park_run, double* partial, hipStream_t s) {
   const dim3 gd(plan_blocks(nrow * nchan));
 #define PLACE(VT, WKV)                                                                                           \
   plan_place_kernel<VT, WKV><<<gd, dim3(256), 0, s>>>(uvw, nrow, fx, nchan, (const VT*)vis, wgt, g, err_flag,  \
-                                                      vis_class, seg_nruns, park_key, park_run, partial)
+                                                      vis_class, blk_cnt, park_key, park_run, partial)
   if (vis_dtype == CIP_C64) {
     if (wgt_dtype == CIP_F32) PLACE(float2, WK_F32);
     else if (wgt_dtype == CIP_F64) PLACE(float2, WK_F64);
@@ -253,53 +263,66 @@ hipError_t launch_plan_place(const double* uvw, int64_t nrow, const double* fx, 
 
 // ---------------------------------------------------------- radix sort ----
 // Stable LSD radix sort of (uint32 key, uint64 run) pairs, 8-bit digits.
-// A block ranks 4096 items (16 per thread, striped: item k * 256 + tid, all
-// loaded up front), so item order within a block is (k, tid) = input order.
-// Per k each wave ranks its 64 items by digit with 8 ballots (peer mask), the
-// waves' digit counts meet in LDS, and a running per-digit offset carries
-// across k. Global bases come from the exclusive scan of the digit-major
-// histogram hist[d * nblocks + b] (plus one trailing entry: after the scan it
-// holds the item count).
+// A block owns 4096 input slots; wave w ranks slots [1024 w, 1024 w + 1024)
+// in order, 64 at a time (8 ballots give each lane its digit's peer mask; a
+// wave-private LDS counter per digit carries the rank across steps, read by
+// every lane and then advanced by the digit's first lane - one wave's LDS ops
+// execute in order, so no barrier is needed). One barrier, a per-digit prefix
+// over the 4 waves, and each item lands at base[d] + its rank: the order of a
+// digit's items is the input order (stable). Global bases: the exclusive scan
+// of the digit-major histogram hist[d * nblocks + b] (+1 trailing entry: the
+// item count). Input: dense (slots [4096 b, 4096 b + 4096) of n), or the
+// place pass's per-block runs (slots [4096 b, 4096 b + blk_cnt[b])).
 constexpr int kRadixThreads = 256;
 constexpr int kRadixPer = 16;
 constexpr int64_t kRadixBlock = (int64_t)kRadixThreads * kRadixPer;
+static_assert(kRadixBlock == 64 * 64, "a radix block covers one place block's park region");
+
+__device__ __forceinline__ int64_t radix_count(int64_t b, int64_t n, const int64_t* __restrict__ blk_cnt) {
+  if (blk_cnt) return blk_cnt[b];
+  const int64_t rem = n - b * kRadixBlock;
+  return rem < kRadixBlock ? rem : kRadixBlock;
+}
 
 __global__ __launch_bounds__(kRadixThreads) void radix_hist_kernel(const uint32_t* __restrict__ keys, int64_t n,
-                                                                   int shift, int64_t nblocks,
-                                                                   int64_t* __restrict__ hist) {
+                                                                   const int64_t* __restrict__ blk_cnt, int shift,
+                                                                   int64_t nblocks, int64_t* __restrict__ hist) {
   __shared__ unsigned cnt[256];
   cnt[threadIdx.x] = 0u;
   __syncthreads();
-  const int64_t i0 = (int64_t)blockIdx.x * kRadixBlock + threadIdx.x;
-#pragma unroll
-  for (int k = 0; k < kRadixPer; ++k) {
-    const int64_t i = i0 + (int64_t)k * kRadixThreads;
-    if (i < n) atomicAdd(&cnt[(keys[i] >> shift) & 255u], 1u);
-  }
+  const int64_t cnt_b = radix_count(blockIdx.x, n, blk_cnt);
+  const uint32_t* kb = keys + (int64_t)blockIdx.x * kRadixBlock;
+  for (int64_t i = threadIdx.x; i < cnt_b; i += kRadixThreads) atomicAdd(&cnt[(kb[i] >> shift) & 255u], 1u);
   __syncthreads();
   hist[(int64_t)threadIdx.x * nblocks + blockIdx.x] = cnt[threadIdx.x];
   if (blockIdx.x == 0 && threadIdx.x == 0) hist[256 * nblocks] = 0;
 }
 
 __global__ __launch_bounds__(kRadixThreads) void radix_scatter_kernel(
-    const uint32_t* __restrict__ keys, const uint64_t* __restrict__ vals, int64_t n, int shift, int64_t nblocks,
-    const int64_t* __restrict__ hist, uint32_t* __restrict__ keys_out, uint64_t* __restrict__ vals_out) {
-  __shared__ unsigned wcnt[4][256];  // per-wave digit counts of the current k
-  __shared__ int64_t base[256];      // global base + running offset per digit
+    const uint32_t* __restrict__ keys, const uint64_t* __restrict__ vals, int64_t n,
+    const int64_t* __restrict__ blk_cnt, int shift, int64_t nblocks, const int64_t* __restrict__ hist,
+    uint32_t* __restrict__ keys_out, uint64_t* __restrict__ vals_out) {
+  __shared__ unsigned wcnt[4][256];  // per-wave running digit counts
+  __shared__ int64_t woff[4][256];   // global position of each wave's first item per digit
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int64_t i0 = (int64_t)blockIdx.x * kRadixBlock + threadIdx.x;
+  const int64_t cnt_b = radix_count(blockIdx.x, n, blk_cnt);
+  const int64_t i0 = (int64_t)blockIdx.x * kRadixBlock + wave * 1024 + lane;
+  const int64_t lim = (int64_t)blockIdx.x * kRadixBlock + cnt_b;
+#pragma unroll
+  for (int w = 0; w < 4; ++w) wcnt[w][threadIdx.x] = 0u;
   uint32_t key[kRadixPer];
   uint64_t val[kRadixPer];
 #pragma unroll
   for (int k = 0; k < kRadixPer; ++k) {
-    const int64_t i = i0 + (int64_t)k * kRadixThreads;
-    key[k] = i < n ? keys[i] : 0u;
-    val[k] = i < n ? vals[i] : 0ull;
+    const int64_t i = i0 + k * 64;
+    key[k] = i < lim ? keys[i] : 0u;
+    val[k] = i < lim ? vals[i] : 0ull;
   }
-  base[threadIdx.x] = hist[(int64_t)threadIdx.x * nblocks + blockIdx.x];
+  __syncthreads();
+  unsigned rank[kRadixPer];
 #pragma unroll
   for (int k = 0; k < kRadixPer; ++k) {
-    const bool valid = i0 + (int64_t)k * kRadixThreads < n;
+    const bool valid = i0 + k * 64 < lim;
     const unsigned d = (key[k] >> shift) & 255u;
     unsigned long long peers = __ballot(valid);
 #pragma unroll
@@ -308,59 +331,28 @@ __global__ __launch_bounds__(kRadixThreads) void radix_scatter_kernel(
       const unsigned long long m = __ballot(bit);
       peers &= bit ? m : ~m;
     }
-    const unsigned rank = (unsigned)__popcll(peers & ((1ull << lane) - 1ull));
-    wcnt[0][threadIdx.x] = 0u;
-    wcnt[1][threadIdx.x] = 0u;
-    wcnt[2][threadIdx.x] = 0u;
-    wcnt[3][threadIdx.x] = 0u;
-    __syncthreads();
-    if (valid && rank == 0) wcnt[wave][d] = (unsigned)__popcll(peers);
-    __syncthreads();
-    // wave prefix per digit; the running base advances by the k-step total
-    const unsigned c0 = wcnt[0][threadIdx.x], c1 = wcnt[1][threadIdx.x], c2 = wcnt[2][threadIdx.x],
-                   c3 = wcnt[3][threadIdx.x];
-    wcnt[0][threadIdx.x] = 0u;
-    wcnt[1][threadIdx.x] = c0;
-    wcnt[2][threadIdx.x] = c0 + c1;
-    wcnt[3][threadIdx.x] = c0 + c1 + c2;
-    const int64_t b0 = base[threadIdx.x];
-    __syncthreads();
-    if (valid) {
-      const int64_t pos = base[d] + wcnt[wave][d] + rank;
+    const unsigned prior = valid ? wcnt[wave][d] : 0u;
+    rank[k] = prior + (unsigned)__popcll(peers & ((1ull << lane) - 1ull));
+    if (valid && (peers & ((1ull << lane) - 1ull)) == 0ull) wcnt[wave][d] = prior + (unsigned)__popcll(peers);
+  }
+  __syncthreads();
+  {
+    const int d = threadIdx.x;
+    int64_t o = hist[(int64_t)d * nblocks + blockIdx.x];
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      woff[w][d] = o;
+      o += wcnt[w][d];
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < kRadixPer; ++k)
+    if (i0 + k * 64 < lim) {
+      const int64_t pos = woff[wave][(key[k] >> shift) & 255u] + rank[k];
       keys_out[pos] = key[k];
       vals_out[pos] = val[k];
     }
-    __syncthreads();
-    base[threadIdx.x] = b0 + c0 + c1 + c2 + c3;
-  }
-}
-
-// the parked runs of each segment -> dense arrays at the scanned offsets
-__global__ void compact_runs_kernel(int64_t nseg, const int64_t* __restrict__ seg_off,
-                                    const uint32_t* __restrict__ park_key, const uint64_t* __restrict__ park_run,
-                                    uint32_t* __restrict__ key_out, uint64_t* __restrict__ run_out) {
-  // one wave per 4 segments (loads of all four issued together), grid-stride
-  const int j = threadIdx.x & 63;
-  for (int64_t seg0 = (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6) * 4; seg0 < nseg;
-       seg0 += (((int64_t)gridDim.x * blockDim.x) >> 6) * 4) {
-    int64_t o[5];
-#pragma unroll
-    for (int k = 0; k < 5; ++k) o[k] = seg_off[seg0 + k < nseg ? seg0 + k : nseg];
-    uint32_t kk[4];
-    uint64_t rr[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const bool v = j < o[k + 1] - o[k];
-      kk[k] = v ? park_key[(seg0 + k) * 64 + j] : 0u;
-      rr[k] = v ? park_run[(seg0 + k) * 64 + j] : 0ull;
-    }
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-      if (j < o[k + 1] - o[k]) {
-        key_out[o[k] + j] = kk[k];
-        run_out[o[k] + j] = rr[k];
-      }
-  }
 }
 
 // tile_run_off[t] = first sorted run with key >= t (t in [0, ntiles])
@@ -379,28 +371,19 @@ __global__ void tile_offsets_kernel(const uint32_t* __restrict__ keys, int64_t n
 
 int64_t radix_blocks(int64_t n) { return (n + kRadixBlock - 1) / kRadixBlock; }
 
-hipError_t launch_radix_hist(const uint32_t* keys, int64_t n, int shift, int64_t* hist, hipStream_t s) {
-  const int64_t nb = radix_blocks(n);
-  if (nb == 0) return hipSuccess;
-  radix_hist_kernel<<<dim3((unsigned)nb), dim3(kRadixThreads), 0, s>>>(keys, n, shift, nb, hist);
+hipError_t launch_radix_hist(const uint32_t* keys, int64_t n, const int64_t* blk_cnt, int64_t nblocks, int shift,
+                             int64_t* hist, hipStream_t s) {
+  if (nblocks == 0) return hipSuccess;
+  radix_hist_kernel<<<dim3((unsigned)nblocks), dim3(kRadixThreads), 0, s>>>(keys, n, blk_cnt, shift, nblocks, hist);
   return hipGetLastError();
 }
 
-hipError_t launch_radix_scatter(const uint32_t* keys, const uint64_t* vals, int64_t n, int shift,
-                                const int64_t* hist, uint32_t* keys_out, uint64_t* vals_out, hipStream_t s) {
-  const int64_t nb = radix_blocks(n);
-  if (nb == 0) return hipSuccess;
-  radix_scatter_kernel<<<dim3((unsigned)nb), dim3(kRadixThreads), 0, s>>>(keys, vals, n, shift, nb, hist, keys_out,
-                                                                          vals_out);
-  return hipGetLastError();
-}
-
-hipError_t launch_compact_runs(int64_t nseg, const int64_t* seg_off, const uint32_t* park_key,
-                               const uint64_t* park_run, uint32_t* key_out, uint64_t* run_out, hipStream_t s) {
-  if (nseg == 0) return hipSuccess;
-  const int64_t nb = (nseg + 15) / 16;
-  compact_runs_kernel<<<dim3((unsigned)(nb < 16384 ? nb : 16384)), dim3(256), 0, s>>>(nseg, seg_off, park_key,
-                                                                                      park_run, key_out, run_out);
+hipError_t launch_radix_scatter(const uint32_t* keys, const uint64_t* vals, int64_t n, const int64_t* blk_cnt,
+                                int64_t nblocks, int shift, const int64_t* hist, uint32_t* keys_out,
+                                uint64_t* vals_out, hipStream_t s) {
+  if (nblocks == 0) return hipSuccess;
+  radix_scatter_kernel<<<dim3((unsigned)nblocks), dim3(kRadixThreads), 0, s>>>(keys, vals, n, blk_cnt, shift, nblocks,
+                                                                              hist, keys_out, vals_out);
   return hipGetLastError();
 }
 
