@@ -15,9 +15,10 @@ from pathlib import Path
 
 def short(name: str) -> str:
     name = name.split("(")[0]
-    for key in ("scatter_kernel", "plan_kernel<true>", "plan_kernel<false>", "prep_kernel", "fft_rtc",
-                "transpose_rtc", "crop_correct", "scan_local", "scan_add", "run_lengths", "tile_vis",
-                "chunk_emit", "chunk_counts", "fillBuffer"):
+    for key in ("scatter_kernel", "plan_place_kernel", "radix_scatter", "radix_hist", "order_kernel",
+                "fft_rows_kernel", "fft_cols_kernel", "fft_rtc", "transpose_rtc", "crop_correct", "scan_local",
+                "scan_add", "run_lengths", "tile_vis", "tile_offsets", "chunk_emit", "chunk_counts",
+                "prep_final", "fillBuffer"):
         if key in name:
             return key
     return name[-60:]
