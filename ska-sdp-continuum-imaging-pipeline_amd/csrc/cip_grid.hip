@@ -232,7 +232,10 @@ __global__ __launch_bounds__(kOrderThreads) void order_kernel(const uint8_t* __r
     const Chunk nx = windows[blockIdx.x + 1];
     if (nx.tile == ch.tile) last = nx.first_run;
   }
-  const int nst = (int)(last - ch.first_run + 1);
+  // (a window of n positions meets at most n slices: the next window may
+  // start exactly at a slice boundary, whose slice is then not this window's)
+  const int64_t nst64 = last - ch.first_run + 1;
+  const int nst = (int)(nst64 < nsb ? nst64 : nsb);
   for (int k = threadIdx.x; k < nst; k += kOrderThreads) {
     s_off[k] = (int)(run_goff[ch.first_run + k] - sb);
     s_rec[k] = runs[ch.first_run + k];

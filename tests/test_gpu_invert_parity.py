@@ -233,3 +233,16 @@ def test_repeatable(gpu_device):
     # per-chunk sums are exact (fixed point); only the fp64 order of the
     # global flush adds may differ between runs
     assert np.abs(a - b).max() <= 1e-13 * np.abs(a).max()
+
+
+def test_dense_single_channel_tiles(gpu_device):
+    # one channel, a small grid: every row slice holds one visibility and the
+    # tiles hold thousands of them, so bank-ordering windows meet 1024 slices
+    uvw, f, vis, w = _case(30_000, 1, n_ant=40, radius=1500.0)
+    npix = 64
+    px = syn.pixel_size_for_grid(uvw, f, npix) * 2.5
+    gpu = gridder.ms2dirty(uvw, f, vis.astype(np.complex128), w.astype(np.float64), npix, npix, px, px,
+                           support=8, do_wstacking=False)
+    ref = oracle.ms2dirty(uvw, f, vis, w, npix, npix, px, px, support=8, do_wstacking=False)
+    sumw = float(w.astype(np.float64).sum())
+    assert _norm_err(gpu, ref, sumw) < TIGHT

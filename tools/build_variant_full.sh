@@ -6,7 +6,7 @@ set -e
 name=$1; defs=$2
 cd "$(dirname "$0")/../ska-sdp-continuum-imaging-pipeline_amd/csrc"
 mkdir -p build_$name ../../tools/variants
-for f in cip_api cip_plan cip_grid cip_tiling; do
+for f in $(ls *.hip | sed "s/\.hip$//"); do
   /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -fPIC -munsafe-fp-atomics -I../../include -I. $defs \
     -c $f.hip -o build_$name/$f.o &
 done
