@@ -216,6 +216,16 @@ def main():
         "bytes_per_launch_alg": int(bytes_launch),
         "launch_ms": round(scatter_ms, 4),
     }
+    # the bound that actually limits the scatter: LDS atomic bytes. Each tap is
+    # a 64-bit fixed-point add to the re and the im plane (16 B of LDS RMW),
+    # and gfx950 sustains one conflict-free 64-lane ds_add_u64 per 8.12
+    # CU-cycles (tools/microbench/lds_ops.hip, profiles/microbench_r01.txt).
+    lds_bytes = vis_per_launch * params.support ** 2 * 16
+    lds_peak = 64 * 8 / 8.12 * 2.4e9 * 256 / 1e9  # GB/s: 256 CUs at 2.4 GHz
+    lds_achieved = lds_bytes / (scatter_ms * 1e-3) / 1e9
+    roofline["lds_atomic"] = {"achieved": round(lds_achieved, 1), "peak": round(lds_peak, 1), "unit": "GB/s",
+                              "frac": round(lds_achieved / lds_peak, 4),
+                              "basis": "16 B of ds_add_u64 per tap; 8.12 CU-cycles per conflict-free wave-instr"}
     tr = traffic_from_profiles(args.config)
     if tr and not args.wstacking:
         roofline["traffic"] = tr.get("hbm_bytes_per_launch")
