@@ -198,12 +198,13 @@ def main():
     scatter_ms = avg["scatter_ms"] / launches
     P = params.nplanes
     taps = params.support ** (3 if args.wstacking else 2)
-    # algorithmic bytes of one scatter launch: every visibility's value (c64,
-    # 8 B), weight (f32, 4 B) and ordered-stream record (8 B) once per plane it
-    # feeds, each row's uvw (24 B) once, and the plane's grid written once
-    # (SURVEY.md 8(d) B_alg; the read-back of the grid belongs to the FFT)
+    # algorithmic bytes of one scatter launch, design-independent (SURVEY.md
+    # 8(d) B_alg): every visibility's value (c64, 8 B) and weight (f32, 4 B)
+    # once per plane it feeds, 32 B per row slice (uvw + channel range) and the
+    # plane's grid written once (its read-back belongs to the FFT). The
+    # ordered-stream record this design adds (8 B/vis) is not counted.
     vis_per_launch = nvis * (params.support if args.wstacking else 1) / (P if args.wstacking else 1)
-    bytes_launch = vis_per_launch * (8 + 4 + 8) + cfg["rows"] * 24 + params.nu * params.nv * 16
+    bytes_launch = vis_per_launch * (8 + 4) + runs / launches * 32 + params.nu * params.nv * 16
     achieved = bytes_launch / (scatter_ms * 1e-3) / 1e9
     roofline = {
         "bound": "hbm",
