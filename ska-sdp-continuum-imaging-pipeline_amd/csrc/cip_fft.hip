@@ -141,6 +141,12 @@ __device__ __forceinline__ void exchange(double2* v, int t, int ns, double* lds)
   }
 }
 
+// Pass A output block width (columns i per contiguous row of a block).
+#ifndef CIP_FFT_COLBLOCK
+#define CIP_FFT_COLBLOCK 8
+#endif
+constexpr int kColBlock = CIP_FFT_COLBLOCK;
+
 // All passes of an N-point transform (log2 N = 4 P + B: P radix-16 passes,
 // then one radix-2^B pass). On return v[m * RF + r] holds frequency
 // out_pos<N, RF>(t, m, r, N / RF).
@@ -192,7 +198,7 @@ __global__ __launch_bounds__(N / 16) void fft_rows_kernel(const double2* __restr
     for (int r = 0; r < S::RF; ++r) {
       const int k = out_pos<N, S::RF>(t, m, r, N / S::RF);
       const int64_t i = (int64_t)((k + (int)(nx / 2)) & (N - 1));
-      if (i < nx) H[((i >> 3) * nv + y) * 8 + (i & 7)] = v[m * S::RF + r];
+      if (i < nx) H[((i / kColBlock) * nv + y) * kColBlock + (i % kColBlock)] = v[m * S::RF + r];
     }
 }
 
@@ -219,11 +225,13 @@ __global__ __launch_bounds__(N / 16) void fft_cols_kernel(const double2* __restr
   const int t = threadIdx.x;
   const int64_t b = blockIdx.x;
   int64_t i = b;
-  if (nx % 64 == 0) i = (b & ~63ll) + ((b & 7) << 3) + ((b >> 3) & 7);
-  const double2* col = H + ((i >> 3) * N) * 8 + (i & 7);
+  // a group of 8 kColBlock consecutive blocks -> one column block per XCD
+  if (nx % (8 * kColBlock) == 0)
+    i = (b / (8 * kColBlock)) * (8 * kColBlock) + (b % 8) * kColBlock + (b / 8) % kColBlock;
+  const double2* col = H + ((i / kColBlock) * N) * kColBlock + (i % kColBlock);
   double2 v[16];
 #pragma unroll
-  for (int r = 0; r < 16; ++r) v[r] = col[(int64_t)(t + r * S::T) * 8];
+  for (int r = 0; r < 16; ++r) v[r] = col[(int64_t)(t + r * S::T) * kColBlock];
   fft_core<N>(v, t, lds, tw);
   const int64_t p = i - nx / 2;
   double* orow = ep.out + i * ny;
@@ -256,7 +264,7 @@ __global__ __launch_bounds__(N / 16) void fft_cols_kernel(const double2* __restr
 static bool fft_len_ok(int64_t n) { return n == 1024 || n == 2048 || n == 4096 || n == 8192; }
 
 bool fast_fft_supported(int64_t nu, int64_t nv, int64_t nx, int64_t ny) {
-  return fft_len_ok(nu) && fft_len_ok(nv) && nx > 0 && ny > 0 && nx <= nu && ny <= nv && nx % 8 == 0 &&
+  return fft_len_ok(nu) && fft_len_ok(nv) && nx > 0 && ny > 0 && nx <= nu && ny <= nv && nx % kColBlock == 0 &&
          ny % 2 == 0;
 }
 
