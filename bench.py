@@ -142,7 +142,7 @@ def main():
     import torch.distributed as dist
 
     from ska_sdp_cip_amd import _lib, gridder
-    from ska_sdp_cip_amd.distributed import reduce_images
+    from ska_sdp_cip_amd.distributed import image_buffer, reduce_images
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -156,8 +156,7 @@ def main():
     nvis = cfg["rows"] * cfg["nchan"]
     npix = cfg["npix"]
     uvw_d, freq_d, vis_d, wgt_d, px, uvw_h, freq_h = make_inputs(cfg, rank, world, device)
-    dirty = torch.empty((npix, npix), dtype=torch.float64, device=device)
-    sumw = torch.zeros(1, dtype=torch.float64, device=device)
+    dirty, sumw = image_buffer(npix, npix, device)  # adjacent: one RCCL reduce per step
 
     def step():
         gridder.device_ms2dirty(uvw_d, freq_d, vis_d, wgt_d, npix, npix, px, px, support=args.support,

@@ -37,14 +37,33 @@ def reduce_images(dirty, sum_weights, *, dst: int = 0, group=None, normalise: bo
     import torch.distributed as dist  # pylint: disable=import-outside-toplevel
 
     if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
-        dist.reduce(dirty, dst, group=group)
-        dist.reduce(sum_weights, dst, group=group)
+        base = dirty.untyped_storage().data_ptr()
+        n = dirty.numel()
+        if (dirty.is_contiguous() and sum_weights.numel() == 1 and dirty.dtype == sum_weights.dtype
+                and sum_weights.untyped_storage().data_ptr() == base
+                and sum_weights.data_ptr() == dirty.data_ptr() + n * dirty.element_size()
+                and dirty.storage_offset() + n + 1 <= dirty.untyped_storage().nbytes() // dirty.element_size()):
+            # image and weight sum adjacent in one buffer (see image_buffer): one collective
+            flat = dirty.new_empty(0).set_(dirty.untyped_storage(), dirty.storage_offset(), (n + 1,), (1,))
+            dist.reduce(flat, dst, group=group)
+        else:
+            dist.reduce(dirty, dst, group=group)
+            dist.reduce(sum_weights, dst, group=group)
         is_dst = dist.get_rank() == dst
     else:
         is_dst = True
     if normalise and is_dst:
         dirty.div_(sum_weights)
     return dirty
+
+
+def image_buffer(npix_x: int, npix_y: int, device):
+    """(dirty (npix_x, npix_y), sum_weights (1,)) fp64 views of ONE buffer, so
+    reduce_images moves both with a single collective."""
+    import torch  # pylint: disable=import-outside-toplevel
+
+    buf = torch.zeros(npix_x * npix_y + 1, dtype=torch.float64, device=device)
+    return buf[:-1].view(npix_x, npix_y), buf[-1:]
 
 
 def invert_sharded(uvw, freq, vis, wgt, npix: int, pixsize: float, *, epsilon: float = 1e-4,
@@ -54,11 +73,9 @@ def invert_sharded(uvw, freq, vis, wgt, npix: int, pixsize: float, *, epsilon: f
     for its own rows. Returns the normalised dirty image on `dst` (the other
     ranks return their partial, unnormalised image).
     """
-    import torch  # pylint: disable=import-outside-toplevel
-
     from .gridder import device_ms2dirty  # pylint: disable=import-outside-toplevel
 
-    sumw = torch.zeros(1, dtype=torch.float64, device=vis.device)
+    out, sumw = image_buffer(npix, npix, vis.device)
     dirty, _ = device_ms2dirty(uvw, freq, vis, wgt, npix, npix, pixsize, pixsize, epsilon=epsilon,
-                               support=support, do_wstacking=do_wstacking, sum_weights=sumw)
+                               support=support, do_wstacking=do_wstacking, out=out, sum_weights=sumw)
     return reduce_images(dirty, sumw, dst=dst, group=group)

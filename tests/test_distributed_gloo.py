@@ -14,7 +14,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from ska_sdp_cip_amd.distributed import reduce_images, shard_rows
+from ska_sdp_cip_amd.distributed import image_buffer, reduce_images, shard_rows
 
 
 def _free_port():
@@ -25,7 +25,7 @@ def _free_port():
     return port
 
 
-def _worker(rank, world, port, npix, q):
+def _worker(rank, world, port, npix, q, fused=False):
     import sys
     from pathlib import Path
 
@@ -42,8 +42,13 @@ def _worker(rank, world, port, npix, q):
     px = syn.pixel_size_for_grid(uvw, f, npix)
     a, b = shard_rows(len(uvw), rank, world)
     part = oracle.ms2dirty(uvw[a:b], f, vis[a:b], w[a:b], npix, npix, px, px, support=8, nthreads=1)
-    img = torch.from_numpy(part.copy())
-    sw = torch.tensor([w[a:b].astype(np.float64).sum()], dtype=torch.float64)
+    if fused:  # image and weight sum in one buffer: a single collective
+        img, sw = image_buffer(npix, npix, "cpu")
+        img.copy_(torch.from_numpy(part))
+        sw.fill_(float(w[a:b].astype(np.float64).sum()))
+    else:
+        img = torch.from_numpy(part.copy())
+        sw = torch.tensor([w[a:b].astype(np.float64).sum()], dtype=torch.float64)
     reduce_images(img, sw, dst=0)
     if rank == 0:
         full = oracle.ms2dirty(uvw, f, vis, w, npix, npix, px, px, support=8, nthreads=1)
@@ -63,11 +68,12 @@ def test_shard_rows_cover_everything():
         shard_rows(10, 3, 3)
 
 
-def test_sharded_invert_reduce_world2():
+@pytest.mark.parametrize("fused", [False, True])
+def test_sharded_invert_reduce_world2(fused):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, 64, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, 64, q, fused)) for r in range(2)]
     for p in procs:
         p.start()
     for p in procs:
