@@ -113,6 +113,32 @@ def device_ms2dirty(
     return out, params
 
 
+def device_stokes_i(vis4: "torch.Tensor", flags4: "torch.Tensor", wgt4: "torch.Tensor"):
+    """
+    Stokes I on the device (cip_stokes_i; reference invert.py:72-116, bit-exact
+    with its numpy arithmetic): (nrow, nchan, 4) complex64 visibilities,
+    bool/uint8 flags and float32 weights -> (vis_i complex64 (nrow, nchan),
+    effective weights float32 (nrow, nchan)).
+    """
+    _require_gpu()
+    if vis4.dtype != torch.complex64 or wgt4.dtype != torch.float32:
+        raise ValueError("vis4 must be complex64 and wgt4 float32")
+    if vis4.dim() != 3 or vis4.shape[-1] != 4 or tuple(flags4.shape) != tuple(vis4.shape) or \
+            tuple(wgt4.shape) != tuple(vis4.shape):
+        raise ValueError("vis4, flags4, wgt4 must all have shape (nrow, nchan, 4)")
+    fl = flags4.to(torch.uint8) if flags4.dtype != torch.uint8 else flags4
+    for t in (vis4, fl, wgt4):
+        if not t.is_contiguous() or not t.is_cuda:
+            raise ValueError("device_stokes_i needs contiguous device tensors")
+    nrow, nchan = vis4.shape[0], vis4.shape[1]
+    vis_i = torch.empty((nrow, nchan), dtype=torch.complex64, device=vis4.device)
+    eff = torch.empty((nrow, nchan), dtype=torch.float32, device=vis4.device)
+    stream = torch.cuda.current_stream(vis4.device).cuda_stream
+    _lib.check(_lib.lib().cip_stokes_i(vis4.data_ptr(), fl.data_ptr(), wgt4.data_ptr(), nrow * nchan, stream,
+                                       vis_i.data_ptr(), None, None, eff.data_ptr()))
+    return vis_i, eff
+
+
 def ms2dirty(  # pylint: disable=too-many-arguments,unused-argument
     uvw,
     freq,

@@ -22,7 +22,7 @@ from typing import Any, Iterable, Optional
 import numpy as np
 from numpy.typing import NDArray
 
-from .gridder import device_ms2dirty, ms2dirty
+from .gridder import device_ms2dirty, device_stokes_i, ms2dirty
 
 # Reference call arguments (invert.py:170-183)
 EPSILON = 1e-4
@@ -100,12 +100,28 @@ def invert_measurement_set(
     epsilon: float = EPSILON,
     do_wstacking: bool = DO_WSTACKING,
     support: Optional[int] = None,
+    stokes_on_device: bool = False,
 ) -> NDArray:
     """
     Invert the given measurement set, returning a dirty image (reference
     :119-149): (1 / total_weight) * image, float32 (num_pixels, num_pixels).
     `nthreads` is accepted for signature compatibility (the GPU ignores it).
+    `stokes_on_device=True` ships the raw (nrow, nchan, 4) columns to the GPU
+    and forms Stokes I there (`device_invert`) instead of in
+    numpy as the reference does; the total weight is then summed in fp64 on
+    the device (the reference sums float32 in numpy).
     """
+    if stokes_on_device:
+        import torch  # pylint: disable=import-outside-toplevel
+
+        dev = torch.device("cuda", torch.cuda.current_device())
+        t = lambda a, dt=None: torch.from_numpy(np.ascontiguousarray(a, dtype=dt)).to(dev)  # noqa: E731
+        image = device_invert(
+            t(ms_reader.visibilities(), np.complex64), t(ms_reader.flags(), np.uint8),
+            t(ms_reader.weights(), np.float32), t(ms_reader.uvw(), np.float64),
+            t(ms_reader.channel_frequencies(), np.float64), num_pixels, pixel_size_asec,
+            epsilon=epsilon, do_wstacking=do_wstacking, support=support)
+        return image.to(torch.float32).cpu().numpy()
     gridding_input = StokesIGridderInput.from_measurement_set_reader(ms_reader)
     image, total_weight = ducc_invert(
         gridding_input, num_pixels, pixel_size_asec, nthreads=nthreads,
@@ -149,6 +165,32 @@ def ducc_invert(
             support=support,
         )
     return image, effective_weights.sum()
+
+
+def device_invert(
+    vis4, flags4, wgt4, uvw, freq,
+    num_pixels: int,
+    pixel_size_asec: float,
+    *,
+    epsilon: float = EPSILON,
+    do_wstacking: bool = DO_WSTACKING,
+    support: Optional[int] = None,
+):
+    """
+    Whole invert on device-resident raw columns: Stokes I and
+    effective weights by cip_stokes_i, the dirty image by cip_ms2dirty, the
+    total weight summed on the device, and the normalised fp64 image returned
+    as a device tensor. Arguments: vis4 (nrow, nchan, 4) complex64, flags4
+    bool/uint8, wgt4 float32, uvw (nrow, 3) f64, freq (nchan,) f64.
+    """
+    import torch  # pylint: disable=import-outside-toplevel
+
+    vis_i, eff = device_stokes_i(vis4, flags4, wgt4)
+    pix = pixel_size_lm(pixel_size_asec)
+    sumw = torch.zeros(1, dtype=torch.float64, device=vis_i.device)
+    dirty, _ = device_ms2dirty(uvw, freq, vis_i, eff, num_pixels, num_pixels, pix, pix, epsilon=epsilon,
+                              support=support, do_wstacking=do_wstacking, sum_weights=sumw)
+    return dirty.div_(sumw)
 
 
 def worker_ducc_invert(

@@ -116,3 +116,14 @@ def test_dask_invert_equals_serial(gpu_device):
     assert np.allclose(image, ref_image, atol=eps * abs(ref_image).max(), rtol=eps)
     image1 = dask_invert_measurement_set(ms, client, num_pixels=64, pixel_size_asec=5.0)
     assert np.allclose(image1, ref_image, atol=eps * abs(ref_image).max(), rtol=eps)
+
+
+def test_invert_with_stokes_on_device(gpu_device):
+    # raw (r, c, 4) columns to the GPU, Stokes I there
+    g, ms = _golden_ms()
+    host = invert_measurement_set(ms, 64, 5.0)
+    dev = invert_measurement_set(ms, 64, 5.0, stokes_on_device=True)
+    assert dev.dtype == np.float32 and dev.shape == host.shape
+    # identical Stokes-I inputs; only the total weight's summation differs
+    # (fp64 on the device, float32 numpy in the reference)
+    assert np.abs(dev - host).max() <= 2e-6 * np.abs(host).max()
