@@ -269,7 +269,30 @@ struct Workspace {
   std::vector<int64_t> corr_key;  // (npix_x, npix_y, nu, nv, W) of the cached cx / cy
   std::vector<double> fw_key;     // (W, dw |nmin|) of the cached w-correction table
   std::vector<int64_t> tw_ready;  // lengths whose FFT twiddle tables are on the device
+  // second stream: zeroes the first grid plane while the planner runs
+  hipStream_t side = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
 };
+
+// Zero `bytes` at `p` on the workspace's side stream, ordered after the work
+// already queued on s; join_side() makes s wait for it.
+static int zero_on_side(Workspace* ws, void* p, size_t bytes, hipStream_t s) {
+  if (!ws->side) {
+    CIP_HIP_CHECK(hipStreamCreateWithFlags(&ws->side, hipStreamNonBlocking));
+    CIP_HIP_CHECK(hipEventCreateWithFlags(&ws->ev_fork, hipEventDisableTiming));
+    CIP_HIP_CHECK(hipEventCreateWithFlags(&ws->ev_join, hipEventDisableTiming));
+  }
+  CIP_HIP_CHECK(hipEventRecord(ws->ev_fork, s));
+  CIP_HIP_CHECK(hipStreamWaitEvent(ws->side, ws->ev_fork, 0));
+  CIP_HIP_CHECK(hipMemsetAsync(p, 0, bytes, ws->side));
+  CIP_HIP_CHECK(hipEventRecord(ws->ev_join, ws->side));
+  return CIP_OK;
+}
+
+static int join_side(Workspace* ws, hipStream_t s) {
+  CIP_HIP_CHECK(hipStreamWaitEvent(s, ws->ev_join, 0));
+  return CIP_OK;
+}
 
 static std::mutex g_ws_mutex;
 static std::map<int, Workspace*> g_ws;
@@ -380,7 +403,7 @@ struct PlanResult {
   int64_t* run_goff = nullptr;
   int64_t* tile_run_off = nullptr;
   Chunk* chunks = nullptr;
-  uint64_t* perm = nullptr;  // bank-class ordered visibility stream, or NULL
+  uint32_t* perm = nullptr;  // bank-class ordered visibility stream, or NULL
 };
 
 // CIP_FFT_PRUNED=0 selects the full 2-D hipFFT transform (A/B experiments)
@@ -388,6 +411,26 @@ static bool fft_pruned() {
   static const bool on = [] {
     const char* e = getenv("CIP_FFT_PRUNED");
     return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+// CIP_OVERLAP_ZERO=0 zeroes the first grid plane in stream order instead of on
+// the side stream beside the planner (A/B experiments)
+static bool overlap_zero() {
+  static const bool on = [] {
+    const char* e = getenv("CIP_OVERLAP_ZERO");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+// CIP_ORDER_CLASS=compute: the order pass recomputes each visibility's bank
+// class instead of gathering the place pass's class bytes (A/B experiments)
+static bool order_gather() {
+  static const bool on = [] {
+    const char* e = getenv("CIP_ORDER_CLASS");
+    return !(e && std::strcmp(e, "compute") == 0);
   }();
   return on;
 }
@@ -417,21 +460,27 @@ static int make_plan(Workspace* ws, const double* uvw, int64_t nrow, const doubl
   CIP_HIP_CHECK(hipMemsetAsync(err, 0, sizeof(unsigned), s));
   const int64_t nvis = nrow * nchan;
   const int nblk = plan_place_blocks(nvis);
-  CIP_ALLOC(vis_class, uint8_t, "vis_class", nvis)
+  // the bank-class order needs a 32-bit flattened index (larger inputs grid in
+  // plain tile order)
+  const bool order = scatter_order() && nvis < ((int64_t)1 << 32);
+  uint8_t* vis_class = nullptr;
+  if (order && order_gather()) {
+    vis_class = buf<uint8_t>(ws, "vis_class", nvis);
+    if (!vis_class) return CIP_ENOMEM;
+  }
   CIP_ALLOC(blk_cnt, int64_t, "blk_cnt", nblk)
   CIP_ALLOC(park_key, uint32_t, "park_key", (int64_t)nblk * 4096)
   CIP_ALLOC(park_run, uint64_t, "park_run", (int64_t)nblk * 4096)
   CIP_ALLOC(partial, double, "prep_partial", 2 * nblk)
-  CIP_HIP_CHECK(launch_plan_place(uvw, nrow, fx, nchan, vis, vis_dtype, wgt, wgt_dtype, g, err, vis_class, blk_cnt,
-                                  park_key, park_run, partial, s));
+  // the place pass also writes radix pass 0's histogram; its scan's last entry = runs
+  CIP_ALLOC(hist0, int64_t, "radix_hist0", 256 * (int64_t)nblk + 1)
+  CIP_ALLOC(scan_h0, int64_t, "scan_hist0", scan_tmp_elems(256 * (int64_t)nblk + 1))
+  CIP_HIP_CHECK(launch_plan_place(uvw, nrow, fx, nchan, vis, vis_dtype, wgt, wgt_dtype, g, err, vis_class, blk_cnt, park_key,
+                                  park_run, partial, hist0, s));
   CIP_HIP_CHECK(launch_prep_final(partial, nblk, red, s));
-  // radix pass 0 histogram over the parked runs; its scan's last entry = runs
   int key_bits = 1;
   while (key_bits < 32 && ((int64_t)1 << key_bits) < ntiles) ++key_bits;
   const int npass = (key_bits + 7) / 8;
-  CIP_ALLOC(hist0, int64_t, "radix_hist0", 256 * (int64_t)nblk + 1)
-  CIP_ALLOC(scan_h0, int64_t, "scan_hist0", scan_tmp_elems(256 * (int64_t)nblk + 1))
-  CIP_HIP_CHECK(launch_radix_hist(park_key, 0, blk_cnt, nblk, 0, hist0, s));
   CIP_HIP_CHECK(exclusive_scan_i64(hist0, 256 * (int64_t)nblk + 1, scan_h0, s));
   int64_t* h = (int64_t*)pinned(ws, 4 * sizeof(int64_t));
   if (!h) return set_error(CIP_ENOMEM, "hipHostMalloc failed");
@@ -479,7 +528,6 @@ static int make_plan(Workspace* ws, const double* uvw, int64_t nrow, const doubl
   CIP_ALLOC(layer_off, int64_t, "layer_off", g.ntw + 1)
   CIP_HIP_CHECK(launch_gather_i64(chunk_off, layer, g.ntw + 1, layer_off, s));
   // bank-class ordering windows: the same split with kOrderWindow
-  const bool order = scatter_order();
   CIP_ALLOC(win_off, int64_t, "win_off", ntiles + 1)
   if (order) {
     CIP_HIP_CHECK(launch_chunk_counts(tile_vis, ntiles, kOrderWindow, win_off, s));
@@ -494,18 +542,18 @@ static int make_plan(Workspace* ws, const double* uvw, int64_t nrow, const doubl
   const int64_t nwin = order ? hl[g.ntw + 1] : 0;
   pr->nchunks = pr->plane_chunk_off.back();
   CIP_ALLOC(chunks, Chunk, "chunks", pr->nchunks)
-  CIP_HIP_CHECK(launch_chunk_emit(tile_vis_off, tile_vis, chunk_off, run_goff, tile_runs, ntiles, cv, chunks,
-                                  s));
+  CIP_HIP_CHECK(launch_chunk_emit(tile_vis_off, tile_vis, chunk_off, run_goff, tile_runs, ntiles, cv, pr->nchunks,
+                                  chunks, s));
   pr->runs = runs;
   pr->run_goff = run_goff;
   pr->tile_run_off = tile_runs;
   pr->chunks = chunks;
   if (order && nwin > 0) {
     CIP_ALLOC(windows, Chunk, "windows", nwin)
-    CIP_HIP_CHECK(launch_chunk_emit(tile_vis_off, tile_vis, win_off, run_goff, tile_runs, ntiles, kOrderWindow, windows,
-                                    s));
-    CIP_ALLOC(perm, uint64_t, "perm", nrow * nchan)
-    CIP_HIP_CHECK(launch_order(vis_class, nchan, runs, run_goff, tile_runs, windows, nwin, perm, s));
+    CIP_HIP_CHECK(launch_chunk_emit(tile_vis_off, tile_vis, win_off, run_goff, tile_runs, ntiles, kOrderWindow, nwin,
+                                    windows, s));
+    CIP_ALLOC(perm, uint32_t, "perm", nrow * nchan)
+    CIP_HIP_CHECK(launch_order(uvw, fx, vis_class, g, nchan, runs, run_goff, tile_runs, windows, nwin, perm, s));
     pr->perm = perm;
   }
   return CIP_OK;
@@ -527,7 +575,7 @@ struct Prepared {
 static int prepare(Workspace* ws, const double* uvw, int64_t nrow, const double* freq, int64_t nchan,
                    const void* vis, int vis_dtype, const void* wgt, int wgt_dtype, int64_t npix_x, int64_t npix_y,
                    double px, double py, double epsilon, int support, int do_wstacking, bool packed,
-                   const cip_gridder_params* given, hipStream_t s, Prepared* out) {
+                   const cip_gridder_params* given, hipStream_t s, Prepared* out, double** grid_out = nullptr) {
   if (!vis_dtype_ok(vis_dtype)) return set_error(CIP_EINVAL, "vis dtype must be complex64 or complex128");
   if (!wgt_dtype_ok(wgt_dtype)) return set_error(CIP_EINVAL, "wgt dtype must be float32, float64 or none");
   if (wgt == nullptr) wgt_dtype = CIP_NONE;
@@ -575,6 +623,15 @@ static int prepare(Workspace* ws, const double* uvw, int64_t nrow, const double*
   out->fixed_scale = 1.0;
   out->fx = fx;
   out->red = red;
+  if (grid_out) {
+    // the grid is known now: zero its first plane beside the planner
+    const size_t gbytes = sizeof(double) * 2 * out->g.nu * out->g.nv;
+    double* grid = buf<double>(ws, "grid", 2 * out->g.nu * out->g.nv);
+    if (!grid) return CIP_ENOMEM;
+    const int zr = zero_on_side(ws, grid, gbytes, s);
+    if (zr != CIP_OK) return zr;
+    *grid_out = grid;
+  }
   hipEvent_t e_prep = g_prof.mark(s);
   g_prof.span(0, g_prof.pool.empty() ? nullptr : g_prof.pool[0], e_prep);
   if (nrow == 0) {
@@ -602,12 +659,13 @@ static int prepare(Workspace* ws, const double* uvw, int64_t nrow, const double*
 }
 
 // transposed: store the grid as gT[y, x] (input layout of the pruned FFT)
+// zeroed: the grid was zeroed already (side stream, joined by the caller)
 static int scatter_plane(const Prepared& pp, int64_t plane, const double* uvw, const void* vis, int vis_dtype,
                          const void* wgt, int wgt_dtype, int64_t nchan, bool transposed, double* grid,
-                         hipStream_t s) {
+                         hipStream_t s, bool zeroed = false) {
   GridGeometry g = pp.g;
   g.transposed = transposed ? 1 : 0;
-  CIP_HIP_CHECK(hipMemsetAsync(grid, 0, sizeof(double) * 2 * g.nu * g.nv, s));
+  if (!zeroed) CIP_HIP_CHECK(hipMemsetAsync(grid, 0, sizeof(double) * 2 * g.nu * g.nv, s));
   if (pp.plan.nchunks == 0) return CIP_OK;
   int64_t lo = 0, hi = 0;  // tile layers feeding this plane
   if (g.do_wstacking) {
@@ -660,12 +718,21 @@ int cip_ms2dirty(const double* uvw, int64_t nrow, const double* freq, int64_t nc
   g_prof.reset();
   hipEvent_t t_start = g_prof.mark(s);
   Prepared pp;
+  double* grid = nullptr;
   int rc = prepare(ws, uvw, nrow, freq, nchan, vis, vis_dtype, wgt, wgt_dtype, npix_x, npix_y, pixsize_x, pixsize_y,
-                   epsilon, support, do_wstacking, packed, nullptr, s, &pp);
+                   epsilon, support, do_wstacking, packed, nullptr, s, &pp, overlap_zero() ? &grid : nullptr);
+  if (grid) {
+    // join the side stream whatever happened (the workspace grid must not be
+    // written by a later call while its memset is still queued)
+    const int jr = join_side(ws, s);
+    if (rc == CIP_OK) rc = jr;
+  }
   if (rc != CIP_OK) return rc;
   if (params_out) *params_out = pp.p;
   const GridGeometry& g = pp.g;
-  CIP_ALLOC(grid, double, "grid", 2 * g.nu * g.nv)
+  const bool zeroed = grid != nullptr;
+  if (!grid) grid = buf<double>(ws, "grid", 2 * g.nu * g.nv);
+  if (!grid) return CIP_ENOMEM;
   CIP_ALLOC(cx, double, "cx", npix_x)
   CIP_ALLOC(cy, double, "cy", npix_y)
   HostKernel hk;
@@ -700,7 +767,7 @@ int cip_ms2dirty(const double* uvw, int64_t nrow, const double* freq, int64_t nc
     if (rc != CIP_OK) return rc;
   }
   for (int64_t p = 0; p < g.nplanes; ++p) {
-    rc = scatter_plane(pp, p, uvw, vis, vis_dtype, wgt, wgt_dtype, nchan, fast, grid, s);
+    rc = scatter_plane(pp, p, uvw, vis, vis_dtype, wgt, wgt_dtype, nchan, fast, grid, s, zeroed && p == 0);
     if (rc != CIP_OK) return rc;
     hipEvent_t f0 = g_prof.mark(s);
     if (fast) {

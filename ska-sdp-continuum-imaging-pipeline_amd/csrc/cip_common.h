@@ -189,6 +189,24 @@ __device__ __forceinline__ bool place_vis(double u_m, double v_m, double w_m, do
   return ok;
 }
 
+// Flattened MS index i = row * nchan + c (< 2^32) -> (row, c): one fp64
+// multiply by 1/nchan (relative error <= 2^-52, so the quotient is off by at
+// most one, fixed by one compare).
+__device__ __forceinline__ void split_index(uint32_t i, int64_t nchan, double inv_nchan, int64_t* row,
+                                           int64_t* c) {
+  int64_t r = (int64_t)((double)i * inv_nchan);
+  int64_t cc = (int64_t)i - r * nchan;
+  if (cc < 0) {
+    --r;
+    cc += nchan;
+  } else if (cc >= nchan) {
+    ++r;
+    cc -= nchan;
+  }
+  *row = r;
+  *c = cc;
+}
+
 __device__ __forceinline__ int64_t tile_key(int64_t ix0, int64_t iy0, int64_t iw0, const GridGeometry& g) {
   return (iw0 * g.nty + iy0 / kTile) * g.ntx + ix0 / kTile;  // g.tile == kTile
 }

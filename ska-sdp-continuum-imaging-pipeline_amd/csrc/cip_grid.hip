@@ -26,30 +26,45 @@ namespace cip {
 // (sets the fixed-point scale): per-block partials come from the planner's
 // place pass (cip_plan.hip); this reduces them in a fixed order.
 
-__global__ __launch_bounds__(256) void prep_final_kernel(const double* partial, int nblocks, double* out2) {
-  double sum = 0.0, mx = 0.0;
-  for (int i = threadIdx.x; i < nblocks; i += 256) {
-    sum += partial[2 * i];
-    mx = fmax(mx, partial[2 * i + 1]);
+// 1024 threads, 4 independent partial sums per thread (the loads of one
+// thread are not serialised behind one accumulator); fixed order throughout.
+__global__ __launch_bounds__(1024) void prep_final_kernel(const double* partial, int nblocks, double* out2) {
+  double sum[4] = {0.0, 0.0, 0.0, 0.0}, mx = 0.0;
+  for (int i0 = threadIdx.x; i0 < nblocks; i0 += 4 * 1024) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int i = i0 + k * 1024;
+      if (i < nblocks) {
+        const double2 p = reinterpret_cast<const double2*>(partial)[i];
+        sum[k] += p.x;
+        mx = fmax(mx, p.y);
+      }
+    }
   }
+  double s = (sum[0] + sum[1]) + (sum[2] + sum[3]);
   for (int d = 32; d > 0; d >>= 1) {
-    sum += __shfl_xor(sum, d, 64);
+    s += __shfl_xor(s, d, 64);
     mx = fmax(mx, __shfl_xor(mx, d, 64));
   }
-  __shared__ double ss[4], sm[4];
+  __shared__ double ss[16], sm[16];
   if ((threadIdx.x & 63) == 0) {
-    ss[threadIdx.x >> 6] = sum;
+    ss[threadIdx.x >> 6] = s;
     sm[threadIdx.x >> 6] = mx;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    out2[0] = (ss[0] + ss[1]) + (ss[2] + ss[3]);
-    out2[1] = fmax(fmax(sm[0], sm[1]), fmax(sm[2], sm[3]));
+    double t = 0.0, m = 0.0;
+    for (int w = 0; w < 16; ++w) {
+      t += ss[w];
+      m = fmax(m, sm[w]);
+    }
+    out2[0] = t;
+    out2[1] = m;
   }
 }
 
 hipError_t launch_prep_final(const double* partial, int nblocks, double* out2, hipStream_t s) {
-  prep_final_kernel<<<dim3(1), dim3(256), 0, s>>>(partial, nblocks, out2);
+  prep_final_kernel<<<dim3(1), dim3(1024), 0, s>>>(partial, nblocks, out2);
   return hipGetLastError();
 }
 
@@ -207,22 +222,62 @@ constexpr int kOrderPer = 4;
 constexpr int kOrderBatch = kOrderThreads * kOrderPer;
 static_assert(kOrderBatch == kOrderWindow, "one order block per window");
 
+// Bank class of a visibility's footprint origin in its tile's LDS sub-grid,
+// recomputed from (u, v, f/c) with place_vis's arithmetic (fp contraction off,
+// so it matches the scatter bit for bit; a mismatch would only cost a bank
+// conflict, never a wrong sum).
+__device__ __forceinline__ unsigned origin_class(double u_m, double v_m, double fx, const GridGeometry& g) {
+#pragma clang fp contract(off)
+  const int hw = g.support / 2;
+  const int P = kTile + g.support - 1;
+  const double x = (u_m * fx) * g.scale_u + (double)(g.nu / 2);
+  const double y = (v_m * fx) * g.scale_v + (double)(g.nv / 2);
+  int64_t ix0, iy0;
+  double t;
+  footprint(x, hw, &ix0, &t);
+  footprint(y, hw, &iy0, &t);
+  ix0 = wrap_index(ix0, g.nu);
+  iy0 = wrap_index(iy0, g.nv);
+  return (unsigned)((((int)ix0 % kTile) * P + (int)iy0 % kTile) & 31);  // ix0, iy0 in [0, 2^31)
+}
+
 // One block per window (<= kOrderWindow consecutive tile-order positions).
-// The window's row slices are staged in LDS (positions relative to the
-// window start; the next window of the tile starts in its last slice), each
-// thread finds the slice of its 4 positions by binary search, gathers the
-// bank class recorded by the place pass and the window is counting-sorted
-// into level-major order: perm[g] = (row << 16) | channel.
-__global__ __launch_bounds__(kOrderThreads) void order_kernel(const uint8_t* __restrict__ vis_class, int64_t nchan,
-                                                              const uint64_t* __restrict__ runs,
+// The window's row slices are staged in LDS with their rows' (u, v)
+// (positions relative to the window start; the next window of the tile starts
+// in its last slice), each thread finds the slice of its 4 positions by binary
+// search, recomputes the bank class of each visibility (no per-visibility
+// class array: a gathered byte per visibility cost more HBM lines than the
+// whole perm stream) and the window is counting-sorted into level-major
+// order: perm[g] = row * nchan + channel (32-bit flattened MS index).
+template <bool GATHER>
+__global__ __launch_bounds__(kOrderThreads) void order_kernel(const double* __restrict__ uvw,
+                                                              const double* __restrict__ fx,
+                                                              const uint8_t* __restrict__ vis_class, GridGeometry g,
+                                                              int64_t nchan, const uint64_t* __restrict__ runs,
                                                               const int64_t* __restrict__ run_goff,
                                                               const int64_t* __restrict__ tile_run_off,
                                                               const Chunk* __restrict__ windows, int64_t nwindows,
-                                                              uint64_t* __restrict__ perm) {
+                                                              uint32_t* __restrict__ perm) {
   __shared__ __attribute__((aligned(16))) unsigned s_cnt[32];
-  __shared__ unsigned s_S[kOrderBatch], s_M[kOrderBatch];
-  __shared__ int s_off[kOrderBatch + 1];  // slice starts relative to the window start
-  __shared__ uint64_t s_rec[kOrderBatch];
+  // the staged slices are dead once every position has its class: the level
+  // tables reuse their space
+  __shared__ union {
+    struct {
+      double2 uv[kOrderBatch];
+      uint64_t rec[kOrderBatch];
+      int off[kOrderBatch + 1];  // slice starts relative to the window start
+      uint16_t idx[kOrderBatch];  // slice of each position
+    } a;
+    struct {
+      unsigned S[kOrderBatch], M[kOrderBatch];
+    } b;
+  } sh;
+  double2* const s_uv = sh.a.uv;
+  uint64_t* const s_rec = sh.a.rec;
+  int* const s_off = sh.a.off;
+  uint16_t* const s_idx = sh.a.idx;
+  unsigned* const s_S = sh.b.S;
+  unsigned* const s_M = sh.b.M;
   const Chunk ch = windows[blockIdx.x];
   const int64_t sb = ch.g0;
   const int nsb = (int)(ch.g1 - ch.g0);
@@ -238,28 +293,40 @@ __global__ __launch_bounds__(kOrderThreads) void order_kernel(const uint8_t* __r
   const int nst = (int)(nst64 < nsb ? nst64 : nsb);
   for (int k = threadIdx.x; k < nst; k += kOrderThreads) {
     s_off[k] = (int)(run_goff[ch.first_run + k] - sb);
-    s_rec[k] = runs[ch.first_run + k];
+    const uint64_t rec = runs[ch.first_run + k];
+    s_rec[k] = rec;
+    if constexpr (!GATHER) {
+      const int64_t row = (int64_t)(rec >> 32);
+      s_uv[k] = make_double2(uvw[3 * row], uvw[3 * row + 1]);
+    }
   }
   if (threadIdx.x < 32) s_cnt[threadIdx.x] = 0u;
   __syncthreads();
-  uint64_t packed[kOrderPer];
+  // expand: every position learns its slice (slices are <= 64 positions long)
+  for (int k = threadIdx.x; k < nst; k += kOrderThreads) {
+    const int a = s_off[k] > 0 ? s_off[k] : 0;
+    const int b = k + 1 < nst ? s_off[k + 1] : nsb;
+    for (int p = a; p < b; ++p) s_idx[p] = (uint16_t)k;
+  }
+  __syncthreads();
+  uint32_t packed[kOrderPer];
   unsigned cls[kOrderPer], rk[kOrderPer];
 #pragma unroll
   for (int k = 0; k < kOrderPer; ++k) {
     const int qi = threadIdx.x + k * kOrderThreads;
     cls[k] = 32u;
     if (qi < nsb) {
-      int lo = 0, hi = nst - 1;
-      while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (s_off[mid] <= qi) lo = mid;
-        else hi = mid - 1;
-      }
+      const int lo = s_idx[qi];
       const uint64_t rec = s_rec[lo];
       const int64_t row = (int64_t)(rec >> 32);
       const int64_t c = (int64_t)((rec >> 16) & 0xffff) + (qi - s_off[lo]);
-      packed[k] = ((uint64_t)row << 16) | (uint64_t)c;
-      cls[k] = vis_class[row * nchan + c];
+      packed[k] = (uint32_t)(row * nchan + c);
+      if constexpr (GATHER) {
+        cls[k] = vis_class[row * nchan + c];
+      } else {
+        const double2 uv = s_uv[lo];
+        cls[k] = origin_class(uv.x, uv.y, fx[c], g);
+      }
     }
   }
 #pragma unroll
@@ -293,12 +360,16 @@ __global__ __launch_bounds__(kOrderThreads) void order_kernel(const uint8_t* __r
     if (cls[k] < 32u) perm[sb + s_S[rk[k]] + __popc(s_M[rk[k]] & ((1u << cls[k]) - 1u))] = packed[k];
 }
 
-hipError_t launch_order(const uint8_t* vis_class, int64_t nchan, const uint64_t* runs, const int64_t* run_goff,
-                        const int64_t* tile_run_off, const Chunk* windows, int64_t nwindows, uint64_t* perm,
-                        hipStream_t s) {
+hipError_t launch_order(const double* uvw, const double* fx, const uint8_t* vis_class, const GridGeometry& g,
+                        int64_t nchan, const uint64_t* runs, const int64_t* run_goff, const int64_t* tile_run_off,
+                        const Chunk* windows, int64_t nwindows, uint32_t* perm, hipStream_t s) {
   if (nwindows <= 0) return hipSuccess;
-  order_kernel<<<dim3((unsigned)nwindows), dim3(kOrderThreads), 0, s>>>(vis_class, nchan, runs, run_goff, tile_run_off,
-                                                                        windows, nwindows, perm);
+  if (vis_class)
+    order_kernel<true><<<dim3((unsigned)nwindows), dim3(kOrderThreads), 0, s>>>(
+        uvw, fx, vis_class, g, nchan, runs, run_goff, tile_run_off, windows, nwindows, perm);
+  else
+    order_kernel<false><<<dim3((unsigned)nwindows), dim3(kOrderThreads), 0, s>>>(
+        uvw, fx, vis_class, g, nchan, runs, run_goff, tile_run_off, windows, nwindows, perm);
   return hipGetLastError();
 }
 
@@ -307,7 +378,7 @@ __global__ __launch_bounds__(kScatterThreads) void scatter_kernel(
     const double* __restrict__ uvw, const double* __restrict__ fx, const VisT* __restrict__ vis,
     const void* __restrict__ wgt, int64_t nchan, const uint64_t* __restrict__ runs,
     const int64_t* __restrict__ run_goff, const int64_t* __restrict__ tile_run_off,
-    const uint64_t* __restrict__ perm, const Chunk* __restrict__ chunks, int64_t chunk_begin, GridGeometry g,
+    const uint32_t* __restrict__ perm, const Chunk* __restrict__ chunks, int64_t chunk_begin, GridGeometry g,
     int64_t plane, double fixed_scale, double inv_scale, double* __restrict__ grid) {
   constexpr int T = kTile;
   constexpr int P = T + W - 1;
@@ -331,17 +402,20 @@ __global__ __launch_bounds__(kScatterThreads) void scatter_kernel(
     int64_t q = ch.g0 + threadIdx.x;
     bool have = q < ch.g1;
     VisFetch cur;
+    const double inv_nchan = 1.0 / (double)nchan;
     if (have) {
-      const uint64_t pk = perm[q];
-      fetch_at<VisT, WK>((int64_t)(pk >> 16), (int64_t)(pk & 0xffff), uvw, fx, vis, wgt, nchan, cur);
+      int64_t r, c;
+      split_index(perm[q], nchan, inv_nchan, &r, &c);
+      fetch_at<VisT, WK>(r, c, uvw, fx, vis, wgt, nchan, cur);
     }
     while (have) {
       const int64_t qn = q + kScatterThreads;
       const bool hn = qn < ch.g1;
       VisFetch nxt;
       if (hn) {
-        const uint64_t pk = perm[qn];
-        fetch_at<VisT, WK>((int64_t)(pk >> 16), (int64_t)(pk & 0xffff), uvw, fx, vis, wgt, nchan, nxt);
+        int64_t r, c;
+        split_index(perm[qn], nchan, inv_nchan, &r, &c);
+        fetch_at<VisT, WK>(r, c, uvw, fx, vis, wgt, nchan, nxt);
       }
       grid_fetched<W, WSTACK, PACK>(cur, g, plane, X0, Y0, fixed_scale, sub);
       cur = nxt;
@@ -411,7 +485,7 @@ template <int W, typename VisT, int WK>
 static hipError_t scatter_dispatch_ws(bool ws, bool pack, dim3 grid_dim, hipStream_t s, const double* uvw,
                                       const double* fx, const void* vis, const void* wgt, int64_t nchan,
                                       const uint64_t* runs, const int64_t* run_goff, const int64_t* tile_run_off,
-                                      const uint64_t* perm, const Chunk* chunks, int64_t chunk_begin,
+                                      const uint32_t* perm, const Chunk* chunks, int64_t chunk_begin,
                                       const GridGeometry& g, int64_t plane, double fs, double* grid) {
 #define LAUNCH(WSV, PRM, PK)                                                                                   \
   scatter_kernel<W, VisT, WK, WSV, PRM, PK><<<grid_dim, dim3(kScatterThreads), 0, s>>>(                        \
@@ -449,7 +523,7 @@ template <int W>
 static hipError_t scatter_dispatch_w(int vis_dtype, int wgt_dtype, bool pack, dim3 gd, hipStream_t s,
                                      const double* uvw, const double* fx, const void* vis, const void* wgt,
                                      int64_t nchan, const uint64_t* runs, const int64_t* run_goff,
-                                     const int64_t* tile_run_off, const uint64_t* perm, const Chunk* chunks,
+                                     const int64_t* tile_run_off, const uint32_t* perm, const Chunk* chunks,
                                      int64_t cb, const GridGeometry& g, int64_t plane, double fs, double* grid) {
   const bool ws = g.do_wstacking != 0;
 #define ARGS \
@@ -467,7 +541,7 @@ static hipError_t scatter_dispatch_w(int vis_dtype, int wgt_dtype, bool pack, di
 
 hipError_t launch_scatter(int support, int vis_dtype, int wgt_dtype, bool packed, const double* uvw,
                           const double* fx, const void* vis, const void* wgt, int64_t nchan, const uint64_t* runs,
-                          const int64_t* run_goff, const int64_t* tile_run_off, const uint64_t* perm,
+                          const int64_t* run_goff, const int64_t* tile_run_off, const uint32_t* perm,
                           const Chunk* chunks, int64_t chunk_begin, int64_t nchunks, const GridGeometry& g,
                           int64_t plane, double fixed_scale, double* grid, hipStream_t s) {
   if (nchunks <= 0) return hipSuccess;

@@ -31,15 +31,17 @@ hipError_t launch_freq_scale(const double* freq, int64_t nchan, double* fx, hipS
 // per-row w range over channels (only f min/max matter): out[0]=min, out[1]=max
 hipError_t launch_w_range(const double* uvw, int64_t nrow, double fxmin, double fxmax, double* partial,
                           int nblocks, hipStream_t s);
-// place pass: per-visibility bank class, the runs of place block b (4096
-// visibilities) parked with their tile keys at slots [4096 b, 4096 b +
-// blk_cnt[b]), and per-block {sum w, max |w V|} partials (2 * plan_place_blocks).
+// place pass: the runs of place block b (4096 visibilities) parked with their
+// tile keys at slots [4096 b, 4096 b + blk_cnt[b]), per-block {sum w, max |w V|}
+// partials (2 * plan_place_blocks) and the radix pass-0 histogram of the parked
+// keys (hist0[d * nblocks + b], 256 * nblocks + 1 entries, last one zeroed);
+// vis_class (optional, nvis bytes): each visibility's LDS bank class.
 // err_flag: bit 0 non-finite uvw / w off the stack, bit 1 non-finite vis or weight.
 int plan_place_blocks(int64_t nvis);
 hipError_t launch_plan_place(const double* uvw, int64_t nrow, const double* fx, int64_t nchan,
                              const void* vis, int vis_dtype, const void* wgt, int wgt_dtype, const GridGeometry& g,
                              unsigned* err_flag, uint8_t* vis_class, int64_t* blk_cnt, uint32_t* park_key,
-                             uint64_t* park_run, double* partial, hipStream_t s);
+                             uint64_t* park_run, double* partial, int64_t* hist0, hipStream_t s);
 // one stable LSD radix sort pass on digit (key >> shift) & 255 over nblocks
 // blocks of 4096 slots: dense (blk_cnt NULL, n items) or the place pass's
 // parked runs (blk_cnt). hist: 256 * nblocks + 1 entries, exclusive-scanned
@@ -59,7 +61,7 @@ hipError_t launch_chunk_counts(const int64_t* tile_vis, int64_t ntiles, int64_t 
                                int64_t* out, hipStream_t s);
 hipError_t launch_chunk_emit(const int64_t* tile_vis_off, const int64_t* tile_vis, const int64_t* chunk_off,
                              const int64_t* run_goff, const int64_t* tile_run_off, int64_t ntiles,
-                             int64_t chunk_vis, Chunk* chunks, hipStream_t s);
+                             int64_t chunk_vis, int64_t nchunks, Chunk* chunks, hipStream_t s);
 hipError_t launch_gather_i64(const int64_t* src, int64_t stride, int64_t count, int64_t* dst,
                              hipStream_t s);
 
@@ -71,16 +73,17 @@ hipError_t launch_prep_final(const double* partial, int nblocks, double* out2, h
 // located through the tile's row slices in tile order).
 hipError_t launch_scatter(int support, int vis_dtype, int wgt_dtype, bool packed, const double* uvw,
                           const double* fx, const void* vis, const void* wgt, int64_t nchan, const uint64_t* runs,
-                          const int64_t* run_goff, const int64_t* tile_run_off, const uint64_t* perm,
+                          const int64_t* run_goff, const int64_t* tile_run_off, const uint32_t* perm,
                           const Chunk* chunks, int64_t chunk_begin, int64_t nchunks, const GridGeometry& g,
                           int64_t plane, double fixed_scale, double* grid, hipStream_t s);
-// perm[g] for every tile-order position g of every chunk (cip_grid.hip)
-// perm (nvis records): the tile-order visibilities as (row << 16) | channel,
-// bank-class sorted within each window (the tiles split into <= kOrderWindow
-// pieces by chunk_emit with cv = kOrderWindow)
-hipError_t launch_order(const uint8_t* vis_class, int64_t nchan, const uint64_t* runs, const int64_t* run_goff,
-                        const int64_t* tile_run_off, const Chunk* windows, int64_t nwindows, uint64_t* perm,
-                        hipStream_t s);
+// perm (nvis 32-bit records, nvis < 2^32): the tile-order visibilities as
+// row * nchan + channel, bank-class sorted within each window (the tiles split
+// into <= kOrderWindow pieces by chunk_emit with cv = kOrderWindow)
+// vis_class: classes from the place pass, or NULL (recomputed from u, v, f)
+hipError_t launch_order(const double* uvw, const double* fx, const uint8_t* vis_class, const GridGeometry& g,
+                        int64_t nchan,
+                        const uint64_t* runs, const int64_t* run_goff, const int64_t* tile_run_off,
+                        const Chunk* windows, int64_t nwindows, uint32_t* perm, hipStream_t s);
 hipError_t launch_crop_correct_2d(const double* grid, const GridGeometry& g, int64_t npix_x, int64_t npix_y,
                                   const double* cx, const double* cy, double* dirty, hipStream_t s);
 hipError_t launch_wplane_accumulate(const double* grid, const GridGeometry& g, int64_t npix_x, int64_t npix_y,

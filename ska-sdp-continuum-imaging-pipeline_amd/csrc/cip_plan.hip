@@ -131,10 +131,9 @@ hipError_t launch_w_range(const double* uvw, int64_t nrow, double fxmin, double 
 // lane: a lane starts a run when its key differs from the previous channel's
 // (or at a row start or the wave's first lane), and the run ends at the next
 // start in the wave (ballot), so runs are split at 64-visibility segment
-// boundaries. The place pass is the only one that places visibilities: it
-// parks each run with its tile key in its segment's slots of a scratch array
-// and records every visibility's LDS bank class for the order pass. The runs
-// are then bucketed by tile with a stable LSD radix sort (8-bit digits, no
+// boundaries. The place pass parks each run with its tile key in its block's
+// slots of a scratch array and counts the keys' low bytes (the histogram of
+// radix pass 0, written digit-major). The runs are then bucketed by tile with a stable LSD radix sort (8-bit digits, no
 // global atomics: scattered device-scope atomics execute at the memory side
 // at ~10-25 G/s on MI355X, which made an atomic counting sort of the 13 M
 // runs of C3 cost more than 1 ms).
@@ -148,10 +147,13 @@ __global__ __launch_bounds__(256) void plan_place_kernel(const double* __restric
                                                          uint8_t* __restrict__ vis_class,
                                                          int64_t* __restrict__ blk_cnt,
                                                          uint32_t* __restrict__ park_key,
-                                                         uint64_t* __restrict__ park_run, double* partial) {
+                                                         uint64_t* __restrict__ park_run, double* partial,
+                                                         int64_t* __restrict__ hist0) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   __shared__ unsigned s_nruns;
+  __shared__ unsigned s_hist[256];
   if (threadIdx.x == 0) s_nruns = 0u;
+  s_hist[threadIdx.x] = 0u;
   __syncthreads();
   // fused prep reduction (sum of weights, max |w V|), fixed order
   double wsum = 0.0, wvmax = 0.0;
@@ -189,10 +191,10 @@ __global__ __launch_bounds__(256) void plan_place_kernel(const double* __restric
       double yu, yv, yw;
       if (place_vis(uvw[3 * r], uvw[3 * r + 1], uvw[3 * r + 2], fx[c], g, &ix0, &yu, &iy0, &yv, &iw0, &yw)) {
         key = tile_key(ix0, iy0, iw0, g);
-        vis_class[i] = (uint8_t)((((int)(ix0 % kTile)) * P + (int)(iy0 % kTile)) & 31);
+        if (vis_class) vis_class[i] = (uint8_t)((((int)ix0 % kTile) * P + (int)iy0 % kTile) & 31);
       } else {
         bad = true;
-        vis_class[i] = 0;
+        if (vis_class) vis_class[i] = 0;
       }
     }
     if (__ballot(bad) != 0ull && lane == 0) atomicOr(err_flag, 1u);
@@ -211,6 +213,7 @@ __global__ __launch_bounds__(256) void plan_place_kernel(const double* __restric
       const int next = above ? (__ffsll((long long)above) - 1) : nvalid;
       const int64_t slot = (int64_t)blockIdx.x * kPlaceSegs * 64 + wbase + __popcll(emits & ((1ull << lane) - 1ull));
       park_key[slot] = (uint32_t)key;
+      atomicAdd(&s_hist[(uint32_t)key & 255u], 1u);
       park_run[slot] = ((uint64_t)r << 32) | ((uint64_t)c << 16) | (uint64_t)(c + (next - lane));
     }
   }
@@ -225,10 +228,12 @@ __global__ __launch_bounds__(256) void plan_place_kernel(const double* __restric
     sm[threadIdx.x >> 6] = wvmax;
   }
   __syncthreads();
+  hist0[(int64_t)threadIdx.x * gridDim.x + blockIdx.x] = s_hist[threadIdx.x];
   if (threadIdx.x == 0) {
     partial[2 * blockIdx.x] = (ss[0] + ss[1]) + (ss[2] + ss[3]);
     partial[2 * blockIdx.x + 1] = fmax(fmax(sm[0], sm[1]), fmax(sm[2], sm[3]));
     blk_cnt[blockIdx.x] = s_nruns;
+    if (blockIdx.x == 0) hist0[256 * (int64_t)gridDim.x] = 0;
   }
 }
 
@@ -243,11 +248,11 @@ int plan_place_blocks(int64_t nvis) { return (int)plan_blocks(nvis); }
 hipError_t launch_plan_place(const double* uvw, int64_t nrow, const double* fx, int64_t nchan,
                              const void* vis, int vis_dtype, const void* wgt, int wgt_dtype, const GridGeometry& g,
                              unsigned* err_flag, uint8_t* vis_class, int64_t* blk_cnt, uint32_t* park_key,
-                             uint64_t* park_run, double* partial, hipStream_t s) {
+                             uint64_t* park_run, double* partial, int64_t* hist0, hipStream_t s) {
   const dim3 gd(plan_blocks(nrow * nchan));
 #define PLACE(VT, WKV)                                                                                           \
   plan_place_kernel<VT, WKV><<<gd, dim3(256), 0, s>>>(uvw, nrow, fx, nchan, (const VT*)vis, wgt, g, err_flag,  \
-                                                      vis_class, blk_cnt, park_key, park_run, partial)
+                                                      vis_class, blk_cnt, park_key, park_run, partial, hist0)
   if (vis_dtype == CIP_C64) {
     if (wgt_dtype == CIP_F32) PLACE(float2, WK_F32);
     else if (wgt_dtype == CIP_F64) PLACE(float2, WK_F64);
@@ -438,38 +443,45 @@ hipError_t launch_chunk_counts(const int64_t* tile_vis, int64_t ntiles, int64_t 
   return hipGetLastError();
 }
 
-__global__ void chunk_emit_kernel(const int64_t* tile_vis_off, const int64_t* tile_vis, const int64_t* chunk_off,
-                                  const int64_t* run_goff, const int64_t* tile_run_off, int64_t ntiles, int64_t cv,
-                                  Chunk* chunks) {
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= ntiles) return;
-  const int64_t nv = tile_vis[t];
-  const int64_t b = chunk_off[t];
-  const int64_t g = tile_vis_off[t];
-  int64_t lo = tile_run_off[t];
-  const int64_t rend = tile_run_off[t + 1];
-  for (int64_t k = 0; k * cv < nv; ++k) {
-    Chunk ch;
-    ch.g0 = g + k * cv;
-    ch.g1 = g + ((k + 1) * cv < nv ? (k + 1) * cv : nv);
-    ch.tile = t;
-    // first run whose end lies beyond g0 (runs of a tile are consecutive)
-    int64_t hi = rend - 1;
-    while (lo < hi) {
-      const int64_t mid = (lo + hi) >> 1;
-      if (run_goff[mid + 1] > ch.g0) hi = mid;
-      else lo = mid + 1;
-    }
-    ch.first_run = lo;
-    chunks[b + k] = ch;
+// One thread per chunk j: its tile t is the last with chunk_off[t] <= j
+// (tiles without chunks repeat an offset), then k = j - chunk_off[t] and the
+// chunk's first run by binary search among the tile's runs.
+__global__ void chunk_emit_kernel(const int64_t* __restrict__ tile_vis_off, const int64_t* __restrict__ tile_vis,
+                                  const int64_t* __restrict__ chunk_off, const int64_t* __restrict__ run_goff,
+                                  const int64_t* __restrict__ tile_run_off, int64_t ntiles, int64_t cv,
+                                  int64_t nchunks, Chunk* __restrict__ chunks) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= nchunks) return;
+  int64_t lo = 0, hi = ntiles - 1;
+  while (lo < hi) {
+    const int64_t mid = (lo + hi + 1) >> 1;
+    if (chunk_off[mid] <= j) lo = mid;
+    else hi = mid - 1;
   }
+  const int64_t t = lo;
+  const int64_t k = j - chunk_off[t];
+  const int64_t g = tile_vis_off[t], nv = tile_vis[t];
+  Chunk ch;
+  ch.g0 = g + k * cv;
+  ch.g1 = g + ((k + 1) * cv < nv ? (k + 1) * cv : nv);
+  ch.tile = t;
+  // first run whose end lies beyond g0 (runs of a tile are consecutive)
+  int64_t rl = tile_run_off[t], rh = tile_run_off[t + 1] - 1;
+  while (rl < rh) {
+    const int64_t mid = (rl + rh) >> 1;
+    if (run_goff[mid + 1] > ch.g0) rh = mid;
+    else rl = mid + 1;
+  }
+  ch.first_run = rl;
+  chunks[j] = ch;
 }
 
 hipError_t launch_chunk_emit(const int64_t* tile_vis_off, const int64_t* tile_vis, const int64_t* chunk_off,
                              const int64_t* run_goff, const int64_t* tile_run_off, int64_t ntiles,
-                             int64_t chunk_vis, Chunk* chunks, hipStream_t s) {
-  chunk_emit_kernel<<<dim3((unsigned)((ntiles + 255) / 256)), dim3(256), 0, s>>>(
-      tile_vis_off, tile_vis, chunk_off, run_goff, tile_run_off, ntiles, chunk_vis, chunks);
+                             int64_t chunk_vis, int64_t nchunks, Chunk* chunks, hipStream_t s) {
+  if (nchunks <= 0) return hipSuccess;
+  chunk_emit_kernel<<<dim3((unsigned)((nchunks + 255) / 256)), dim3(256), 0, s>>>(
+      tile_vis_off, tile_vis, chunk_off, run_goff, tile_run_off, ntiles, chunk_vis, nchunks, chunks);
   return hipGetLastError();
 }
 
