@@ -157,6 +157,43 @@ __device__ __forceinline__ int64_t wrap_index(int64_t i, int64_t n) {
   return i;
 }
 
+__device__ __forceinline__ int wrap_index32(int i, int n) {
+  if (i >= n) {
+    i -= n;
+    if (i >= n) i %= n;
+  } else if (i < 0) {
+    i += n;
+    if (i < 0) {
+      i %= n;
+      if (i < 0) i += n;
+    }
+  }
+  return i;
+}
+
+// Footprint origins (ix0, iy0) of grid coordinates (x, y), wrapped into
+// [0, nu) x [0, nv), and the kernel variables. 32-bit integer arithmetic (one
+// v_cvt_i32_f64 per axis; the f64 -> i64 conversion and 64-bit wrap are a
+// dozen VALU instructions each); a wave-uniform branch takes the 64-bit path
+// when any active lane is 2^30 cells or more from the origin (or not finite).
+// The same integers either way.
+__device__ __forceinline__ void uv_origin(double x, double y, int hw, const GridGeometry& g, int64_t* ix0,
+                                          double* yu, int64_t* iy0, double* yv) {
+#pragma clang fp contract(off)
+  const double sx = x - (double)hw, sy = y - (double)hw;
+  const double flx = floor(sx), fly = floor(sy);
+  *yu = 2.0 * (sx - flx) - 1.0;
+  *yv = 2.0 * (sy - fly) - 1.0;
+  const bool small = fabs(flx) < 1073741824.0 && fabs(fly) < 1073741824.0;
+  if (__ballot(!small) == 0ull) {
+    *ix0 = wrap_index32((int)flx + 1, (int)g.nu);
+    *iy0 = wrap_index32((int)fly + 1, (int)g.nv);
+  } else {
+    *ix0 = wrap_index(small || isfinite(flx) ? (int64_t)flx + 1 : 0, g.nu);
+    *iy0 = wrap_index(small || isfinite(fly) ? (int64_t)fly + 1 : 0, g.nv);
+  }
+}
+
 // Place one visibility (metres, fx = f / c) on the grid. Returns false when the
 // footprint leaves the grid (or the w-plane stack). The arithmetic order is
 // pinned (no contraction) so the planner and the scatter agree bit for bit and
@@ -168,13 +205,10 @@ __device__ __forceinline__ bool place_vis(double u_m, double v_m, double w_m, do
   const int hw = g.support / 2;
   const double x = (u_m * fx) * g.scale_u + (double)(g.nu / 2);
   const double y = (v_m * fx) * g.scale_v + (double)(g.nv / 2);
-  footprint(x, hw, ix0, yu);
-  footprint(y, hw, iy0, yv);
   // The dirty image is sampled at l = k * pixsize, so it is periodic in u with
   // period 1 / pixsize = the grid extent: coordinates beyond the grid wrap
   // (exactly, as ducc0 does), and the footprint origin is taken modulo nu.
-  *ix0 = wrap_index(*ix0, g.nu);
-  *iy0 = wrap_index(*iy0, g.nv);
+  uv_origin(x, y, hw, g, ix0, yu, iy0, yv);
   bool ok = true;
   if (g.do_wstacking) {
     const double xw = ((w_m * fx) - g.w0) / g.dw;
@@ -187,6 +221,23 @@ __device__ __forceinline__ bool place_vis(double u_m, double v_m, double w_m, do
   // non-finite coordinates are an error (the planner raises)
   ok = ok && isfinite(x) && isfinite(y) && fabs(x) < 9.0e15 && fabs(y) < 9.0e15;
   return ok;
+}
+
+// Flattened MS index i = row * nchan + c (< 2^52) -> (row, c): i * (1/nchan)
+// in fp64 is within one of the quotient (one compare fixes it).
+__device__ __forceinline__ void split_index64(int64_t i, int64_t nchan, double inv_nchan, int64_t* row,
+                                             int64_t* c) {
+  int64_t r = (int64_t)((double)i * inv_nchan);
+  int64_t cc = i - r * nchan;
+  if (cc < 0) {
+    --r;
+    cc += nchan;
+  } else if (cc >= nchan) {
+    ++r;
+    cc -= nchan;
+  }
+  *row = r;
+  *c = cc;
 }
 
 // Flattened MS index i = row * nchan + c (< 2^32) -> (row, c): one fp64
@@ -208,7 +259,8 @@ __device__ __forceinline__ void split_index(uint32_t i, int64_t nchan, double in
 }
 
 __device__ __forceinline__ int64_t tile_key(int64_t ix0, int64_t iy0, int64_t iw0, const GridGeometry& g) {
-  return (iw0 * g.nty + iy0 / kTile) * g.ntx + ix0 / kTile;  // g.tile == kTile
+  // ix0, iy0 in [0, 2^31) after wrapping: unsigned division
+  return (iw0 * g.nty + (int64_t)((uint32_t)iy0 / (uint32_t)kTile)) * g.ntx + (int64_t)((uint32_t)ix0 / (uint32_t)kTile);
 }
 
 // visibility / weight loads by dtype (CIP_C64 -> float2, CIP_C128 -> double2)

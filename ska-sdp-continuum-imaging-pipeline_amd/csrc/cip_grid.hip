@@ -233,11 +233,8 @@ __device__ __forceinline__ unsigned origin_class(double u_m, double v_m, double 
   const double x = (u_m * fx) * g.scale_u + (double)(g.nu / 2);
   const double y = (v_m * fx) * g.scale_v + (double)(g.nv / 2);
   int64_t ix0, iy0;
-  double t;
-  footprint(x, hw, &ix0, &t);
-  footprint(y, hw, &iy0, &t);
-  ix0 = wrap_index(ix0, g.nu);
-  iy0 = wrap_index(iy0, g.nv);
+  double t0, t1;
+  uv_origin(x, y, hw, g, &ix0, &t0, &iy0, &t1);
   return (unsigned)((((int)ix0 % kTile) * P + (int)iy0 % kTile) & 31);  // ix0, iy0 in [0, 2^31)
 }
 
@@ -263,7 +260,7 @@ __global__ __launch_bounds__(kOrderThreads) void order_kernel(const double* __re
   // tables reuse their space
   __shared__ union {
     struct {
-      double2 uv[kOrderBatch];
+      double2 uv[GATHER ? 1 : kOrderBatch];  // (u, v) of each slice's row (recompute only)
       uint64_t rec[kOrderBatch];
       int off[kOrderBatch + 1];  // slice starts relative to the window start
       uint16_t idx[kOrderBatch];  // slice of each position

@@ -138,6 +138,7 @@ hipError_t launch_w_range(const double* uvw, int64_t nrow, double fxmin, double 
 // at ~10-25 G/s on MI355X, which made an atomic counting sort of the 13 M
 // runs of C3 cost more than 1 ms).
 constexpr int kPlaceSegs = 64;  // 64-visibility segments per place block (4096 visibilities)
+constexpr uint32_t kNoKey = 0xffffffffu;  // visibility off the grid (tile keys are < 2^32 - 1)
 
 template <typename VisT, int WK>
 __global__ __launch_bounds__(256) void plan_place_kernel(const double* __restrict__ uvw, int64_t nrow,
@@ -162,46 +163,49 @@ __global__ __launch_bounds__(256) void plan_place_kernel(const double* __restric
   const int64_t nseg = (nvis + 63) / 64;
   const int P = kTile + g.support - 1;
   // block b owns segments [64 b, 64 b + 64): wave w takes every 4th
-  for (int64_t seg = (int64_t)blockIdx.x * kPlaceSegs + wave; seg < nseg && seg < ((int64_t)blockIdx.x + 1) * kPlaceSegs;
-       seg += 4) {
+  const int64_t seg_end = ((int64_t)blockIdx.x + 1) * kPlaceSegs < nseg ? ((int64_t)blockIdx.x + 1) * kPlaceSegs : nseg;
+  // (row, channel) of the lane's visibility, advanced by 256 visibilities per
+  // step without a division
+  int64_t r0, c0;
+  split_index64(((int64_t)blockIdx.x * kPlaceSegs + wave) * 64 + lane, nchan, 1.0 / (double)nchan, &r0, &c0);
+  const int64_t step_r = 256 / nchan, step_c = 256 % nchan;
+  for (int64_t seg = (int64_t)blockIdx.x * kPlaceSegs + wave; seg < seg_end; seg += 4) {
     const int64_t i = seg * 64 + lane;
     const bool valid = i < nvis;
-    int64_t key = -1, r = 0, c = 0;
+    uint32_t key = kNoKey;
+    const int64_t r = r0, c = c0;
+    c0 += step_c;
+    r0 += step_r;
+    if (c0 >= nchan) {
+      c0 -= nchan;
+      ++r0;
+    }
     bool bad = false;
     if (valid) {
       const double wt = load_weight<WK>(wgt, i);
       double vr, vi;
       load_vis(vis, i, vr, vi);
+      const double u = uvw[3 * r], v = uvw[3 * r + 1], w = uvw[3 * r + 2], f = fx[c];
       // zero-weight visibilities are skipped by the scatter, whatever they hold
       const double a = wt == 0.0 ? 0.0 : fabs(wt) * fmax(fabs(vr), fabs(vi));
       nonfinite = nonfinite || (wt != 0.0 && !(isfinite(wt) && isfinite(vr) && isfinite(vi)));
       wsum += wt;
       wvmax = fmax(wvmax, a);
-      // i / nchan through fp64 (exact after one correction for i < 2^52)
-      r = (int64_t)((double)i / (double)nchan);
-      c = i - r * nchan;
-      if (c < 0) {
-        --r;
-        c += nchan;
-      } else if (c >= nchan) {
-        ++r;
-        c -= nchan;
-      }
       int64_t ix0, iy0, iw0;
       double yu, yv, yw;
-      if (place_vis(uvw[3 * r], uvw[3 * r + 1], uvw[3 * r + 2], fx[c], g, &ix0, &yu, &iy0, &yv, &iw0, &yw)) {
-        key = tile_key(ix0, iy0, iw0, g);
-        if (vis_class) vis_class[i] = (uint8_t)((((int)ix0 % kTile) * P + (int)iy0 % kTile) & 31);
+      if (place_vis(u, v, w, f, g, &ix0, &yu, &iy0, &yv, &iw0, &yw)) {
+        key = (uint32_t)tile_key(ix0, iy0, iw0, g);
+        if (vis_class) vis_class[i] = (uint8_t)((((unsigned)ix0 % kTile) * P + (unsigned)iy0 % kTile) & 31u);
       } else {
         bad = true;
         if (vis_class) vis_class[i] = 0;
       }
     }
     if (__ballot(bad) != 0ull && lane == 0) atomicOr(err_flag, 1u);
-    const int64_t prev = __shfl_up(key, 1, 64);
+    const uint32_t prev = __shfl_up(key, 1, 64);
     const bool start = valid && (lane == 0 || c == 0 || key != prev);
     const unsigned long long starts = __ballot(start);
-    const bool emit = start && key >= 0;
+    const bool emit = start && key != kNoKey;
     const unsigned long long emits = __ballot(emit);
     const int nvalid = __popcll(__ballot(valid));  // wave-uniform: outside the branch
     // the block's runs are parked densely from slot 64 * kPlaceSegs * b on
@@ -212,8 +216,8 @@ __global__ __launch_bounds__(256) void plan_place_kernel(const double* __restric
       const unsigned long long above = starts & ~((2ull << lane) - 1ull);  // lane 63: 2 << 63 == 0
       const int next = above ? (__ffsll((long long)above) - 1) : nvalid;
       const int64_t slot = (int64_t)blockIdx.x * kPlaceSegs * 64 + wbase + __popcll(emits & ((1ull << lane) - 1ull));
-      park_key[slot] = (uint32_t)key;
-      atomicAdd(&s_hist[(uint32_t)key & 255u], 1u);
+      park_key[slot] = key;
+      atomicAdd(&s_hist[key & 255u], 1u);
       park_run[slot] = ((uint64_t)r << 32) | ((uint64_t)c << 16) | (uint64_t)(c + (next - lane));
     }
   }
@@ -311,8 +315,15 @@ __global__ __launch_bounds__(kRadixThreads) void radix_scatter_kernel(
   __shared__ int64_t woff[4][256];   // global position of each wave's first item per digit
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int64_t cnt_b = radix_count(blockIdx.x, n, blk_cnt);
-  const int64_t i0 = (int64_t)blockIdx.x * kRadixBlock + wave * 1024 + lane;
-  const int64_t lim = (int64_t)blockIdx.x * kRadixBlock + cnt_b;
+  // the block's items are split into 4 contiguous, 64-aligned wave ranges of
+  // q items (q = 1024 for a full block; a parked block holds ~500 runs, which
+  // would otherwise all fall to wave 0); wave ranges in order keep it stable
+  const int steps = (int)((cnt_b + 255) / 256);  // 64-item steps per wave
+  const int q = 64 * steps;
+  const int64_t i0 = (int64_t)blockIdx.x * kRadixBlock + wave * q + lane;
+  const int64_t wlim = (int64_t)blockIdx.x * kRadixBlock + (int64_t)(wave + 1) * q;
+  const int64_t blim = (int64_t)blockIdx.x * kRadixBlock + cnt_b;
+  const int64_t lim = wlim < blim ? wlim : blim;
 #pragma unroll
   for (int w = 0; w < 4; ++w) wcnt[w][threadIdx.x] = 0u;
   uint32_t key[kRadixPer];
@@ -327,18 +338,20 @@ __global__ __launch_bounds__(kRadixThreads) void radix_scatter_kernel(
   unsigned rank[kRadixPer];
 #pragma unroll
   for (int k = 0; k < kRadixPer; ++k) {
-    const bool valid = i0 + k * 64 < lim;
-    const unsigned d = (key[k] >> shift) & 255u;
-    unsigned long long peers = __ballot(valid);
+    if (k < steps) {  // block-uniform
+      const bool valid = i0 + k * 64 < lim;
+      const unsigned d = (key[k] >> shift) & 255u;
+      unsigned long long peers = __ballot(valid);
 #pragma unroll
-    for (int b = 0; b < 8; ++b) {
-      const bool bit = (d >> b) & 1u;
-      const unsigned long long m = __ballot(bit);
-      peers &= bit ? m : ~m;
+      for (int b = 0; b < 8; ++b) {
+        const bool bit = (d >> b) & 1u;
+        const unsigned long long m = __ballot(bit);
+        peers &= bit ? m : ~m;
+      }
+      const unsigned prior = valid ? wcnt[wave][d] : 0u;
+      rank[k] = prior + (unsigned)__popcll(peers & ((1ull << lane) - 1ull));
+      if (valid && (peers & ((1ull << lane) - 1ull)) == 0ull) wcnt[wave][d] = prior + (unsigned)__popcll(peers);
     }
-    const unsigned prior = valid ? wcnt[wave][d] : 0u;
-    rank[k] = prior + (unsigned)__popcll(peers & ((1ull << lane) - 1ull));
-    if (valid && (peers & ((1ull << lane) - 1ull)) == 0ull) wcnt[wave][d] = prior + (unsigned)__popcll(peers);
   }
   __syncthreads();
   {
