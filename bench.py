@@ -129,8 +129,8 @@ def cpu_baseline(uvw, freq, npix, px, nvis_full, support, nthreads, sample_rows)
 def main():
     ap = argparse.ArgumentParser(description=__doc__.splitlines()[1])
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--support", type=int, default=8)
     ap.add_argument("--wstacking", action="store_true", help="w-stacking mode (secondary measurement)")
@@ -156,18 +156,37 @@ def main():
     nvis = cfg["rows"] * cfg["nchan"]
     npix = cfg["npix"]
     uvw_d, freq_d, vis_d, wgt_d, px, uvw_h, freq_h = make_inputs(cfg, rank, world, device)
-    dirty, sumw = image_buffer(npix, npix, device)  # adjacent: one RCCL reduce per step
+    # two image buffers (image + weight sum adjacent: one RCCL reduce each):
+    # step k's reduce runs on the communicator's stream while step k + 1
+    # inverts into the other buffer; a buffer is rewritten only after its
+    # previous reduce (and the normalisation on rank 0) completed
+    bufs = [image_buffer(npix, npix, device) for _ in range(2)]
+    pending = [None, None]
+    nstep = [0]
 
     def step():
+        k = nstep[0] % 2
+        nstep[0] += 1
+        if pending[k] is not None:
+            pending[k].wait()
+        dirty, sumw = bufs[k]
         gridder.device_ms2dirty(uvw_d, freq_d, vis_d, wgt_d, npix, npix, px, px, support=args.support,
                                 do_wstacking=args.wstacking, out=dirty, sum_weights=sumw)
-        # RCCL reduce of the partial images + weights to rank 0, normalise there
-        reduce_images(dirty, sumw, dst=0)
+        # RCCL reduce of the partial images + weights to rank 0, normalised there
+        pending[k] = reduce_images(dirty, sumw, dst=0, async_op=True)
+
+    def drain():
+        for k in range(2):
+            if pending[k] is not None:
+                pending[k].wait()
+                pending[k] = None
 
     log(f"[bench] rank {rank}/{world} config {args.config}: {nvis:,} vis/GPU, {npix}^2 image, "
         f"pixsize {px:.3e} rad, support {args.support}, wstacking={args.wstacking}")
     for _ in range(args.warmup):
         step()
+    drain()
+    dirty, sumw = bufs[0]
     _, params = gridder.device_ms2dirty(uvw_d, freq_d, vis_d, wgt_d, npix, npix, px, px, support=args.support,
                                         do_wstacking=args.wstacking, out=dirty, sum_weights=sumw)
     _lib.profile_enable(True)
@@ -178,7 +197,8 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
-        phases.append(_lib.profile_last())
+        phases.append(_lib.profile_last())  # host-side copy of the call's phase times (no sync)
+    drain()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

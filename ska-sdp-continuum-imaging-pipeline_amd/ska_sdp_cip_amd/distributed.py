@@ -28,14 +28,43 @@ def shard_rows(nrow: int, rank: int, world: int) -> tuple[int, int]:
     return list(balanced_chunk_bounds(0, nrow, world))[rank]
 
 
-def reduce_images(dirty, sum_weights, *, dst: int = 0, group=None, normalise: bool = True):
+class PendingReduce:
+    """
+    An image reduce in flight (`reduce_images(..., async_op=True)`): the
+    collective runs on the communicator's stream while the caller's stream
+    goes on (e.g. with the next shard's invert into another buffer).
+    `wait()` orders the caller's current stream after it and normalises on
+    `dst`; the buffers must not be written before then.
+    """
+
+    def __init__(self, works, dirty, sum_weights, normalise: bool):
+        self._works = works
+        self._dirty = dirty
+        self._sumw = sum_weights
+        self._normalise = normalise
+        self._done = False
+
+    def wait(self):
+        if not self._done:
+            for w in self._works:
+                w.wait()
+            if self._normalise:
+                self._dirty.div_(self._sumw)
+            self._done = True
+        return self._dirty
+
+
+def reduce_images(dirty, sum_weights, *, dst: int = 0, group=None, normalise: bool = True,
+                  async_op: bool = False):
     """
     Sum the partial dirty images and weight sums of all ranks onto `dst`
     (in place) and, on `dst`, divide by the total weight. Works for CUDA
-    tensors (RCCL) and CPU tensors (gloo).
+    tensors (RCCL) and CPU tensors (gloo). With `async_op=True` returns a
+    `PendingReduce` (call `.wait()` before reading or rewriting the buffers).
     """
     import torch.distributed as dist  # pylint: disable=import-outside-toplevel
 
+    works = []
     if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
         base = dirty.untyped_storage().data_ptr()
         n = dirty.numel()
@@ -45,16 +74,15 @@ def reduce_images(dirty, sum_weights, *, dst: int = 0, group=None, normalise: bo
                 and dirty.storage_offset() + n + 1 <= dirty.untyped_storage().nbytes() // dirty.element_size()):
             # image and weight sum adjacent in one buffer (see image_buffer): one collective
             flat = dirty.new_empty(0).set_(dirty.untyped_storage(), dirty.storage_offset(), (n + 1,), (1,))
-            dist.reduce(flat, dst, group=group)
+            works.append(dist.reduce(flat, dst, group=group, async_op=async_op))
         else:
-            dist.reduce(dirty, dst, group=group)
-            dist.reduce(sum_weights, dst, group=group)
+            works.append(dist.reduce(dirty, dst, group=group, async_op=async_op))
+            works.append(dist.reduce(sum_weights, dst, group=group, async_op=async_op))
         is_dst = dist.get_rank() == dst
     else:
         is_dst = True
-    if normalise and is_dst:
-        dirty.div_(sum_weights)
-    return dirty
+    pending = PendingReduce([w for w in works if w is not None], dirty, sum_weights, normalise and is_dst)
+    return pending if async_op else pending.wait()
 
 
 def image_buffer(npix_x: int, npix_y: int, device):

@@ -25,7 +25,7 @@ def _free_port():
     return port
 
 
-def _worker(rank, world, port, npix, q, fused=False):
+def _worker(rank, world, port, npix, q, fused=False, async_op=False):
     import sys
     from pathlib import Path
 
@@ -49,7 +49,11 @@ def _worker(rank, world, port, npix, q, fused=False):
     else:
         img = torch.from_numpy(part.copy())
         sw = torch.tensor([w[a:b].astype(np.float64).sum()], dtype=torch.float64)
-    reduce_images(img, sw, dst=0)
+    if async_op:  # pipelined form (bench.py): the collective in flight, then wait()
+        pending = reduce_images(img, sw, dst=0, async_op=True)
+        assert pending.wait() is img
+    else:
+        reduce_images(img, sw, dst=0)
     if rank == 0:
         full = oracle.ms2dirty(uvw, f, vis, w, npix, npix, px, px, support=8, nthreads=1)
         q.put(float(np.abs(img.numpy() - full / w.astype(np.float64).sum()).max()))
@@ -68,12 +72,12 @@ def test_shard_rows_cover_everything():
         shard_rows(10, 3, 3)
 
 
-@pytest.mark.parametrize("fused", [False, True])
-def test_sharded_invert_reduce_world2(fused):
+@pytest.mark.parametrize("fused,async_op", [(False, False), (True, False), (True, True)])
+def test_sharded_invert_reduce_world2(fused, async_op):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, 64, q, fused)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, 64, q, fused, async_op)) for r in range(2)]
     for p in procs:
         p.start()
     for p in procs:

@@ -11,4 +11,5 @@ timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 && echo "smoke ok" &&
 timeout -k 10 600 python bench.py > $OUT/bench.json 2> $OUT/bench.err && echo "bench ok" &&
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $PWD/$OUT/prof -o $ROUND --output-format csv -- \
-    python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > $OUT/bench_prof.json 2> $OUT/bench_prof.err && echo "prof ok"
+    python3 bench.py --no-cpu-baseline > $OUT/bench_prof.json 2> $OUT/bench_prof.err && echo "prof ok" &&
+python3 tools/trace_summary.py $OUT/prof/${ROUND}_kernel_trace.csv 20 $OUT/${ROUND}_kernel_summary.md > /dev/null
