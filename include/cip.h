@@ -101,6 +101,44 @@ int cip_grid_plane(const double* uvw, int64_t nrow, const double* freq,
                    double pixsize_y, int64_t plane, int flags,
                    void* hip_stream, double* grid_out);
 
+/* Accumulating gridder (chunked / streamed inputs): grids
+ * holds params->nplanes planes of nu x nv complex128 (DEVICE, zeroed by the
+ * caller before the first chunk) in the layout cip_grid_layout reports for
+ * the target image (1: each plane stored transposed, gT[y][x]; 0: g[x][y]).
+ * Every call adds its visibilities onto the planes and its weight sum onto
+ * *sum_wgt (device f64, may be NULL); params must be the same for every chunk
+ * (cip_choose_params over the whole data set's w range). */
+int cip_grid_layout(const cip_gridder_params* params, int64_t npix_x,
+                    int64_t npix_y);
+
+/* Dense chunk: MS rows, as cip_ms2dirty (uvw (nrow,3), vis/wgt (nrow,nchan)). */
+int cip_grid_ms(const double* uvw, int64_t nrow, const double* freq,
+                int64_t nchan, const void* vis, int vis_dtype,
+                const void* wgt, int wgt_dtype,
+                const cip_gridder_params* params, double pixsize_x,
+                double pixsize_y, int64_t npix_x, int64_t npix_y, int flags,
+                void* hip_stream, double* grids, double* sum_wgt);
+
+/* Tile-sorted chunk (the uvw_tiling Tile layout, reference
+ * uvw_tiling/tile.py:14-124, the reorder output): nslices row slices with
+ * uvw (nslices,3) f64 metres and channel ranges [chan_start, chan_stop)
+ * (int32); vis (nvis) and wgt (nvis, or NULL) hold the slices' visibilities
+ * concatenated in slice order (nvis = sum of the range lengths). */
+int cip_grid_tiles(const double* slice_uvw, const int32_t* chan_start,
+                   const int32_t* chan_stop, int64_t nslices,
+                   const double* freq, int64_t nchan, const void* vis,
+                   int64_t nvis, int vis_dtype, const void* wgt, int wgt_dtype,
+                   const cip_gridder_params* params, double pixsize_x,
+                   double pixsize_y, int64_t npix_x, int64_t npix_y, int flags,
+                   void* hip_stream, double* grids, double* sum_wgt);
+
+/* The accumulated planes -> dirty image (device (npix_x,npix_y) f64, not
+ * normalised): FFT, w-screens and grid correction as in cip_ms2dirty. The
+ * planes are consumed (used as FFT scratch). */
+int cip_grid_to_dirty(double* grids, const cip_gridder_params* params,
+                      int64_t npix_x, int64_t npix_y, double pixsize_x,
+                      double pixsize_y, void* hip_stream, double* dirty_out);
+
 /* Reference-exact UVW tile keys and constant-key channel runs (one run per
  * maximal range of channels with equal (iu, iv, iw) in a row), rows in
  * order, runs in channel order: key = floor(f/c * (uvw / tile) + 0.5) in

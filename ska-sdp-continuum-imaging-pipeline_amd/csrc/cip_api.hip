@@ -446,7 +446,7 @@ static bool scatter_order() {
 
 // Also reduces {sum w, max |w V|} into red (device) and returns max |w V| in
 // *maxabs (the place pass reads the visibilities anyway).
-static int make_plan(Workspace* ws, const double* uvw, int64_t nrow, const double* fx, int64_t nchan,
+static int make_plan(Workspace* ws, const double* uvw, const double* fx, const RowMap& m,
                      const void* vis, int vis_dtype, const void* wgt, int wgt_dtype, double* red,
                      const GridGeometry& g, int64_t cv, hipStream_t s, PlanResult* pr, double* maxabs) {
   const int64_t ntiles = g.ntx * g.nty * g.ntw;
@@ -458,7 +458,7 @@ static int make_plan(Workspace* ws, const double* uvw, int64_t nrow, const doubl
   CIP_ALLOC(err, unsigned, "err_flag", 1)
   CIP_ALLOC(scan_tmp, int64_t, "scan_tmp", scan_tmp_elems(ntiles + 1))
   CIP_HIP_CHECK(hipMemsetAsync(err, 0, sizeof(unsigned), s));
-  const int64_t nvis = nrow * nchan;
+  const int64_t nvis = m.nvis;
   const int nblk = plan_place_blocks(nvis);
   // the bank-class order needs a 32-bit flattened index (larger inputs grid in
   // plain tile order)
@@ -475,7 +475,7 @@ static int make_plan(Workspace* ws, const double* uvw, int64_t nrow, const doubl
   // the place pass also writes radix pass 0's histogram; its scan's last entry = runs
   CIP_ALLOC(hist0, int64_t, "radix_hist0", 256 * (int64_t)nblk + 1)
   CIP_ALLOC(scan_h0, int64_t, "scan_hist0", scan_tmp_elems(256 * (int64_t)nblk + 1))
-  CIP_HIP_CHECK(launch_plan_place(uvw, nrow, fx, nchan, vis, vis_dtype, wgt, wgt_dtype, g, err, vis_class, blk_cnt, park_key,
+  CIP_HIP_CHECK(launch_plan_place(uvw, fx, m, vis, vis_dtype, wgt, wgt_dtype, g, err, vis_class, blk_cnt, park_key,
                                   park_run, partial, hist0, s));
   CIP_HIP_CHECK(launch_prep_final(partial, nblk, red, s));
   int key_bits = 1;
@@ -552,8 +552,8 @@ static int make_plan(Workspace* ws, const double* uvw, int64_t nrow, const doubl
     CIP_ALLOC(windows, Chunk, "windows", nwin)
     CIP_HIP_CHECK(launch_chunk_emit(tile_vis_off, tile_vis, win_off, run_goff, tile_runs, ntiles, kOrderWindow, nwin,
                                     windows, s));
-    CIP_ALLOC(perm, uint32_t, "perm", nrow * nchan)
-    CIP_HIP_CHECK(launch_order(uvw, fx, vis_class, g, nchan, runs, run_goff, tile_runs, windows, nwin, perm, s));
+    CIP_ALLOC(perm, uint32_t, "perm", nvis)
+    CIP_HIP_CHECK(launch_order(uvw, fx, vis_class, g, m, runs, run_goff, tile_runs, windows, nwin, perm, s));
     pr->perm = perm;
   }
   return CIP_OK;
@@ -569,13 +569,24 @@ struct Prepared {
   bool packed;  // single-precision class (CIP_ACC_SINGLE)
   double* fx;
   double* red;  // device [sum_w, max|wV|]
+  RowMap m;     // (row, channel) -> visibility index
   PlanResult plan;
+};
+
+// Row slices of the ragged (tile) input layout: row r holds channels
+// [chan_start[r], chan_stop[r]) and the visibilities are concatenated in row
+// order (reference uvw_tiling/tile.py:83-115), nvis in total.
+struct RaggedRows {
+  const int32_t* chan_start;
+  const int32_t* chan_stop;
+  int64_t nvis;
 };
 
 static int prepare(Workspace* ws, const double* uvw, int64_t nrow, const double* freq, int64_t nchan,
                    const void* vis, int vis_dtype, const void* wgt, int wgt_dtype, int64_t npix_x, int64_t npix_y,
                    double px, double py, double epsilon, int support, int do_wstacking, bool packed,
-                   const cip_gridder_params* given, hipStream_t s, Prepared* out, double** grid_out = nullptr) {
+                   const cip_gridder_params* given, hipStream_t s, Prepared* out, double** grid_out = nullptr,
+                   const RaggedRows* ragged = nullptr) {
   if (!vis_dtype_ok(vis_dtype)) return set_error(CIP_EINVAL, "vis dtype must be complex64 or complex128");
   if (!wgt_dtype_ok(wgt_dtype)) return set_error(CIP_EINVAL, "wgt dtype must be float32, float64 or none");
   if (wgt == nullptr) wgt_dtype = CIP_NONE;
@@ -594,6 +605,37 @@ static int prepare(Workspace* ws, const double* uvw, int64_t nrow, const double*
     fxmax = std::fmax(fxmax, h[4 + c]);
   }
   if (!(fxmin > 0.0)) return set_error(CIP_EINVAL, "channel frequencies must be positive");
+  RowMap& m = out->m;
+  m.nchan = nchan;
+  m.inv_nchan = 1.0 / (double)nchan;
+  m.delta = nullptr;
+  m.vis_row = nullptr;
+  m.nvis = nrow * nchan;
+  if (ragged) {
+    if (ragged->nvis < 0 || ragged->nvis >= ((int64_t)1 << 40)) return set_error(CIP_EINVAL, "bad visibility count");
+    m.nvis = ragged->nvis;
+    if (nrow > 0) {
+      int64_t* off = buf<int64_t>(ws, "ragged_off", nrow + 1);
+      int64_t* delta = buf<int64_t>(ws, "ragged_delta", nrow);
+      uint32_t* vis_row = buf<uint32_t>(ws, "ragged_vis_row", ragged->nvis);
+      int64_t* scan_tmp = buf<int64_t>(ws, "ragged_scan", scan_tmp_elems(nrow + 1));
+      unsigned* rerr = buf<unsigned>(ws, "ragged_err", 1);
+      if (!off || !delta || !vis_row || !scan_tmp || !rerr) return CIP_ENOMEM;
+      CIP_HIP_CHECK(hipMemsetAsync(rerr, 0, sizeof(unsigned), s));
+      CIP_HIP_CHECK(launch_ragged_lengths(ragged->chan_start, ragged->chan_stop, nrow, nchan, off, rerr, s));
+      CIP_HIP_CHECK(exclusive_scan_i64(off, nrow + 1, scan_tmp, s));
+      int64_t* hr = (int64_t*)pinned(ws, 2 * sizeof(int64_t));
+      if (!hr) return set_error(CIP_ENOMEM, "hipHostMalloc failed");
+      CIP_HIP_CHECK(hipMemcpyAsync(&hr[0], off + nrow, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+      CIP_HIP_CHECK(hipMemcpyAsync(&hr[1], rerr, sizeof(unsigned), hipMemcpyDeviceToHost, s));
+      CIP_HIP_CHECK(hipStreamSynchronize(s));
+      if ((unsigned)hr[1] != 0u) return set_error(CIP_EINVAL, "row slice channel range outside [0, nchan)");
+      if (hr[0] != ragged->nvis) return set_error(CIP_EINVAL, "visibility count differs from the row slices' total");
+      CIP_HIP_CHECK(launch_ragged_expand(off, ragged->chan_start, nrow, delta, vis_row, s));
+      m.delta = delta;
+      m.vis_row = vis_row;
+    }
+  }
   double wmin = 0.0, wmax = 0.0;
   if (do_wstacking && nrow > 0 && given == nullptr) {
     const int nb = 256;
@@ -641,7 +683,13 @@ static int prepare(Workspace* ws, const double* uvw, int64_t nrow, const double*
     return CIP_OK;
   }
   double maxabs = 0.0;
-  const int rc = make_plan(ws, uvw, nrow, fx, nchan, vis, vis_dtype, wgt, wgt_dtype, red, out->g, chunk_vis(packed),
+  if (m.nvis == 0) {
+    CIP_HIP_CHECK(hipMemsetAsync(red, 0, 2 * sizeof(double), s));
+    out->plan = PlanResult();
+    out->plan.plane_chunk_off.assign(out->g.ntw + 1, 0);
+    return CIP_OK;
+  }
+  const int rc = make_plan(ws, uvw, fx, m, vis, vis_dtype, wgt, wgt_dtype, red, out->g, chunk_vis(packed),
                            s, &out->plan, &maxabs);
   g_prof.span(1, e_prep, g_prof.mark(s));
   if (rc != CIP_OK) return rc;
@@ -651,7 +699,7 @@ static int prepare(Workspace* ws, const double* uvw, int64_t nrow, const double*
   int e2 = 0;
   if (maxabs > 0.0) std::frexp(maxabs, &e2);  // maxabs < 2^e2
   out->fixed_scale = std::ldexp(1.0, (packed ? kPackedBits : kFixedBits) - e2);
-  g_prof.counts[0] = nrow * nchan;
+  g_prof.counts[0] = m.nvis;
   g_prof.counts[1] = out->plan.nruns;
   g_prof.counts[2] = out->plan.nchunks;
   g_prof.counts[3] = out->g.nplanes;
@@ -661,7 +709,7 @@ static int prepare(Workspace* ws, const double* uvw, int64_t nrow, const double*
 // transposed: store the grid as gT[y, x] (input layout of the pruned FFT)
 // zeroed: the grid was zeroed already (side stream, joined by the caller)
 static int scatter_plane(const Prepared& pp, int64_t plane, const double* uvw, const void* vis, int vis_dtype,
-                         const void* wgt, int wgt_dtype, int64_t nchan, bool transposed, double* grid,
+                         const void* wgt, int wgt_dtype, bool transposed, double* grid,
                          hipStream_t s, bool zeroed = false) {
   GridGeometry g = pp.g;
   g.transposed = transposed ? 1 : 0;
@@ -677,12 +725,161 @@ static int scatter_plane(const Prepared& pp, int64_t plane, const double* uvw, c
   const int64_t cb = pp.plan.plane_chunk_off[lo], ce = pp.plan.plane_chunk_off[hi + 1];
   if (wgt == nullptr) wgt_dtype = CIP_NONE;
   hipEvent_t a = g_prof.mark(s);
-  CIP_HIP_CHECK(launch_scatter(g.support, vis_dtype, wgt_dtype, pp.packed, uvw, pp.fx, vis, wgt, nchan, pp.plan.runs,
+  CIP_HIP_CHECK(launch_scatter(g.support, vis_dtype, wgt_dtype, pp.packed, uvw, pp.fx, vis, wgt, pp.m, pp.plan.runs,
                                pp.plan.run_goff, pp.plan.tile_run_off, pp.plan.perm, pp.plan.chunks, cb, ce - cb,
                                g, plane,
                                pp.fixed_scale, grid, s));
   g_prof.span(2, a, g_prof.mark(s));
   if (ce > cb) g_prof.counts[4] += 1;
+  return CIP_OK;
+}
+
+// ------------------------------------------- grid -> dirty image (shared) ----
+// Correction vectors, FFT plan / twiddles and the pass-A buffer for one
+// (grid, image) geometry; then per plane: FFT + crop/correct (2-D) or the
+// w-screen accumulation, and the final w-stacking correction.
+struct DirtyStage {
+  int64_t npix_x = 0, npix_y = 0;
+  double px = 0, py = 0;
+  bool fast = false;
+  hipfftHandle plan = nullptr;
+  double *tw_u = nullptr, *tw_v = nullptr, *fft_h = nullptr, *cx = nullptr, *cy = nullptr;
+};
+
+// the HBM layout of the uv grid the FFT stage expects: gT[y, x] when the
+// pruned FFT runs
+static bool grid_is_transposed(const GridGeometry& g, int64_t npix_x, int64_t npix_y) {
+  return fft_pruned() && fast_fft_supported(g.nu, g.nv, npix_x, npix_y);
+}
+
+static int dirty_stage(Workspace* ws, const GridGeometry& g, int64_t npix_x, int64_t npix_y, double px, double py,
+                       hipStream_t s, DirtyStage* st) {
+  st->npix_x = npix_x;
+  st->npix_y = npix_y;
+  st->px = px;
+  st->py = py;
+  CIP_ALLOC(cx, double, "cx", npix_x)
+  CIP_ALLOC(cy, double, "cy", npix_y)
+  st->cx = cx;
+  st->cy = cy;
+  HostKernel hk;
+  host_kernel(g.support, &hk);
+  KernelFT F(hk);
+  // the correction vectors depend only on (npix, grid, W): cache them per device
+  const std::vector<int64_t> corr_key = {npix_x, npix_y, g.nu, g.nv, g.support};
+  if (ws->corr_key != corr_key) {
+    ws->corr_key.clear();
+    std::vector<double> hx(npix_x), hy(npix_y);
+    for (int64_t i = 0; i < npix_x; ++i) hx[i] = 1.0 / F((double)(i - npix_x / 2) / (double)g.nu);
+    for (int64_t j = 0; j < npix_y; ++j) hy[j] = 1.0 / F((double)(j - npix_y / 2) / (double)g.nv);
+    CIP_HIP_CHECK(hipMemcpyAsync(cx, hx.data(), sizeof(double) * npix_x, hipMemcpyHostToDevice, s));
+    CIP_HIP_CHECK(hipMemcpyAsync(cy, hy.data(), sizeof(double) * npix_y, hipMemcpyHostToDevice, s));
+    CIP_HIP_CHECK(hipStreamSynchronize(s));  // host vectors go out of scope
+    ws->corr_key = corr_key;
+  }
+  // pruned FFT (cip_fft.hip) for power-of-two grids; hipFFT 2-D otherwise
+  // (CIP_FFT_PRUNED=0 forces the latter)
+  st->fast = grid_is_transposed(g, npix_x, npix_y);
+  if (st->fast) {
+    int rc = fft_twiddles(ws, g.nu, s, &st->tw_u);
+    if (rc != CIP_OK) return rc;
+    rc = fft_twiddles(ws, g.nv, s, &st->tw_v);
+    if (rc != CIP_OK) return rc;
+    st->fft_h = buf<double>(ws, "fft_pass_a", 2 * npix_x * g.nv);
+    if (!st->fft_h) return CIP_ENOMEM;
+  } else {
+    const int rc = fft_plan(ws, g.nu, g.nv, s, &st->plan);
+    if (rc != CIP_OK) return rc;
+  }
+  return CIP_OK;
+}
+
+// plane p's grid (consumed: the hipFFT path transforms it in place) into
+// dirty_out (overwritten for p == 0, accumulated after it)
+static int plane_to_dirty(const DirtyStage& st, const GridGeometry& g, int64_t p, double* grid, double* dirty_out,
+                          hipStream_t s) {
+  hipEvent_t f0 = g_prof.mark(s);
+  if (st.fast) {
+    CIP_HIP_CHECK(launch_fft_rows(grid, g.nu, g.nv, st.npix_x, st.tw_u, st.fft_h, s));
+  } else if (hipfftExecZ2Z(st.plan, (hipfftDoubleComplex*)grid, (hipfftDoubleComplex*)grid, HIPFFT_BACKWARD) !=
+             HIPFFT_SUCCESS) {
+    return set_error(CIP_EHIP, "hipfftExecZ2Z failed");
+  }
+  const double w_plane = g.w0 + (double)p * g.dw;
+  // pass B carries the crop epilogue: it is booked under "fft"
+  if (st.fast)
+    CIP_HIP_CHECK(launch_fft_cols(st.fft_h, g.nv, st.npix_x, st.npix_y, st.tw_v, g.do_wstacking ? 1 : 0, dirty_out,
+                                  st.cx, st.cy, st.px, st.py, w_plane, p == 0, s));
+  hipEvent_t f1 = g_prof.mark(s);
+  g_prof.span(3, f0, f1);
+  if (st.fast) {
+  } else if (g.do_wstacking) {
+    CIP_HIP_CHECK(launch_wplane_accumulate(grid, g, st.npix_x, st.npix_y, st.px, st.py, w_plane, p == 0, dirty_out,
+                                           s));
+  } else {
+    CIP_HIP_CHECK(launch_crop_correct_2d(grid, g, st.npix_x, st.npix_y, st.cx, st.cy, dirty_out, s));
+  }
+  g_prof.span(4, f1, g_prof.mark(s));
+  return CIP_OK;
+}
+
+// after the last plane: the w-stacking correction (2-D: nothing)
+static int finish_dirty(Workspace* ws, const DirtyStage& st, const cip_gridder_params& prm, const GridGeometry& g,
+                        double* dirty_out, hipStream_t s) {
+  if (!g.do_wstacking) return CIP_OK;
+  HostKernel hk;
+  host_kernel(g.support, &hk);
+  KernelFT F(hk);
+  const int64_t fw_n = 4100;
+  const double numax = g.dw * std::fabs(prm.nmin);
+  const double dnu = (numax > 0 ? numax : 1e-3) * 1.0001 / 4096.0;
+  CIP_ALLOC(fwd, double, "fw_table", fw_n)
+  const std::vector<double> fw_key = {(double)g.support, numax};
+  if (ws->fw_key != fw_key) {
+    ws->fw_key.clear();
+    std::vector<double> fw(fw_n);
+    for (int64_t k = 0; k < fw_n; ++k) fw[k] = F((double)k * dnu);
+    CIP_HIP_CHECK(hipMemcpyAsync(fwd, fw.data(), sizeof(double) * fw_n, hipMemcpyHostToDevice, s));
+    CIP_HIP_CHECK(hipStreamSynchronize(s));
+    ws->fw_key = fw_key;
+  }
+  CIP_HIP_CHECK(launch_wfinal_correct(dirty_out, st.npix_x, st.npix_y, st.px, st.py, st.cx, st.cy, fwd, fw_n, dnu,
+                                      g.dw, s));
+  return CIP_OK;
+}
+
+// Grid visibilities (dense MS rows, or ragged row slices) onto nplanes
+// resident accumulator planes (no zeroing: += onto what they hold), and add
+// their weight sum to *sum_wgt.
+static int grid_accumulate(const double* uvw, int64_t nrow, const double* freq, int64_t nchan, const void* vis,
+                           int vis_dtype, const void* wgt, int wgt_dtype, const cip_gridder_params* params,
+                           double pixsize_x, double pixsize_y, int64_t npix_x, int64_t npix_y, int flags,
+                           void* hip_stream, double* grids, double* sum_wgt, const RaggedRows* ragged) {
+  g_last_error.clear();
+  if (flags & ~CIP_ACC_SINGLE) return set_error(CIP_EINVAL, "unknown flags");
+  if (!params || !grids) return set_error(CIP_EINVAL, "NULL params or grids");
+  if (nrow > 0 && (!uvw || !freq || !vis)) return set_error(CIP_EINVAL, "NULL input pointer");
+  hipStream_t s = (hipStream_t)hip_stream;
+  Workspace* ws = workspace();
+  if (!ws) return set_error(CIP_EHIP, "no HIP device");
+  g_prof.reset();
+  hipEvent_t t_start = g_prof.mark(s);
+  Prepared pp;
+  int rc = prepare(ws, uvw, nrow, freq, nchan, vis, vis_dtype, wgt, wgt_dtype, 2, 2, pixsize_x, pixsize_y, 0.0,
+                   params->support, params->do_wstacking, (flags & CIP_ACC_SINGLE) != 0, params, s, &pp, nullptr,
+                   ragged);
+  if (rc != CIP_OK) return rc;
+  const GridGeometry& g = pp.g;
+  const bool transposed = grid_is_transposed(g, npix_x, npix_y);
+  const int64_t plane_elems = 2 * g.nu * g.nv;
+  for (int64_t p = 0; p < g.nplanes; ++p) {
+    rc = scatter_plane(pp, p, uvw, vis, vis_dtype, wgt, wgt_dtype, transposed, grids + p * plane_elems, s, true);
+    if (rc != CIP_OK) return rc;
+  }
+  if (sum_wgt) CIP_HIP_CHECK(launch_add_scalar(pp.red, sum_wgt, s));
+  g_prof.span(5, t_start, g_prof.mark(s));
+  CIP_HIP_CHECK(hipStreamSynchronize(s));
+  g_prof.finish();
   return CIP_OK;
 }
 
@@ -733,84 +930,71 @@ int cip_ms2dirty(const double* uvw, int64_t nrow, const double* freq, int64_t nc
   const bool zeroed = grid != nullptr;
   if (!grid) grid = buf<double>(ws, "grid", 2 * g.nu * g.nv);
   if (!grid) return CIP_ENOMEM;
-  CIP_ALLOC(cx, double, "cx", npix_x)
-  CIP_ALLOC(cy, double, "cy", npix_y)
-  HostKernel hk;
-  host_kernel(g.support, &hk);
-  KernelFT F(hk);
-  // the correction vectors depend only on (npix, grid, W): cache them per device
-  const std::vector<int64_t> corr_key = {npix_x, npix_y, g.nu, g.nv, g.support};
-  if (ws->corr_key != corr_key) {
-    ws->corr_key.clear();
-    std::vector<double> hx(npix_x), hy(npix_y);
-    for (int64_t i = 0; i < npix_x; ++i) hx[i] = 1.0 / F((double)(i - npix_x / 2) / (double)g.nu);
-    for (int64_t j = 0; j < npix_y; ++j) hy[j] = 1.0 / F((double)(j - npix_y / 2) / (double)g.nv);
-    CIP_HIP_CHECK(hipMemcpyAsync(cx, hx.data(), sizeof(double) * npix_x, hipMemcpyHostToDevice, s));
-    CIP_HIP_CHECK(hipMemcpyAsync(cy, hy.data(), sizeof(double) * npix_y, hipMemcpyHostToDevice, s));
-    CIP_HIP_CHECK(hipStreamSynchronize(s));  // host vectors go out of scope
-    ws->corr_key = corr_key;
-  }
-  // pruned FFT (cip_fft.hip) for power-of-two grids; hipFFT 2-D otherwise
-  // (CIP_FFT_PRUNED=0 forces the latter)
-  const bool fast = fft_pruned() && fast_fft_supported(g.nu, g.nv, npix_x, npix_y);
-  hipfftHandle plan = nullptr;
-  double *tw_u = nullptr, *tw_v = nullptr, *fft_h = nullptr;
-  if (fast) {
-    rc = fft_twiddles(ws, g.nu, s, &tw_u);
-    if (rc != CIP_OK) return rc;
-    rc = fft_twiddles(ws, g.nv, s, &tw_v);
-    if (rc != CIP_OK) return rc;
-    fft_h = buf<double>(ws, "fft_pass_a", 2 * npix_x * g.nv);
-    if (!fft_h) return CIP_ENOMEM;
-  } else {
-    rc = fft_plan(ws, g.nu, g.nv, s, &plan);
-    if (rc != CIP_OK) return rc;
-  }
+  DirtyStage st;
+  rc = dirty_stage(ws, g, npix_x, npix_y, pixsize_x, pixsize_y, s, &st);
+  if (rc != CIP_OK) return rc;
   for (int64_t p = 0; p < g.nplanes; ++p) {
-    rc = scatter_plane(pp, p, uvw, vis, vis_dtype, wgt, wgt_dtype, nchan, fast, grid, s, zeroed && p == 0);
+    rc = scatter_plane(pp, p, uvw, vis, vis_dtype, wgt, wgt_dtype, st.fast, grid, s, zeroed && p == 0);
     if (rc != CIP_OK) return rc;
-    hipEvent_t f0 = g_prof.mark(s);
-    if (fast) {
-      CIP_HIP_CHECK(launch_fft_rows(grid, g.nu, g.nv, npix_x, tw_u, fft_h, s));
-    } else if (hipfftExecZ2Z(plan, (hipfftDoubleComplex*)grid, (hipfftDoubleComplex*)grid, HIPFFT_BACKWARD) !=
-               HIPFFT_SUCCESS) {
-      return set_error(CIP_EHIP, "hipfftExecZ2Z failed");
-    }
-    const double w_plane = g.w0 + (double)p * g.dw;
-    // pass B carries the crop epilogue: it is booked under "fft"
-    if (fast)
-      CIP_HIP_CHECK(launch_fft_cols(fft_h, g.nv, npix_x, npix_y, tw_v, g.do_wstacking ? 1 : 0, dirty_out, cx, cy,
-                                    pixsize_x, pixsize_y, w_plane, p == 0, s));
-    hipEvent_t f1 = g_prof.mark(s);
-    g_prof.span(3, f0, f1);
-    if (fast) {
-    } else if (g.do_wstacking) {
-      CIP_HIP_CHECK(launch_wplane_accumulate(grid, g, npix_x, npix_y, pixsize_x, pixsize_y, w_plane, p == 0,
-                                             dirty_out, s));
-    } else {
-      CIP_HIP_CHECK(launch_crop_correct_2d(grid, g, npix_x, npix_y, cx, cy, dirty_out, s));
-    }
-    g_prof.span(4, f1, g_prof.mark(s));
+    rc = plane_to_dirty(st, g, p, grid, dirty_out, s);
+    if (rc != CIP_OK) return rc;
   }
-  if (g.do_wstacking) {
-    const int64_t fw_n = 4100;
-    const double numax = g.dw * std::fabs(pp.p.nmin);
-    const double dnu = (numax > 0 ? numax : 1e-3) * 1.0001 / 4096.0;
-    CIP_ALLOC(fwd, double, "fw_table", fw_n)
-    const std::vector<double> fw_key = {(double)g.support, numax};
-    if (ws->fw_key != fw_key) {
-      ws->fw_key.clear();
-      std::vector<double> fw(fw_n);
-      for (int64_t k = 0; k < fw_n; ++k) fw[k] = F((double)k * dnu);
-      CIP_HIP_CHECK(hipMemcpyAsync(fwd, fw.data(), sizeof(double) * fw_n, hipMemcpyHostToDevice, s));
-      CIP_HIP_CHECK(hipStreamSynchronize(s));
-      ws->fw_key = fw_key;
-    }
-    CIP_HIP_CHECK(
-        launch_wfinal_correct(dirty_out, npix_x, npix_y, pixsize_x, pixsize_y, cx, cy, fwd, fw_n, dnu, g.dw, s));
-    CIP_HIP_CHECK(hipStreamSynchronize(s));
-  }
+  rc = finish_dirty(ws, st, pp.p, g, dirty_out, s);
+  if (rc != CIP_OK) return rc;
   if (sum_wgt_out) CIP_HIP_CHECK(hipMemcpyAsync(sum_wgt_out, pp.red, sizeof(double), hipMemcpyDeviceToDevice, s));
+  g_prof.span(5, t_start, g_prof.mark(s));
+  CIP_HIP_CHECK(hipStreamSynchronize(s));
+  g_prof.finish();
+  return CIP_OK;
+}
+
+int cip_grid_layout(const cip_gridder_params* params, int64_t npix_x, int64_t npix_y) {
+  g_last_error.clear();
+  if (!params) return set_error(CIP_EINVAL, "params is NULL");
+  return fft_pruned() && fast_fft_supported(params->nu, params->nv, npix_x, npix_y) ? 1 : 0;
+}
+
+int cip_grid_ms(const double* uvw, int64_t nrow, const double* freq, int64_t nchan, const void* vis, int vis_dtype,
+                const void* wgt, int wgt_dtype, const cip_gridder_params* params, double pixsize_x, double pixsize_y,
+                int64_t npix_x, int64_t npix_y, int flags, void* hip_stream, double* grids, double* sum_wgt) {
+  if (nrow < 0) return set_error(CIP_EINVAL, "nrow must be >= 0");
+  return grid_accumulate(uvw, nrow, freq, nchan, vis, vis_dtype, wgt, wgt_dtype, params, pixsize_x, pixsize_y,
+                         npix_x, npix_y, flags, hip_stream, grids, sum_wgt, nullptr);
+}
+
+int cip_grid_tiles(const double* slice_uvw, const int32_t* chan_start, const int32_t* chan_stop, int64_t nslices,
+                   const double* freq, int64_t nchan, const void* vis, int64_t nvis, int vis_dtype, const void* wgt,
+                   int wgt_dtype, const cip_gridder_params* params, double pixsize_x, double pixsize_y,
+                   int64_t npix_x, int64_t npix_y, int flags, void* hip_stream, double* grids, double* sum_wgt) {
+  if (nslices < 0 || nvis < 0) return set_error(CIP_EINVAL, "nslices and nvis must be >= 0");
+  if (nslices > 0 && (!chan_start || !chan_stop)) return set_error(CIP_EINVAL, "NULL channel ranges");
+  if (nslices >= ((int64_t)1 << 32) - 1) return set_error(CIP_EINVAL, "nslices must be < 2^32 - 1");
+  const RaggedRows rr{chan_start, chan_stop, nvis};
+  return grid_accumulate(slice_uvw, nslices, freq, nchan, vis, vis_dtype, wgt, wgt_dtype, params, pixsize_x,
+                         pixsize_y, npix_x, npix_y, flags, hip_stream, grids, sum_wgt, &rr);
+}
+
+int cip_grid_to_dirty(double* grids, const cip_gridder_params* params, int64_t npix_x, int64_t npix_y,
+                      double pixsize_x, double pixsize_y, void* hip_stream, double* dirty_out) {
+  g_last_error.clear();
+  if (!params || !grids || !dirty_out) return set_error(CIP_EINVAL, "NULL params, grids or dirty_out");
+  if (npix_x < 1 || npix_y < 1 || npix_x > params->nu || npix_y > params->nv)
+    return set_error(CIP_EINVAL, "image larger than the grid");
+  hipStream_t s = (hipStream_t)hip_stream;
+  Workspace* ws = workspace();
+  if (!ws) return set_error(CIP_EHIP, "no HIP device");
+  g_prof.reset();
+  hipEvent_t t_start = g_prof.mark(s);
+  const GridGeometry g = geometry(*params, pixsize_x, pixsize_y);
+  DirtyStage st;
+  int rc = dirty_stage(ws, g, npix_x, npix_y, pixsize_x, pixsize_y, s, &st);
+  if (rc != CIP_OK) return rc;
+  for (int64_t p = 0; p < g.nplanes; ++p) {
+    rc = plane_to_dirty(st, g, p, grids + p * 2 * g.nu * g.nv, dirty_out, s);
+    if (rc != CIP_OK) return rc;
+  }
+  rc = finish_dirty(ws, st, *params, g, dirty_out, s);
+  if (rc != CIP_OK) return rc;
   g_prof.span(5, t_start, g_prof.mark(s));
   CIP_HIP_CHECK(hipStreamSynchronize(s));
   g_prof.finish();
@@ -834,7 +1018,7 @@ int cip_grid_plane(const double* uvw, int64_t nrow, const double* freq, int64_t 
   int rc = prepare(ws, uvw, nrow, freq, nchan, vis, vis_dtype, wgt, wgt_dtype, 2, 2, pixsize_x, pixsize_y, 0.0,
                    params->support, params->do_wstacking, (flags & CIP_ACC_SINGLE) != 0, params, s, &pp);
   if (rc != CIP_OK) return rc;
-  rc = scatter_plane(pp, plane, uvw, vis, vis_dtype, wgt, wgt_dtype, nchan, false, grid_out, s);
+  rc = scatter_plane(pp, plane, uvw, vis, vis_dtype, wgt, wgt_dtype, false, grid_out, s);
   if (rc != CIP_OK) return rc;
   g_prof.span(5, t_start, g_prof.mark(s));
   CIP_HIP_CHECK(hipStreamSynchronize(s));

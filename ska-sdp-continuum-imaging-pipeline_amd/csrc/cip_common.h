@@ -258,6 +258,34 @@ __device__ __forceinline__ void split_index(uint32_t i, int64_t nchan, double in
   *c = cc;
 }
 
+// How a (row, channel) pair maps to its visibility. Dense: the MS layout,
+// row-major (nrow, nchan), index row * nchan + c. Ragged: row slices (the
+// uvw_tiling Tile layout, reference uvw_tiling/tile.py:14-124): row r holds
+// channels [c0_r, c1_r) at vis[off_r, off_r + c1_r - c0_r), so the index is
+// delta[r] + c with delta[r] = off_r - c0_r, and vis_row[i] is the row of
+// visibility i.
+struct RowMap {
+  int64_t nchan;            // channels (f/c entries)
+  int64_t nvis;             // visibilities
+  double inv_nchan;         // 1 / nchan
+  const int64_t* delta;     // ragged: per-row index offset; NULL = dense
+  const uint32_t* vis_row;  // ragged: row of each visibility
+};
+
+__device__ __forceinline__ int64_t vis_index(const RowMap& m, int64_t r, int64_t c) {
+  return m.delta ? m.delta[r] + c : r * m.nchan + c;
+}
+
+__device__ __forceinline__ void vis_rowchan(const RowMap& m, int64_t i, int64_t* r, int64_t* c) {
+  if (m.delta) {
+    const int64_t rr = (int64_t)m.vis_row[i];
+    *r = rr;
+    *c = i - m.delta[rr];
+  } else {
+    split_index64(i, m.nchan, m.inv_nchan, r, c);
+  }
+}
+
 __device__ __forceinline__ int64_t tile_key(int64_t ix0, int64_t iy0, int64_t iw0, const GridGeometry& g) {
   // ix0, iy0 in [0, 2^31) after wrapping: unsigned division
   return (iw0 * g.nty + (int64_t)((uint32_t)iy0 / (uint32_t)kTile)) * g.ntx + (int64_t)((uint32_t)ix0 / (uint32_t)kTile);

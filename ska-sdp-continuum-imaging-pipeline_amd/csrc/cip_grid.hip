@@ -68,6 +68,16 @@ hipError_t launch_prep_final(const double* partial, int nblocks, double* out2, h
   return hipGetLastError();
 }
 
+// *dst += *src (one device scalar; the accumulating gridder's weight sum)
+__global__ void add_scalar_kernel(const double* src, double* dst) {
+  if (threadIdx.x == 0) *dst += *src;
+}
+
+hipError_t launch_add_scalar(const double* src, double* dst, hipStream_t s) {
+  add_scalar_kernel<<<dim3(1), dim3(64), 0, s>>>(src, dst);
+  return hipGetLastError();
+}
+
 // ------------------------------------------------------------ scatter ----
 constexpr int kScatterThreads = 256;
 constexpr int kRunBatch = 256;
@@ -93,10 +103,9 @@ __device__ __forceinline__ void locate_vis(int64_t q, const int64_t* s_voff, con
 }
 
 template <typename VisT, int WK>
-__device__ __forceinline__ void fetch_at(int64_t irow, int64_t c, const double* __restrict__ uvw,
+__device__ __forceinline__ void fetch_at(int64_t irow, int64_t c, int64_t idx, const double* __restrict__ uvw,
                                          const double* __restrict__ fx, const VisT* __restrict__ vis,
-                                         const void* __restrict__ wgt, int64_t nchan, VisFetch& f) {
-  const int64_t idx = irow * nchan + c;
+                                         const void* __restrict__ wgt, VisFetch& f) {
   f.u = uvw[3 * irow];
   f.v = uvw[3 * irow + 1];
   f.w = uvw[3 * irow + 2];
@@ -109,10 +118,10 @@ template <typename VisT, int WK>
 __device__ __forceinline__ void fetch_vis(int64_t q, const int64_t* s_voff, const uint64_t* s_run, int nst,
                                           const double* __restrict__ uvw, const double* __restrict__ fx,
                                           const VisT* __restrict__ vis, const void* __restrict__ wgt,
-                                          int64_t nchan, VisFetch& f) {
+                                          const RowMap& m, VisFetch& f) {
   int64_t irow, c;
   locate_vis(q, s_voff, s_run, nst, &irow, &c);
-  const int64_t idx = irow * nchan + c;
+  const int64_t idx = vis_index(m, irow, c);
   f.u = uvw[3 * irow];
   f.v = uvw[3 * irow + 1];
   f.w = uvw[3 * irow + 2];
@@ -250,7 +259,7 @@ template <bool GATHER>
 __global__ __launch_bounds__(kOrderThreads) void order_kernel(const double* __restrict__ uvw,
                                                               const double* __restrict__ fx,
                                                               const uint8_t* __restrict__ vis_class, GridGeometry g,
-                                                              int64_t nchan, const uint64_t* __restrict__ runs,
+                                                              RowMap m, const uint64_t* __restrict__ runs,
                                                               const int64_t* __restrict__ run_goff,
                                                               const int64_t* __restrict__ tile_run_off,
                                                               const Chunk* __restrict__ windows, int64_t nwindows,
@@ -317,9 +326,10 @@ __global__ __launch_bounds__(kOrderThreads) void order_kernel(const double* __re
       const uint64_t rec = s_rec[lo];
       const int64_t row = (int64_t)(rec >> 32);
       const int64_t c = (int64_t)((rec >> 16) & 0xffff) + (qi - s_off[lo]);
-      packed[k] = (uint32_t)(row * nchan + c);
+      const int64_t idx = vis_index(m, row, c);
+      packed[k] = (uint32_t)idx;
       if constexpr (GATHER) {
-        cls[k] = vis_class[row * nchan + c];
+        cls[k] = vis_class[idx];
       } else {
         const double2 uv = s_uv[lo];
         cls[k] = origin_class(uv.x, uv.y, fx[c], g);
@@ -358,22 +368,22 @@ __global__ __launch_bounds__(kOrderThreads) void order_kernel(const double* __re
 }
 
 hipError_t launch_order(const double* uvw, const double* fx, const uint8_t* vis_class, const GridGeometry& g,
-                        int64_t nchan, const uint64_t* runs, const int64_t* run_goff, const int64_t* tile_run_off,
+                        const RowMap& m, const uint64_t* runs, const int64_t* run_goff, const int64_t* tile_run_off,
                         const Chunk* windows, int64_t nwindows, uint32_t* perm, hipStream_t s) {
   if (nwindows <= 0) return hipSuccess;
   if (vis_class)
     order_kernel<true><<<dim3((unsigned)nwindows), dim3(kOrderThreads), 0, s>>>(
-        uvw, fx, vis_class, g, nchan, runs, run_goff, tile_run_off, windows, nwindows, perm);
+        uvw, fx, vis_class, g, m, runs, run_goff, tile_run_off, windows, nwindows, perm);
   else
     order_kernel<false><<<dim3((unsigned)nwindows), dim3(kOrderThreads), 0, s>>>(
-        uvw, fx, vis_class, g, nchan, runs, run_goff, tile_run_off, windows, nwindows, perm);
+        uvw, fx, vis_class, g, m, runs, run_goff, tile_run_off, windows, nwindows, perm);
   return hipGetLastError();
 }
 
 template <int W, typename VisT, int WK, bool WSTACK, bool PERM, bool PACK>
 __global__ __launch_bounds__(kScatterThreads) void scatter_kernel(
     const double* __restrict__ uvw, const double* __restrict__ fx, const VisT* __restrict__ vis,
-    const void* __restrict__ wgt, int64_t nchan, const uint64_t* __restrict__ runs,
+    const void* __restrict__ wgt, RowMap m, const uint64_t* __restrict__ runs,
     const int64_t* __restrict__ run_goff, const int64_t* __restrict__ tile_run_off,
     const uint32_t* __restrict__ perm, const Chunk* __restrict__ chunks, int64_t chunk_begin, GridGeometry g,
     int64_t plane, double fixed_scale, double inv_scale, double* __restrict__ grid) {
@@ -399,20 +409,21 @@ __global__ __launch_bounds__(kScatterThreads) void scatter_kernel(
     int64_t q = ch.g0 + threadIdx.x;
     bool have = q < ch.g1;
     VisFetch cur;
-    const double inv_nchan = 1.0 / (double)nchan;
     if (have) {
+      const int64_t i = (int64_t)perm[q];
       int64_t r, c;
-      split_index(perm[q], nchan, inv_nchan, &r, &c);
-      fetch_at<VisT, WK>(r, c, uvw, fx, vis, wgt, nchan, cur);
+      vis_rowchan(m, i, &r, &c);
+      fetch_at<VisT, WK>(r, c, i, uvw, fx, vis, wgt, cur);
     }
     while (have) {
       const int64_t qn = q + kScatterThreads;
       const bool hn = qn < ch.g1;
       VisFetch nxt;
       if (hn) {
+        const int64_t i = (int64_t)perm[qn];
         int64_t r, c;
-        split_index(perm[qn], nchan, inv_nchan, &r, &c);
-        fetch_at<VisT, WK>(r, c, uvw, fx, vis, wgt, nchan, nxt);
+        vis_rowchan(m, i, &r, &c);
+        fetch_at<VisT, WK>(r, c, i, uvw, fx, vis, wgt, nxt);
       }
       grid_fetched<W, WSTACK, PACK>(cur, g, plane, X0, Y0, fixed_scale, sub);
       cur = nxt;
@@ -436,12 +447,12 @@ __global__ __launch_bounds__(kScatterThreads) void scatter_kernel(
       int64_t q = v + threadIdx.x;
       bool have = q < bend;
       VisFetch cur;
-      if (have) fetch_vis<VisT, WK>(q, s_voff, s_run, nst, uvw, fx, vis, wgt, nchan, cur);
+      if (have) fetch_vis<VisT, WK>(q, s_voff, s_run, nst, uvw, fx, vis, wgt, m, cur);
       while (have) {
         const int64_t qn = q + kScatterThreads;
         const bool hn = qn < bend;
         VisFetch nxt;
-        if (hn) fetch_vis<VisT, WK>(qn, s_voff, s_run, nst, uvw, fx, vis, wgt, nchan, nxt);
+        if (hn) fetch_vis<VisT, WK>(qn, s_voff, s_run, nst, uvw, fx, vis, wgt, m, nxt);
         grid_fetched<W, WSTACK, PACK>(cur, g, plane, X0, Y0, fixed_scale, sub);
         cur = nxt;
         q = qn;
@@ -480,13 +491,13 @@ __global__ __launch_bounds__(kScatterThreads) void scatter_kernel(
 
 template <int W, typename VisT, int WK>
 static hipError_t scatter_dispatch_ws(bool ws, bool pack, dim3 grid_dim, hipStream_t s, const double* uvw,
-                                      const double* fx, const void* vis, const void* wgt, int64_t nchan,
+                                      const double* fx, const void* vis, const void* wgt, const RowMap& m,
                                       const uint64_t* runs, const int64_t* run_goff, const int64_t* tile_run_off,
                                       const uint32_t* perm, const Chunk* chunks, int64_t chunk_begin,
                                       const GridGeometry& g, int64_t plane, double fs, double* grid) {
 #define LAUNCH(WSV, PRM, PK)                                                                                   \
   scatter_kernel<W, VisT, WK, WSV, PRM, PK><<<grid_dim, dim3(kScatterThreads), 0, s>>>(                        \
-      uvw, fx, (const VisT*)vis, wgt, nchan, runs, run_goff, tile_run_off, perm, chunks, chunk_begin, g, plane, \
+      uvw, fx, (const VisT*)vis, wgt, m, runs, run_goff, tile_run_off, perm, chunks, chunk_begin, g, plane,     \
       fs, 1.0 / fs, grid)
 #define LAUNCH_WS(PRM, PK)      \
   if (ws) LAUNCH(true, PRM, PK); \
@@ -519,12 +530,12 @@ static hipError_t scatter_dispatch_ws(bool ws, bool pack, dim3 grid_dim, hipStre
 template <int W>
 static hipError_t scatter_dispatch_w(int vis_dtype, int wgt_dtype, bool pack, dim3 gd, hipStream_t s,
                                      const double* uvw, const double* fx, const void* vis, const void* wgt,
-                                     int64_t nchan, const uint64_t* runs, const int64_t* run_goff,
+                                     const RowMap& m, const uint64_t* runs, const int64_t* run_goff,
                                      const int64_t* tile_run_off, const uint32_t* perm, const Chunk* chunks,
                                      int64_t cb, const GridGeometry& g, int64_t plane, double fs, double* grid) {
   const bool ws = g.do_wstacking != 0;
 #define ARGS \
-  ws, pack, gd, s, uvw, fx, vis, wgt, nchan, runs, run_goff, tile_run_off, perm, chunks, cb, g, plane, fs, grid
+  ws, pack, gd, s, uvw, fx, vis, wgt, m, runs, run_goff, tile_run_off, perm, chunks, cb, g, plane, fs, grid
   if (vis_dtype == CIP_C64) {
     if (wgt_dtype == CIP_F32) return scatter_dispatch_ws<W, float2, WK_F32>(ARGS);
     if (wgt_dtype == CIP_F64) return scatter_dispatch_ws<W, float2, WK_F64>(ARGS);
@@ -537,7 +548,7 @@ static hipError_t scatter_dispatch_w(int vis_dtype, int wgt_dtype, bool pack, di
 }
 
 hipError_t launch_scatter(int support, int vis_dtype, int wgt_dtype, bool packed, const double* uvw,
-                          const double* fx, const void* vis, const void* wgt, int64_t nchan, const uint64_t* runs,
+                          const double* fx, const void* vis, const void* wgt, const RowMap& m, const uint64_t* runs,
                           const int64_t* run_goff, const int64_t* tile_run_off, const uint32_t* perm,
                           const Chunk* chunks, int64_t chunk_begin, int64_t nchunks, const GridGeometry& g,
                           int64_t plane, double fixed_scale, double* grid, hipStream_t s) {
@@ -546,7 +557,7 @@ hipError_t launch_scatter(int support, int vis_dtype, int wgt_dtype, bool packed
   const dim3 gd((unsigned)nchunks);
 #define CASE(WW)                                                                                             \
   case WW:                                                                                                   \
-    return scatter_dispatch_w<WW>(vis_dtype, wgt_dtype, packed, gd, s, uvw, fx, vis, wgt, nchan, runs,       \
+    return scatter_dispatch_w<WW>(vis_dtype, wgt_dtype, packed, gd, s, uvw, fx, vis, wgt, m, runs,           \
                                   run_goff, tile_run_off, perm, chunks, chunk_begin, g, plane, fixed_scale, grid);
   switch (support) {
     CASE(4)

@@ -38,10 +38,18 @@ hipError_t launch_w_range(const double* uvw, int64_t nrow, double fxmin, double 
 // vis_class (optional, nvis bytes): each visibility's LDS bank class.
 // err_flag: bit 0 non-finite uvw / w off the stack, bit 1 non-finite vis or weight.
 int plan_place_blocks(int64_t nvis);
-hipError_t launch_plan_place(const double* uvw, int64_t nrow, const double* fx, int64_t nchan,
+hipError_t launch_plan_place(const double* uvw, const double* fx, const RowMap& m,
                              const void* vis, int vis_dtype, const void* wgt, int wgt_dtype, const GridGeometry& g,
                              unsigned* err_flag, uint8_t* vis_class, int64_t* blk_cnt, uint32_t* park_key,
                              uint64_t* park_run, double* partial, int64_t* hist0, hipStream_t s);
+// ragged rows: out[r] = chan_stop[r] - chan_start[r] (out[nrow] = 0; err bit
+// set for a range outside [0, nchan)); after the exclusive scan (off[r] = row
+// r's first visibility), launch_ragged_expand writes delta[r] = off[r] -
+// chan_start[r] and vis_row for every visibility.
+hipError_t launch_ragged_lengths(const int32_t* c0, const int32_t* c1, int64_t nrow, int64_t nchan, int64_t* out,
+                                 unsigned* err, hipStream_t s);
+hipError_t launch_ragged_expand(const int64_t* off, const int32_t* c0, int64_t nrow, int64_t* delta,
+                                uint32_t* vis_row, hipStream_t s);
 // one stable LSD radix sort pass on digit (key >> shift) & 255 over nblocks
 // blocks of 4096 slots: dense (blk_cnt NULL, n items) or the place pass's
 // parked runs (blk_cnt). hist: 256 * nblocks + 1 entries, exclusive-scanned
@@ -67,12 +75,13 @@ hipError_t launch_gather_i64(const int64_t* src, int64_t stride, int64_t count, 
 
 // ---- gridding (cip_grid.hip) -----------------------------------------------
 // out2 = {sum, max} of the place pass's 2 * nblocks partials
+hipError_t launch_add_scalar(const double* src, double* dst, hipStream_t s);
 hipError_t launch_prep_final(const double* partial, int nblocks, double* out2, hipStream_t s);
 // packed: single-precision class (re/im packed in one 64-bit integer), complex64
 // only. perm: bank-class ordered stream from launch_order, or NULL (visibilities
 // located through the tile's row slices in tile order).
 hipError_t launch_scatter(int support, int vis_dtype, int wgt_dtype, bool packed, const double* uvw,
-                          const double* fx, const void* vis, const void* wgt, int64_t nchan, const uint64_t* runs,
+                          const double* fx, const void* vis, const void* wgt, const RowMap& m, const uint64_t* runs,
                           const int64_t* run_goff, const int64_t* tile_run_off, const uint32_t* perm,
                           const Chunk* chunks, int64_t chunk_begin, int64_t nchunks, const GridGeometry& g,
                           int64_t plane, double fixed_scale, double* grid, hipStream_t s);
@@ -81,7 +90,7 @@ hipError_t launch_scatter(int support, int vis_dtype, int wgt_dtype, bool packed
 // into <= kOrderWindow pieces by chunk_emit with cv = kOrderWindow)
 // vis_class: classes from the place pass, or NULL (recomputed from u, v, f)
 hipError_t launch_order(const double* uvw, const double* fx, const uint8_t* vis_class, const GridGeometry& g,
-                        int64_t nchan,
+                        const RowMap& m,
                         const uint64_t* runs, const int64_t* run_goff, const int64_t* tile_run_off,
                         const Chunk* windows, int64_t nwindows, uint32_t* perm, hipStream_t s);
 hipError_t launch_crop_correct_2d(const double* grid, const GridGeometry& g, int64_t npix_x, int64_t npix_y,

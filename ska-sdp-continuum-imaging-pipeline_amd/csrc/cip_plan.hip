@@ -141,8 +141,8 @@ constexpr int kPlaceSegs = 64;  // 64-visibility segments per place block (4096 
 constexpr uint32_t kNoKey = 0xffffffffu;  // visibility off the grid (tile keys are < 2^32 - 1)
 
 template <typename VisT, int WK>
-__global__ __launch_bounds__(256) void plan_place_kernel(const double* __restrict__ uvw, int64_t nrow,
-                                                         const double* __restrict__ fx, int64_t nchan,
+__global__ __launch_bounds__(256) void plan_place_kernel(const double* __restrict__ uvw,
+                                                         const double* __restrict__ fx, RowMap m,
                                                          const VisT* __restrict__ vis, const void* __restrict__ wgt,
                                                          GridGeometry g, unsigned* err_flag,
                                                          uint8_t* __restrict__ vis_class,
@@ -159,26 +159,32 @@ __global__ __launch_bounds__(256) void plan_place_kernel(const double* __restric
   // fused prep reduction (sum of weights, max |w V|), fixed order
   double wsum = 0.0, wvmax = 0.0;
   bool nonfinite = false;
-  const int64_t nvis = nrow * nchan;
+  const int64_t nvis = m.nvis, nchan = m.nchan;
+  const bool ragged = m.delta != nullptr;
   const int64_t nseg = (nvis + 63) / 64;
   const int P = kTile + g.support - 1;
   // block b owns segments [64 b, 64 b + 64): wave w takes every 4th
   const int64_t seg_end = ((int64_t)blockIdx.x + 1) * kPlaceSegs < nseg ? ((int64_t)blockIdx.x + 1) * kPlaceSegs : nseg;
   // (row, channel) of the lane's visibility, advanced by 256 visibilities per
   // step without a division
-  int64_t r0, c0;
-  split_index64(((int64_t)blockIdx.x * kPlaceSegs + wave) * 64 + lane, nchan, 1.0 / (double)nchan, &r0, &c0);
+  // (ragged rows: looked up per visibility)
+  int64_t r0 = 0, c0 = 0;
+  if (!ragged) split_index64(((int64_t)blockIdx.x * kPlaceSegs + wave) * 64 + lane, nchan, m.inv_nchan, &r0, &c0);
   const int64_t step_r = 256 / nchan, step_c = 256 % nchan;
   for (int64_t seg = (int64_t)blockIdx.x * kPlaceSegs + wave; seg < seg_end; seg += 4) {
     const int64_t i = seg * 64 + lane;
     const bool valid = i < nvis;
     uint32_t key = kNoKey;
-    const int64_t r = r0, c = c0;
-    c0 += step_c;
-    r0 += step_r;
-    if (c0 >= nchan) {
-      c0 -= nchan;
-      ++r0;
+    int64_t r = r0, c = c0;
+    if (ragged) {
+      if (valid) vis_rowchan(m, i, &r, &c);
+    } else {
+      c0 += step_c;
+      r0 += step_r;
+      if (c0 >= nchan) {
+        c0 -= nchan;
+        ++r0;
+      }
     }
     bool bad = false;
     if (valid) {
@@ -203,7 +209,8 @@ __global__ __launch_bounds__(256) void plan_place_kernel(const double* __restric
     }
     if (__ballot(bad) != 0ull && lane == 0) atomicOr(err_flag, 1u);
     const uint32_t prev = __shfl_up(key, 1, 64);
-    const bool start = valid && (lane == 0 || c == 0 || key != prev);
+    const uint32_t prev_r = __shfl_up((uint32_t)r, 1, 64);  // rows < 2^32
+    const bool start = valid && (lane == 0 || (uint32_t)r != prev_r || key != prev);
     const unsigned long long starts = __ballot(start);
     const bool emit = start && key != kNoKey;
     const unsigned long long emits = __ballot(emit);
@@ -249,13 +256,13 @@ static unsigned plan_blocks(int64_t nvis) {
 
 int plan_place_blocks(int64_t nvis) { return (int)plan_blocks(nvis); }
 
-hipError_t launch_plan_place(const double* uvw, int64_t nrow, const double* fx, int64_t nchan,
+hipError_t launch_plan_place(const double* uvw, const double* fx, const RowMap& m,
                              const void* vis, int vis_dtype, const void* wgt, int wgt_dtype, const GridGeometry& g,
                              unsigned* err_flag, uint8_t* vis_class, int64_t* blk_cnt, uint32_t* park_key,
                              uint64_t* park_run, double* partial, int64_t* hist0, hipStream_t s) {
-  const dim3 gd(plan_blocks(nrow * nchan));
+  const dim3 gd(plan_blocks(m.nvis));
 #define PLACE(VT, WKV)                                                                                           \
-  plan_place_kernel<VT, WKV><<<gd, dim3(256), 0, s>>>(uvw, nrow, fx, nchan, (const VT*)vis, wgt, g, err_flag,  \
+  plan_place_kernel<VT, WKV><<<gd, dim3(256), 0, s>>>(uvw, fx, m, (const VT*)vis, wgt, g, err_flag,       \
                                                       vis_class, blk_cnt, park_key, park_run, partial, hist0)
   if (vis_dtype == CIP_C64) {
     if (wgt_dtype == CIP_F32) PLACE(float2, WK_F32);
@@ -267,6 +274,48 @@ hipError_t launch_plan_place(const double* uvw, int64_t nrow, const double* fx, 
     else PLACE(double2, WK_NONE);
   }
 #undef PLACE
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------- ragged rows ----
+__global__ void ragged_lengths_kernel(const int32_t* __restrict__ c0, const int32_t* __restrict__ c1, int64_t nrow,
+                                      int64_t nchan, int64_t* __restrict__ out, unsigned* err) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r < nrow) {
+    const int32_t a = c0[r], b = c1[r];
+    const bool ok = a >= 0 && a <= b && (int64_t)b <= nchan;
+    if (!ok) atomicOr(err, 1u);
+    out[r] = ok ? (int64_t)(b - a) : 0;
+  } else if (r == nrow) {
+    out[r] = 0;
+  }
+}
+
+hipError_t launch_ragged_lengths(const int32_t* c0, const int32_t* c1, int64_t nrow, int64_t nchan, int64_t* out,
+                                 unsigned* err, hipStream_t s) {
+  ragged_lengths_kernel<<<dim3((unsigned)((nrow + 256) / 256)), dim3(256), 0, s>>>(c0, c1, nrow, nchan, out, err);
+  return hipGetLastError();
+}
+
+// one wave per row: delta[r] = off[r] - chan_start[r], and its lanes write the
+// row index over the row's visibility slots
+__global__ __launch_bounds__(256) void ragged_expand_kernel(const int64_t* __restrict__ off,
+                                                            const int32_t* __restrict__ c0, int64_t nrow,
+                                                            int64_t* __restrict__ delta,
+                                                            uint32_t* __restrict__ vis_row) {
+  const int64_t r = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (r >= nrow) return;
+  const int64_t a = off[r], b = off[r + 1];
+  for (int64_t i = a + lane; i < b; i += 64) vis_row[i] = (uint32_t)r;
+  if (lane == 0) delta[r] = a - (int64_t)c0[r];
+}
+
+hipError_t launch_ragged_expand(const int64_t* off, const int32_t* c0, int64_t nrow, int64_t* delta,
+                                uint32_t* vis_row, hipStream_t s) {
+  if (nrow <= 0) return hipSuccess;
+  ragged_expand_kernel<<<dim3((unsigned)((nrow * 64 + 255) / 256)), dim3(256), 0, s>>>(off, c0, nrow, delta,
+                                                                                      vis_row);
   return hipGetLastError();
 }
 

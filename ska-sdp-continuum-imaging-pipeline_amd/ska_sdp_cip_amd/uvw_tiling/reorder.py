@@ -40,10 +40,14 @@ def reorder_by_uvw_tile(  # pylint: disable=too-many-locals
     *,
     num_time_intervals: Optional[int] = None,
     max_vis_per_chunk: int = 5_000_000,
+    with_weights: bool = False,
 ) -> list[Path]:
     """
     Convert to Stokes I and reorder into UVW tile chunk files (reference
-    :19-111). Returns the written chunk paths.
+    :19-111). Returns the written chunk paths. `with_weights=True` also stores
+    each visibility's Stokes-I effective weight (flags folded in, reference
+    invert.py:72-116) under the npz key `weights`; the
+    reference's files carry none, and its readers ignore the extra key.
     """
     if num_time_intervals is None:
         num_time_intervals = max(2 * len(client.scheduler_info()["workers"]), 2)
@@ -54,7 +58,7 @@ def reorder_by_uvw_tile(  # pylint: disable=too-many-locals
         mapping = client.submit(create_time_interval_tile_mapping, interval_reader, tile_size, channel_freqs,
                                 resources={"gpu": 1})
         futures.append(client.submit(reorder_time_interval, interval_reader, mapping, outdir,
-                                     interval_index=interval_index))
+                                     interval_index=interval_index, with_weights=with_weights))
     coords_set = set()
     for fut in _as_completed(futures):
         coords_set.update(fut.result())
@@ -69,14 +73,19 @@ def create_time_interval_tile_mapping(ms_reader, tile_size: TileCoords, channel_
 
 
 def reorder_time_interval(ms_reader, tile_mapping: TileMapping, outdir: Path, *,
-                          interval_index: int) -> list[TileCoords]:
+                          interval_index: int, with_weights: bool = False) -> list[TileCoords]:
     """Write one interval's tiles; returns their coordinates (reference :129-155)."""
     uvw = ms_reader.uvw()
     vis = ms_reader.visibilities()
     stokes_i_vis = 0.5 * (vis[..., 0] + vis[..., 3])
+    eff_w = None
+    if with_weights:
+        from ..invert import StokesIGridderInput  # pylint: disable=import-outside-toplevel
+
+        eff_w = StokesIGridderInput.from_measurement_set_reader(ms_reader).effective_weights()
     for coords, row_slices in tile_mapping.items():
         tile = Tile._from_jagged_visibilities_slice(  # pylint: disable=protected-access
-            stokes_i_vis, uvw, coords, row_slices)
+            stokes_i_vis, uvw, coords, row_slices, weights=eff_w)
         tile.save_npz(Path(outdir) / _tile_filename(coords, interval_index))
     return list(tile_mapping.keys())
 
