@@ -47,6 +47,9 @@ extern "C" {
 
 /* flags of cip_ms2dirty / cip_grid_plane */
 #define CIP_WSTACKING 1  /* w-stacking planes (cip_ms2dirty only; else 2-D) */
+#define CIP_PSF 4        /* grid unit visibilities (vis ignored, may be NULL):
+                          * the point-spread function with the same weights
+                          * (cip_ms2dirty, cip_grid_ms, cip_grid_tiles) */
 #define CIP_ACC_SINGLE 2 /* complex64 only: single-precision accumulation
                           * class, the reference's ducc0 float gridding (re/im
                           * packed in one 64-bit fixed-point LDS cell, W^2
@@ -158,6 +161,30 @@ int cip_tile_runs(const double* uvw, int64_t nrow, const double* freq,
 int cip_stokes_i(const void* vis4, const uint8_t* flags4, const float* wgt4,
                  int64_t n, void* hip_stream, void* vis_i, uint8_t* flag_i,
                  float* wgt_i, float* eff_w);
+
+/* Any Stokes parameter from linear feeds (pols XX, XY, YX, YY): I as
+ * cip_stokes_i; Q = 0.5 (XX - YY) with I's flags and weights; U =
+ * 0.5 (XY + YX), V = -0.5 i (XY - YX) with flags XY | YX and weights
+ * 4/(1/w_XY + 1/w_YX). Beyond the reference (Stokes I only), SURVEY.md 8(f)4. */
+#define CIP_STOKES_I 0
+#define CIP_STOKES_Q 1
+#define CIP_STOKES_U 2
+#define CIP_STOKES_V 3
+int cip_stokes(const void* vis4, const uint8_t* flags4, const float* wgt4,
+               int64_t n, int stokes, void* hip_stream, void* vis_out,
+               uint8_t* flag_out, float* wgt_out, float* eff_w);
+
+/* Facet: rephase the data to the facet centre
+ * (l0, m0) of the original tangent plane and rotate the baselines into the
+ * facet's frame (minimal rotation taking the phase centre to the facet
+ * centre), so that cip_ms2dirty of (uvw_out, vis_out) is the dirty image on
+ * the facet's own tangent plane, centred on (l0, m0). uvw_out (nrow,3) f64;
+ * vis_out (nrow,nchan) of vis_dtype, may equal vis (in place) or be NULL
+ * (uvw only, e.g. for a PSF). DEVICE pointers. */
+int cip_facet_rephase(const double* uvw, int64_t nrow, const double* freq,
+                      int64_t nchan, const void* vis, int vis_dtype, double l0,
+                      double m0, void* hip_stream, double* uvw_out,
+                      void* vis_out);
 
 /* Last error message of the calling thread ("" if none). */
 const char* cip_last_error(void);

@@ -216,6 +216,60 @@ def dft_dirty(uvw, freq, vis, wgt, npix_x, npix_y, px, py, apply_w=False, nthrea
     return out
 
 
+def dft_directions(uvw, freq, vis, wgt, l, m):
+    """Direct fp64 dirty image values at arbitrary directions (l, m) of the
+    original tangent plane (same definition as dft_dirty, w term included):
+    sum w Re{V exp(2 pi i f/c (u l + v m - w (n - 1)))}. Small cases only."""
+    uvw = np.asarray(uvw, dtype=np.float64)
+    fx = np.asarray(freq, dtype=np.float64) / SPEED_OF_LIGHT
+    vis = np.asarray(vis).astype(np.complex128)
+    wgt = np.ones(vis.shape) if wgt is None else np.asarray(wgt, dtype=np.float64)
+    l = np.asarray(l, dtype=np.float64).ravel()
+    m = np.asarray(m, dtype=np.float64).ravel()
+    nm1 = -(l * l + m * m) / (np.sqrt(1.0 - l * l - m * m) + 1.0)
+    out = np.zeros(l.size)
+    wv = (wgt * vis)
+    for c in range(fx.size):
+        ph = 2.0 * np.pi * fx[c] * (np.outer(uvw[:, 0], l) + np.outer(uvw[:, 1], m) - np.outer(uvw[:, 2], nm1))
+        out += (wv[:, c, None] * np.exp(1j * ph)).real.sum(axis=0)
+    return out
+
+
+def facet_rotation(l0, m0):
+    """Q (3x3): the minimal rotation taking the phase centre (0, 0, 1) to the
+    facet centre (l0, m0, n0) (restated for the facet tests: a facet pixel at
+    (l', m') of the facet's tangent plane is the direction Q (l', m', n'))."""
+    n0 = np.sqrt(1.0 - l0 * l0 - m0 * m0)
+    axis = np.cross([0.0, 0.0, 1.0], [l0, m0, n0])
+    s = np.linalg.norm(axis)
+    if s == 0.0:
+        return np.eye(3)
+    k = axis / s
+    kx = np.array([[0.0, -k[2], k[1]], [k[2], 0.0, -k[0]], [-k[1], k[0], 0.0]])
+    return np.eye(3) + s * kx + (1.0 - n0) * (kx @ kx)
+
+
+def stokes(vis4, flags4, wgt4, which):
+    """Stokes `which` from linear feeds (XX, XY, YX, YY) in numpy float32 /
+    complex64 arithmetic (I as stokes_i) -> (vis c64, eff_w f32)."""
+    vis4 = np.asarray(vis4)
+    a, b = (0, 3) if which in "IQ" else (1, 2)
+    half = np.float32(0.5)
+    if which == "I":
+        v = half * (vis4[..., 0] + vis4[..., 3])
+    elif which == "Q":
+        v = half * (vis4[..., 0] - vis4[..., 3])
+    elif which == "U":
+        v = half * (vis4[..., 1] + vis4[..., 2])
+    else:
+        d = vis4[..., 1] - vis4[..., 2]
+        v = (half * d.imag + 1j * (-half * d.real)).astype(np.complex64)
+    fl = np.logical_or(flags4[..., a], flags4[..., b])
+    with np.errstate(divide="ignore", invalid="ignore"):
+        w = (np.float32(4.0) / (np.float32(1.0) / wgt4[..., a] + np.float32(1.0) / wgt4[..., b])).astype(np.float32)
+    return v.astype(np.complex64), (np.logical_not(fl) * w).astype(np.float32)
+
+
 # ---------------------------------------------------- reference restated ----
 def stokes_i(vis4, flags4, wgt4):
     """invert.py:86-116 and :72-76 -> (vis_i c64, flags_i bool, wgt_i f32, eff_w f32)."""

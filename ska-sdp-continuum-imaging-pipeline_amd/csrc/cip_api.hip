@@ -856,9 +856,13 @@ static int grid_accumulate(const double* uvw, int64_t nrow, const double* freq, 
                            double pixsize_x, double pixsize_y, int64_t npix_x, int64_t npix_y, int flags,
                            void* hip_stream, double* grids, double* sum_wgt, const RaggedRows* ragged) {
   g_last_error.clear();
-  if (flags & ~CIP_ACC_SINGLE) return set_error(CIP_EINVAL, "unknown flags");
+  if (flags & ~(CIP_ACC_SINGLE | CIP_PSF)) return set_error(CIP_EINVAL, "unknown flags");
   if (!params || !grids) return set_error(CIP_EINVAL, "NULL params or grids");
-  if (nrow > 0 && (!uvw || !freq || !vis)) return set_error(CIP_EINVAL, "NULL input pointer");
+  if (flags & CIP_PSF) {
+    vis = nullptr;
+    vis_dtype = CIP_C64;
+  }
+  if (nrow > 0 && (!uvw || !freq || (!vis && !(flags & CIP_PSF)))) return set_error(CIP_EINVAL, "NULL input pointer");
   hipStream_t s = (hipStream_t)hip_stream;
   Workspace* ws = workspace();
   if (!ws) return set_error(CIP_EHIP, "no HIP device");
@@ -904,11 +908,15 @@ int cip_ms2dirty(const double* uvw, int64_t nrow, const double* freq, int64_t nc
                  double pixsize_y, double epsilon, int support, int flags, void* hip_stream,
                  double* dirty_out, double* sum_wgt_out, cip_gridder_params* params_out) {
   g_last_error.clear();
-  if (flags & ~(CIP_WSTACKING | CIP_ACC_SINGLE)) return set_error(CIP_EINVAL, "unknown flags");
+  if (flags & ~(CIP_WSTACKING | CIP_ACC_SINGLE | CIP_PSF)) return set_error(CIP_EINVAL, "unknown flags");
   const int do_wstacking = (flags & CIP_WSTACKING) ? 1 : 0;
   const bool packed = (flags & CIP_ACC_SINGLE) != 0;
+  if (flags & CIP_PSF) {
+    vis = nullptr;
+    vis_dtype = CIP_C64;
+  }
   if (!dirty_out) return set_error(CIP_EINVAL, "dirty_out is NULL");
-  if (nrow > 0 && (!uvw || !freq || !vis)) return set_error(CIP_EINVAL, "NULL input pointer");
+  if (nrow > 0 && (!uvw || !freq || (!vis && !(flags & CIP_PSF)))) return set_error(CIP_EINVAL, "NULL input pointer");
   hipStream_t s = (hipStream_t)hip_stream;
   Workspace* ws = workspace();
   if (!ws) return set_error(CIP_EHIP, "no HIP device");
@@ -1065,16 +1073,61 @@ int cip_tile_runs(const double* uvw, int64_t nrow, const double* freq, int64_t n
   return CIP_OK;
 }
 
-int cip_stokes_i(const void* vis4, const uint8_t* flags4, const float* wgt4, int64_t n, void* hip_stream,
-                 void* vis_i, uint8_t* flag_i, float* wgt_i, float* eff_w) {
+int cip_stokes(const void* vis4, const uint8_t* flags4, const float* wgt4, int64_t n, int stokes, void* hip_stream,
+               void* vis_out, uint8_t* flag_out, float* wgt_out, float* eff_w) {
   g_last_error.clear();
   if (n < 0) return set_error(CIP_EINVAL, "n must be >= 0");
+  if (stokes < CIP_STOKES_I || stokes > CIP_STOKES_V) return set_error(CIP_EINVAL, "stokes must be I, Q, U or V");
   if (n == 0) return CIP_OK;
-  if (vis_i && !vis4) return set_error(CIP_EINVAL, "vis_i requested without vis4");
-  if ((wgt_i || eff_w) && !wgt4) return set_error(CIP_EINVAL, "weights requested without wgt4");
-  if ((flag_i || eff_w) && !flags4) return set_error(CIP_EINVAL, "flags requested without flags4");
+  if (vis_out && !vis4) return set_error(CIP_EINVAL, "visibilities requested without vis4");
+  if ((wgt_out || eff_w) && !wgt4) return set_error(CIP_EINVAL, "weights requested without wgt4");
+  if ((flag_out || eff_w) && !flags4) return set_error(CIP_EINVAL, "flags requested without flags4");
   hipStream_t s = (hipStream_t)hip_stream;
-  CIP_HIP_CHECK(launch_stokes_i(vis4, flags4, wgt4, n, vis_i, flag_i, wgt_i, eff_w, s));
+  CIP_HIP_CHECK(launch_stokes(stokes, vis4, flags4, wgt4, n, vis_out, flag_out, wgt_out, eff_w, s));
+  CIP_HIP_CHECK(hipStreamSynchronize(s));
+  return CIP_OK;
+}
+
+int cip_stokes_i(const void* vis4, const uint8_t* flags4, const float* wgt4, int64_t n, void* hip_stream,
+                 void* vis_i, uint8_t* flag_i, float* wgt_i, float* eff_w) {
+  return cip_stokes(vis4, flags4, wgt4, n, CIP_STOKES_I, hip_stream, vis_i, flag_i, wgt_i, eff_w);
+}
+
+int cip_facet_rephase(const double* uvw, int64_t nrow, const double* freq, int64_t nchan, const void* vis,
+                      int vis_dtype, double l0, double m0, void* hip_stream, double* uvw_out, void* vis_out) {
+  g_last_error.clear();
+  if (nrow < 0 || nchan < 1) return set_error(CIP_EINVAL, "need nrow >= 0 and nchan >= 1");
+  if (!vis_dtype_ok(vis_dtype)) return set_error(CIP_EINVAL, "vis dtype must be complex64 or complex128");
+  if (!(l0 * l0 + m0 * m0 < 1.0)) return set_error(CIP_EINVAL, "facet centre outside the unit circle");
+  if (nrow == 0) return CIP_OK;
+  if (!uvw || !freq || !uvw_out || (vis_out && !vis)) return set_error(CIP_EINVAL, "NULL pointer");
+  hipStream_t s = (hipStream_t)hip_stream;
+  Workspace* ws = workspace();
+  if (!ws) return set_error(CIP_EHIP, "no HIP device");
+  CIP_ALLOC(delay, double, "facet_delay", nrow)
+  // Q: the minimal rotation taking z = (0, 0, 1) to s0 (Rodrigues about z x s0)
+  const double n0 = std::sqrt(1.0 - l0 * l0 - m0 * m0);
+  const double kx = -m0, ky = l0;  // z x s0 (unnormalised; |k| = sin theta)
+  const double sn2 = kx * kx + ky * ky, c = n0;
+  double Q[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+  if (sn2 > 0.0) {
+    const double f = (1.0 - c) / sn2;  // (1 - cos) / sin^2 on the unnormalised axis
+    // Q = I + [k]x + f [k]x^2, [k]x = ((0, 0, ky), (0, 0, -kx), (-ky, kx, 0))
+    Q[0] = 1.0 - f * ky * ky;
+    Q[1] = f * kx * ky;
+    Q[2] = ky;
+    Q[3] = f * kx * ky;
+    Q[4] = 1.0 - f * kx * kx;
+    Q[5] = -kx;
+    Q[6] = -ky;
+    Q[7] = kx;
+    Q[8] = 1.0 - f * sn2;
+  }
+  double qt[9];
+  for (int a = 0; a < 3; ++a)
+    for (int b = 0; b < 3; ++b) qt[3 * a + b] = Q[3 * b + a];
+  CIP_HIP_CHECK(launch_facet_rephase(uvw, nrow, freq, nchan, vis_out ? vis : nullptr, vis_dtype == CIP_C128, qt, l0, m0,
+                                     uvw_out, delay, vis_out, s));
   CIP_HIP_CHECK(hipStreamSynchronize(s));
   return CIP_OK;
 }

@@ -301,7 +301,13 @@ __device__ __forceinline__ double load_weight(const void* __restrict__ w, int64_
   return 1.0;
 }
 
+// p == NULL: unit visibilities (the point-spread function, CIP_PSF)
 __device__ __forceinline__ void load_vis(const float2* __restrict__ p, int64_t i, double& re, double& im) {
+  if (p == nullptr) {
+    re = 1.0;
+    im = 0.0;
+    return;
+  }
   const float2 v = p[i];
   re = v.x;
   im = v.y;

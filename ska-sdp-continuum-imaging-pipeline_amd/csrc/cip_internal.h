@@ -121,7 +121,10 @@ hipError_t launch_tile_run_emit(const double* uvw, int64_t nrow, const double* w
                                 int64_t* run_key, int64_t* run_row, int32_t* run_c0, int32_t* run_c1,
                                 hipStream_t s);
 hipError_t launch_wavelength_inv(const double* freq, int64_t nchan, double* winv, hipStream_t s);
-hipError_t launch_stokes_i(const void* vis4, const uint8_t* flags4, const float* wgt4, int64_t n,
-                           void* vis_i, uint8_t* flag_i, float* wgt_i, float* eff_w, hipStream_t s);
+hipError_t launch_facet_rephase(const double* uvw, int64_t nrow, const double* freq, int64_t nchan, const void* vis,
+                                int vis_c128, const double qt[9], double l0, double m0, double* uvw_out,
+                                double* delay, void* vis_out, hipStream_t s);
+hipError_t launch_stokes(int stokes, const void* vis4, const uint8_t* flags4, const float* wgt4, int64_t n,
+                         void* vis_i, uint8_t* flag_i, float* wgt_i, float* eff_w, hipStream_t s);
 
 }  // namespace cip

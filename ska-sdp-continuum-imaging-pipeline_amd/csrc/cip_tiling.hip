@@ -88,35 +88,115 @@ hipError_t launch_tile_run_emit(const double* uvw, int64_t nrow, const double* w
   return hipGetLastError();
 }
 
-// Stokes I (reference invert.py:86-116, :72-76): one thread per (row, chan).
-__global__ void stokes_i_kernel(const float2* __restrict__ vis4, const uint8_t* __restrict__ flags4,
-                                const float* __restrict__ wgt4, int64_t n, float2* vis_i, uint8_t* flag_i,
-                                float* wgt_i, float* eff_w) {
+// Stokes parameters from linear feeds (XX, XY, YX, YY) = pols (0, 1, 2, 3),
+// one thread per (row, chan). I (reference invert.py:86-116, :72-76, its
+// numpy float32 arithmetic): 0.5 (XX + YY), flags F0 | F3, weight
+// 4 / (1/w0 + 1/w3). Q = 0.5 (XX - YY) with I's flags and weights; U =
+// 0.5 (XY + YX) and V = -0.5 i (XY - YX) with pols 1 and 2's.
+template <int STOKES>
+__global__ void stokes_kernel(const float2* __restrict__ vis4, const uint8_t* __restrict__ flags4,
+                              const float* __restrict__ wgt4, int64_t n, float2* vis_i, uint8_t* flag_i,
+                              float* wgt_i, float* eff_w) {
+  constexpr int A = STOKES <= 1 ? 0 : 1, B = STOKES <= 1 ? 3 : 2;
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   if (vis_i) {
-    const float2 a = vis4[4 * i], d = vis4[4 * i + 3];
+    const float2 a = vis4[4 * i + A], d = vis4[4 * i + B];
     // numpy: 0.5 * (vis[..., 0] + vis[..., 3]) in complex64
-    vis_i[i] = make_float2(0.5f * (a.x + d.x), 0.5f * (a.y + d.y));
+    if constexpr (STOKES == 0 || STOKES == 2) vis_i[i] = make_float2(0.5f * (a.x + d.x), 0.5f * (a.y + d.y));
+    if constexpr (STOKES == 1) vis_i[i] = make_float2(0.5f * (a.x - d.x), 0.5f * (a.y - d.y));
+    if constexpr (STOKES == 3) vis_i[i] = make_float2(0.5f * (a.y - d.y), -0.5f * (a.x - d.x));
   }
   bool fl = false;
-  if (flags4) fl = (flags4[4 * i] != 0) || (flags4[4 * i + 3] != 0);
+  if (flags4) fl = (flags4[4 * i + A] != 0) || (flags4[4 * i + B] != 0);
   if (flag_i) flag_i[i] = fl ? 1 : 0;
   if (wgt4) {
-    const float wxx = wgt4[4 * i], wyy = wgt4[4 * i + 3];
+    const float wa = wgt4[4 * i + A], wb = wgt4[4 * i + B];
     // numpy float32: 4.0 / (1.0 / wxx + 1.0 / wyy); a zero weight gives
     // 1/0 = inf and 4/inf = 0 exactly as in the reference.
-    const float w = 4.0f / (1.0f / wxx + 1.0f / wyy);
+    const float w = 4.0f / (1.0f / wa + 1.0f / wb);
     if (wgt_i) wgt_i[i] = w;
     // numpy: logical_not(flags) * weights (so 0 * inf / nan propagate)
     if (eff_w) eff_w[i] = (fl ? 0.0f : 1.0f) * w;
   }
 }
 
-hipError_t launch_stokes_i(const void* vis4, const uint8_t* flags4, const float* wgt4, int64_t n, void* vis_i,
-                           uint8_t* flag_i, float* wgt_i, float* eff_w, hipStream_t s) {
-  stokes_i_kernel<<<dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s>>>(
-      (const float2*)vis4, flags4, wgt4, n, (float2*)vis_i, flag_i, wgt_i, eff_w);
+hipError_t launch_stokes(int stokes, const void* vis4, const uint8_t* flags4, const float* wgt4, int64_t n,
+                         void* vis_i, uint8_t* flag_i, float* wgt_i, float* eff_w, hipStream_t s) {
+  const dim3 gd((unsigned)((n + 255) / 256)), bd(256);
+#define STK(K)                                                                                              \
+  stokes_kernel<K><<<gd, bd, 0, s>>>((const float2*)vis4, flags4, wgt4, n, (float2*)vis_i, flag_i, wgt_i, eff_w)
+  switch (stokes) {
+    case 0: STK(0); break;
+    case 1: STK(1); break;
+    case 2: STK(2); break;
+    case 3: STK(3); break;
+    default: return hipErrorInvalidValue;
+  }
+#undef STK
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------ facets ----
+// Rephase to a facet centre s0 = (l0, m0, n0) of the original tangent plane
+// and rotate the baselines into the facet's frame. In the convention of
+// ms2dirty (dirty = sum Re{V exp(2 pi i f/c (u l + v m - w (n - 1)))}) a source
+// at s has delay d(s) = b.s - b.z with b = (u, v, -w); the facet data are
+// V' = V exp(+2 pi i f/c d(s0)) and b' = Q^T b (Q: the rotation taking z to
+// s0, rows q_k), stored back as (u', v', w') = (b'_0, b'_1, -b'_2).
+// One thread per row rotates uvw; one per visibility rotates the phase.
+struct Rot3 {
+  double q[9];  // row-major Q^T
+};
+
+__global__ void facet_uvw_kernel(const double* __restrict__ uvw, int64_t nrow, Rot3 qt, double l0, double m0,
+                                 double n0m1, double* __restrict__ uvw_out, double* __restrict__ delay) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= nrow) return;
+  const double b0 = uvw[3 * r], b1 = uvw[3 * r + 1], b2 = -uvw[3 * r + 2];
+  delay[r] = b0 * l0 + b1 * m0 + b2 * n0m1;  // b.s0 - b.z (metres)
+  uvw_out[3 * r] = qt.q[0] * b0 + qt.q[1] * b1 + qt.q[2] * b2;
+  uvw_out[3 * r + 1] = qt.q[3] * b0 + qt.q[4] * b1 + qt.q[5] * b2;
+  uvw_out[3 * r + 2] = -(qt.q[6] * b0 + qt.q[7] * b1 + qt.q[8] * b2);
+}
+
+template <typename VisT>
+__global__ void facet_phase_kernel(const VisT* __restrict__ vis, const double* __restrict__ delay,
+                                   const double* __restrict__ freq, int64_t nrow, int64_t nchan,
+                                   VisT* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nrow * nchan) return;
+  const int64_t r = i / nchan, c = i - r * nchan;
+  // phase in turns, reduced before sincospi keeps the argument small
+  double turns = delay[r] * (freq[c] / CIP_SPEED_OF_LIGHT);
+  turns -= rint(turns);
+  double sn, cs;
+  sincospi(2.0 * turns, &sn, &cs);
+  const double vr = (double)vis[i].x, vi = (double)vis[i].y;
+  VisT o;
+  o.x = vr * cs - vi * sn;
+  o.y = vr * sn + vi * cs;
+  out[i] = o;
+}
+
+hipError_t launch_facet_rephase(const double* uvw, int64_t nrow, const double* freq, int64_t nchan, const void* vis,
+                                int vis_c128, const double qt[9], double l0, double m0, double* uvw_out,
+                                double* delay, void* vis_out, hipStream_t s) {
+  Rot3 q;
+  for (int k = 0; k < 9; ++k) q.q[k] = qt[k];
+  const double n0m1 = -(l0 * l0 + m0 * m0) / (sqrt(1.0 - l0 * l0 - m0 * m0) + 1.0);  // n0 - 1, no cancellation
+  facet_uvw_kernel<<<dim3((unsigned)((nrow + 255) / 256)), dim3(256), 0, s>>>(uvw, nrow, q, l0, m0, n0m1, uvw_out,
+                                                                               delay);
+  const int64_t n = nrow * nchan;
+  if (n > 0 && vis != nullptr && vis_out != nullptr) {  // uvw only (PSF): no phase pass
+    const dim3 gd((unsigned)((n + 255) / 256));
+    if (vis_c128)
+      facet_phase_kernel<double2><<<gd, dim3(256), 0, s>>>((const double2*)vis, delay, freq, nrow, nchan,
+                                                           (double2*)vis_out);
+    else
+      facet_phase_kernel<float2><<<gd, dim3(256), 0, s>>>((const float2*)vis, delay, freq, nrow, nchan,
+                                                          (float2*)vis_out);
+  }
   return hipGetLastError();
 }
 

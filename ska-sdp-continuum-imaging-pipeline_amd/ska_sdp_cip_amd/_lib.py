@@ -29,6 +29,8 @@ CIP_F32 = 3
 CIP_F64 = 4
 CIP_WSTACKING = 1
 CIP_ACC_SINGLE = 2
+CIP_PSF = 4
+STOKES_CODES = {"I": 0, "Q": 1, "U": 2, "V": 3}
 
 # every symbol declared in include/cip.h
 EXPORTED_SYMBOLS = (
@@ -41,6 +43,8 @@ EXPORTED_SYMBOLS = (
     "cip_grid_to_dirty",
     "cip_tile_runs",
     "cip_stokes_i",
+    "cip_stokes",
+    "cip_facet_rephase",
     "cip_last_error",
     "cip_release_workspace",
     "cip_profile_enable",
@@ -111,13 +115,15 @@ def lib() -> ctypes.CDLL:
     so.cip_tile_runs.argtypes = [_vp, _i64, _vp, _i64, ctypes.POINTER(ctypes.c_double), _i64, _vp,
                                  ctypes.POINTER(ctypes.c_int64), _vp, _vp, _vp, _vp]
     so.cip_stokes_i.argtypes = [_vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp]
+    so.cip_stokes.argtypes = [_vp, _vp, _vp, _i64, _i32, _vp, _vp, _vp, _vp, _vp]
+    so.cip_facet_rephase.argtypes = [_vp, _i64, _vp, _i64, _vp, _i32, _f64, _f64, _vp, _vp, _vp]
     so.cip_profile_enable.argtypes = [_i32]
     so.cip_profile_last.argtypes = [_vp, _vp]
     so.cip_last_error.restype = ctypes.c_char_p
     so.cip_build_info.restype = ctypes.c_char_p
     for name in ("cip_choose_params", "cip_ms2dirty", "cip_grid_plane", "cip_grid_layout", "cip_grid_ms",
                  "cip_grid_tiles", "cip_grid_to_dirty", "cip_tile_runs",
-                 "cip_stokes_i", "cip_release_workspace", "cip_profile_enable", "cip_profile_last"):
+                 "cip_stokes_i", "cip_stokes", "cip_facet_rephase", "cip_release_workspace", "cip_profile_enable", "cip_profile_last"):
         getattr(so, name).restype = ctypes.c_int
     _LIB = so
     return so

@@ -69,6 +69,7 @@ def device_ms2dirty(
     out: Optional["torch.Tensor"] = None,
     sum_weights: Optional["torch.Tensor"] = None,
     single_precision_accumulation: bool = False,
+    psf: bool = False,
 ) -> tuple["torch.Tensor", _lib.GridderParams]:
     """
     Device-resident ms2dirty: all tensors already in HBM on the current device.
@@ -78,39 +79,101 @@ def device_ms2dirty(
     single-precision class (CIP_ACC_SINGLE, include/cip.h): quantisation
     2^-19 of max|w V| per contribution, like ducc0's float gridding; the
     default accumulates every input in 64-bit fixed point (fp64 class).
+    `psf=True` grids unit visibilities instead of `vis` (the point-spread
+    function with the same weights; `vis` may then be None).
     """
     vis_codes, wgt_codes = _codes()
-    if vis.dtype not in vis_codes:
-        raise ValueError(f"vis dtype must be complex64/complex128, got {vis.dtype}")
+    if psf:
+        vis = None  # never read
+    elif vis is None or vis.dtype not in vis_codes:
+        raise ValueError(f"vis dtype must be complex64/complex128, got {getattr(vis, 'dtype', None)}")
     if wgt is not None and wgt.dtype not in wgt_codes:
         raise ValueError(f"wgt dtype must be float32/float64, got {wgt.dtype}")
     nrow = uvw.shape[0]
     nchan = freq.shape[0]
     if tuple(uvw.shape) != (nrow, 3):
         raise ValueError("uvw must have shape (nrow, 3)")
-    if tuple(vis.shape) != (nrow, nchan):
+    if vis is not None and tuple(vis.shape) != (nrow, nchan):
         raise ValueError(f"ms must have shape ({nrow}, {nchan}), got {tuple(vis.shape)}")
     if wgt is not None and tuple(wgt.shape) != (nrow, nchan):
         raise ValueError("wgt must have the shape of ms")
-    for t in (uvw, freq, vis) + ((wgt,) if wgt is not None else ()):
+    for t in (uvw, freq) + ((vis,) if vis is not None else ()) + ((wgt,) if wgt is not None else ()):
         if not t.is_contiguous() or not t.is_cuda:
             raise ValueError("device_ms2dirty needs contiguous device tensors")
     if out is None:
-        out = torch.empty((npix_x, npix_y), dtype=torch.float64, device=vis.device)
+        out = torch.empty((npix_x, npix_y), dtype=torch.float64, device=uvw.device)
     params = _lib.GridderParams()
-    stream = torch.cuda.current_stream(vis.device).cuda_stream
+    stream = torch.cuda.current_stream(uvw.device).cuda_stream
     rc = _lib.lib().cip_ms2dirty(
-        uvw.data_ptr(), nrow, freq.data_ptr(), nchan, vis.data_ptr(), vis_codes[vis.dtype],
+        uvw.data_ptr(), nrow, freq.data_ptr(), nchan, None if vis is None else vis.data_ptr(),
+        _lib.CIP_C64 if vis is None else vis_codes[vis.dtype],
         wgt.data_ptr() if wgt is not None else None,
         wgt_codes[wgt.dtype] if wgt is not None else _lib.CIP_NONE,
         int(npix_x), int(npix_y), float(pixsize_x), float(pixsize_y), float(epsilon),
         int(support or 0),
         (_lib.CIP_WSTACKING if do_wstacking else 0)
-        | (_lib.CIP_ACC_SINGLE if single_precision_accumulation else 0),
+        | (_lib.CIP_ACC_SINGLE if single_precision_accumulation else 0)
+        | (_lib.CIP_PSF if psf else 0),
         stream, out.data_ptr(),
         sum_weights.data_ptr() if sum_weights is not None else None, params)
     _lib.check(rc)
     return out, params
+
+
+def device_stokes(vis4: "torch.Tensor", flags4: "torch.Tensor", wgt4: "torch.Tensor", stokes: str = "I"):
+    """
+    Stokes parameter `stokes` ("I", "Q", "U", "V") on the device (cip_stokes;
+    linear feeds XX, XY, YX, YY; I is the reference's invert.py:72-116,
+    bit-exact): -> (visibilities complex64 (nrow, nchan), effective weights
+    float32 (nrow, nchan)).
+    """
+    _require_gpu()
+    if stokes not in _lib.STOKES_CODES:
+        raise ValueError(f"stokes must be one of I, Q, U, V, got {stokes!r}")
+    if vis4.dtype != torch.complex64 or wgt4.dtype != torch.float32:
+        raise ValueError("vis4 must be complex64 and wgt4 float32")
+    if vis4.dim() != 3 or vis4.shape[-1] != 4 or tuple(flags4.shape) != tuple(vis4.shape) or \
+            tuple(wgt4.shape) != tuple(vis4.shape):
+        raise ValueError("vis4, flags4, wgt4 must all have shape (nrow, nchan, 4)")
+    fl = flags4.to(torch.uint8) if flags4.dtype != torch.uint8 else flags4
+    for t in (vis4, fl, wgt4):
+        if not t.is_contiguous() or not t.is_cuda:
+            raise ValueError("device_stokes needs contiguous device tensors")
+    nrow, nchan = vis4.shape[0], vis4.shape[1]
+    vis_s = torch.empty((nrow, nchan), dtype=torch.complex64, device=vis4.device)
+    eff = torch.empty((nrow, nchan), dtype=torch.float32, device=vis4.device)
+    stream = torch.cuda.current_stream(vis4.device).cuda_stream
+    _lib.check(_lib.lib().cip_stokes(vis4.data_ptr(), fl.data_ptr(), wgt4.data_ptr(), nrow * nchan,
+                                     _lib.STOKES_CODES[stokes], stream, vis_s.data_ptr(), None, None,
+                                     eff.data_ptr()))
+    return vis_s, eff
+
+
+def device_facet_rephase(uvw: "torch.Tensor", freq: "torch.Tensor", vis: Optional["torch.Tensor"],
+                         l0: float, m0: float):
+    """
+    Facet data (cip_facet_rephase): visibilities rephased to the facet centre
+    (l0, m0) of the image plane and baselines rotated into the facet's frame,
+    so that device_ms2dirty of the result is the dirty image on the facet's own
+    tangent plane centred on (l0, m0). Returns (uvw_f, vis_f); vis may be None
+    (uvw only, for a facet PSF).
+    """
+    _require_gpu()
+    vis_codes, _ = _codes()
+    nrow, nchan = uvw.shape[0], freq.shape[0]
+    if vis is not None and (vis.dtype not in vis_codes or tuple(vis.shape) != (nrow, nchan)):
+        raise ValueError("vis must be complex64/complex128 of shape (nrow, nchan)")
+    for t in (uvw, freq) + ((vis,) if vis is not None else ()):
+        if not t.is_contiguous() or not t.is_cuda:
+            raise ValueError("device_facet_rephase needs contiguous device tensors")
+    uvw_f = torch.empty_like(uvw)
+    vis_f = torch.empty_like(vis) if vis is not None else None
+    stream = torch.cuda.current_stream(uvw.device).cuda_stream
+    _lib.check(_lib.lib().cip_facet_rephase(
+        uvw.data_ptr(), nrow, freq.data_ptr(), nchan, vis.data_ptr() if vis is not None else None,
+        vis_codes[vis.dtype] if vis is not None else _lib.CIP_C64, float(l0), float(m0), stream, uvw_f.data_ptr(),
+        vis_f.data_ptr() if vis_f is not None else None))
+    return uvw_f, vis_f
 
 
 def device_stokes_i(vis4: "torch.Tensor", flags4: "torch.Tensor", wgt4: "torch.Tensor"):
