@@ -186,6 +186,16 @@ int cip_facet_rephase(const double* uvw, int64_t nrow, const double* freq,
                       double m0, void* hip_stream, double* uvw_out,
                       void* vis_out);
 
+/* RCCL reduction (sum, fp64) of nelem values held by each of ndev devices
+ * in ONE process: grids[k] is a device pointer on
+ * devices[k]; root >= 0 sums onto grids[root] (ncclReduce), root < 0 sums
+ * into every grid (ncclAllReduce). hip_streams: one per device, or NULL.
+ * Returns when done. The communicator clique is cached per device list
+ * (cip_release_collectives frees them). */
+int cip_allreduce_grid(void* const* grids, const int* devices, int ndev,
+                       int64_t nelem, int root, void* const* hip_streams);
+int cip_release_collectives(void);
+
 /* Last error message of the calling thread ("" if none). */
 const char* cip_last_error(void);
 

@@ -45,6 +45,8 @@ EXPORTED_SYMBOLS = (
     "cip_stokes_i",
     "cip_stokes",
     "cip_facet_rephase",
+    "cip_allreduce_grid",
+    "cip_release_collectives",
     "cip_last_error",
     "cip_release_workspace",
     "cip_profile_enable",
@@ -116,6 +118,7 @@ def lib() -> ctypes.CDLL:
                                  ctypes.POINTER(ctypes.c_int64), _vp, _vp, _vp, _vp]
     so.cip_stokes_i.argtypes = [_vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp]
     so.cip_stokes.argtypes = [_vp, _vp, _vp, _i64, _i32, _vp, _vp, _vp, _vp, _vp]
+    so.cip_allreduce_grid.argtypes = [_vp, _vp, _i32, _i64, _i32, _vp]
     so.cip_facet_rephase.argtypes = [_vp, _i64, _vp, _i64, _vp, _i32, _f64, _f64, _vp, _vp, _vp]
     so.cip_profile_enable.argtypes = [_i32]
     so.cip_profile_last.argtypes = [_vp, _vp]
@@ -123,7 +126,8 @@ def lib() -> ctypes.CDLL:
     so.cip_build_info.restype = ctypes.c_char_p
     for name in ("cip_choose_params", "cip_ms2dirty", "cip_grid_plane", "cip_grid_layout", "cip_grid_ms",
                  "cip_grid_tiles", "cip_grid_to_dirty", "cip_tile_runs",
-                 "cip_stokes_i", "cip_stokes", "cip_facet_rephase", "cip_release_workspace", "cip_profile_enable", "cip_profile_last"):
+                 "cip_stokes_i", "cip_stokes", "cip_facet_rephase", "cip_allreduce_grid", "cip_release_collectives",
+                 "cip_release_workspace", "cip_profile_enable", "cip_profile_last"):
         getattr(so, name).restype = ctypes.c_int
     _LIB = so
     return so

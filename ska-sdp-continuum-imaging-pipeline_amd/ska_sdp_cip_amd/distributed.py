@@ -107,3 +107,33 @@ def invert_sharded(uvw, freq, vis, wgt, npix: int, pixsize: float, *, epsilon: f
     dirty, _ = device_ms2dirty(uvw, freq, vis, wgt, npix, npix, pixsize, pixsize, epsilon=epsilon,
                                support=support, do_wstacking=do_wstacking, out=out, sum_weights=sumw)
     return reduce_images(dirty, sumw, dst=dst, group=group)
+
+
+def allreduce_grids(tensors, root: Optional[int] = None):
+    """
+    Single-process multi-GPU reduction through the C ABI (cip_allreduce_grid,
+    RCCL): `tensors` are fp64 device tensors of equal size, one per device;
+    their sum lands in tensors[root] (or in every tensor when root is None).
+    The one-process-per-GPU path above (reduce_images) is what the pipeline
+    and bench use; this is the native equivalent for a host that drives all
+    devices itself.
+    """
+    import ctypes  # pylint: disable=import-outside-toplevel
+
+    import torch  # pylint: disable=import-outside-toplevel
+
+    from . import _lib  # pylint: disable=import-outside-toplevel
+
+    tensors = list(tensors)
+    if not tensors:
+        raise ValueError("no tensors")
+    n = tensors[0].numel()
+    for t in tensors:
+        if t.dtype != torch.float64 or not t.is_cuda or not t.is_contiguous() or t.numel() != n:
+            raise ValueError("tensors must be contiguous fp64 device tensors of one size")
+    ptrs = (ctypes.c_void_p * len(tensors))(*[t.data_ptr() for t in tensors])
+    devs = (ctypes.c_int * len(tensors))(*[t.device.index for t in tensors])
+    streams = (ctypes.c_void_p * len(tensors))(*[torch.cuda.current_stream(t.device).cuda_stream for t in tensors])
+    _lib.check(_lib.lib().cip_allreduce_grid(ptrs, devs, len(tensors), n, -1 if root is None else int(root),
+                                             streams))
+    return tensors

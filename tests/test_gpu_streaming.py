@@ -147,3 +147,22 @@ def test_invert_measurement_set_streamed_equals_one_shot(gpu_device):
         assert img.dtype == np.float32 and img.shape == one.shape
         # same gridding; the reference sums the total weight in float32 numpy
         assert np.abs(img - one).max() <= 2e-6 * np.abs(one).max()
+
+
+def test_allreduce_grids_native_rccl(gpu_device):
+    # cip_allreduce_grid (single process, RCCL): on the one-GPU test box the
+    # clique has one device (sum of one); with more devices every one holds
+    # the sum of all
+    import torch
+
+    from ska_sdp_cip_amd.distributed import allreduce_grids
+
+    ndev = torch.cuda.device_count()
+    ts = [torch.full((1000,), float(k + 1), dtype=torch.float64, device=f"cuda:{k}") for k in range(ndev)]
+    allreduce_grids(ts)
+    want = ndev * (ndev + 1) / 2
+    for t in ts:
+        assert torch.all(t == want)
+    ts = [torch.arange(10, dtype=torch.float64, device=f"cuda:{k}") for k in range(ndev)]
+    allreduce_grids(ts, root=0)
+    assert torch.equal(ts[0].cpu(), ndev * torch.arange(10, dtype=torch.float64))
