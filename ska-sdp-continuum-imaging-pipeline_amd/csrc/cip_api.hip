@@ -272,6 +272,10 @@ struct Workspace {
   // second stream: zeroes the first grid plane while the planner runs
   hipStream_t side = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  bool side_pending = false;
+  // the "grid" buffer when it is known all-zero (the masked FFT pass A zeroes
+  // what the scatter wrote), else NULL
+  double* grid_clean = nullptr;
 };
 
 // Zero `bytes` at `p` on the workspace's side stream, ordered after the work
@@ -286,10 +290,13 @@ static int zero_on_side(Workspace* ws, void* p, size_t bytes, hipStream_t s) {
   CIP_HIP_CHECK(hipStreamWaitEvent(ws->side, ws->ev_fork, 0));
   CIP_HIP_CHECK(hipMemsetAsync(p, 0, bytes, ws->side));
   CIP_HIP_CHECK(hipEventRecord(ws->ev_join, ws->side));
+  ws->side_pending = true;
   return CIP_OK;
 }
 
 static int join_side(Workspace* ws, hipStream_t s) {
+  if (!ws->side_pending) return CIP_OK;
+  ws->side_pending = false;
   CIP_HIP_CHECK(hipStreamWaitEvent(s, ws->ev_join, 0));
   return CIP_OK;
 }
@@ -314,6 +321,7 @@ static T* buf(Workspace* ws, const char* name, int64_t count) {
   const size_t bytes = (size_t)(count > 0 ? count : 1) * sizeof(T);
   DevBuf& b = ws->bufs[name];
   if (b.bytes < bytes) {
+    if (b.ptr && b.ptr == (void*)ws->grid_clean) ws->grid_clean = nullptr;  // a new buffer is not known zero
     if (b.ptr) (void)hipFree(b.ptr);
     b.ptr = nullptr;
     b.bytes = 0;
@@ -404,6 +412,7 @@ struct PlanResult {
   int64_t* tile_run_off = nullptr;
   Chunk* chunks = nullptr;
   uint32_t* perm = nullptr;  // bank-class ordered visibility stream, or NULL
+  uint32_t* dmask = nullptr;  // grid tiles the scatter writes (bit-packed, ntx / 32 words per tile row)
 };
 
 // CIP_FFT_PRUNED=0 selects the full 2-D hipFFT transform (A/B experiments)
@@ -431,6 +440,16 @@ static bool order_gather() {
   static const bool on = [] {
     const char* e = getenv("CIP_ORDER_CLASS");
     return !(e && std::strcmp(e, "compute") == 0);
+  }();
+  return on;
+}
+
+// CIP_GRID_MASK=0: no dirty-tile mask - the grid is zeroed in full before
+// every scatter and pass A reads all of it (A/B experiments)
+static bool grid_mask() {
+  static const bool on = [] {
+    const char* e = getenv("CIP_GRID_MASK");
+    return !(e && e[0] == '0');
   }();
   return on;
 }
@@ -521,6 +540,13 @@ static int make_plan(Workspace* ws, const double* uvw, const double* fx, const R
   CIP_HIP_CHECK(launch_run_lengths(runs, nruns, run_goff, s));
   CIP_HIP_CHECK(exclusive_scan_i64(run_goff, nruns + 1, scan_tmp2, s));
   CIP_HIP_CHECK(launch_tile_vis(run_goff, tile_run_off, ntiles, tile_vis_off, tile_vis, s));
+  if (g.ntx % 32 == 0 && grid_mask()) {
+    CIP_ALLOC(dmask, uint8_t, "dirty_mask", g.ntx * g.nty)
+    CIP_ALLOC(dbits, uint32_t, "dirty_bits", g.ntx * g.nty / 32)
+    CIP_HIP_CHECK(hipMemsetAsync(dmask, 0, (size_t)(g.ntx * g.nty), s));
+    CIP_HIP_CHECK(launch_dirty_mask(tile_vis, g.ntx, g.nty, g.ntw, dmask, dbits, s));
+    pr->dmask = dbits;
+  }
   CIP_HIP_CHECK(launch_chunk_counts(tile_vis, ntiles, cv, chunk_off, s));
   CIP_HIP_CHECK(exclusive_scan_i64(chunk_off, ntiles + 1, scan_tmp, s));
   // chunk offsets of each w tile layer
@@ -670,8 +696,10 @@ static int prepare(Workspace* ws, const double* uvw, int64_t nrow, const double*
     const size_t gbytes = sizeof(double) * 2 * out->g.nu * out->g.nv;
     double* grid = buf<double>(ws, "grid", 2 * out->g.nu * out->g.nv);
     if (!grid) return CIP_ENOMEM;
-    const int zr = zero_on_side(ws, grid, gbytes, s);
-    if (zr != CIP_OK) return zr;
+    if (ws->grid_clean != grid) {
+      const int zr = zero_on_side(ws, grid, gbytes, s);
+      if (zr != CIP_OK) return zr;
+    }
     *grid_out = grid;
   }
   hipEvent_t e_prep = g_prof.mark(s);
@@ -796,11 +824,13 @@ static int dirty_stage(Workspace* ws, const GridGeometry& g, int64_t npix_x, int
 
 // plane p's grid (consumed: the hipFFT path transforms it in place) into
 // dirty_out (overwritten for p == 0, accumulated after it)
+// dmask (pruned FFT only, may be NULL): the grid tiles the scatter wrote; the
+// rest of the grid is zero, and pass A zeroes the masked tiles after reading
 static int plane_to_dirty(const DirtyStage& st, const GridGeometry& g, int64_t p, double* grid, double* dirty_out,
-                          hipStream_t s) {
+                          hipStream_t s, const uint32_t* dmask = nullptr) {
   hipEvent_t f0 = g_prof.mark(s);
   if (st.fast) {
-    CIP_HIP_CHECK(launch_fft_rows(grid, g.nu, g.nv, st.npix_x, st.tw_u, st.fft_h, s));
+    CIP_HIP_CHECK(launch_fft_rows(grid, g.nu, g.nv, st.npix_x, st.tw_u, st.fft_h, dmask, g.ntx, s));
   } else if (hipfftExecZ2Z(st.plan, (hipfftDoubleComplex*)grid, (hipfftDoubleComplex*)grid, HIPFFT_BACKWARD) !=
              HIPFFT_SUCCESS) {
     return set_error(CIP_EHIP, "hipfftExecZ2Z failed");
@@ -935,23 +965,29 @@ int cip_ms2dirty(const double* uvw, int64_t nrow, const double* freq, int64_t nc
   if (rc != CIP_OK) return rc;
   if (params_out) *params_out = pp.p;
   const GridGeometry& g = pp.g;
-  const bool zeroed = grid != nullptr;
+  // zeroed beside the planner, or left all-zero by the previous call
+  bool clean = grid != nullptr;
   if (!grid) grid = buf<double>(ws, "grid", 2 * g.nu * g.nv);
   if (!grid) return CIP_ENOMEM;
+  clean = clean || ws->grid_clean == grid;
   DirtyStage st;
   rc = dirty_stage(ws, g, npix_x, npix_y, pixsize_x, pixsize_y, s, &st);
   if (rc != CIP_OK) return rc;
+  ws->grid_clean = nullptr;  // dirty until a masked pass A has consumed every written tile
+  const uint32_t* dmask = st.fast ? pp.plan.dmask : nullptr;
   for (int64_t p = 0; p < g.nplanes; ++p) {
-    rc = scatter_plane(pp, p, uvw, vis, vis_dtype, wgt, wgt_dtype, st.fast, grid, s, zeroed && p == 0);
+    rc = scatter_plane(pp, p, uvw, vis, vis_dtype, wgt, wgt_dtype, st.fast, grid, s, clean);
     if (rc != CIP_OK) return rc;
-    rc = plane_to_dirty(st, g, p, grid, dirty_out, s);
+    rc = plane_to_dirty(st, g, p, grid, dirty_out, s, dmask);
     if (rc != CIP_OK) return rc;
+    clean = dmask != nullptr;
   }
   rc = finish_dirty(ws, st, pp.p, g, dirty_out, s);
   if (rc != CIP_OK) return rc;
   if (sum_wgt_out) CIP_HIP_CHECK(hipMemcpyAsync(sum_wgt_out, pp.red, sizeof(double), hipMemcpyDeviceToDevice, s));
   g_prof.span(5, t_start, g_prof.mark(s));
   CIP_HIP_CHECK(hipStreamSynchronize(s));
+  if (clean) ws->grid_clean = grid;
   g_prof.finish();
   return CIP_OK;
 }

@@ -180,17 +180,39 @@ __device__ __forceinline__ void fft_core(double2* v, int t, double* lds, const d
 // -> the nx kept frequencies, i = (k + nx/2) mod N < nx, stored in blocks of
 // 8 columns: H[((i / 8) nv + y) 8 + i % 8] (128-byte rows per block, so pass
 // B's 8 columns of a block read whole lines between them).
-template <int N>
-__global__ __launch_bounds__(N / 16) void fft_rows_kernel(const double2* __restrict__ gT, int64_t nv, int64_t nx,
-                                                          const double2* __restrict__ tw, double2* __restrict__ H) {
+// MASKED: only the row's cells in dirty tiles (dmask, kTile-cell segments)
+// are read - the rest of the grid is zero - and those are zeroed after the
+// read, so the next scatter needs no memset of the whole grid.
+template <int N, bool MASKED>
+__global__ __launch_bounds__(N / 16) void fft_rows_kernel(double2* __restrict__ gT, int64_t nv, int64_t nx,
+                                                          const double2* __restrict__ tw, double2* __restrict__ H,
+                                                          const uint32_t* __restrict__ dmask, int64_t ntx) {
   using S = FftShape<N>;
   __shared__ double lds[N + N / 16];
   const int t = threadIdx.x;
   const int64_t y = blockIdx.x;
-  const double2* row = gT + y * N;
+  double2* row = gT + y * N;
   double2 v[16];
+  if constexpr (MASKED) {
+    // the 32-tile word of element r is uniform over the block (T = N / 16
+    // threads, t < T: (t + r T) / (32 kTile) = r T / 1024 for every t), so the
+    // mask words are scalar loads and each lane tests one bit
+    static_assert(kTile == 32 && 1024 % S::T == 0, "mask word per element uniform");
+    const uint32_t* mrow = dmask + (y / kTile) * (ntx / 32);
 #pragma unroll
-  for (int r = 0; r < 16; ++r) v[r] = row[t + r * S::T];
+    for (int r = 0; r < 16; ++r) {
+      const int x = t + r * S::T;
+      const uint32_t word = mrow[(r * S::T) >> 10];
+      v[r] = make_double2(0.0, 0.0);
+      if ((word >> ((x >> 5) & 31)) & 1u) {
+        v[r] = row[x];
+        row[x] = make_double2(0.0, 0.0);
+      }
+    }
+  } else {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v[r] = row[t + r * S::T];
+  }
   fft_core<N>(v, t, lds, tw);
 #pragma unroll
   for (int m = 0; m < 16 / S::RF; ++m)
@@ -268,19 +290,28 @@ bool fast_fft_supported(int64_t nu, int64_t nv, int64_t nx, int64_t ny) {
          ny % 2 == 0;
 }
 
-hipError_t launch_fft_rows(const double* gT, int64_t nu, int64_t nv, int64_t nx, const double* tw_u, double* H,
-                           hipStream_t s) {
+hipError_t launch_fft_rows(double* gT, int64_t nu, int64_t nv, int64_t nx, const double* tw_u, double* H,
+                           const uint32_t* dmask, int64_t ntx, hipStream_t s) {
+  if (!fft_len_ok(nu) || !fft_len_ok(nv) || nx > nu) return hipErrorInvalidValue;
+  if (dmask && (nu % kTile != 0 || nv % kTile != 0 || ntx * kTile != nu || ntx % 32 != 0))
+    return hipErrorInvalidValue;
   const dim3 gd((unsigned)nv);
-  const double2* g = (const double2*)gT;
+  double2* g = (double2*)gT;
   const double2* tw = (const double2*)tw_u;
   double2* h = (double2*)H;
+#define ROWS(NN)                                                                                         \
+  case NN:                                                                                               \
+    if (dmask) fft_rows_kernel<NN, true><<<gd, dim3(NN / 16), 0, s>>>(g, nv, nx, tw, h, dmask, ntx);    \
+    else fft_rows_kernel<NN, false><<<gd, dim3(NN / 16), 0, s>>>(g, nv, nx, tw, h, nullptr, 0);         \
+    break;
   switch (nu) {
-    case 1024: fft_rows_kernel<1024><<<gd, dim3(64), 0, s>>>(g, nv, nx, tw, h); break;
-    case 2048: fft_rows_kernel<2048><<<gd, dim3(128), 0, s>>>(g, nv, nx, tw, h); break;
-    case 4096: fft_rows_kernel<4096><<<gd, dim3(256), 0, s>>>(g, nv, nx, tw, h); break;
-    case 8192: fft_rows_kernel<8192><<<gd, dim3(512), 0, s>>>(g, nv, nx, tw, h); break;
+    ROWS(1024)
+    ROWS(2048)
+    ROWS(4096)
+    ROWS(8192)
     default: return hipErrorInvalidValue;
   }
+#undef ROWS
   return hipGetLastError();
 }
 

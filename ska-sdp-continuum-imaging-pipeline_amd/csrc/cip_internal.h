@@ -62,6 +62,9 @@ hipError_t launch_radix_scatter(const uint32_t* keys, const uint64_t* vals, int6
                                 uint64_t* vals_out, hipStream_t s);
 hipError_t launch_tile_offsets(const uint32_t* keys, int64_t nruns, int64_t ntiles, int64_t* tile_run_off,
                                hipStream_t s);
+// bits (optional, ntx % 32 == 0): the mask bit-packed, ntx / 32 words per tile row
+hipError_t launch_dirty_mask(const int64_t* tile_vis, int64_t ntx, int64_t nty, int64_t ntw, uint8_t* mask,
+                             uint32_t* bits, hipStream_t s);
 hipError_t launch_tile_vis(const int64_t* run_goff, const int64_t* tile_run_off, int64_t ntiles,
                            int64_t* tile_vis_off, int64_t* tile_vis, hipStream_t s);
 hipError_t launch_run_lengths(const uint64_t* runs, int64_t nruns, int64_t* out, hipStream_t s);
@@ -107,8 +110,12 @@ hipError_t launch_wfinal_correct(double* acc, int64_t npix_x, int64_t npix_y, do
 // tw_u / tw_v: exp(+2 pi i m / n), m < n (interleaved re, im).
 // mode 0: out = dirty (crop + cx cy); mode 1: out = w-plane accumulator.
 bool fast_fft_supported(int64_t nu, int64_t nv, int64_t nx, int64_t ny);
-hipError_t launch_fft_rows(const double* gT, int64_t nu, int64_t nv, int64_t nx, const double* tw_u, double* H,
-                           hipStream_t s);
+// dmask (bit-packed dirty tiles, ntx / 32 words per 32-cell tile row of gT,
+// NULL = dense): cells of tiles whose bit is 0 are known zero and not read;
+// cells of marked tiles are read and then ZEROED (the grid is left all-zero
+// for the next scatter)
+hipError_t launch_fft_rows(double* gT, int64_t nu, int64_t nv, int64_t nx, const double* tw_u, double* H,
+                           const uint32_t* dmask, int64_t ntx, hipStream_t s);
 hipError_t launch_fft_cols(const double* H, int64_t nv, int64_t nx, int64_t ny, const double* tw_v, int mode,
                            double* out, const double* cx, const double* cy, double px, double py, double w_plane,
                            int first, hipStream_t s);

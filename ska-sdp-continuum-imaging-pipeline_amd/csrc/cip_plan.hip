@@ -485,6 +485,45 @@ __global__ void tile_vis_kernel(const int64_t* run_goff, const int64_t* tile_run
   if (t < ntiles) tile_vis[t] = run_goff[tile_run_off[t + 1]] - a;
 }
 
+// Dirty-tile mask of the HBM grid (ntx x nty bytes, zeroed by the caller):
+// tile (tx, ty) is written by the scatter's flush when a visibility lands in
+// it or, through the (T + W - 1)^2 sub-grid's halo (W - 1 < T cells), in its
+// -x, -y or -x-y neighbour (periodic grid); any w layer counts.
+__global__ void dirty_mask_kernel(const int64_t* __restrict__ tile_vis, int64_t ntx, int64_t nty, int64_t ntw,
+                                  uint8_t* __restrict__ mask) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= ntx * nty) return;
+  bool touched = false;
+  for (int64_t w = 0; w < ntw && !touched; ++w) touched = tile_vis[w * ntx * nty + t] > 0;
+  if (!touched) return;
+  const int64_t tx = t % ntx, ty = t / ntx;
+  const int64_t tx1 = tx + 1 < ntx ? tx + 1 : 0, ty1 = ty + 1 < nty ? ty + 1 : 0;
+  mask[ty * ntx + tx] = 1;  // idempotent stores: no atomics needed
+  mask[ty * ntx + tx1] = 1;
+  mask[ty1 * ntx + tx] = 1;
+  mask[ty1 * ntx + tx1] = 1;
+}
+
+// bit-pack the byte mask: bit tx % 32 of word ty * (ntx / 32) + tx / 32
+__global__ void pack_mask_kernel(const uint8_t* __restrict__ mask, int64_t nwords, uint32_t* __restrict__ bits) {
+  const int64_t wd = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (wd >= nwords) return;
+  uint32_t b = 0u;
+  for (int k = 0; k < 32; ++k) b |= (uint32_t)(mask[32 * wd + k] != 0) << k;
+  bits[wd] = b;
+}
+
+hipError_t launch_dirty_mask(const int64_t* tile_vis, int64_t ntx, int64_t nty, int64_t ntw, uint8_t* mask,
+                             uint32_t* bits, hipStream_t s) {
+  dirty_mask_kernel<<<dim3((unsigned)((ntx * nty + 255) / 256)), dim3(256), 0, s>>>(tile_vis, ntx, nty, ntw, mask);
+  if (bits) {
+    if (ntx % 32 != 0) return hipErrorInvalidValue;
+    const int64_t nw = ntx * nty / 32;
+    pack_mask_kernel<<<dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, s>>>(mask, nw, bits);
+  }
+  return hipGetLastError();
+}
+
 hipError_t launch_tile_vis(const int64_t* run_goff, const int64_t* tile_run_off, int64_t ntiles,
                            int64_t* tile_vis_off, int64_t* tile_vis, hipStream_t s) {
   tile_vis_kernel<<<dim3((unsigned)((ntiles + 256) / 256)), dim3(256), 0, s>>>(run_goff, tile_run_off, ntiles,

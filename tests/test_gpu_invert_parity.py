@@ -246,3 +246,30 @@ def test_dense_single_channel_tiles(gpu_device):
     ref = oracle.ms2dirty(uvw, f, vis, w, npix, npix, px, px, support=8, do_wstacking=False)
     sumw = float(w.astype(np.float64).sum())
     assert _norm_err(gpu, ref, sumw) < TIGHT
+
+
+def test_grid_left_clean_between_calls(gpu_device):
+    # the pruned FFT's pass A zeroes the grid tiles the scatter wrote (no
+    # whole-grid memset per call): a call after one with different uv coverage,
+    # w-stacking planes or an error must not see any residue
+    # complex128 visibilities: fp64 output (complex64 returns float32, as ducc0 does)
+    a = _case(2_000, 8, n_ant=16, radius=1500.0, seed=21)
+    b = _case(1_500, 4, n_ant=10, radius=400.0, seed=22)
+    a = (a[0], a[1], a[2].astype(np.complex128), a[3])
+    b = (b[0], b[1], b[2].astype(np.complex128), b[3])
+    npix = 1024  # grid 2048: power of two -> pruned FFT path
+    res = {}
+    for name, (uvw, f, vis, w) in (("a", a), ("b", b)):
+        px = syn.pixel_size_for_grid(uvw, f, npix, support=8)
+        res[name] = (px, oracle.ms2dirty(uvw, f, vis, w, npix, npix, px, px, support=8, do_wstacking=False))
+    for name, ws in (("a", False), ("b", False), ("a", True), ("a", False), ("b", False)):
+        uvw, f, vis, w = a if name == "a" else b
+        px, ref = res[name]
+        gpu = gridder.ms2dirty(uvw, f, vis, w, npix, npix, px, px, support=8, do_wstacking=ws)
+        if not ws:
+            assert _norm_err(gpu, ref, float(w.astype(np.float64).sum())) < TIGHT, name
+        if name == "b":  # an error after planning leaves the grid dirty: the next call must still be exact
+            bad = vis.copy()
+            bad[3, 1] = np.nan
+            with pytest.raises(ValueError):
+                gridder.ms2dirty(uvw, f, bad, w, npix, npix, px, px, support=8, do_wstacking=False)
