@@ -121,6 +121,7 @@ struct Chunk {
   int64_t g0, g1;
   int64_t tile;
   int64_t first_run;  // first row slice of the tile overlapping [g0, g1)
+  int64_t last_run;   // last row slice overlapping [g0, g1)
 };
 
 // Everything the planner and the scatter need to place a visibility.

@@ -256,7 +256,7 @@ __device__ __forceinline__ unsigned origin_class(double u_m, double v_m, double 
 // whole perm stream) and the window is counting-sorted into level-major
 // order: perm[g] = row * nchan + channel (32-bit flattened MS index).
 template <bool GATHER>
-__global__ __launch_bounds__(kOrderThreads) void order_kernel(const double* __restrict__ uvw,
+__global__ __launch_bounds__(kOrderThreads, 8) void order_kernel(const double* __restrict__ uvw,
                                                               const double* __restrict__ fx,
                                                               const uint8_t* __restrict__ vis_class, GridGeometry g,
                                                               RowMap m, const uint64_t* __restrict__ runs,
@@ -287,16 +287,8 @@ __global__ __launch_bounds__(kOrderThreads) void order_kernel(const double* __re
   const Chunk ch = windows[blockIdx.x];
   const int64_t sb = ch.g0;
   const int nsb = (int)(ch.g1 - ch.g0);
-  // slices [first_run, last]: the next window of this tile starts in `last`
-  int64_t last = tile_run_off[ch.tile + 1] - 1;
-  if (blockIdx.x + 1 < nwindows) {
-    const Chunk nx = windows[blockIdx.x + 1];
-    if (nx.tile == ch.tile) last = nx.first_run;
-  }
-  // (a window of n positions meets at most n slices: the next window may
-  // start exactly at a slice boundary, whose slice is then not this window's)
-  const int64_t nst64 = last - ch.first_run + 1;
-  const int nst = (int)(nst64 < nsb ? nst64 : nsb);
+  // the window's slices [first_run, last_run] (at most one per position)
+  const int nst = (int)(ch.last_run - ch.first_run + 1);
   for (int k = threadIdx.x; k < nst; k += kOrderThreads) {
     s_off[k] = (int)(run_goff[ch.first_run + k] - sb);
     const uint64_t rec = runs[ch.first_run + k];
@@ -340,23 +332,16 @@ __global__ __launch_bounds__(kOrderThreads) void order_kernel(const double* __re
   for (int k = 0; k < kOrderPer; ++k)
     if (cls[k] < 32u) rk[k] = atomicAdd(&s_cnt[cls[k]], 1u);
   __syncthreads();
-  unsigned cnt[32], maxcnt = 0;
+  unsigned maxcnt = 0;
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const uint4 c4 = reinterpret_cast<const uint4*>(s_cnt)[i];
-    cnt[4 * i] = c4.x;
-    cnt[4 * i + 1] = c4.y;
-    cnt[4 * i + 2] = c4.z;
-    cnt[4 * i + 3] = c4.w;
-  }
-#pragma unroll
-  for (int i = 0; i < 32; ++i) maxcnt = cnt[i] > maxcnt ? cnt[i] : maxcnt;
+  for (int i = 0; i < 32; ++i) maxcnt = s_cnt[i] > maxcnt ? s_cnt[i] : maxcnt;  // LDS broadcast reads
   for (unsigned r = threadIdx.x; r < maxcnt; r += kOrderThreads) {
     unsigned S = 0, M = 0;
 #pragma unroll
     for (int c2 = 0; c2 < 32; ++c2) {
-      S += cnt[c2] < r ? cnt[c2] : r;
-      M |= (cnt[c2] > r ? 1u : 0u) << c2;
+      const unsigned cnt = s_cnt[c2];
+      S += cnt < r ? cnt : r;
+      M |= (cnt > r ? 1u : 0u) << c2;
     }
     s_S[r] = S;
     s_M[r] = M;

@@ -574,6 +574,14 @@ __global__ void chunk_emit_kernel(const int64_t* __restrict__ tile_vis_off, cons
     else rl = mid + 1;
   }
   ch.first_run = rl;
+  // last run whose start lies before g1 (the one holding position g1 - 1)
+  rh = tile_run_off[t + 1] - 1;
+  while (rl < rh) {
+    const int64_t mid = (rl + rh + 1) >> 1;
+    if (run_goff[mid] < ch.g1) rl = mid;
+    else rh = mid - 1;
+  }
+  ch.last_run = rl;
   chunks[j] = ch;
 }
 
