@@ -537,8 +537,7 @@ static int make_plan(Workspace* ws, const double* uvw, const double* fx, const R
   const int64_t* tile_run_off = tile_runs;
   CIP_ALLOC(run_goff, int64_t, "run_goff", nruns + 1)
   CIP_ALLOC(scan_tmp2, int64_t, "scan_tmp2", scan_tmp_elems(nruns + 1))
-  CIP_HIP_CHECK(launch_run_lengths(runs, nruns, run_goff, s));
-  CIP_HIP_CHECK(exclusive_scan_i64(run_goff, nruns + 1, scan_tmp2, s));
+  CIP_HIP_CHECK(scan_run_offsets(runs, nruns, run_goff, scan_tmp2, s));
   CIP_HIP_CHECK(launch_tile_vis(run_goff, tile_run_off, ntiles, tile_vis_off, tile_vis, s));
   if (g.ntx % 32 == 0 && grid_mask()) {
     CIP_ALLOC(dmask, uint8_t, "dirty_mask", g.ntx * g.nty)

@@ -24,6 +24,9 @@ int set_error(int code, const std::string& msg);
 // ---- scan (cip_plan.hip) -------------------------------------------------
 // In-place exclusive scan of n int64 values; tmp must hold scan_tmp_elems(n).
 int64_t scan_tmp_elems(int64_t n);
+// run_goff[k] = sum of the lengths of runs [0, k), k in [0, nruns] (fused
+// run-length + exclusive scan)
+hipError_t scan_run_offsets(const uint64_t* runs, int64_t nruns, int64_t* run_goff, int64_t* tmp, hipStream_t s);
 hipError_t exclusive_scan_i64(int64_t* data, int64_t n, int64_t* tmp, hipStream_t s);
 
 // ---- gridder planner (cip_plan.hip) ----------------------------------------

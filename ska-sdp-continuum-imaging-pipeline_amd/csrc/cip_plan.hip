@@ -12,14 +12,27 @@ constexpr int kScanThreads = 1024;
 constexpr int kScanItems = 4;
 constexpr int64_t kScanBlock = (int64_t)kScanThreads * kScanItems;
 
-__global__ __launch_bounds__(kScanThreads) void scan_local_kernel(int64_t* data, int64_t n, int64_t* block_sums) {
+// RUNS: the input is the run records (n - 1 of them): item k is run k's
+// length (channel stop - start), item n - 1 is 0, and the scan goes to `data`
+// (the fused run-length pass of the slice offsets)
+template <bool RUNS>
+__global__ __launch_bounds__(kScanThreads) void scan_local_kernel(int64_t* data, int64_t n, int64_t* block_sums,
+                                                                  const uint64_t* __restrict__ runs) {
   __shared__ int64_t wave_tot[kScanThreads / 64];
   const int64_t base = (int64_t)blockIdx.x * kScanBlock + (int64_t)threadIdx.x * kScanItems;
   int64_t v[kScanItems];
   int64_t tsum = 0;
 #pragma unroll
   for (int i = 0; i < kScanItems; ++i) {
-    v[i] = (base + i < n) ? data[base + i] : 0;
+    if constexpr (RUNS) {
+      v[i] = 0;
+      if (base + i < n - 1) {
+        const uint64_t rec = runs[base + i];
+        v[i] = (int64_t)(rec & 0xffff) - (int64_t)((rec >> 16) & 0xffff);
+      }
+    } else {
+      v[i] = (base + i < n) ? data[base + i] : 0;
+    }
     tsum += v[i];
   }
   // inclusive wave scan of the thread sums
@@ -71,16 +84,27 @@ int64_t scan_tmp_elems(int64_t n) {
   return total + 1;
 }
 
-hipError_t exclusive_scan_i64(int64_t* data, int64_t n, int64_t* tmp, hipStream_t s) {
+static hipError_t scan_impl(int64_t* data, int64_t n, int64_t* tmp, const uint64_t* runs, hipStream_t s) {
   if (n <= 0) return hipSuccess;
   const int64_t nb = (n + kScanBlock - 1) / kScanBlock;
-  scan_local_kernel<<<dim3((unsigned)nb), dim3(kScanThreads), 0, s>>>(data, n, tmp);
+  if (runs)
+    scan_local_kernel<true><<<dim3((unsigned)nb), dim3(kScanThreads), 0, s>>>(data, n, tmp, runs);
+  else
+    scan_local_kernel<false><<<dim3((unsigned)nb), dim3(kScanThreads), 0, s>>>(data, n, tmp, nullptr);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || nb == 1) return e;
-  e = exclusive_scan_i64(tmp, nb, tmp + nb, s);
+  e = scan_impl(tmp, nb, tmp + nb, nullptr, s);
   if (e != hipSuccess) return e;
   scan_add_kernel<<<dim3((unsigned)nb), dim3(kScanThreads), 0, s>>>(data, n, tmp);
   return hipGetLastError();
+}
+
+hipError_t exclusive_scan_i64(int64_t* data, int64_t n, int64_t* tmp, hipStream_t s) {
+  return scan_impl(data, n, tmp, nullptr, s);
+}
+
+hipError_t scan_run_offsets(const uint64_t* runs, int64_t nruns, int64_t* run_goff, int64_t* tmp, hipStream_t s) {
+  return scan_impl(run_goff, nruns + 1, tmp, runs, s);
 }
 
 // ------------------------------------------------------------ helpers ----
