@@ -14,7 +14,10 @@
 #include <type_traits>
 
 // Experiment-only builds (tools/build_variant.sh): 1 = conflict-free LDS
-// addresses, 2 = no LDS atomics, 3 = no kernel evaluation. 0 in the library.
+// addresses, 2 = no LDS atomics, 3 = no kernel evaluation, 4 = no flush to
+// HBM (timing only, wrong images). 0 in the library. Measured at C3
+// (profiles/microbench_r01.txt): kernel evaluation ~0.2 ms, flush ~0.1 ms of
+// the 3.1 ms scatter.
 #ifndef CIP_ABLATE
 #define CIP_ABLATE 0
 #endif
@@ -462,7 +465,11 @@ __global__ __launch_bounds__(kScatterThreads) void scatter_kernel(
       re = (long long)sub[lcell];
       im = (long long)sub[P * P + lcell];
     }
+#if CIP_ABLATE == 4
+    if (((re | im) != 0) && re == 0x123456789ll) {  // ablation: no flush (timing only)
+#else
     if ((re | im) != 0) {
+#endif
       // the sub-grid of an edge tile wraps around the periodic grid
       int64_t gx = X0 + lcell / P, gy = Y0 + lcell % P;
       gx -= (gx >= g.nu) ? g.nu : 0;

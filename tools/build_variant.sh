@@ -11,6 +11,7 @@ done
 wait
 for n in "$@"; do
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o ../../tools/variants/libcip_hip_abl$n.so \
-    build/cip_api.o build/cip_plan.o build/cip_grid_abl$n.o build/cip_tiling.o -L/opt/rocm/lib -lhipfft \
+    build/cip_api.o build/cip_plan.o build/cip_grid_abl$n.o build/cip_tiling.o build/cip_fft.o \
+    build/cip_collective.o -L/opt/rocm/lib -lhipfft -lrccl \
     -Wl,-rpath,/opt/rocm/lib
 done
