@@ -89,11 +89,15 @@ __device__ __forceinline__ void stockham_pass(double2* v, int t, int ns, const d
     const int j = t + m * T;
     const int k = j & (ns - 1);
     if (ns > 1) {
+      // exp(+2 pi i r k / (ns R)) = w^r, w = tw[k N / (ns R)]: one table load
+      // per butterfly (the loads were latency on the critical path), powers by
+      // repeated products (error grows by ~1 ulp per power, R <= 16)
+      const double2 w = tw[(k * (N / (ns * R))) & (N - 1)];
+      double2 wr = w;
 #pragma unroll
       for (int r = 1; r < R; ++r) {
-        // exp(+2 pi i r k / (ns R)) = tw[r k N / (ns R)]
-        const int e = (r * k * (N / (ns * R))) & (N - 1);
-        v[m * R + r] = cmul(v[m * R + r], tw[e]);
+        v[m * R + r] = cmul(v[m * R + r], wr);
+        if (r + 1 < R) wr = cmul(wr, w);
       }
     }
     dft<R>(v + m * R);
