@@ -202,3 +202,40 @@ def test_synthetic_ms_shapes():
     assert ms.visibilities().dtype == np.complex64 and ms.visibilities().shape == (500, 4, 4)
     assert ms.flags().dtype == bool and ms.weights().dtype == np.float32
     assert ms.uvw().shape == (500, 3) and ms.uvw().dtype == np.float64
+
+
+def test_w_ranges_and_facet_centres():
+    # host helpers of the accumulating gridder and the continuum products
+    from ska_sdp_cip_amd.accumulate import merge_w_ranges, w_range_rows, w_range_slices
+    from ska_sdp_cip_amd.continuum import facet_centres
+
+    rng = np.random.default_rng(0)
+    uvw = rng.normal(0.0, 500.0, (200, 3))
+    f = np.linspace(0.9e9, 1.7e9, 16)
+    lo, hi = w_range_rows(uvw, f)
+    w = uvw[:, 2:3] * (f[None, :] / 299792458.0)
+    assert np.isclose(lo, w.min()) and np.isclose(hi, w.max())
+    # slices of every row: the same range; empty slices are ignored
+    c0 = np.zeros(200, np.int32)
+    c1 = np.full(200, 16, np.int32)
+    c1[::3] = 0
+    lo2, hi2 = w_range_slices(uvw, c0, c1, f)
+    keep = c1 > c0
+    assert (lo2, hi2) == w_range_rows(uvw[keep], f)
+    assert w_range_slices(uvw, c0, c0, f) == (np.inf, -np.inf)
+    assert merge_w_ranges([(1.0, 2.0), (-3.0, 0.5), (np.inf, -np.inf)]) == (-3.0, 2.0)
+    cen = facet_centres(3, 2, 100, 1e-5)
+    assert len(cen) == 6 and cen[0] == (-1e-3, -5e-4) and cen[-1] == (1e-3, 5e-4)
+    assert np.allclose(np.mean(cen, axis=0), 0.0)
+
+
+def test_oracle_stokes_and_facet_rotation():
+    # the oracle's restatements used by the GPU tests: Stokes I equals the
+    # golden-pinned stokes_i; the facet rotation takes the pole to the centre
+    g = np.load(GOLD / "stokes_i.npz")
+    v, eff = oracle.stokes(g["vis4"], g["flags4"], g["weights4"], "I")
+    assert np.array_equal(v, g["vis_i"]) and np.array_equal(eff, g["eff_w"])
+    for l0, m0 in [(0.0, 0.0), (0.05, -0.02), (-0.3, 0.4)]:
+        q = oracle.facet_rotation(l0, m0)
+        assert np.allclose(q @ q.T, np.eye(3), atol=1e-14)
+        assert np.allclose(q @ [0.0, 0.0, 1.0], [l0, m0, np.sqrt(1 - l0 * l0 - m0 * m0)], atol=1e-14)
