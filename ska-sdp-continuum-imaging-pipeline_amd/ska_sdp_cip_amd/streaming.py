@@ -56,13 +56,29 @@ class ChunkStager:
     gridding call that read it returned (the gridder calls are synchronous).
     """
 
-    def __init__(self, device, nslots: int = 2):
+    # host copies into the pinned slots are split over threads (one numpy copy
+    # runs at ~6 GB/s and capped the pipeline; numpy releases the GIL for them)
+    _COPY_PIECE = 8 << 20
+    _pool = None
+
+    def __init__(self, device, nslots: int = 2, copy_threads: int = 8):
         self.device = torch.device(device)
         self.copy_stream = torch.cuda.Stream(device=self.device)
         self._host = [dict() for _ in range(nslots)]
         self._dev = [dict() for _ in range(nslots)]
         self._ready = [None] * nslots
         self.bytes_staged = 0
+        if ChunkStager._pool is None and copy_threads > 1:
+            ChunkStager._pool = cf.ThreadPoolExecutor(max_workers=copy_threads)
+
+    @classmethod
+    def _copy(cls, dst: np.ndarray, src: np.ndarray) -> None:
+        n = src.size
+        if cls._pool is None or n <= cls._COPY_PIECE:
+            dst[:] = src
+            return
+        step = max(cls._COPY_PIECE, -(-n // 32))
+        list(cls._pool.map(lambda a: np.copyto(dst[a:a + step], src[a:a + step]), range(0, n, step)))
 
     @staticmethod
     def _grow(pool: dict, name: str, nbytes: int, **kw):
@@ -82,7 +98,7 @@ class ChunkStager:
                 nb = a.nbytes
                 h = self._grow(self._host[slot], name, nb, pin_memory=True)[:nb]
                 if nb:
-                    h.numpy()[:] = a.reshape(-1).view(np.uint8)
+                    self._copy(h.numpy(), a.reshape(-1).view(np.uint8))
                 d = self._grow(self._dev[slot], name, nb, device=self.device)[:nb]
                 d.copy_(h, non_blocking=True)
                 out[name] = d.view(_torch_dtype(a.dtype)).view(a.shape)
@@ -96,29 +112,43 @@ class ChunkStager:
         torch.cuda.current_stream(self.device).wait_event(self._ready[slot])
 
 
-def _pipeline(loaders: Sequence[Callable[[], dict]], stager: ChunkStager, consume: Callable[[dict], None]) -> None:
+def _pipeline(loaders: Sequence[Callable[[], dict]], stager: ChunkStager, consume: Callable[[dict], None],
+              readers: int = 4) -> None:
     """
-    Read + stage on a worker thread (disk -> pinned -> copy stream), consume
-    on the caller's thread (compute stream). Chunk k + 1 is read and staged
-    while chunk k is gridded; chunk k + 2's staging is queued only once chunk
-    k's (synchronous) gridding returned, since it reuses chunk k's slot.
+    Read on `readers` threads (up to that many chunks ahead: a reader's copy
+    out of the measurement set or an npz file is single-threaded, ~3-6 GB/s),
+    stage in order on one thread (pinned slot -> copy stream), consume on the
+    caller's thread (compute stream). Chunk k + 1 is staged while chunk k is
+    gridded; chunk k + 2's staging is queued only once chunk k's (synchronous)
+    gridding returned, since it reuses chunk k's slot.
     """
     n = len(loaders)
     if n == 0:
         return
+    with cf.ThreadPoolExecutor(max_workers=max(1, readers)) as rpool, \
+            cf.ThreadPoolExecutor(max_workers=1) as spool:
+        reads = {}
 
-    def job(k):
-        with torch.cuda.device(stager.device):
-            return stager.stage(k % 2, loaders[k]())
+        def read_upto(k):
+            for j in range(k):
+                if j < n and j not in reads:
+                    reads[j] = rpool.submit(loaders[j])
 
-    with cf.ThreadPoolExecutor(max_workers=1) as pool:
-        pending = {k: pool.submit(job, k) for k in range(min(2, n))}
+        def job(k):
+            arrays = reads[k].result()
+            with torch.cuda.device(stager.device):
+                return stager.stage(k % 2, arrays)
+
+        read_upto(readers + 1)
+        pending = {k: spool.submit(job, k) for k in range(min(2, n))}
         for k in range(n):
             staged = pending.pop(k).result()
+            reads.pop(k, None)
+            read_upto(k + readers + 2)
             stager.wait(k % 2)
             consume(staged)
             if k + 2 < n:
-                pending[k + 2] = pool.submit(job, k + 2)
+                pending[k + 2] = spool.submit(job, k + 2)
 
 
 def _npz_w_range(path, freq) -> tuple[float, float]:
