@@ -82,6 +82,9 @@ hipError_t launch_add_scalar(const double* src, double* dst, hipStream_t s) {
 }
 
 // ------------------------------------------------------------ scatter ----
+#ifndef CIP_SCATTER_WAVES
+#define CIP_SCATTER_WAVES 4  // min waves per SIMD the scatter is compiled for (register budget)
+#endif
 constexpr int kScatterThreads = 256;
 constexpr int kRunBatch = 256;
 
@@ -369,7 +372,7 @@ hipError_t launch_order(const double* uvw, const double* fx, const uint8_t* vis_
 }
 
 template <int W, typename VisT, int WK, bool WSTACK, bool PERM, bool PACK>
-__global__ __launch_bounds__(kScatterThreads) void scatter_kernel(
+__global__ __launch_bounds__(kScatterThreads, CIP_SCATTER_WAVES) void scatter_kernel(
     const double* __restrict__ uvw, const double* __restrict__ fx, const VisT* __restrict__ vis,
     const void* __restrict__ wgt, RowMap m, const uint64_t* __restrict__ runs,
     const int64_t* __restrict__ run_goff, const int64_t* __restrict__ tile_run_off,
