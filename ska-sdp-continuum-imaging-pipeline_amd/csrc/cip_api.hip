@@ -412,7 +412,7 @@ struct PlanResult {
   int64_t* tile_run_off = nullptr;
   Chunk* chunks = nullptr;
   uint32_t* perm = nullptr;  // bank-class ordered visibility stream, or NULL
-  uint32_t* dmask = nullptr;  // grid tiles the scatter writes (bit-packed, ntx / 32 words per tile row)
+  uint32_t* dmask = nullptr;  // grid tiles the scatter writes, per plane (bit-packed, ntx / 32 words per tile row)
 };
 
 // CIP_FFT_PRUNED=0 selects the full 2-D hipFFT transform (A/B experiments)
@@ -540,10 +540,10 @@ static int make_plan(Workspace* ws, const double* uvw, const double* fx, const R
   CIP_HIP_CHECK(scan_run_offsets(runs, nruns, run_goff, scan_tmp2, s));
   CIP_HIP_CHECK(launch_tile_vis(run_goff, tile_run_off, ntiles, tile_vis_off, tile_vis, s));
   if (g.ntx % 32 == 0 && grid_mask()) {
-    CIP_ALLOC(dmask, uint8_t, "dirty_mask", g.ntx * g.nty)
-    CIP_ALLOC(dbits, uint32_t, "dirty_bits", g.ntx * g.nty / 32)
-    CIP_HIP_CHECK(hipMemsetAsync(dmask, 0, (size_t)(g.ntx * g.nty), s));
-    CIP_HIP_CHECK(launch_dirty_mask(tile_vis, g.ntx, g.nty, g.ntw, dmask, dbits, s));
+    CIP_ALLOC(dmask, uint8_t, "dirty_mask", g.ntx * g.nty * g.nplanes)
+    CIP_ALLOC(dbits, uint32_t, "dirty_bits", g.ntx * g.nty / 32 * g.nplanes)
+    CIP_HIP_CHECK(hipMemsetAsync(dmask, 0, (size_t)(g.ntx * g.nty * g.nplanes), s));
+    CIP_HIP_CHECK(launch_dirty_mask(tile_vis, g.ntx, g.nty, g.ntw, g.support, g.nplanes, dmask, dbits, s));
     pr->dmask = dbits;
   }
   CIP_HIP_CHECK(launch_chunk_counts(tile_vis, ntiles, cv, chunk_off, s));
@@ -977,7 +977,7 @@ int cip_ms2dirty(const double* uvw, int64_t nrow, const double* freq, int64_t nc
   for (int64_t p = 0; p < g.nplanes; ++p) {
     rc = scatter_plane(pp, p, uvw, vis, vis_dtype, wgt, wgt_dtype, st.fast, grid, s, clean);
     if (rc != CIP_OK) return rc;
-    rc = plane_to_dirty(st, g, p, grid, dirty_out, s, dmask);
+    rc = plane_to_dirty(st, g, p, grid, dirty_out, s, dmask ? dmask + p * (g.ntx * g.nty / 32) : nullptr);
     if (rc != CIP_OK) return rc;
     clean = dmask != nullptr;
   }

@@ -65,9 +65,10 @@ hipError_t launch_radix_scatter(const uint32_t* keys, const uint64_t* vals, int6
                                 uint64_t* vals_out, hipStream_t s);
 hipError_t launch_tile_offsets(const uint32_t* keys, int64_t nruns, int64_t ntiles, int64_t* tile_run_off,
                                hipStream_t s);
-// bits (optional, ntx % 32 == 0): the mask bit-packed, ntx / 32 words per tile row
-hipError_t launch_dirty_mask(const int64_t* tile_vis, int64_t ntx, int64_t nty, int64_t ntw, uint8_t* mask,
-                             uint32_t* bits, hipStream_t s);
+// per grid plane (nplanes x ntx x nty bytes); bits (optional, ntx % 32 ==
+// 0): the masks bit-packed, ntx / 32 words per tile row, ntx nty / 32 per plane
+hipError_t launch_dirty_mask(const int64_t* tile_vis, int64_t ntx, int64_t nty, int64_t ntw, int support,
+                             int64_t nplanes, uint8_t* mask, uint32_t* bits, hipStream_t s);
 hipError_t launch_tile_vis(const int64_t* run_goff, const int64_t* tile_run_off, int64_t ntiles,
                            int64_t* tile_vis_off, int64_t* tile_vis, hipStream_t s);
 hipError_t launch_run_lengths(const uint64_t* runs, int64_t nruns, int64_t* out, hipStream_t s);

@@ -509,23 +509,33 @@ __global__ void tile_vis_kernel(const int64_t* run_goff, const int64_t* tile_run
   if (t < ntiles) tile_vis[t] = run_goff[tile_run_off[t + 1]] - a;
 }
 
-// Dirty-tile mask of the HBM grid (ntx x nty bytes, zeroed by the caller):
-// tile (tx, ty) is written by the scatter's flush when a visibility lands in
-// it or, through the (T + W - 1)^2 sub-grid's halo (W - 1 < T cells), in its
-// -x, -y or -x-y neighbour (periodic grid); any w layer counts.
+// Dirty-tile masks of the HBM grid, one per grid plane (nplanes x ntx x nty
+// bytes, zeroed by the caller): tile (tx, ty) of plane p is written by the
+// scatter's flush when a visibility of a tile layer feeding p (w-stacking:
+// layers p - W + 1 .. p; 2-D: the one layer) lands in it or, through the
+// (T + W - 1)^2 sub-grid's halo (W - 1 < T cells), in its -x, -y or -x-y
+// neighbour (periodic grid).
 __global__ void dirty_mask_kernel(const int64_t* __restrict__ tile_vis, int64_t ntx, int64_t nty, int64_t ntw,
-                                  uint8_t* __restrict__ mask) {
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= ntx * nty) return;
+                                  int support, int64_t nplanes, uint8_t* __restrict__ mask) {
+  const int64_t id = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t nt = ntx * nty;
+  if (id >= nt * nplanes) return;
+  const int64_t p = id / nt, t = id - p * nt;
+  int64_t lo = 0, hi = 0;
+  if (nplanes > 1) {
+    lo = p - support + 1 > 0 ? p - support + 1 : 0;
+    hi = p < ntw - 1 ? p : ntw - 1;
+  }
   bool touched = false;
-  for (int64_t w = 0; w < ntw && !touched; ++w) touched = tile_vis[w * ntx * nty + t] > 0;
+  for (int64_t w = lo; w <= hi && !touched; ++w) touched = tile_vis[w * nt + t] > 0;
   if (!touched) return;
   const int64_t tx = t % ntx, ty = t / ntx;
   const int64_t tx1 = tx + 1 < ntx ? tx + 1 : 0, ty1 = ty + 1 < nty ? ty + 1 : 0;
-  mask[ty * ntx + tx] = 1;  // idempotent stores: no atomics needed
-  mask[ty * ntx + tx1] = 1;
-  mask[ty1 * ntx + tx] = 1;
-  mask[ty1 * ntx + tx1] = 1;
+  uint8_t* m = mask + p * nt;
+  m[ty * ntx + tx] = 1;  // idempotent stores: no atomics needed
+  m[ty * ntx + tx1] = 1;
+  m[ty1 * ntx + tx] = 1;
+  m[ty1 * ntx + tx1] = 1;
 }
 
 // bit-pack the byte mask: bit tx % 32 of word ty * (ntx / 32) + tx / 32
@@ -537,12 +547,14 @@ __global__ void pack_mask_kernel(const uint8_t* __restrict__ mask, int64_t nword
   bits[wd] = b;
 }
 
-hipError_t launch_dirty_mask(const int64_t* tile_vis, int64_t ntx, int64_t nty, int64_t ntw, uint8_t* mask,
-                             uint32_t* bits, hipStream_t s) {
-  dirty_mask_kernel<<<dim3((unsigned)((ntx * nty + 255) / 256)), dim3(256), 0, s>>>(tile_vis, ntx, nty, ntw, mask);
+hipError_t launch_dirty_mask(const int64_t* tile_vis, int64_t ntx, int64_t nty, int64_t ntw, int support,
+                             int64_t nplanes, uint8_t* mask, uint32_t* bits, hipStream_t s) {
+  const int64_t n = ntx * nty * nplanes;
+  dirty_mask_kernel<<<dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s>>>(tile_vis, ntx, nty, ntw, support,
+                                                                           nplanes, mask);
   if (bits) {
     if (ntx % 32 != 0) return hipErrorInvalidValue;
-    const int64_t nw = ntx * nty / 32;
+    const int64_t nw = n / 32;
     pack_mask_kernel<<<dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, s>>>(mask, nw, bits);
   }
   return hipGetLastError();
