@@ -21,11 +21,11 @@ namespace cip {
 // (ds_add_u64: 8 CU-cycles/wave-instruction vs 16 for ds_add_f64 measured on
 // gfx950, tools/microbench/lds_ops.hip). Integer sums are exact and
 // order-independent; a chunk holds <= kChunkVis visibilities so a cell sum
-// stays below 2^61.
+// stays below 2^60.
 constexpr double kMagic = 6755399441055744.0;  // 1.5 * 2^52
 constexpr uint32_t kMagicHi = 0x43380000u;      // high word of kMagic
 constexpr int kFixedBits = 46;
-constexpr int64_t kChunkVis = 32768;
+constexpr int64_t kChunkVis = 16384;  // 16384 vs 32768: 2 % less scatter tail at C3 (tools/sweep_cv.sh)
 
 // Packed single-precision class (complex64 input, ducc0's float gridding):
 // (re, im) of a cell share ONE 64-bit integer, re * 2^32 + im, so a

@@ -1,7 +1,7 @@
 #!/bin/bash
 set -o pipefail
 mkdir -p gpurun_out; rm -f gpurun_out/sweep.txt
-for cv in 32768 8192 2048 1024; do
-  CIP_CHUNK_VIS=$cv timeout -k 10 200 python bench.py --no-cpu-baseline --steps 3 --warmup 1 > gpurun_out/cv_$cv.json 2>/dev/null || exit 1
+for cv in 32768 16384 8192 4096; do
+  CIP_CHUNK_VIS=$cv timeout -k 10 200 python bench.py --no-cpu-baseline --steps 10 --warmup 10 > gpurun_out/cv_$cv.json 2>/dev/null || exit 1
   python -c "import json; d=json.load(open('gpurun_out/cv_$cv.json')); print('cv', $cv, d['phases_ms'])" >> gpurun_out/sweep.txt
 done
