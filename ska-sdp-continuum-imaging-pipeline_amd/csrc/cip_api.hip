@@ -454,6 +454,16 @@ static bool grid_mask() {
   return on;
 }
 
+// CIP_CHUNK_ORDER=tile: 2-D work units in tile order instead of full chunks
+// first (A/B experiments)
+static bool chunks_full_first() {
+  static const bool on = [] {
+    const char* e = getenv("CIP_CHUNK_ORDER");
+    return !(e && std::strcmp(e, "tile") == 0);
+  }();
+  return on;
+}
+
 // CIP_SCATTER_ORDER=0 skips the bank-class order (A/B experiments)
 static bool scatter_order() {
   static const bool on = [] {
@@ -473,7 +483,7 @@ static int make_plan(Workspace* ws, const double* uvw, const double* fx, const R
   CIP_ALLOC(tile_runs, int64_t, "tile_runs", ntiles + 1)
   CIP_ALLOC(tile_vis, int64_t, "tile_vis", ntiles + 1)
   CIP_ALLOC(tile_vis_off, int64_t, "tile_vis_off", ntiles + 1)
-  CIP_ALLOC(chunk_off, int64_t, "chunk_off", ntiles + 1)
+  CIP_ALLOC(chunk_off, int64_t, "chunk_off", 2 * ntiles + 1)
   CIP_ALLOC(err, unsigned, "err_flag", 1)
   CIP_ALLOC(scan_tmp, int64_t, "scan_tmp", scan_tmp_elems(ntiles + 1))
   CIP_HIP_CHECK(hipMemsetAsync(err, 0, sizeof(unsigned), s));
@@ -546,16 +556,22 @@ static int make_plan(Workspace* ws, const double* uvw, const double* fx, const R
     CIP_HIP_CHECK(launch_dirty_mask(tile_vis, g.ntx, g.nty, g.ntw, g.support, g.nplanes, dmask, dbits, s));
     pr->dmask = dbits;
   }
-  CIP_HIP_CHECK(launch_chunk_counts(tile_vis, ntiles, cv, chunk_off, s));
-  CIP_HIP_CHECK(exclusive_scan_i64(chunk_off, ntiles + 1, scan_tmp, s));
+  // 2-D: the scatter's work units largest first (one tile layer, so the
+  // plane's chunk range stays contiguous); w-stacking: tile order (each plane
+  // takes the chunks of its tile layers)
+  const int full_first = (g.ntw == 1 && chunks_full_first()) ? 1 : 0;
+  const int64_t nent = full_first ? 2 * ntiles : ntiles;
+  CIP_ALLOC(scan_tmpc, int64_t, "scan_tmp_chunks", scan_tmp_elems(2 * ntiles + 1))
+  CIP_HIP_CHECK(launch_chunk_counts(tile_vis, ntiles, cv, full_first, chunk_off, s));
+  CIP_HIP_CHECK(exclusive_scan_i64(chunk_off, nent + 1, scan_tmpc, s));
   // chunk offsets of each w tile layer
-  const int64_t layer = g.ntx * g.nty;
+  const int64_t layer = full_first ? nent : g.ntx * g.nty;
   CIP_ALLOC(layer_off, int64_t, "layer_off", g.ntw + 1)
   CIP_HIP_CHECK(launch_gather_i64(chunk_off, layer, g.ntw + 1, layer_off, s));
   // bank-class ordering windows: the same split with kOrderWindow
   CIP_ALLOC(win_off, int64_t, "win_off", ntiles + 1)
   if (order) {
-    CIP_HIP_CHECK(launch_chunk_counts(tile_vis, ntiles, kOrderWindow, win_off, s));
+    CIP_HIP_CHECK(launch_chunk_counts(tile_vis, ntiles, kOrderWindow, 0, win_off, s));
     CIP_HIP_CHECK(exclusive_scan_i64(win_off, ntiles + 1, scan_tmp, s));
   }
   int64_t* hl = (int64_t*)pinned(ws, sizeof(int64_t) * (g.ntw + 2));
@@ -567,15 +583,15 @@ static int make_plan(Workspace* ws, const double* uvw, const double* fx, const R
   const int64_t nwin = order ? hl[g.ntw + 1] : 0;
   pr->nchunks = pr->plane_chunk_off.back();
   CIP_ALLOC(chunks, Chunk, "chunks", pr->nchunks)
-  CIP_HIP_CHECK(launch_chunk_emit(tile_vis_off, tile_vis, chunk_off, run_goff, tile_runs, ntiles, cv, pr->nchunks,
-                                  chunks, s));
+  CIP_HIP_CHECK(launch_chunk_emit(tile_vis_off, tile_vis, chunk_off, run_goff, tile_runs, ntiles, cv, full_first,
+                                  pr->nchunks, chunks, s));
   pr->runs = runs;
   pr->run_goff = run_goff;
   pr->tile_run_off = tile_runs;
   pr->chunks = chunks;
   if (order && nwin > 0) {
     CIP_ALLOC(windows, Chunk, "windows", nwin)
-    CIP_HIP_CHECK(launch_chunk_emit(tile_vis_off, tile_vis, win_off, run_goff, tile_runs, ntiles, kOrderWindow, nwin,
+    CIP_HIP_CHECK(launch_chunk_emit(tile_vis_off, tile_vis, win_off, run_goff, tile_runs, ntiles, kOrderWindow, 0, nwin,
                                     windows, s));
     CIP_ALLOC(perm, uint32_t, "perm", nvis)
     CIP_HIP_CHECK(launch_order(uvw, fx, vis_class, g, m, runs, run_goff, tile_runs, windows, nwin, perm, s));

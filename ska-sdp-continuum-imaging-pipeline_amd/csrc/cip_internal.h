@@ -72,11 +72,13 @@ hipError_t launch_dirty_mask(const int64_t* tile_vis, int64_t ntx, int64_t nty, 
 hipError_t launch_tile_vis(const int64_t* run_goff, const int64_t* tile_run_off, int64_t ntiles,
                            int64_t* tile_vis_off, int64_t* tile_vis, hipStream_t s);
 hipError_t launch_run_lengths(const uint64_t* runs, int64_t nruns, int64_t* out, hipStream_t s);
-hipError_t launch_chunk_counts(const int64_t* tile_vis, int64_t ntiles, int64_t chunk_vis,
+// full_first: full chunks of every tile before the partial ones (chunk_off
+// then has 2 ntiles + 1 entries), else per tile in tile order (ntiles + 1)
+hipError_t launch_chunk_counts(const int64_t* tile_vis, int64_t ntiles, int64_t chunk_vis, int full_first,
                                int64_t* out, hipStream_t s);
 hipError_t launch_chunk_emit(const int64_t* tile_vis_off, const int64_t* tile_vis, const int64_t* chunk_off,
                              const int64_t* run_goff, const int64_t* tile_run_off, int64_t ntiles,
-                             int64_t chunk_vis, int64_t nchunks, Chunk* chunks, hipStream_t s);
+                             int64_t chunk_vis, int full_first, int64_t nchunks, Chunk* chunks, hipStream_t s);
 hipError_t launch_gather_i64(const int64_t* src, int64_t stride, int64_t count, int64_t* dst,
                              hipStream_t s);
 

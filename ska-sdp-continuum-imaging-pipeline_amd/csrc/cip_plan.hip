@@ -567,36 +567,55 @@ hipError_t launch_tile_vis(const int64_t* run_goff, const int64_t* tile_run_off,
   return hipGetLastError();
 }
 
-__global__ void chunk_counts_kernel(const int64_t* tile_vis, int64_t ntiles, int64_t cv, int64_t* out) {
+// Chunks per tile: out[t] = ceil(tile_vis[t] / cv), out[ntiles] = 0. With
+// full_first (largest work units first: a 2-D scatter dispatch then ends on
+// the small ones, not on a full chunk that started late), full and partial
+// chunks are counted separately: out[t] = tile_vis[t] / cv, out[ntiles + t] =
+// 1 if a partial remainder exists, out[2 ntiles] = 0 - the exclusive scan then
+// places every full chunk before every partial one.
+__global__ void chunk_counts_kernel(const int64_t* tile_vis, int64_t ntiles, int64_t cv, int full_first,
+                                    int64_t* out) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t < ntiles) out[t] = (tile_vis[t] + cv - 1) / cv;
-  else if (t == ntiles) out[t] = 0;
+  if (!full_first) {
+    if (t < ntiles) out[t] = (tile_vis[t] + cv - 1) / cv;
+    else if (t == ntiles) out[t] = 0;
+    return;
+  }
+  if (t < ntiles) {
+    out[t] = tile_vis[t] / cv;
+    out[ntiles + t] = (tile_vis[t] % cv) != 0 ? 1 : 0;
+  } else if (t == ntiles) {
+    out[2 * ntiles] = 0;
+  }
 }
 
-hipError_t launch_chunk_counts(const int64_t* tile_vis, int64_t ntiles, int64_t chunk_vis, int64_t* out,
-                               hipStream_t s) {
+hipError_t launch_chunk_counts(const int64_t* tile_vis, int64_t ntiles, int64_t chunk_vis, int full_first,
+                               int64_t* out, hipStream_t s) {
   chunk_counts_kernel<<<dim3((unsigned)((ntiles + 256) / 256)), dim3(256), 0, s>>>(tile_vis, ntiles, chunk_vis,
-                                                                                   out);
+                                                                                   full_first, out);
   return hipGetLastError();
 }
 
-// One thread per chunk j: its tile t is the last with chunk_off[t] <= j
-// (tiles without chunks repeat an offset), then k = j - chunk_off[t] and the
-// chunk's first run by binary search among the tile's runs.
+// One thread per chunk j: its entry e is the last with chunk_off[e] <= j
+// (entries without chunks repeat an offset); entry e < ntiles is tile e's
+// chunk k = j - chunk_off[e], entry ntiles + t (full_first) tile t's partial
+// chunk k = tile_vis[t] / cv. The chunk's first and last runs by binary search
+// among the tile's runs.
 __global__ void chunk_emit_kernel(const int64_t* __restrict__ tile_vis_off, const int64_t* __restrict__ tile_vis,
                                   const int64_t* __restrict__ chunk_off, const int64_t* __restrict__ run_goff,
                                   const int64_t* __restrict__ tile_run_off, int64_t ntiles, int64_t cv,
-                                  int64_t nchunks, Chunk* __restrict__ chunks) {
+                                  int full_first, int64_t nchunks, Chunk* __restrict__ chunks) {
   const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= nchunks) return;
-  int64_t lo = 0, hi = ntiles - 1;
+  int64_t lo = 0, hi = (full_first ? 2 * ntiles : ntiles) - 1;
   while (lo < hi) {
     const int64_t mid = (lo + hi + 1) >> 1;
     if (chunk_off[mid] <= j) lo = mid;
     else hi = mid - 1;
   }
-  const int64_t t = lo;
-  const int64_t k = j - chunk_off[t];
+  const bool partial = lo >= ntiles;
+  const int64_t t = partial ? lo - ntiles : lo;
+  const int64_t k = partial ? tile_vis[t] / cv : j - chunk_off[lo];
   const int64_t g = tile_vis_off[t], nv = tile_vis[t];
   Chunk ch;
   ch.g0 = g + k * cv;
@@ -623,10 +642,10 @@ __global__ void chunk_emit_kernel(const int64_t* __restrict__ tile_vis_off, cons
 
 hipError_t launch_chunk_emit(const int64_t* tile_vis_off, const int64_t* tile_vis, const int64_t* chunk_off,
                              const int64_t* run_goff, const int64_t* tile_run_off, int64_t ntiles,
-                             int64_t chunk_vis, int64_t nchunks, Chunk* chunks, hipStream_t s) {
+                             int64_t chunk_vis, int full_first, int64_t nchunks, Chunk* chunks, hipStream_t s) {
   if (nchunks <= 0) return hipSuccess;
   chunk_emit_kernel<<<dim3((unsigned)((nchunks + 255) / 256)), dim3(256), 0, s>>>(
-      tile_vis_off, tile_vis, chunk_off, run_goff, tile_run_off, ntiles, chunk_vis, nchunks, chunks);
+      tile_vis_off, tile_vis, chunk_off, run_goff, tile_run_off, ntiles, chunk_vis, full_first, nchunks, chunks);
   return hipGetLastError();
 }
 
