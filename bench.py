@@ -134,6 +134,9 @@ def main():
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--support", type=int, default=8)
     ap.add_argument("--wstacking", action="store_true", help="w-stacking mode (secondary measurement)")
+    ap.add_argument("--single", action="store_true",
+                    help="packed single-precision accumulation class (CIP_ACC_SINGLE; the precision class of the "
+                         "reference's float32 ducc0 call) - secondary measurement, not the f64 metric")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-rows", type=int, default=8192)
     args = ap.parse_args()
@@ -171,7 +174,8 @@ def main():
             pending[k].wait()
         dirty, sumw = bufs[k]
         gridder.device_ms2dirty(uvw_d, freq_d, vis_d, wgt_d, npix, npix, px, px, support=args.support,
-                                do_wstacking=args.wstacking, out=dirty, sum_weights=sumw)
+                                do_wstacking=args.wstacking, out=dirty, sum_weights=sumw,
+                                single_precision_accumulation=args.single)
         # RCCL reduce of the partial images + weights to rank 0, normalised there
         pending[k] = reduce_images(dirty, sumw, dst=0, async_op=True)
 
@@ -188,7 +192,8 @@ def main():
     drain()
     dirty, sumw = bufs[0]
     _, params = gridder.device_ms2dirty(uvw_d, freq_d, vis_d, wgt_d, npix, npix, px, px, support=args.support,
-                                        do_wstacking=args.wstacking, out=dirty, sum_weights=sumw)
+                                        do_wstacking=args.wstacking, out=dirty, sum_weights=sumw,
+                                        single_precision_accumulation=args.single)
     _lib.profile_enable(True)
     phases = []
     if world > 1:
@@ -240,12 +245,13 @@ def main():
     # a 64-bit fixed-point add to the re and the im plane (16 B of LDS RMW),
     # and gfx950 sustains one conflict-free 64-lane ds_add_u64 per 8.12
     # CU-cycles (tools/microbench/lds_ops.hip, profiles/microbench_r01.txt).
-    lds_bytes = vis_per_launch * params.support ** 2 * 16
+    lds_bytes = vis_per_launch * params.support ** 2 * (8 if args.single else 16)  # packed: one u64 per tap
     lds_peak = 64 * 8 / 8.12 * 2.4e9 * 256 / 1e9  # GB/s: 256 CUs at 2.4 GHz
     lds_achieved = lds_bytes / (scatter_ms * 1e-3) / 1e9
     roofline["lds_atomic"] = {"achieved": round(lds_achieved, 1), "peak": round(lds_peak, 1), "unit": "GB/s",
                               "frac": round(lds_achieved / lds_peak, 4),
-                              "basis": "16 B of ds_add_u64 per tap; 8.12 CU-cycles per conflict-free wave-instr"}
+                              "basis": f"{8 if args.single else 16} B of ds_add_u64 per tap; 8.12 CU-cycles per "
+                                       "conflict-free wave-instr"}
     tr = traffic_from_profiles(args.config)
     if tr and not args.wstacking:
         roofline["traffic"] = tr.get("hbm_bytes_per_launch")
@@ -261,7 +267,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f64",
+        "dtype": "f32-class (packed 2x32-bit)" if args.single else "f64",
         "data": "synthetic (seeded MeerKAT-like uvw tracks, random complex64 vis, float32 weights, 5% flagged)",
         "config": {
             "workload": (f"{args.config.upper()}: {cfg['rows']:,} rows x {cfg['nchan']} ch = {nvis:,} vis/GPU -> "
