@@ -18,7 +18,8 @@
  *                         run search, uvw_tiling/tiling_plan.py:29-61,150-181
  *   cip_stokes_i       <- StokesIGridderInput.from_measurement_set_reader +
  *                         effective_weights, invert.py:72-116
- *   cip_release_workspace - frees the per-device workspace cache (no reference
+ *   cip_release_workspace - frees the calling thread's workspace cache on the
+ *                         current device (no reference
  *                         counterpart; ducc allocates per call).
  *   cip_profile_*      <- observability of the hot path (the reference's
  *                         dask task stream, task_metrics.py:88-135).
@@ -199,7 +200,9 @@ int cip_release_collectives(void);
 /* Last error message of the calling thread ("" if none). */
 const char* cip_last_error(void);
 
-/* Free the workspace cached for the current device. */
+/* Free the calling thread's workspace cached for the current device
+ * (workspaces are per device and host thread: two threads may each run
+ * calls on their own stream, on one GPU, without sharing buffers). */
 int cip_release_workspace(void);
 
 /* Per-phase timing of cip_ms2dirty / cip_grid_plane on the calling thread

@@ -8,6 +8,7 @@
 #include <cstring>
 #include <map>
 #include <mutex>
+#include <thread>
 #include <string>
 #include <vector>
 
@@ -302,16 +303,20 @@ static int join_side(Workspace* ws, hipStream_t s) {
 }
 
 static std::mutex g_ws_mutex;
-static std::map<int, Workspace*> g_ws;
+// One workspace per (device, host thread): calls from different threads (e.g.
+// two inverts in flight on one GPU, each thread on its own stream) never
+// share buffers, the side stream or the clean-grid state.
+static std::map<std::pair<int, std::thread::id>, Workspace*> g_ws;
 
 static Workspace* workspace() {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  const auto key = std::make_pair(dev, std::this_thread::get_id());
   std::lock_guard<std::mutex> lock(g_ws_mutex);
-  auto it = g_ws.find(dev);
+  auto it = g_ws.find(key);
   if (it != g_ws.end()) return it->second;
   Workspace* ws = new Workspace();
-  g_ws[dev] = ws;
+  g_ws[key] = ws;
   return ws;
 }
 
@@ -1200,7 +1205,7 @@ int cip_release_workspace(void) {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return set_error(CIP_EHIP, "no HIP device");
   std::lock_guard<std::mutex> lock(g_ws_mutex);
-  auto it = g_ws.find(dev);
+  auto it = g_ws.find(std::make_pair(dev, std::this_thread::get_id()));
   if (it == g_ws.end()) return CIP_OK;
   Workspace* ws = it->second;
   for (auto& kv : ws->bufs)
