@@ -489,9 +489,8 @@ static int make_plan(Workspace* ws, const double* uvw, const double* fx, const R
   CIP_ALLOC(tile_vis, int64_t, "tile_vis", ntiles + 1)
   CIP_ALLOC(tile_vis_off, int64_t, "tile_vis_off", ntiles + 1)
   CIP_ALLOC(chunk_off, int64_t, "chunk_off", 2 * ntiles + 1)
-  CIP_ALLOC(err, unsigned, "err_flag", 1)
+  CIP_ALLOC(err, unsigned, "err_flag", 1)  // cleared by prepare() before the frequency check
   CIP_ALLOC(scan_tmp, int64_t, "scan_tmp", scan_tmp_elems(ntiles + 1))
-  CIP_HIP_CHECK(hipMemsetAsync(err, 0, sizeof(unsigned), s));
   const int64_t nvis = m.nvis;
   const int nblk = plan_place_blocks(nvis);
   // the bank-class order needs a 32-bit flattened index (larger inputs grid in
@@ -525,6 +524,7 @@ static int make_plan(Workspace* ws, const double* uvw, const double* fx, const R
   const int64_t nruns = h[0];
   const unsigned errbits = (unsigned)h[1];
   std::memcpy(maxabs, &h[2], sizeof(double));
+  if (errbits & 4u) return set_error(CIP_EINVAL, "channel frequencies must be positive");
   if (errbits & 2u) return set_error(CIP_EINVAL, "non-finite visibility or weight");
   if (errbits & 1u)
     return set_error(CIP_ERANGE, "non-finite (u, v, w) coordinates, or w outside the w-plane stack");
@@ -640,17 +640,28 @@ static int prepare(Workspace* ws, const double* uvw, int64_t nrow, const double*
   if (nrow >= ((int64_t)1 << 32)) return set_error(CIP_EINVAL, "nrow must be < 2^32");
   CIP_ALLOC(fx, double, "fx", nchan)
   CIP_ALLOC(red, double, "red", 4)
-  CIP_HIP_CHECK(launch_freq_scale(freq, nchan, fx, s));
-  double* h = (double*)pinned(ws, sizeof(double) * (4 + (size_t)nchan));
-  if (!h) return set_error(CIP_ENOMEM, "hipHostMalloc failed");
-  CIP_HIP_CHECK(hipMemcpyAsync(h + 4, fx, sizeof(double) * nchan, hipMemcpyDeviceToHost, s));
-  CIP_HIP_CHECK(hipStreamSynchronize(s));
-  double fxmin = h[4], fxmax = h[4];
-  for (int64_t c = 1; c < nchan; ++c) {
-    fxmin = std::fmin(fxmin, h[4 + c]);
-    fxmax = std::fmax(fxmax, h[4 + c]);
+  // the planner's error bits: cleared here, read back with the run count
+  CIP_ALLOC(err, unsigned, "err_flag", 1)
+  CIP_HIP_CHECK(hipMemsetAsync(err, 0, sizeof(unsigned), s));
+  CIP_HIP_CHECK(launch_freq_scale(freq, nchan, fx, err, s));
+  // the frequency range on the host only where the w range needs it (the
+  // positivity check otherwise travels as error bit 2 to the planner's
+  // readback: one host synchronisation less per 2-D call)
+  const bool host_fx = nrow == 0 || (do_wstacking && given == nullptr);
+  double fxmin = 0.0, fxmax = 0.0;
+  if (host_fx) {
+    double* h = (double*)pinned(ws, sizeof(double) * (4 + (size_t)nchan));
+    if (!h) return set_error(CIP_ENOMEM, "hipHostMalloc failed");
+    CIP_HIP_CHECK(hipMemcpyAsync(h + 4, fx, sizeof(double) * nchan, hipMemcpyDeviceToHost, s));
+    CIP_HIP_CHECK(hipStreamSynchronize(s));
+    fxmin = h[4];
+    fxmax = h[4];
+    for (int64_t c = 1; c < nchan; ++c) {
+      fxmin = std::fmin(fxmin, h[4 + c]);
+      fxmax = std::fmax(fxmax, h[4 + c]);
+    }
+    if (!(fxmin > 0.0) || !std::isfinite(fxmax)) return set_error(CIP_EINVAL, "channel frequencies must be positive");
   }
-  if (!(fxmin > 0.0)) return set_error(CIP_EINVAL, "channel frequencies must be positive");
   RowMap& m = out->m;
   m.nchan = nchan;
   m.inv_nchan = 1.0 / (double)nchan;

@@ -30,7 +30,8 @@ hipError_t scan_run_offsets(const uint64_t* runs, int64_t nruns, int64_t* run_go
 hipError_t exclusive_scan_i64(int64_t* data, int64_t n, int64_t* tmp, hipStream_t s);
 
 // ---- gridder planner (cip_plan.hip) ----------------------------------------
-hipError_t launch_freq_scale(const double* freq, int64_t nchan, double* fx, hipStream_t s);
+// err (may be NULL): bit 2 set when a frequency is not finite and positive
+hipError_t launch_freq_scale(const double* freq, int64_t nchan, double* fx, unsigned* err, hipStream_t s);
 // per-row w range over channels (only f min/max matter): out[0]=min, out[1]=max
 hipError_t launch_w_range(const double* uvw, int64_t nrow, double fxmin, double fxmax, double* partial,
                           int nblocks, hipStream_t s);

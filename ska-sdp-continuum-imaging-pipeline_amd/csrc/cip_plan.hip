@@ -108,13 +108,18 @@ hipError_t scan_run_offsets(const uint64_t* runs, int64_t nruns, int64_t* run_go
 }
 
 // ------------------------------------------------------------ helpers ----
-__global__ void freq_scale_kernel(const double* freq, int64_t nchan, double* fx) {
+// fx = f / c; err bit 2 (value 4) when a frequency is not finite and positive
+__global__ void freq_scale_kernel(const double* freq, int64_t nchan, double* fx, unsigned* err) {
   const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (c < nchan) fx[c] = freq[c] / CIP_SPEED_OF_LIGHT;
+  if (c < nchan) {
+    const double f = freq[c];
+    fx[c] = f / CIP_SPEED_OF_LIGHT;
+    if (err && !(f > 0.0 && isfinite(f))) atomicOr(err, 4u);
+  }
 }
 
-hipError_t launch_freq_scale(const double* freq, int64_t nchan, double* fx, hipStream_t s) {
-  freq_scale_kernel<<<dim3((unsigned)((nchan + 255) / 256)), dim3(256), 0, s>>>(freq, nchan, fx);
+hipError_t launch_freq_scale(const double* freq, int64_t nchan, double* fx, unsigned* err, hipStream_t s) {
+  freq_scale_kernel<<<dim3((unsigned)((nchan + 255) / 256)), dim3(256), 0, s>>>(freq, nchan, fx, err);
   return hipGetLastError();
 }
 

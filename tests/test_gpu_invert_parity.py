@@ -213,6 +213,16 @@ def test_bad_arguments_raise(gpu_device):
         gridder.ms2dirty(uvw, f, vis, w, 64, 64, px, px, support=7)
     with pytest.raises(ValueError):
         gridder.ms2dirty(uvw, f, vis[:, :0], w[:, :0], 64, 64, px, px)
+    # non-positive / non-finite frequencies: caught on the host (w-stacking
+    # needs the range there) or by the device check (2-D), the same error
+    for bad in (0.0, -1.0e9, np.nan):
+        fb = f.copy()
+        fb[0] = bad
+        for ws in (False, True):
+            with pytest.raises(ValueError, match="frequencies"):
+                gridder.ms2dirty(uvw, fb, vis, w, 64, 64, px, px, do_wstacking=ws)
+    # and a later call with good input is unaffected
+    assert np.isfinite(gridder.ms2dirty(uvw, f, vis, w, 64, 64, px, px)).all()
 
 
 def test_zero_rows_gives_zero_image(gpu_device):
