@@ -169,8 +169,11 @@ hipError_t launch_w_range(const double* uvw, int64_t nrow, double fxmin, double 
 constexpr int kPlaceSegs = 64;  // 64-visibility segments per place block (4096 visibilities)
 constexpr uint32_t kNoKey = 0xffffffffu;  // visibility off the grid (tile keys are < 2^32 - 1)
 
+#ifndef CIP_PLACE_WAVES
+#define CIP_PLACE_WAVES 1  // min waves per SIMD the place pass is compiled for
+#endif
 template <typename VisT, int WK>
-__global__ __launch_bounds__(256) void plan_place_kernel(const double* __restrict__ uvw,
+__global__ __launch_bounds__(256, CIP_PLACE_WAVES) void plan_place_kernel(const double* __restrict__ uvw,
                                                          const double* __restrict__ fx, RowMap m,
                                                          const VisT* __restrict__ vis, const void* __restrict__ wgt,
                                                          GridGeometry g, unsigned* err_flag,
@@ -217,10 +220,12 @@ __global__ __launch_bounds__(256) void plan_place_kernel(const double* __restric
     }
     bool bad = false;
     if (valid) {
+      // position loads first: the visibility load of a PSF call is a branch,
+      // and the wait inside it then covers every load (one memory round trip)
+      const double u = uvw[3 * r], v = uvw[3 * r + 1], w = uvw[3 * r + 2], f = fx[c];
       const double wt = load_weight<WK>(wgt, i);
       double vr, vi;
       load_vis(vis, i, vr, vi);
-      const double u = uvw[3 * r], v = uvw[3 * r + 1], w = uvw[3 * r + 2], f = fx[c];
       // zero-weight visibilities are skipped by the scatter, whatever they hold
       const double a = wt == 0.0 ? 0.0 : fabs(wt) * fmax(fabs(vr), fabs(vi));
       nonfinite = nonfinite || (wt != 0.0 && !(isfinite(wt) && isfinite(vr) && isfinite(vi)));
