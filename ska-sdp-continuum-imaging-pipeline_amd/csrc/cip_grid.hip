@@ -315,22 +315,32 @@ __global__ __launch_bounds__(kOrderThreads, 8) void order_kernel(const double* _
   __syncthreads();
   uint32_t packed[kOrderPer];
   unsigned cls[kOrderPer], rk[kOrderPer];
+  int slice[kOrderPer];
+  int64_t chan[kOrderPer];
+  // indices first, then the class loads back to back: one memory round trip
+  // for the thread's positions instead of one each
 #pragma unroll
   for (int k = 0; k < kOrderPer; ++k) {
     const int qi = threadIdx.x + k * kOrderThreads;
-    cls[k] = 32u;
     if (qi < nsb) {
       const int lo = s_idx[qi];
       const uint64_t rec = s_rec[lo];
       const int64_t row = (int64_t)(rec >> 32);
       const int64_t c = (int64_t)((rec >> 16) & 0xffff) + (qi - s_off[lo]);
-      const int64_t idx = vis_index(m, row, c);
-      packed[k] = (uint32_t)idx;
+      packed[k] = (uint32_t)vis_index(m, row, c);
+      slice[k] = lo;
+      chan[k] = c;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < kOrderPer; ++k) {
+    cls[k] = 32u;
+    if (threadIdx.x + k * kOrderThreads < nsb) {
       if constexpr (GATHER) {
-        cls[k] = vis_class[idx];
+        cls[k] = vis_class[packed[k]];
       } else {
-        const double2 uv = s_uv[lo];
-        cls[k] = origin_class(uv.x, uv.y, fx[c], g);
+        const double2 uv = s_uv[slice[k]];
+        cls[k] = origin_class(uv.x, uv.y, fx[chan[k]], g);
       }
     }
   }

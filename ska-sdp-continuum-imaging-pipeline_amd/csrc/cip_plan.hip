@@ -22,19 +22,34 @@ __global__ __launch_bounds__(kScanThreads) void scan_local_kernel(int64_t* data,
   const int64_t base = (int64_t)blockIdx.x * kScanBlock + (int64_t)threadIdx.x * kScanItems;
   int64_t v[kScanItems];
   int64_t tsum = 0;
+  // threads with all their items in range load them unconditionally (the
+  // loads issue back to back; a per-item branch waits for each in turn)
+  if (base + kScanItems <= (RUNS ? n - 1 : n)) {
 #pragma unroll
-  for (int i = 0; i < kScanItems; ++i) {
-    if constexpr (RUNS) {
-      v[i] = 0;
-      if (base + i < n - 1) {
+    for (int i = 0; i < kScanItems; ++i) {
+      if constexpr (RUNS) {
         const uint64_t rec = runs[base + i];
         v[i] = (int64_t)(rec & 0xffff) - (int64_t)((rec >> 16) & 0xffff);
+      } else {
+        v[i] = data[base + i];
       }
-    } else {
-      v[i] = (base + i < n) ? data[base + i] : 0;
     }
-    tsum += v[i];
+  } else {
+#pragma unroll
+    for (int i = 0; i < kScanItems; ++i) {
+      if constexpr (RUNS) {
+        v[i] = 0;
+        if (base + i < n - 1) {
+          const uint64_t rec = runs[base + i];
+          v[i] = (int64_t)(rec & 0xffff) - (int64_t)((rec >> 16) & 0xffff);
+        }
+      } else {
+        v[i] = (base + i < n) ? data[base + i] : 0;
+      }
+    }
   }
+#pragma unroll
+  for (int i = 0; i < kScanItems; ++i) tsum += v[i];
   // inclusive wave scan of the thread sums
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   int64_t incl = tsum;
@@ -67,6 +82,14 @@ __global__ __launch_bounds__(kScanThreads) void scan_local_kernel(int64_t* data,
 __global__ void scan_add_kernel(int64_t* data, int64_t n, const int64_t* offsets) {
   const int64_t i = (int64_t)blockIdx.x * kScanBlock + threadIdx.x;
   const int64_t off = offsets[blockIdx.x];
+  if (i + (int64_t)(kScanItems - 1) * kScanThreads < n) {
+    int64_t v[kScanItems];
+#pragma unroll
+    for (int k = 0; k < kScanItems; ++k) v[k] = data[i + (int64_t)k * kScanThreads];
+#pragma unroll
+    for (int k = 0; k < kScanItems; ++k) data[i + (int64_t)k * kScanThreads] = v[k] + off;
+    return;
+  }
 #pragma unroll
   for (int k = 0; k < kScanItems; ++k) {
     const int64_t j = i + (int64_t)k * kScanThreads;
