@@ -34,6 +34,18 @@ namespace cip {
 __global__ __launch_bounds__(1024) void prep_final_kernel(const double* partial, int nblocks, double* out2) {
   double sum[4] = {0.0, 0.0, 0.0, 0.0}, mx = 0.0;
   for (int i0 = threadIdx.x; i0 < nblocks; i0 += 4 * 1024) {
+    if (i0 + 3 * 1024 < nblocks) {
+      // all 4 in range: the loads issue back to back (same order of sums)
+      double2 p[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) p[k] = reinterpret_cast<const double2*>(partial)[i0 + k * 1024];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        sum[k] += p[k].x;
+        mx = fmax(mx, p[k].y);
+      }
+      continue;
+    }
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const int i = i0 + k * 1024;

@@ -407,7 +407,16 @@ __global__ __launch_bounds__(kRadixThreads) void radix_hist_kernel(const uint32_
   __syncthreads();
   const int64_t cnt_b = radix_count(blockIdx.x, n, blk_cnt);
   const uint32_t* kb = keys + (int64_t)blockIdx.x * kRadixBlock;
-  for (int64_t i = threadIdx.x; i < cnt_b; i += kRadixThreads) atomicAdd(&cnt[(kb[i] >> shift) & 255u], 1u);
+  if (cnt_b == kRadixBlock) {
+    // full block: the loads issue back to back (the loop below waits for each)
+    uint32_t kk[kRadixPer];
+#pragma unroll
+    for (int k = 0; k < kRadixPer; ++k) kk[k] = kb[threadIdx.x + k * kRadixThreads];
+#pragma unroll
+    for (int k = 0; k < kRadixPer; ++k) atomicAdd(&cnt[(kk[k] >> shift) & 255u], 1u);
+  } else {
+    for (int64_t i = threadIdx.x; i < cnt_b; i += kRadixThreads) atomicAdd(&cnt[(kb[i] >> shift) & 255u], 1u);
+  }
   __syncthreads();
   hist[(int64_t)threadIdx.x * nblocks + blockIdx.x] = cnt[threadIdx.x];
   if (blockIdx.x == 0 && threadIdx.x == 0) hist[256 * nblocks] = 0;
