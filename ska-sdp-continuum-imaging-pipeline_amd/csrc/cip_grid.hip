@@ -148,6 +148,49 @@ __device__ __forceinline__ void fetch_vis(int64_t q, const int64_t* s_voff, cons
   f.wt = load_weight<WK>(wgt, idx);
 }
 
+// The same, as loaded (complex64 / float32 kept in their own types): the
+// position-ordered path converts only at use, so nothing waits for a load
+// next to it and the loads of position q + 256 stay in flight while q grids.
+template <typename VisT, int WK>
+struct RawFetch {
+  using WT = typename std::conditional<WK == WK_F64, double, float>::type;
+  double u, v, w, fx;
+  VisT vis;
+  WT wt;
+};
+
+// Branch-free loads of MS visibility i (lanes with !ok load element 0; a PSF
+// call, vis == NULL, reads its ignored visibility from uvw[0..1]).
+template <typename VisT, int WK>
+__device__ __forceinline__ void fetch_raw(int64_t i, bool ok, const double* __restrict__ uvw,
+                                          const double* __restrict__ fx, const VisT* __restrict__ vis_ld,
+                                          bool unit_vis, const void* __restrict__ wgt, const RowMap& m,
+                                          RawFetch<VisT, WK>& f) {
+  using WT = typename RawFetch<VisT, WK>::WT;
+  const int64_t il = ok ? i : 0;
+  int64_t r, c;
+  vis_rowchan(m, il, &r, &c);
+  f.u = uvw[3 * r];
+  f.v = uvw[3 * r + 1];
+  f.w = uvw[3 * r + 2];
+  f.fx = fx[c];
+  f.vis = vis_ld[unit_vis ? 0 : il];
+  if constexpr (WK != WK_NONE) f.wt = ((const WT*)wgt)[il];
+}
+
+template <typename VisT, int WK>
+__device__ __forceinline__ VisFetch from_raw(const RawFetch<VisT, WK>& r, bool unit_vis) {
+  VisFetch f;
+  f.u = r.u;
+  f.v = r.v;
+  f.w = r.w;
+  f.fx = r.fx;
+  f.vr = unit_vis ? 1.0 : (double)r.vis.x;
+  f.vi = unit_vis ? 0.0 : (double)r.vis.y;
+  f.wt = WK == WK_NONE ? 1.0 : (double)r.wt;
+  return f;
+}
+
 template <int W, bool WSTACK, bool PACK>
 __device__ __forceinline__ void grid_fetched(const VisFetch& f, const GridGeometry& g, int64_t plane, int64_t X0,
                                              int64_t Y0, double fixed_scale, unsigned long long* sub) {
@@ -416,32 +459,34 @@ __global__ __launch_bounds__(kScatterThreads, CIP_SCATTER_WAVES) void scatter_ke
     inv_scale = 1.0 / fixed_scale;
   }
   if constexpr (PERM) {
-    // bank-class ordered stream (order_kernel); software pipeline: fetch
-    // position q + 256 while gridding q
+    // bank-class ordered stream (order_kernel); software pipeline, two
+    // deep: perm record of q + 512 and data of q + 256 in flight while q grids
     __syncthreads();
+    const bool unit_vis = vis == nullptr;
+    const VisT* vis_ld = unit_vis ? (const VisT*)uvw : vis;
     int64_t q = ch.g0 + threadIdx.x;
     bool have = q < ch.g1;
-    VisFetch cur;
+    RawFetch<VisT, WK> cur;
+    int64_t qn = q + kScatterThreads;
+    bool hn = qn < ch.g1;
+    uint32_t pn = 0;
     if (have) {
-      const int64_t i = (int64_t)perm[q];
-      int64_t r, c;
-      vis_rowchan(m, i, &r, &c);
-      fetch_at<VisT, WK>(r, c, i, uvw, fx, vis, wgt, cur);
+      fetch_raw<VisT, WK>((int64_t)perm[q], true, uvw, fx, vis_ld, unit_vis, wgt, m, cur);
+      pn = perm[hn ? qn : q];
     }
     while (have) {
-      const int64_t qn = q + kScatterThreads;
-      const bool hn = qn < ch.g1;
-      VisFetch nxt;
-      if (hn) {
-        const int64_t i = (int64_t)perm[qn];
-        int64_t r, c;
-        vis_rowchan(m, i, &r, &c);
-        fetch_at<VisT, WK>(r, c, i, uvw, fx, vis, wgt, nxt);
-      }
-      grid_fetched<W, WSTACK, PACK>(cur, g, plane, X0, Y0, fixed_scale, sub);
+      const int64_t qnn = qn + kScatterThreads;
+      const bool hnn = qnn < ch.g1;
+      const uint32_t pnn = perm[hnn ? qnn : q];
+      RawFetch<VisT, WK> nxt;
+      fetch_raw<VisT, WK>((int64_t)pn, hn, uvw, fx, vis_ld, unit_vis, wgt, m, nxt);
+      grid_fetched<W, WSTACK, PACK>(from_raw<VisT, WK>(cur, unit_vis), g, plane, X0, Y0, fixed_scale, sub);
       cur = nxt;
       q = qn;
       have = hn;
+      qn = qnn;
+      hn = hnn;
+      pn = pnn;
     }
   } else {
     const int64_t rb = tile_run_off[t + 1];
