@@ -175,9 +175,10 @@ def main():
         dirty, sumw = bufs[k]
         gridder.device_ms2dirty(uvw_d, freq_d, vis_d, wgt_d, npix, npix, px, px, support=args.support,
                                 do_wstacking=args.wstacking, out=dirty, sum_weights=sumw,
-                                single_precision_accumulation=args.single)
+                                single_precision_accumulation=args.single, normalise=world == 1)
         # RCCL reduce of the partial images + weights to rank 0, normalised there
-        pending[k] = reduce_images(dirty, sumw, dst=0, async_op=True)
+        # (one GPU: the image is already normalised in the FFT epilogue)
+        pending[k] = reduce_images(dirty, sumw, dst=0, async_op=True, normalise=world > 1)
 
     def drain():
         for k in range(2):

@@ -48,6 +48,12 @@ extern "C" {
 
 /* flags of cip_ms2dirty / cip_grid_plane */
 #define CIP_WSTACKING 1  /* w-stacking planes (cip_ms2dirty only; else 2-D) */
+#define CIP_NORMALISE 8  /* cip_ms2dirty only: dirty_out is divided by the
+                          * call's weight sum (the reference's
+                          * (1 / total_weight) * image, invert.py:119-149),
+                          * fused into the pruned FFT's epilogue in 2-D mode.
+                          * sum_wgt_out still receives the raw sum. Not for
+                          * partial images that are reduced across ranks. */
 #define CIP_PSF 4        /* grid unit visibilities (vis ignored, may be NULL):
                           * the point-spread function with the same weights
                           * (cip_ms2dirty, cip_grid_ms, cip_grid_tiles) */

@@ -857,8 +857,10 @@ static int dirty_stage(Workspace* ws, const GridGeometry& g, int64_t npix_x, int
 // dirty_out (overwritten for p == 0, accumulated after it)
 // dmask (pruned FFT only, may be NULL): the grid tiles the scatter wrote; the
 // rest of the grid is zero, and pass A zeroes the masked tiles after reading
+// norm (pruned 2-D path only, may be NULL): device weight sum the image is
+// divided by in pass B's epilogue (CIP_NORMALISE)
 static int plane_to_dirty(const DirtyStage& st, const GridGeometry& g, int64_t p, double* grid, double* dirty_out,
-                          hipStream_t s, const uint32_t* dmask = nullptr) {
+                          hipStream_t s, const uint32_t* dmask = nullptr, const double* norm = nullptr) {
   hipEvent_t f0 = g_prof.mark(s);
   if (st.fast) {
     CIP_HIP_CHECK(launch_fft_rows(grid, g.nu, g.nv, st.npix_x, st.tw_u, st.fft_h, dmask, g.ntx, s));
@@ -870,7 +872,7 @@ static int plane_to_dirty(const DirtyStage& st, const GridGeometry& g, int64_t p
   // pass B carries the crop epilogue: it is booked under "fft"
   if (st.fast)
     CIP_HIP_CHECK(launch_fft_cols(st.fft_h, g.nv, st.npix_x, st.npix_y, st.tw_v, g.do_wstacking ? 1 : 0, dirty_out,
-                                  st.cx, st.cy, st.px, st.py, w_plane, p == 0, s));
+                                  st.cx, st.cy, st.px, st.py, w_plane, p == 0, g.do_wstacking ? nullptr : norm, s));
   hipEvent_t f1 = g_prof.mark(s);
   g_prof.span(3, f0, f1);
   if (st.fast) {
@@ -969,8 +971,10 @@ int cip_ms2dirty(const double* uvw, int64_t nrow, const double* freq, int64_t nc
                  double pixsize_y, double epsilon, int support, int flags, void* hip_stream,
                  double* dirty_out, double* sum_wgt_out, cip_gridder_params* params_out) {
   g_last_error.clear();
-  if (flags & ~(CIP_WSTACKING | CIP_ACC_SINGLE | CIP_PSF)) return set_error(CIP_EINVAL, "unknown flags");
+  if (flags & ~(CIP_WSTACKING | CIP_ACC_SINGLE | CIP_PSF | CIP_NORMALISE))
+    return set_error(CIP_EINVAL, "unknown flags");
   const int do_wstacking = (flags & CIP_WSTACKING) ? 1 : 0;
+  const bool normalise = (flags & CIP_NORMALISE) != 0;
   const bool packed = (flags & CIP_ACC_SINGLE) != 0;
   if (flags & CIP_PSF) {
     vis = nullptr;
@@ -1009,12 +1013,16 @@ int cip_ms2dirty(const double* uvw, int64_t nrow, const double* freq, int64_t nc
   for (int64_t p = 0; p < g.nplanes; ++p) {
     rc = scatter_plane(pp, p, uvw, vis, vis_dtype, wgt, wgt_dtype, st.fast, grid, s, clean);
     if (rc != CIP_OK) return rc;
-    rc = plane_to_dirty(st, g, p, grid, dirty_out, s, dmask ? dmask + p * (g.ntx * g.nty / 32) : nullptr);
+    rc = plane_to_dirty(st, g, p, grid, dirty_out, s, dmask ? dmask + p * (g.ntx * g.nty / 32) : nullptr,
+                        normalise ? pp.red : nullptr);
     if (rc != CIP_OK) return rc;
     clean = dmask != nullptr;
   }
   rc = finish_dirty(ws, st, pp.p, g, dirty_out, s);
   if (rc != CIP_OK) return rc;
+  // fused into pass B on the pruned 2-D path; a separate pass otherwise
+  if (normalise && (!st.fast || g.do_wstacking))
+    CIP_HIP_CHECK(launch_scale_inverse(dirty_out, npix_x * npix_y, pp.red, s));
   if (sum_wgt_out) CIP_HIP_CHECK(hipMemcpyAsync(sum_wgt_out, pp.red, sizeof(double), hipMemcpyDeviceToDevice, s));
   g_prof.span(5, t_start, g_prof.mark(s));
   CIP_HIP_CHECK(hipStreamSynchronize(s));

@@ -241,6 +241,7 @@ struct ColEpilogue {
   const double* cy;
   double px, py, w_plane;
   int first;
+  const double* norm;  // MODE 0: divide by *norm (the weight sum), NULL = no
 };
 
 template <int N, int MODE>
@@ -261,6 +262,7 @@ __global__ __launch_bounds__(N / 16) void fft_cols_kernel(const double2* __restr
   fft_core<N>(v, t, lds, tw);
   const int64_t p = i - nx / 2;
   double* orow = ep.out + i * ny;
+  const double cxi = MODE == 0 ? (ep.norm ? ep.cx[i] / *ep.norm : ep.cx[i]) : 0.0;
 #pragma unroll
   for (int m = 0; m < 16 / S::RF; ++m)
 #pragma unroll
@@ -272,7 +274,7 @@ __global__ __launch_bounds__(N / 16) void fft_cols_kernel(const double2* __restr
         const double sgn = ((p + q) & 1) ? -1.0 : 1.0;
         const double2 g = v[m * S::RF + r];
         if constexpr (MODE == 0) {
-          orow[j] = sgn * g.x * ep.cx[i] * ep.cy[j];
+          orow[j] = sgn * g.x * cxi * ep.cy[j];
         } else {
           const double l = (double)p * ep.px, mm = (double)q * ep.py;
           const double e = l * l + mm * mm;
@@ -321,11 +323,11 @@ hipError_t launch_fft_rows(double* gT, int64_t nu, int64_t nv, int64_t nx, const
 
 hipError_t launch_fft_cols(const double* H, int64_t nv, int64_t nx, int64_t ny, const double* tw_v, int mode,
                            double* out, const double* cx, const double* cy, double px, double py, double w_plane,
-                           int first, hipStream_t s) {
+                           int first, const double* norm, hipStream_t s) {
   const dim3 gd((unsigned)nx);
   const double2* h = (const double2*)H;
   const double2* tw = (const double2*)tw_v;
-  const ColEpilogue ep{out, cx, cy, px, py, w_plane, first};
+  const ColEpilogue ep{out, cx, cy, px, py, w_plane, first, norm};
 #define COLS(NN)                                                                    \
   case NN:                                                                          \
     if (mode == 0) fft_cols_kernel<NN, 0><<<gd, dim3(NN / 16), 0, s>>>(h, nx, ny, tw, ep); \
@@ -340,6 +342,20 @@ hipError_t launch_fft_cols(const double* H, int64_t nv, int64_t nx, int64_t ny, 
       return hipErrorInvalidValue;
   }
 #undef COLS
+  return hipGetLastError();
+}
+
+// out[k] /= *sumw (CIP_NORMALISE on the paths without the fused epilogue)
+__global__ void scale_inverse_kernel(double* __restrict__ out, int64_t n, const double* __restrict__ sumw) {
+  const double d = *sumw;
+  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (int64_t)gridDim.x * blockDim.x)
+    out[k] /= d;
+}
+
+hipError_t launch_scale_inverse(double* out, int64_t n, const double* sumw, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  const int64_t nb = std::min<int64_t>((n + 255) / 256, 4096);
+  scale_inverse_kernel<<<dim3((unsigned)nb), dim3(256), 0, s>>>(out, n, sumw);
   return hipGetLastError();
 }
 

@@ -125,7 +125,9 @@ hipError_t launch_fft_rows(double* gT, int64_t nu, int64_t nv, int64_t nx, const
                            const uint32_t* dmask, int64_t ntx, hipStream_t s);
 hipError_t launch_fft_cols(const double* H, int64_t nv, int64_t nx, int64_t ny, const double* tw_v, int mode,
                            double* out, const double* cx, const double* cy, double px, double py, double w_plane,
-                           int first, hipStream_t s);
+                           int first, const double* norm, hipStream_t s);
+// out[0..n) /= *sumw (device scalar)
+hipError_t launch_scale_inverse(double* out, int64_t n, const double* sumw, hipStream_t s);
 
 // ---- reference tiling + Stokes I (cip_tiling.hip) --------------------------
 hipError_t launch_tile_run_count(const double* uvw, int64_t nrow, const double* winv, int64_t nchan,

@@ -30,6 +30,7 @@ CIP_F64 = 4
 CIP_WSTACKING = 1
 CIP_ACC_SINGLE = 2
 CIP_PSF = 4
+CIP_NORMALISE = 8
 STOKES_CODES = {"I": 0, "Q": 1, "U": 2, "V": 3}
 
 # every symbol declared in include/cip.h

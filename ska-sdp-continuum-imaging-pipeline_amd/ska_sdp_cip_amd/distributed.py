@@ -103,10 +103,14 @@ def invert_sharded(uvw, freq, vis, wgt, npix: int, pixsize: float, *, epsilon: f
     """
     from .gridder import device_ms2dirty  # pylint: disable=import-outside-toplevel
 
+    import torch.distributed as dist  # pylint: disable=import-outside-toplevel
+
+    single = not (dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1)
     out, sumw = image_buffer(npix, npix, vis.device)
     dirty, _ = device_ms2dirty(uvw, freq, vis, wgt, npix, npix, pixsize, pixsize, epsilon=epsilon,
-                               support=support, do_wstacking=do_wstacking, out=out, sum_weights=sumw)
-    return reduce_images(dirty, sumw, dst=dst, group=group)
+                               support=support, do_wstacking=do_wstacking, out=out, sum_weights=sumw,
+                               normalise=single)
+    return reduce_images(dirty, sumw, dst=dst, group=group, normalise=not single)
 
 
 def allreduce_grids(tensors, root: Optional[int] = None):

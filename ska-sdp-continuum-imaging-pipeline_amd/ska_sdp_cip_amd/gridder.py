@@ -70,6 +70,7 @@ def device_ms2dirty(
     sum_weights: Optional["torch.Tensor"] = None,
     single_precision_accumulation: bool = False,
     psf: bool = False,
+    normalise: bool = False,
 ) -> tuple["torch.Tensor", _lib.GridderParams]:
     """
     Device-resident ms2dirty: all tensors already in HBM on the current device.
@@ -81,6 +82,10 @@ def device_ms2dirty(
     default accumulates every input in 64-bit fixed point (fp64 class).
     `psf=True` grids unit visibilities instead of `vis` (the point-spread
     function with the same weights; `vis` may then be None).
+    `normalise=True` (CIP_NORMALISE) returns the image divided by the weight
+    sum of this call (the reference's (1 / total_weight) * image,
+    invert.py:119-149), fused into the FFT epilogue; not for partial images
+    that are summed across ranks afterwards.
     """
     vis_codes, wgt_codes = _codes()
     if psf:
@@ -113,7 +118,8 @@ def device_ms2dirty(
         int(support or 0),
         (_lib.CIP_WSTACKING if do_wstacking else 0)
         | (_lib.CIP_ACC_SINGLE if single_precision_accumulation else 0)
-        | (_lib.CIP_PSF if psf else 0),
+        | (_lib.CIP_PSF if psf else 0)
+        | (_lib.CIP_NORMALISE if normalise else 0),
         stream, out.data_ptr(),
         sum_weights.data_ptr() if sum_weights is not None else None, params)
     _lib.check(rc)

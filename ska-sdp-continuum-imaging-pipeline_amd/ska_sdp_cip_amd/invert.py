@@ -189,8 +189,8 @@ def device_invert(
     pix = pixel_size_lm(pixel_size_asec)
     sumw = torch.zeros(1, dtype=torch.float64, device=vis_i.device)
     dirty, _ = device_ms2dirty(uvw, freq, vis_i, eff, num_pixels, num_pixels, pix, pix, epsilon=epsilon,
-                              support=support, do_wstacking=do_wstacking, sum_weights=sumw)
-    return dirty.div_(sumw)
+                              support=support, do_wstacking=do_wstacking, sum_weights=sumw, normalise=True)
+    return dirty
 
 
 def worker_ducc_invert(
