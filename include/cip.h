@@ -206,9 +206,12 @@ int cip_release_collectives(void);
 /* Last error message of the calling thread ("" if none). */
 const char* cip_last_error(void);
 
-/* Free the calling thread's workspace cached for the current device
- * (workspaces are per device and host thread: two threads may each run
- * calls on their own stream, on one GPU, without sharing buffers). */
+/* Free the calling thread's workspace cached for the current device: its
+ * buffers, FFT plans, pinned staging, side stream and events (workspaces are
+ * per device and host thread: two threads may each run calls on their own
+ * stream, on one GPU, without sharing buffers). The workspaces of a worker
+ * thread are also freed automatically when that thread exits; those of the
+ * thread that loaded the library live until the process ends. */
 int cip_release_workspace(void);
 
 /* Per-phase timing of cip_ms2dirty / cip_grid_plane on the calling thread

@@ -305,13 +305,59 @@ static int join_side(Workspace* ws, hipStream_t s) {
 static std::mutex g_ws_mutex;
 // One workspace per (device, host thread): calls from different threads (e.g.
 // two inverts in flight on one GPU, each thread on its own stream) never
-// share buffers, the side stream or the clean-grid state.
+// share buffers, the side stream or the clean-grid state. A workspace holds
+// the uv grid (16 nu nv bytes) and planner buffers that grow with the
+// visibility count, so it lives only as long as its thread: a thread-exit hook
+// frees the workspaces of every worker thread that made one (dask worker
+// pools keep HBM use at one workspace per live thread), and
+// cip_release_workspace frees the calling thread's on demand.
 static std::map<std::pair<int, std::thread::id>, Workspace*> g_ws;
+// the thread that loaded the library: its workspaces are left to process
+// teardown (its thread-exit hook runs inside exit(), where the HIP runtime
+// may already be shutting down)
+static const std::thread::id g_load_thread = std::this_thread::get_id();
+
+static void destroy_workspace(Workspace* ws) {
+  for (auto& kv : ws->bufs)
+    if (kv.second.ptr) (void)hipFree(kv.second.ptr);
+  for (auto& p : ws->plans) (void)hipfftDestroy(p.h);
+  if (ws->pinned) (void)hipHostFree(ws->pinned);
+  if (ws->side) {
+    (void)hipStreamSynchronize(ws->side);
+    (void)hipStreamDestroy(ws->side);
+  }
+  if (ws->ev_fork) (void)hipEventDestroy(ws->ev_fork);
+  if (ws->ev_join) (void)hipEventDestroy(ws->ev_join);
+  delete ws;
+}
+
+// Frees the calling thread's workspaces (every device) when the thread ends.
+struct WorkspaceReaper {
+  bool armed = false;
+  ~WorkspaceReaper() {
+    if (!armed || std::this_thread::get_id() == g_load_thread) return;
+    std::vector<Workspace*> mine;
+    {
+      std::lock_guard<std::mutex> lock(g_ws_mutex);
+      for (auto it = g_ws.begin(); it != g_ws.end();) {
+        if (it->first.second == std::this_thread::get_id()) {
+          mine.push_back(it->second);
+          it = g_ws.erase(it);
+        } else {
+          ++it;
+        }
+      }
+    }
+    for (Workspace* ws : mine) destroy_workspace(ws);
+  }
+};
+static thread_local WorkspaceReaper g_reaper;
 
 static Workspace* workspace() {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return nullptr;
   const auto key = std::make_pair(dev, std::this_thread::get_id());
+  g_reaper.armed = true;
   std::lock_guard<std::mutex> lock(g_ws_mutex);
   auto it = g_ws.find(key);
   if (it != g_ws.end()) return it->second;
@@ -1227,12 +1273,8 @@ int cip_release_workspace(void) {
   auto it = g_ws.find(std::make_pair(dev, std::this_thread::get_id()));
   if (it == g_ws.end()) return CIP_OK;
   Workspace* ws = it->second;
-  for (auto& kv : ws->bufs)
-    if (kv.second.ptr) (void)hipFree(kv.second.ptr);
-  for (auto& p : ws->plans) (void)hipfftDestroy(p.h);
-  if (ws->pinned) (void)hipHostFree(ws->pinned);
-  delete ws;
   g_ws.erase(it);
+  destroy_workspace(ws);
   return CIP_OK;
 }
 

@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <map>
 #include <mutex>
 #include <string>
@@ -22,6 +23,16 @@ int nccl_fail(ncclResult_t r, const char* what) {
   return cip::set_error(CIP_EHIP, std::string(what) + ": " + ncclGetErrorString(r));
 }
 
+// Restores the caller's current device on every exit path.
+struct DeviceGuard {
+  int prev = 0;
+  bool ok = false;
+  DeviceGuard() { ok = hipGetDevice(&prev) == hipSuccess; }
+  ~DeviceGuard() {
+    if (ok) (void)hipSetDevice(prev);
+  }
+};
+
 }  // namespace
 
 extern "C" int cip_allreduce_grid(void* const* grids, const int* devices, int ndev, int64_t nelem, int root,
@@ -31,8 +42,16 @@ extern "C" int cip_allreduce_grid(void* const* grids, const int* devices, int nd
   if (root >= ndev) return cip::set_error(CIP_EINVAL, "root must be < ndev (or < 0 for all-reduce)");
   for (int k = 0; k < ndev; ++k)
     if (!grids[k]) return cip::set_error(CIP_EINVAL, "NULL grid");
-  if (nelem == 0) return CIP_OK;
   std::vector<int> devs(devices, devices + ndev);
+  {
+    std::vector<int> sorted = devs;
+    std::sort(sorted.begin(), sorted.end());
+    if (std::adjacent_find(sorted.begin(), sorted.end()) != sorted.end())
+      return cip::set_error(CIP_EINVAL, "devices must be distinct (one communicator rank per device)");
+    if (sorted.front() < 0) return cip::set_error(CIP_EINVAL, "negative device index");
+  }
+  if (nelem == 0) return CIP_OK;
+  const DeviceGuard guard;  // ncclCommInitAll and the synchronisation loop switch devices
   std::vector<ncclComm_t>* comms = nullptr;
   {
     std::lock_guard<std::mutex> lock(g_comm_mutex);
@@ -45,8 +64,6 @@ extern "C" int cip_allreduce_grid(void* const* grids, const int* devices, int nd
     }
     comms = &it->second;
   }
-  int prev = 0;
-  (void)hipGetDevice(&prev);
   // fp64 sums (the grids / images are fp64); one group call over all devices
   ncclResult_t r = ncclGroupStart();
   if (r != ncclSuccess) return nccl_fail(r, "ncclGroupStart");
@@ -68,7 +85,6 @@ extern "C" int cip_allreduce_grid(void* const* grids, const int* devices, int nd
     hipStream_t s = hip_streams ? (hipStream_t)hip_streams[k] : nullptr;
     if (hipStreamSynchronize(s) != hipSuccess) return cip::set_error(CIP_EHIP, "hipStreamSynchronize failed");
   }
-  (void)hipSetDevice(prev);
   return CIP_OK;
 }
 

@@ -110,12 +110,14 @@ class GridAccumulator:
         nrow, nchan = uvw.shape[0], freq.shape[0]
         if tuple(vis.shape) != (nrow, nchan) or (wgt is not None and tuple(wgt.shape) != (nrow, nchan)):
             raise ValueError("vis / wgt must have shape (nrow, nchan)")
-        stream = torch.cuda.current_stream(self.device).cuda_stream
-        _lib.check(_lib.lib().cip_grid_ms(
-            uvw.data_ptr(), nrow, freq.data_ptr(), nchan, vis.data_ptr(), vis_codes[vis.dtype],
-            wgt.data_ptr() if wgt is not None else None, wgt_codes[wgt.dtype] if wgt is not None else _lib.CIP_NONE,
-            self.params, self.pixsize_x, self.pixsize_y, self.npix_x, self.npix_y, self.flags, stream,
-            self.planes.data_ptr(), self.sum_weights.data_ptr()))
+        with torch.cuda.device(self.device):
+            stream = torch.cuda.current_stream(self.device).cuda_stream
+            _lib.check(_lib.lib().cip_grid_ms(
+                uvw.data_ptr(), nrow, freq.data_ptr(), nchan, vis.data_ptr(), vis_codes[vis.dtype],
+                wgt.data_ptr() if wgt is not None else None,
+                wgt_codes[wgt.dtype] if wgt is not None else _lib.CIP_NONE,
+                self.params, self.pixsize_x, self.pixsize_y, self.npix_x, self.npix_y, self.flags, stream,
+                self.planes.data_ptr(), self.sum_weights.data_ptr()))
         self.num_visibilities += nrow * nchan
 
     def add_tile(self, slice_uvw, chan_start, chan_stop, freq, vis, wgt=None) -> None:
@@ -130,13 +132,15 @@ class GridAccumulator:
         nvis = vis.shape[0]
         if wgt is not None and tuple(wgt.shape) != (nvis,):
             raise ValueError("wgt must have the shape of vis")
-        stream = torch.cuda.current_stream(self.device).cuda_stream
-        _lib.check(_lib.lib().cip_grid_tiles(
-            slice_uvw.data_ptr(), chan_start.data_ptr(), chan_stop.data_ptr(), ns, freq.data_ptr(), freq.shape[0],
-            vis.data_ptr(), nvis, vis_codes[vis.dtype],
-            wgt.data_ptr() if wgt is not None else None, wgt_codes[wgt.dtype] if wgt is not None else _lib.CIP_NONE,
-            self.params, self.pixsize_x, self.pixsize_y, self.npix_x, self.npix_y, self.flags, stream,
-            self.planes.data_ptr(), self.sum_weights.data_ptr()))
+        with torch.cuda.device(self.device):
+            stream = torch.cuda.current_stream(self.device).cuda_stream
+            _lib.check(_lib.lib().cip_grid_tiles(
+                slice_uvw.data_ptr(), chan_start.data_ptr(), chan_stop.data_ptr(), ns, freq.data_ptr(),
+                freq.shape[0], vis.data_ptr(), nvis, vis_codes[vis.dtype],
+                wgt.data_ptr() if wgt is not None else None,
+                wgt_codes[wgt.dtype] if wgt is not None else _lib.CIP_NONE,
+                self.params, self.pixsize_x, self.pixsize_y, self.npix_x, self.npix_y, self.flags, stream,
+                self.planes.data_ptr(), self.sum_weights.data_ptr()))
         self.num_visibilities += nvis
 
     def dirty(self, out=None):
@@ -145,9 +149,15 @@ class GridAccumulator:
         self._check()
         if out is None:
             out = torch.empty((self.npix_x, self.npix_y), dtype=torch.float64, device=self.device)
-        stream = torch.cuda.current_stream(self.device).cuda_stream
-        _lib.check(_lib.lib().cip_grid_to_dirty(self.planes.data_ptr(), self.params, self.npix_x, self.npix_y,
-                                                self.pixsize_x, self.pixsize_y, stream, out.data_ptr()))
+        elif out.dtype != torch.float64 or tuple(out.shape) != (self.npix_x, self.npix_y) or \
+                not out.is_contiguous() or out.device != self.device:
+            raise ValueError(f"out must be a contiguous float64 ({self.npix_x}, {self.npix_y}) tensor on "
+                             f"{self.device}")
+        with torch.cuda.device(self.device):
+            stream = torch.cuda.current_stream(self.device).cuda_stream
+            _lib.check(_lib.lib().cip_grid_to_dirty(self.planes.data_ptr(), self.params, self.npix_x,
+                                                    self.npix_y, self.pixsize_x, self.pixsize_y, stream,
+                                                    out.data_ptr()))
         self._done = True
         return out, self.sum_weights
 

@@ -102,14 +102,47 @@ def device_ms2dirty(
         raise ValueError(f"ms must have shape ({nrow}, {nchan}), got {tuple(vis.shape)}")
     if wgt is not None and tuple(wgt.shape) != (nrow, nchan):
         raise ValueError("wgt must have the shape of ms")
+    if uvw.dtype != torch.float64 or freq.dtype != torch.float64:
+        raise ValueError("uvw and freq must be float64")
     for t in (uvw, freq) + ((vis,) if vis is not None else ()) + ((wgt,) if wgt is not None else ()):
-        if not t.is_contiguous() or not t.is_cuda:
-            raise ValueError("device_ms2dirty needs contiguous device tensors")
+        _check_device_tensor(t, uvw.device, "device_ms2dirty inputs")
     if out is None:
         out = torch.empty((npix_x, npix_y), dtype=torch.float64, device=uvw.device)
+    else:
+        # the library writes npix_x * npix_y doubles through the raw pointer
+        if out.dtype != torch.float64 or tuple(out.shape) != (int(npix_x), int(npix_y)):
+            raise ValueError(f"out must be float64 of shape ({npix_x}, {npix_y}), "
+                             f"got {out.dtype} {tuple(out.shape)}")
+        _check_device_tensor(out, uvw.device, "out")
+    if sum_weights is not None:
+        if sum_weights.dtype != torch.float64 or sum_weights.numel() != 1:
+            raise ValueError("sum_weights must be a float64 tensor of one element")
+        _check_device_tensor(sum_weights, uvw.device, "sum_weights")
     params = _lib.GridderParams()
-    stream = torch.cuda.current_stream(uvw.device).cuda_stream
-    rc = _lib.lib().cip_ms2dirty(
+    with torch.cuda.device(uvw.device):
+        stream = torch.cuda.current_stream(uvw.device).cuda_stream
+        rc = _ms2dirty_call(uvw, freq, vis, wgt, vis_codes, wgt_codes, npix_x, npix_y, pixsize_x, pixsize_y,
+                            epsilon, support, do_wstacking, single_precision_accumulation, psf, normalise,
+                            stream, out, sum_weights, params)
+    _lib.check(rc)
+    return out, params
+
+
+def _check_device_tensor(t, device, what):
+    """Contiguous, on a GPU, and on `device` (the library works on the current
+    device, which the callers set to `device`)."""
+    if not t.is_cuda or not t.is_contiguous():
+        raise ValueError(f"{what}: need contiguous device tensors")
+    if t.device != device:
+        raise ValueError(f"{what}: tensor on {t.device}, expected {device}")
+
+
+def _ms2dirty_call(uvw, freq, vis, wgt, vis_codes, wgt_codes, npix_x, npix_y, pixsize_x, pixsize_y, epsilon,
+                   support, do_wstacking, single_precision_accumulation, psf, normalise, stream, out,
+                   sum_weights, params):
+    nrow = uvw.shape[0]
+    nchan = freq.shape[0]
+    return _lib.lib().cip_ms2dirty(
         uvw.data_ptr(), nrow, freq.data_ptr(), nchan, None if vis is None else vis.data_ptr(),
         _lib.CIP_C64 if vis is None else vis_codes[vis.dtype],
         wgt.data_ptr() if wgt is not None else None,
@@ -122,8 +155,6 @@ def device_ms2dirty(
         | (_lib.CIP_NORMALISE if normalise else 0),
         stream, out.data_ptr(),
         sum_weights.data_ptr() if sum_weights is not None else None, params)
-    _lib.check(rc)
-    return out, params
 
 
 def device_stokes(vis4: "torch.Tensor", flags4: "torch.Tensor", wgt4: "torch.Tensor", stokes: str = "I"):
@@ -148,10 +179,11 @@ def device_stokes(vis4: "torch.Tensor", flags4: "torch.Tensor", wgt4: "torch.Ten
     nrow, nchan = vis4.shape[0], vis4.shape[1]
     vis_s = torch.empty((nrow, nchan), dtype=torch.complex64, device=vis4.device)
     eff = torch.empty((nrow, nchan), dtype=torch.float32, device=vis4.device)
-    stream = torch.cuda.current_stream(vis4.device).cuda_stream
-    _lib.check(_lib.lib().cip_stokes(vis4.data_ptr(), fl.data_ptr(), wgt4.data_ptr(), nrow * nchan,
-                                     _lib.STOKES_CODES[stokes], stream, vis_s.data_ptr(), None, None,
-                                     eff.data_ptr()))
+    with torch.cuda.device(vis4.device):
+        stream = torch.cuda.current_stream(vis4.device).cuda_stream
+        _lib.check(_lib.lib().cip_stokes(vis4.data_ptr(), fl.data_ptr(), wgt4.data_ptr(), nrow * nchan,
+                                         _lib.STOKES_CODES[stokes], stream, vis_s.data_ptr(), None, None,
+                                         eff.data_ptr()))
     return vis_s, eff
 
 
@@ -174,11 +206,12 @@ def device_facet_rephase(uvw: "torch.Tensor", freq: "torch.Tensor", vis: Optiona
             raise ValueError("device_facet_rephase needs contiguous device tensors")
     uvw_f = torch.empty_like(uvw)
     vis_f = torch.empty_like(vis) if vis is not None else None
-    stream = torch.cuda.current_stream(uvw.device).cuda_stream
-    _lib.check(_lib.lib().cip_facet_rephase(
-        uvw.data_ptr(), nrow, freq.data_ptr(), nchan, vis.data_ptr() if vis is not None else None,
-        vis_codes[vis.dtype] if vis is not None else _lib.CIP_C64, float(l0), float(m0), stream, uvw_f.data_ptr(),
-        vis_f.data_ptr() if vis_f is not None else None))
+    with torch.cuda.device(uvw.device):
+        stream = torch.cuda.current_stream(uvw.device).cuda_stream
+        _lib.check(_lib.lib().cip_facet_rephase(
+            uvw.data_ptr(), nrow, freq.data_ptr(), nchan, vis.data_ptr() if vis is not None else None,
+            vis_codes[vis.dtype] if vis is not None else _lib.CIP_C64, float(l0), float(m0), stream,
+            uvw_f.data_ptr(), vis_f.data_ptr() if vis_f is not None else None))
     return uvw_f, vis_f
 
 
@@ -202,9 +235,10 @@ def device_stokes_i(vis4: "torch.Tensor", flags4: "torch.Tensor", wgt4: "torch.T
     nrow, nchan = vis4.shape[0], vis4.shape[1]
     vis_i = torch.empty((nrow, nchan), dtype=torch.complex64, device=vis4.device)
     eff = torch.empty((nrow, nchan), dtype=torch.float32, device=vis4.device)
-    stream = torch.cuda.current_stream(vis4.device).cuda_stream
-    _lib.check(_lib.lib().cip_stokes_i(vis4.data_ptr(), fl.data_ptr(), wgt4.data_ptr(), nrow * nchan, stream,
-                                       vis_i.data_ptr(), None, None, eff.data_ptr()))
+    with torch.cuda.device(vis4.device):
+        stream = torch.cuda.current_stream(vis4.device).cuda_stream
+        _lib.check(_lib.lib().cip_stokes_i(vis4.data_ptr(), fl.data_ptr(), wgt4.data_ptr(), nrow * nchan, stream,
+                                           vis_i.data_ptr(), None, None, eff.data_ptr()))
     return vis_i, eff
 
 

@@ -1,0 +1,102 @@
+"""
+GPU tests of the host-side argument checks of the device drop-in
+(`gridder.device_ms2dirty`, `accumulate.GridAccumulator.dirty`): the library
+writes npix_x * npix_y doubles through `out` and one double through
+`sum_weights`, so a wrong dtype, shape, layout or device must raise
+ValueError before the call instead of corrupting HBM.
+"""
+import numpy as np
+import pytest
+
+from ska_sdp_cip_amd import gridder, synthetic as syn
+
+pytestmark = pytest.mark.gpu
+
+
+def _inputs(npix=64):
+    import torch
+
+    uvw = syn.uvw_tracks(200, 8, array_radius_m=500.0, seed=2)
+    f = syn.channel_frequencies(4)
+    rng = np.random.default_rng(0)
+    vis = (rng.standard_normal((uvw.shape[0], 4)) + 1j).astype(np.complex64)
+    w = np.ones(vis.shape, np.float32)
+    px = syn.pixel_size_for_grid(uvw, f, npix)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
+    return (t(uvw), t(f), t(vis), t(w), npix, npix, px, px)
+
+
+@pytest.mark.parametrize("bad", ["f32", "shape", "strided", "cpu"])
+def test_out_is_validated(gpu_device, bad):
+    import torch
+
+    args = _inputs()
+    out = {
+        "f32": lambda: torch.zeros((64, 64), dtype=torch.float32, device="cuda"),
+        "shape": lambda: torch.zeros((32, 64), dtype=torch.float64, device="cuda"),
+        "strided": lambda: torch.zeros((64, 128), dtype=torch.float64, device="cuda")[:, ::2],
+        "cpu": lambda: torch.zeros((64, 64), dtype=torch.float64),
+    }[bad]()
+    with pytest.raises(ValueError):
+        gridder.device_ms2dirty(*args, support=8, out=out)
+
+
+@pytest.mark.parametrize("bad", ["f32", "two", "cpu"])
+def test_sum_weights_is_validated(gpu_device, bad):
+    import torch
+
+    args = _inputs()
+    sw = {
+        "f32": lambda: torch.zeros(1, dtype=torch.float32, device="cuda"),
+        "two": lambda: torch.zeros(2, dtype=torch.float64, device="cuda"),
+        "cpu": lambda: torch.zeros(1, dtype=torch.float64),
+    }[bad]()
+    with pytest.raises(ValueError):
+        gridder.device_ms2dirty(*args, support=8, sum_weights=sw)
+
+
+def test_valid_out_and_sum_weights_are_used(gpu_device):
+    import torch
+
+    args = _inputs()
+    out = torch.full((64, 64), 7.0, dtype=torch.float64, device="cuda")
+    sw = torch.zeros(1, dtype=torch.float64, device="cuda")
+    res, _ = gridder.device_ms2dirty(*args, support=8, out=out, sum_weights=sw)
+    torch.cuda.synchronize()
+    assert res.data_ptr() == out.data_ptr()
+    assert float(sw.item()) == float(args[3].double().sum().item())
+    assert not torch.any(out == 7.0)
+
+
+def test_workspace_release_and_thread_exit(gpu_device):
+    """cip_release_workspace frees the calling thread's workspace (a later call
+    rebuilds it); workspaces of a worker thread are freed when it exits."""
+    import threading
+
+    import torch
+
+    from ska_sdp_cip_amd import _lib
+
+    args = _inputs(1024)  # 2048^2 grid: 64 MiB per workspace
+    ref, _ = gridder.device_ms2dirty(*args, support=8)
+    ref = ref.clone()
+    _lib.check(_lib.lib().cip_release_workspace())
+    again, _ = gridder.device_ms2dirty(*args, support=8)
+    assert torch.equal(ref, again)
+    free0 = torch.cuda.mem_get_info()[0]
+    results = []
+
+    def worker():
+        d, _ = gridder.device_ms2dirty(*args, support=8)
+        torch.cuda.synchronize()
+        results.append(d.clone())
+
+    for _ in range(3):
+        th = threading.Thread(target=worker)
+        th.start()
+        th.join()
+    torch.cuda.synchronize()
+    assert all(torch.equal(ref, r) for r in results)
+    # three exited threads hold no workspace: free memory is back within
+    # 32 MiB of where it was (each workspace holds a 64 MiB grid)
+    assert torch.cuda.mem_get_info()[0] > free0 - 32 * 1024 * 1024

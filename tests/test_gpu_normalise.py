@@ -22,10 +22,19 @@ def _t(a):
     return torch.from_numpy(np.ascontiguousarray(a)).cuda()
 
 
-@pytest.mark.parametrize("npix,wstack,psf", [(256, False, False), (256, True, False), (250, False, False),
-                                             (256, False, True)])
-def test_normalise_equals_divide(gpu_device, npix, wstack, psf):
+# grids of 1024..8192 cells per axis (npix 512..4096, power of two) take the
+# pruned FFT, whose pass-B epilogue divides by the weight sum (2-D); the other
+# sizes, and w-stacking on any size, take the separate scale pass
+@pytest.mark.parametrize("npix,wstack,psf,fused", [
+    (256, False, False, False), (256, True, False, False), (250, False, False, False), (256, False, True, False),
+    (512, False, False, True), (1024, False, False, True), ((512, 1024), False, False, True),
+    ((1024, 512), False, True, True), (512, True, False, False)])
+def test_normalise_equals_divide(gpu_device, npix, wstack, psf, fused):
     import torch
+
+    from ska_sdp_cip_amd import _lib
+
+    nx, ny = (npix, npix) if isinstance(npix, int) else npix
 
     uvw = syn.uvw_tracks(1_500, 16, array_radius_m=900.0, seed=11)
     f = syn.channel_frequencies(8)
@@ -33,15 +42,20 @@ def test_normalise_equals_divide(gpu_device, npix, wstack, psf):
     vis = (rng.standard_normal((uvw.shape[0], f.size)) + 1j * rng.standard_normal((uvw.shape[0], f.size)))
     vis = vis.astype(np.complex64)
     w = rng.uniform(0.5, 2.0, vis.shape).astype(np.float32)
-    px = syn.pixel_size_for_grid(uvw, f, npix)
-    args = (_t(uvw), _t(f), None if psf else _t(vis), _t(w), npix, npix, px, px)
+    px = syn.pixel_size_for_grid(uvw, f, max(nx, ny))
+    args = (_t(uvw), _t(f), None if psf else _t(vis), _t(w), nx, ny, px, px)
     kw = dict(support=8, do_wstacking=wstack, psf=psf)
     s0 = torch.zeros(1, dtype=torch.float64, device="cuda")
     s1 = torch.zeros(1, dtype=torch.float64, device="cuda")
     raw, _ = gridder.device_ms2dirty(*args, sum_weights=s0, **kw)
     raw = raw.clone()
-    nrm, _ = gridder.device_ms2dirty(*args, sum_weights=s1, normalise=True, **kw)
+    nrm, params = gridder.device_ms2dirty(*args, sum_weights=s1, normalise=True, **kw)
     torch.cuda.synchronize()
+    # the layout the library chose: 1 = pruned FFT (pass-B epilogue divides)
+    pruned = bool(_lib.lib().cip_grid_layout(params, nx, ny))
+    pow2 = all(n >= 512 and n & (n - 1) == 0 for n in (nx, ny))
+    assert pruned == pow2
+    assert fused == (pruned and not wstack)
     sw = float(s0.item())
     assert float(s1.item()) == sw  # the raw weight sum is still returned
     assert sw == pytest.approx(float(w.astype(np.float64).sum()), rel=1e-12)
@@ -49,9 +63,9 @@ def test_normalise_equals_divide(gpu_device, npix, wstack, psf):
     n = nrm.cpu().numpy()
     assert np.abs(n - r / sw).max() <= 1e-15 * np.abs(r / sw).max() * 4
     if psf:
-        assert abs(n[npix // 2, npix // 2] - 1.0) < 1e-6  # gridding accuracy, as test_gpu_continuum
+        assert abs(n[nx // 2, ny // 2] - 1.0) < 1e-6  # gridding accuracy, as test_gpu_continuum
     else:
-        ref = oracle.ms2dirty(uvw, f, vis, w, npix, npix, px, px, support=8, do_wstacking=wstack)
+        ref = oracle.ms2dirty(uvw, f, vis, w, nx, ny, px, px, support=8, do_wstacking=wstack)
         assert np.abs(n - ref / sw).max() < 1e-6 * np.abs(ref / sw).max() + 1e-12
 
 

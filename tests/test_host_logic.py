@@ -239,3 +239,20 @@ def test_oracle_stokes_and_facet_rotation():
         q = oracle.facet_rotation(l0, m0)
         assert np.allclose(q @ q.T, np.eye(3), atol=1e-14)
         assert np.allclose(q @ [0.0, 0.0, 1.0], [l0, m0, np.sqrt(1 - l0 * l0 - m0 * m0)], atol=1e-14)
+
+
+def test_allreduce_rejects_duplicate_devices():
+    """cip_allreduce_grid validates its device list before any HIP/RCCL call
+    (a repeated device would otherwise reach ncclCommInitAll)."""
+    import ctypes
+
+    from ska_sdp_cip_amd import _lib
+
+    L = _lib.lib()
+    bufs = (ctypes.c_double * 4)()
+    grids = (ctypes.c_void_p * 2)(ctypes.addressof(bufs), ctypes.addressof(bufs))
+    devs = (ctypes.c_int * 2)(0, 0)
+    assert L.cip_allreduce_grid(grids, devs, 2, 4, -1, None) == _lib.CIP_EINVAL
+    assert b"distinct" in L.cip_last_error()
+    devs = (ctypes.c_int * 2)(-1, 1)
+    assert L.cip_allreduce_grid(grids, devs, 2, 4, -1, None) == _lib.CIP_EINVAL
