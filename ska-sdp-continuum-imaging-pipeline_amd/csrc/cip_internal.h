@@ -90,6 +90,13 @@ hipError_t launch_prep_final(const double* partial, int nblocks, double* out2, h
 // packed: single-precision class (re/im packed in one 64-bit integer), complex64
 // only. perm: bank-class ordered stream from launch_order, or NULL (visibilities
 // located through the tile's row slices in tile order).
+// one kernel support W (instantiated in cip_scatter_w.hip for W = 4, 6, ..., 16)
+template <int W>
+hipError_t launch_scatter_w(int vis_dtype, int wgt_dtype, bool pack, dim3 gd, hipStream_t s, const double* uvw,
+                            const double* fx, const void* vis, const void* wgt, const RowMap& m,
+                            const uint64_t* runs, const int64_t* run_goff, const int64_t* tile_run_off,
+                            const uint32_t* perm, const Chunk* chunks, int64_t cb, const GridGeometry& g,
+                            int64_t plane, double fs, double* grid);
 hipError_t launch_scatter(int support, int vis_dtype, int wgt_dtype, bool packed, const double* uvw,
                           const double* fx, const void* vis, const void* wgt, const RowMap& m, const uint64_t* runs,
                           const int64_t* run_goff, const int64_t* tile_run_off, const uint32_t* perm,
