@@ -57,6 +57,11 @@ extern "C" {
 #define CIP_PSF 4        /* grid unit visibilities (vis ignored, may be NULL):
                           * the point-spread function with the same weights
                           * (cip_ms2dirty, cip_grid_ms, cip_grid_tiles) */
+#define CIP_ASYNC 16     /* cip_ms2dirty only: return once the work is queued on
+                          * hip_stream instead of synchronising it (the
+                          * planner's two readbacks still synchronise mid-call).
+                          * dirty_out / sum_wgt_out are valid when the stream
+                          * reaches this point. Ignored while profiling is on. */
 #define CIP_ACC_SINGLE 2 /* complex64 only: single-precision accumulation
                           * class, the reference's ducc0 float gridding (re/im
                           * packed in one 64-bit fixed-point LDS cell, W^2

@@ -277,6 +277,14 @@ struct Workspace {
   // the "grid" buffer when it is known all-zero (the masked FFT pass A zeroes
   // what the scatter wrote), else NULL
   double* grid_clean = nullptr;
+  // CIP_ASYNC pipelining (cip_ms2dirty): the planner runs on plan_stream
+  // after the previous call's last scatter (ev_scattered), so it overlaps that
+  // call's FFT; the caller's stream waits for it (ev_planned). The planner
+  // outputs the FFT still reads (weight sum, dirty-tile masks) alternate
+  // between two buffer sets (parity).
+  hipStream_t plan_stream = nullptr;
+  hipEvent_t ev_scattered = nullptr, ev_planned = nullptr;
+  int parity = 0;
 };
 
 // Zero `bytes` at `p` on the workspace's side stream, ordered after the work
@@ -328,6 +336,12 @@ static void destroy_workspace(Workspace* ws) {
   }
   if (ws->ev_fork) (void)hipEventDestroy(ws->ev_fork);
   if (ws->ev_join) (void)hipEventDestroy(ws->ev_join);
+  if (ws->plan_stream) {
+    (void)hipStreamSynchronize(ws->plan_stream);
+    (void)hipStreamDestroy(ws->plan_stream);
+  }
+  if (ws->ev_scattered) (void)hipEventDestroy(ws->ev_scattered);
+  if (ws->ev_planned) (void)hipEventDestroy(ws->ev_planned);
   delete ws;
 }
 
@@ -602,7 +616,7 @@ static int make_plan(Workspace* ws, const double* uvw, const double* fx, const R
   CIP_HIP_CHECK(launch_tile_vis(run_goff, tile_run_off, ntiles, tile_vis_off, tile_vis, s));
   if (g.ntx % 32 == 0 && grid_mask()) {
     CIP_ALLOC(dmask, uint8_t, "dirty_mask", g.ntx * g.nty * g.nplanes)
-    CIP_ALLOC(dbits, uint32_t, "dirty_bits", g.ntx * g.nty / 32 * g.nplanes)
+    CIP_ALLOC(dbits, uint32_t, ws->parity ? "dirty_bits1" : "dirty_bits0", g.ntx * g.nty / 32 * g.nplanes)
     CIP_HIP_CHECK(hipMemsetAsync(dmask, 0, (size_t)(g.ntx * g.nty * g.nplanes), s));
     CIP_HIP_CHECK(launch_dirty_mask(tile_vis, g.ntx, g.nty, g.ntw, g.support, g.nplanes, dmask, dbits, s));
     pr->dmask = dbits;
@@ -685,7 +699,7 @@ static int prepare(Workspace* ws, const double* uvw, int64_t nrow, const double*
   if (nrow < 0 || nchan < 1 || nchan > 65535) return set_error(CIP_EINVAL, "need 1 <= nchan <= 65535, nrow >= 0");
   if (nrow >= ((int64_t)1 << 32)) return set_error(CIP_EINVAL, "nrow must be < 2^32");
   CIP_ALLOC(fx, double, "fx", nchan)
-  CIP_ALLOC(red, double, "red", 4)
+  CIP_ALLOC(red, double, ws->parity ? "red1" : "red0", 4)
   // the planner's error bits: cleared here, read back with the run count
   CIP_ALLOC(err, unsigned, "err_flag", 1)
   CIP_HIP_CHECK(hipMemsetAsync(err, 0, sizeof(unsigned), s));
@@ -1017,7 +1031,7 @@ int cip_ms2dirty(const double* uvw, int64_t nrow, const double* freq, int64_t nc
                  double pixsize_y, double epsilon, int support, int flags, void* hip_stream,
                  double* dirty_out, double* sum_wgt_out, cip_gridder_params* params_out) {
   g_last_error.clear();
-  if (flags & ~(CIP_WSTACKING | CIP_ACC_SINGLE | CIP_PSF | CIP_NORMALISE))
+  if (flags & ~(CIP_WSTACKING | CIP_ACC_SINGLE | CIP_PSF | CIP_NORMALISE | CIP_ASYNC))
     return set_error(CIP_EINVAL, "unknown flags");
   const int do_wstacking = (flags & CIP_WSTACKING) ? 1 : 0;
   const bool normalise = (flags & CIP_NORMALISE) != 0;
@@ -1033,10 +1047,47 @@ int cip_ms2dirty(const double* uvw, int64_t nrow, const double* freq, int64_t nc
   if (!ws) return set_error(CIP_EHIP, "no HIP device");
   g_prof.reset();
   hipEvent_t t_start = g_prof.mark(s);
+  // CIP_ASYNC: the planner on the workspace's plan stream, after the previous
+  // call's last scatter - it then overlaps that call's FFT on s
+  const bool pipelined = (flags & CIP_ASYNC) && !g_prof.on;
+  hipStream_t ps = s;
+  if (pipelined) {
+    if (!ws->plan_stream) {
+      // (measured at C3: the overlapped FFT pass A runs ~4x slower beside the
+      // place pass, whatever the stream priority, so the gain is ~1.5 %)
+      CIP_HIP_CHECK(hipStreamCreateWithFlags(&ws->plan_stream, hipStreamNonBlocking));
+      CIP_HIP_CHECK(hipEventCreateWithFlags(&ws->ev_scattered, hipEventDisableTiming));
+      CIP_HIP_CHECK(hipEventCreateWithFlags(&ws->ev_planned, hipEventDisableTiming));
+      // the first pipelined call: the planner starts after the work already on s
+      CIP_HIP_CHECK(hipEventRecord(ws->ev_scattered, s));
+    }
+    CIP_HIP_CHECK(hipStreamWaitEvent(ws->plan_stream, ws->ev_scattered, 0));
+    ws->parity ^= 1;
+    ps = ws->plan_stream;
+  } else {
+    ws->parity = 0;
+  }
+  // whatever happens below, the next pipelined call's planner starts only
+  // after everything this call queued on s so far (an early error return
+  // included); the normal path records the event right after the last scatter
+  struct ScatteredMark {
+    Workspace* ws;
+    hipStream_t s;
+    bool armed;
+    ~ScatteredMark() {
+      if (armed) (void)hipEventRecord(ws->ev_scattered, s);
+    }
+  } scattered_mark{ws, s, pipelined};
   Prepared pp;
   double* grid = nullptr;
   int rc = prepare(ws, uvw, nrow, freq, nchan, vis, vis_dtype, wgt, wgt_dtype, npix_x, npix_y, pixsize_x, pixsize_y,
-                   epsilon, support, do_wstacking, packed, nullptr, s, &pp, overlap_zero() ? &grid : nullptr);
+                   epsilon, support, do_wstacking, packed, nullptr, ps, &pp,
+                   (overlap_zero() && !pipelined) ? &grid : nullptr);
+  if (pipelined) {
+    // s continues once the plan exists (also after a failed one: nothing then runs on it)
+    CIP_HIP_CHECK(hipEventRecord(ws->ev_planned, ps));
+    CIP_HIP_CHECK(hipStreamWaitEvent(s, ws->ev_planned, 0));
+  }
   if (grid) {
     // join the side stream whatever happened (the workspace grid must not be
     // written by a later call while its memset is still queued)
@@ -1059,6 +1110,11 @@ int cip_ms2dirty(const double* uvw, int64_t nrow, const double* freq, int64_t nc
   for (int64_t p = 0; p < g.nplanes; ++p) {
     rc = scatter_plane(pp, p, uvw, vis, vis_dtype, wgt, wgt_dtype, st.fast, grid, s, clean);
     if (rc != CIP_OK) return rc;
+    // the next pipelined call's planner may overwrite the plan from here on
+    if (pipelined && p == g.nplanes - 1) {
+      CIP_HIP_CHECK(hipEventRecord(ws->ev_scattered, s));
+      scattered_mark.armed = false;
+    }
     rc = plane_to_dirty(st, g, p, grid, dirty_out, s, dmask ? dmask + p * (g.ntx * g.nty / 32) : nullptr,
                         normalise ? pp.red : nullptr);
     if (rc != CIP_OK) return rc;
@@ -1071,7 +1127,10 @@ int cip_ms2dirty(const double* uvw, int64_t nrow, const double* freq, int64_t nc
     CIP_HIP_CHECK(launch_scale_inverse(dirty_out, npix_x * npix_y, pp.red, s));
   if (sum_wgt_out) CIP_HIP_CHECK(hipMemcpyAsync(sum_wgt_out, pp.red, sizeof(double), hipMemcpyDeviceToDevice, s));
   g_prof.span(5, t_start, g_prof.mark(s));
-  CIP_HIP_CHECK(hipStreamSynchronize(s));
+  // CIP_ASYNC: the workspace (grid, planner buffers) is reused by later calls
+  // of this thread in stream order, so nothing on the host waits for it; the
+  // grid-clean mark holds in stream order too
+  if (!(flags & CIP_ASYNC) || g_prof.on) CIP_HIP_CHECK(hipStreamSynchronize(s));
   if (clean) ws->grid_clean = grid;
   g_prof.finish();
   return CIP_OK;

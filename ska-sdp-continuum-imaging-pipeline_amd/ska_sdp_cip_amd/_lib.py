@@ -31,6 +31,7 @@ CIP_WSTACKING = 1
 CIP_ACC_SINGLE = 2
 CIP_PSF = 4
 CIP_NORMALISE = 8
+CIP_ASYNC = 16
 STOKES_CODES = {"I": 0, "Q": 1, "U": 2, "V": 3}
 
 # every symbol declared in include/cip.h

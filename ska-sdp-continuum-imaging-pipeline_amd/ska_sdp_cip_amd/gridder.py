@@ -71,6 +71,7 @@ def device_ms2dirty(
     single_precision_accumulation: bool = False,
     psf: bool = False,
     normalise: bool = False,
+    synchronize: bool = True,
 ) -> tuple["torch.Tensor", _lib.GridderParams]:
     """
     Device-resident ms2dirty: all tensors already in HBM on the current device.
@@ -86,6 +87,10 @@ def device_ms2dirty(
     sum of this call (the reference's (1 / total_weight) * image,
     invert.py:119-149), fused into the FFT epilogue; not for partial images
     that are summed across ranks afterwards.
+    `synchronize=False` (CIP_ASYNC) returns once the work is queued on the
+    current stream: `out` / `sum_weights` are valid in stream order (the next
+    kernel or copy on that stream sees them; the host must synchronise before
+    reading them). The planner's two mid-call readbacks still wait.
     """
     vis_codes, wgt_codes = _codes()
     if psf:
@@ -123,7 +128,7 @@ def device_ms2dirty(
         stream = torch.cuda.current_stream(uvw.device).cuda_stream
         rc = _ms2dirty_call(uvw, freq, vis, wgt, vis_codes, wgt_codes, npix_x, npix_y, pixsize_x, pixsize_y,
                             epsilon, support, do_wstacking, single_precision_accumulation, psf, normalise,
-                            stream, out, sum_weights, params)
+                            stream, out, sum_weights, params, synchronize)
     _lib.check(rc)
     return out, params
 
@@ -139,7 +144,7 @@ def _check_device_tensor(t, device, what):
 
 def _ms2dirty_call(uvw, freq, vis, wgt, vis_codes, wgt_codes, npix_x, npix_y, pixsize_x, pixsize_y, epsilon,
                    support, do_wstacking, single_precision_accumulation, psf, normalise, stream, out,
-                   sum_weights, params):
+                   sum_weights, params, synchronize=True):
     nrow = uvw.shape[0]
     nchan = freq.shape[0]
     return _lib.lib().cip_ms2dirty(
@@ -152,7 +157,8 @@ def _ms2dirty_call(uvw, freq, vis, wgt, vis_codes, wgt_codes, npix_x, npix_y, pi
         (_lib.CIP_WSTACKING if do_wstacking else 0)
         | (_lib.CIP_ACC_SINGLE if single_precision_accumulation else 0)
         | (_lib.CIP_PSF if psf else 0)
-        | (_lib.CIP_NORMALISE if normalise else 0),
+        | (_lib.CIP_NORMALISE if normalise else 0)
+        | (0 if synchronize else _lib.CIP_ASYNC),
         stream, out.data_ptr(),
         sum_weights.data_ptr() if sum_weights is not None else None, params)
 

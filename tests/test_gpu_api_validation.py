@@ -107,3 +107,27 @@ def test_workspace_release_and_thread_exit(gpu_device):
     # exited threads hold no workspace: each one would keep a 64 MiB grid and
     # a 32 MiB FFT intermediate, so three leaked workspaces lose > 280 MiB
     assert torch.cuda.mem_get_info()[0] > free1 - 32 * 1024 * 1024
+
+
+@pytest.mark.parametrize("wstack", [False, True])
+def test_async_call_matches_synchronous(gpu_device, wstack):
+    """synchronize=False (CIP_ASYNC) queues the whole invert and returns, its
+    planner on the workspace's plan stream overlapping the previous call's FFT;
+    in stream order each image and weight sum equal the synchronous call's,
+    also for back-to-back pipelined calls (alternating planner buffers)."""
+    import torch
+
+    args = _inputs(512)
+    ref, _ = gridder.device_ms2dirty(*args, support=8, normalise=True, do_wstacking=wstack)
+    ref = ref.clone()
+    outs = []
+    for _ in range(4):
+        out = torch.empty_like(ref)
+        sw = torch.empty(1, dtype=torch.float64, device=ref.device)
+        gridder.device_ms2dirty(*args, support=8, normalise=True, out=out, sum_weights=sw, synchronize=False,
+                                do_wstacking=wstack)
+        outs.append((out, sw))
+    torch.cuda.synchronize()
+    for out, sw in outs:
+        assert torch.equal(out, ref)
+        assert float(sw.item()) == float(args[3].double().sum().item())
