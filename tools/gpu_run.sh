@@ -1,5 +1,6 @@
 #!/bin/bash
-# One GPU session: parity tests, smoke, bench, kernel-trace profile.
+# One GPU session: parity tests, smoke, bench, kernel-trace profile (summary
+# over the bench's 10 profiled, synchronous calls after its timed region).
 # Every GPU step has its own time limit; steps are chained with && so the
 # first failure (fault, abort, timeout) ends the session.
 set -o pipefail
@@ -12,4 +13,4 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smok
 timeout -k 10 600 python bench.py > $OUT/bench.json 2> $OUT/bench.err && echo "bench ok" &&
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $PWD/$OUT/prof -o $ROUND --output-format csv -- \
     python3 bench.py --no-cpu-baseline > $OUT/bench_prof.json 2> $OUT/bench_prof.err && echo "prof ok" &&
-python3 tools/trace_summary.py $OUT/prof/${ROUND}_kernel_trace.csv 20 $OUT/${ROUND}_kernel_summary.md > /dev/null
+python3 tools/trace_summary.py $OUT/prof/${ROUND}_kernel_trace.csv 10 $OUT/${ROUND}_kernel_summary.md > /dev/null
