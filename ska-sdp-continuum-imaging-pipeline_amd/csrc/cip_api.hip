@@ -277,14 +277,16 @@ struct Workspace {
   // the "grid" buffer when it is known all-zero (the masked FFT pass A zeroes
   // what the scatter wrote), else NULL
   double* grid_clean = nullptr;
-  // CIP_ASYNC pipelining (cip_ms2dirty): the planner runs on plan_stream
-  // after the previous call's last scatter (ev_scattered), so it overlaps that
-  // call's FFT; the caller's stream waits for it (ev_planned). The planner
-  // outputs the FFT still reads (weight sum, dirty-tile masks) alternate
-  // between two buffer sets (parity).
+  // CIP_ASYNC pipelining (cip_ms2dirty): consecutive calls alternate between
+  // two sets of planner buffers (parity; buf() appends the parity to buffer
+  // names while parity_scope is set), so the planner of call k + 1 runs on
+  // plan_stream beside call k's scatter and FFT; it only waits for the last
+  // scatter of call k - 1 (ev_scattered[parity]), the caller's stream waits
+  // for it (ev_planned).
   hipStream_t plan_stream = nullptr;
-  hipEvent_t ev_scattered = nullptr, ev_planned = nullptr;
+  hipEvent_t ev_scattered[2] = {nullptr, nullptr}, ev_planned = nullptr;
   int parity = 0;
+  bool parity_scope = false;
 };
 
 // Zero `bytes` at `p` on the workspace's side stream, ordered after the work
@@ -340,7 +342,8 @@ static void destroy_workspace(Workspace* ws) {
     (void)hipStreamSynchronize(ws->plan_stream);
     (void)hipStreamDestroy(ws->plan_stream);
   }
-  if (ws->ev_scattered) (void)hipEventDestroy(ws->ev_scattered);
+  for (hipEvent_t e : ws->ev_scattered)
+    if (e) (void)hipEventDestroy(e);
   if (ws->ev_planned) (void)hipEventDestroy(ws->ev_planned);
   delete ws;
 }
@@ -384,7 +387,7 @@ static Workspace* workspace() {
 template <typename T>
 static T* buf(Workspace* ws, const char* name, int64_t count) {
   const size_t bytes = (size_t)(count > 0 ? count : 1) * sizeof(T);
-  DevBuf& b = ws->bufs[name];
+  DevBuf& b = ws->bufs[(ws->parity_scope && ws->parity) ? std::string(name) + "~1" : std::string(name)];
   if (b.bytes < bytes) {
     if (b.ptr && b.ptr == (void*)ws->grid_clean) ws->grid_clean = nullptr;  // a new buffer is not known zero
     if (b.ptr) (void)hipFree(b.ptr);
@@ -616,7 +619,7 @@ static int make_plan(Workspace* ws, const double* uvw, const double* fx, const R
   CIP_HIP_CHECK(launch_tile_vis(run_goff, tile_run_off, ntiles, tile_vis_off, tile_vis, s));
   if (g.ntx % 32 == 0 && grid_mask()) {
     CIP_ALLOC(dmask, uint8_t, "dirty_mask", g.ntx * g.nty * g.nplanes)
-    CIP_ALLOC(dbits, uint32_t, ws->parity ? "dirty_bits1" : "dirty_bits0", g.ntx * g.nty / 32 * g.nplanes)
+    CIP_ALLOC(dbits, uint32_t, "dirty_bits", g.ntx * g.nty / 32 * g.nplanes)
     CIP_HIP_CHECK(hipMemsetAsync(dmask, 0, (size_t)(g.ntx * g.nty * g.nplanes), s));
     CIP_HIP_CHECK(launch_dirty_mask(tile_vis, g.ntx, g.nty, g.ntw, g.support, g.nplanes, dmask, dbits, s));
     pr->dmask = dbits;
@@ -699,7 +702,7 @@ static int prepare(Workspace* ws, const double* uvw, int64_t nrow, const double*
   if (nrow < 0 || nchan < 1 || nchan > 65535) return set_error(CIP_EINVAL, "need 1 <= nchan <= 65535, nrow >= 0");
   if (nrow >= ((int64_t)1 << 32)) return set_error(CIP_EINVAL, "nrow must be < 2^32");
   CIP_ALLOC(fx, double, "fx", nchan)
-  CIP_ALLOC(red, double, ws->parity ? "red1" : "red0", 4)
+  CIP_ALLOC(red, double, "red", 4)
   // the planner's error bits: cleared here, read back with the run count
   CIP_ALLOC(err, unsigned, "err_flag", 1)
   CIP_HIP_CHECK(hipMemsetAsync(err, 0, sizeof(unsigned), s));
@@ -1047,24 +1050,27 @@ int cip_ms2dirty(const double* uvw, int64_t nrow, const double* freq, int64_t nc
   if (!ws) return set_error(CIP_EHIP, "no HIP device");
   g_prof.reset();
   hipEvent_t t_start = g_prof.mark(s);
-  // CIP_ASYNC: the planner on the workspace's plan stream, after the previous
-  // call's last scatter - it then overlaps that call's FFT on s
+  // CIP_ASYNC: the planner on the workspace's plan stream with this call's
+  // parity of planner buffers, after the last scatter of the call before the
+  // previous one (the last user of those buffers) - it then runs beside the
+  // previous call's scatter and FFT on s
   const bool pipelined = (flags & CIP_ASYNC) && !g_prof.on;
   hipStream_t ps = s;
   if (pipelined) {
     if (!ws->plan_stream) {
-      // (measured at C3: the overlapped FFT pass A runs ~4x slower beside the
-      // place pass, whatever the stream priority, so the gain is ~1.5 %)
       CIP_HIP_CHECK(hipStreamCreateWithFlags(&ws->plan_stream, hipStreamNonBlocking));
-      CIP_HIP_CHECK(hipEventCreateWithFlags(&ws->ev_scattered, hipEventDisableTiming));
       CIP_HIP_CHECK(hipEventCreateWithFlags(&ws->ev_planned, hipEventDisableTiming));
-      // the first pipelined call: the planner starts after the work already on s
-      CIP_HIP_CHECK(hipEventRecord(ws->ev_scattered, s));
+      for (hipEvent_t& e : ws->ev_scattered) {
+        CIP_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        // the first pipelined calls: the planner starts after the work already on s
+        CIP_HIP_CHECK(hipEventRecord(e, s));
+      }
     }
-    CIP_HIP_CHECK(hipStreamWaitEvent(ws->plan_stream, ws->ev_scattered, 0));
     ws->parity ^= 1;
+    CIP_HIP_CHECK(hipStreamWaitEvent(ws->plan_stream, ws->ev_scattered[ws->parity], 0));
     ps = ws->plan_stream;
-  } else {
+  } else if (ws->parity) {
+    // back to the parity-0 buffers: their last pipelined user may still be queued on s
     ws->parity = 0;
   }
   // whatever happens below, the next pipelined call's planner starts only
@@ -1075,14 +1081,16 @@ int cip_ms2dirty(const double* uvw, int64_t nrow, const double* freq, int64_t nc
     hipStream_t s;
     bool armed;
     ~ScatteredMark() {
-      if (armed) (void)hipEventRecord(ws->ev_scattered, s);
+      if (armed) (void)hipEventRecord(ws->ev_scattered[ws->parity], s);
     }
   } scattered_mark{ws, s, pipelined};
   Prepared pp;
   double* grid = nullptr;
+  ws->parity_scope = pipelined;
   int rc = prepare(ws, uvw, nrow, freq, nchan, vis, vis_dtype, wgt, wgt_dtype, npix_x, npix_y, pixsize_x, pixsize_y,
                    epsilon, support, do_wstacking, packed, nullptr, ps, &pp,
                    (overlap_zero() && !pipelined) ? &grid : nullptr);
+  ws->parity_scope = false;
   if (pipelined) {
     // s continues once the plan exists (also after a failed one: nothing then runs on it)
     CIP_HIP_CHECK(hipEventRecord(ws->ev_planned, ps));
@@ -1112,7 +1120,7 @@ int cip_ms2dirty(const double* uvw, int64_t nrow, const double* freq, int64_t nc
     if (rc != CIP_OK) return rc;
     // the next pipelined call's planner may overwrite the plan from here on
     if (pipelined && p == g.nplanes - 1) {
-      CIP_HIP_CHECK(hipEventRecord(ws->ev_scattered, s));
+      CIP_HIP_CHECK(hipEventRecord(ws->ev_scattered[ws->parity], s));
       scattered_mark.armed = false;
     }
     rc = plane_to_dirty(st, g, p, grid, dirty_out, s, dmask ? dmask + p * (g.ntx * g.nty / 32) : nullptr,
