@@ -138,6 +138,8 @@ def main():
                     help="packed single-precision accumulation class (CIP_ACC_SINGLE; the precision class of the "
                          "reference's float32 ducc0 call) - secondary measurement, not the f64 metric")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--sync", action="store_true",
+                    help="synchronous steps (diagnostic: per-kernel times without the pipelined overlap)")
     ap.add_argument("--cpu-sample-rows", type=int, default=8192)
     args = ap.parse_args()
 
@@ -192,7 +194,7 @@ def main():
     log(f"[bench] rank {rank}/{world} config {args.config}: {nvis:,} vis/GPU, {npix}^2 image, "
         f"pixsize {px:.3e} rad, support {args.support}, wstacking={args.wstacking}")
     for _ in range(args.warmup):
-        step()
+        step(sync=args.sync)
     drain()
     dirty, sumw = bufs[0]
     _, params = gridder.device_ms2dirty(uvw_d, freq_d, vis_d, wgt_d, npix, npix, px, px, support=args.support,
@@ -203,7 +205,7 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step()
+        step(sync=args.sync)
     drain()
     torch.cuda.synchronize()
     if world > 1:

@@ -224,6 +224,48 @@ __device__ __forceinline__ bool place_vis(double u_m, double v_m, double w_m, do
   return ok;
 }
 
+// The planner's placement: the footprint origins place_vis computes (the same
+// integers), without the kernel variables and without divergent branches in
+// the common case - |origin| < 2^30 and within one grid period of the grid,
+// so one select-add per axis wraps it; a wave with any other lane takes
+// place_vis itself (a wave-uniform branch).
+__device__ __forceinline__ bool place_origin(double u_m, double v_m, double w_m, double fx, const GridGeometry& g,
+                                             int* ix0, int* iy0, int64_t* iw0) {
+#pragma clang fp contract(off)
+  const int hw = g.support / 2;
+  const double x = (u_m * fx) * g.scale_u + (double)(g.nu / 2);
+  const double y = (v_m * fx) * g.scale_v + (double)(g.nv / 2);
+  const double flx = floor(x - (double)hw), fly = floor(y - (double)hw);
+  const int nu = (int)g.nu, nv = (int)g.nv;
+  const bool small = fabs(flx) < 1073741824.0 && fabs(fly) < 1073741824.0;
+  int ix = small ? (int)flx + 1 : 0, iy = small ? (int)fly + 1 : 0;
+  ix = ix >= nu ? ix - nu : ix;
+  ix = ix < 0 ? ix + nu : ix;
+  iy = iy >= nv ? iy - nv : iy;
+  iy = iy < 0 ? iy + nv : iy;
+  const bool fits = small & (ix >= 0) & (ix < nu) & (iy >= 0) & (iy < nv);
+  if (__ballot(!fits) != 0ull) {
+    int64_t a, b, c;
+    double ya, yb, yc;
+    const bool ok = place_vis(u_m, v_m, w_m, fx, g, &a, &ya, &b, &yb, &c, &yc);
+    *ix0 = (int)a;
+    *iy0 = (int)b;
+    *iw0 = c;
+    return ok;
+  }
+  *ix0 = ix;
+  *iy0 = iy;
+  if (g.do_wstacking) {
+    const double xw = ((w_m * fx) - g.w0) / g.dw;
+    double yw;
+    footprint(xw, hw, iw0, &yw);
+    // |x|, |y| < 2^30 + W here: finite and inside place_vis's bound
+    return (*iw0 >= 0) & (*iw0 + g.support <= g.nplanes);
+  }
+  *iw0 = 0;
+  return true;
+}
+
 // Flattened MS index i = row * nchan + c (< 2^52) -> (row, c): i * (1/nchan)
 // in fp64 is within one of the quotient (one compare fixes it).
 __device__ __forceinline__ void split_index64(int64_t i, int64_t nchan, double inv_nchan, int64_t* row,

@@ -192,6 +192,9 @@ hipError_t launch_w_range(const double* uvw, int64_t nrow, double fxmin, double 
 constexpr int kPlaceSegs = 64;  // 64-visibility segments per place block (4096 visibilities)
 constexpr uint32_t kNoKey = 0xffffffffu;  // visibility off the grid (tile keys are < 2^32 - 1)
 
+#ifndef CIP_PLACE_ABL
+#define CIP_PLACE_ABL 0  // experiment builds only: 1 no visibility load, 2 no run parking, 3 no class store
+#endif
 #ifndef CIP_PLACE_WAVES
 #define CIP_PLACE_WAVES 1  // min waves per SIMD the place pass is compiled for
 #endif
@@ -229,10 +232,12 @@ __global__ __launch_bounds__(256, CIP_PLACE_WAVES) void plan_place_kernel(const 
   for (int64_t seg = (int64_t)blockIdx.x * kPlaceSegs + wave; seg < seg_end; seg += 4) {
     const int64_t i = seg * 64 + lane;
     const bool valid = i < nvis;
-    uint32_t key = kNoKey;
     int64_t r = r0, c = c0;
+    // lanes past the end load index 0's data (no divergent branch around the
+    // loads); their results are masked by `valid`
+    const int64_t il = valid ? i : 0;
     if (ragged) {
-      if (valid) vis_rowchan(m, i, &r, &c);
+      vis_rowchan(m, il, &r, &c);
     } else {
       c0 += step_c;
       r0 += step_r;
@@ -241,29 +246,35 @@ __global__ __launch_bounds__(256, CIP_PLACE_WAVES) void plan_place_kernel(const 
         ++r0;
       }
     }
-    bool bad = false;
-    if (valid) {
-      // position loads first: the visibility load of a PSF call is a branch,
-      // and the wait inside it then covers every load (one memory round trip)
-      const double u = uvw[3 * r], v = uvw[3 * r + 1], w = uvw[3 * r + 2], f = fx[c];
-      const double wt = load_weight<WK>(wgt, i);
-      double vr, vi;
-      load_vis(vis, i, vr, vi);
-      // zero-weight visibilities are skipped by the scatter, whatever they hold
-      const double a = wt == 0.0 ? 0.0 : fabs(wt) * fmax(fabs(vr), fabs(vi));
-      nonfinite = nonfinite || (wt != 0.0 && !(isfinite(wt) && isfinite(vr) && isfinite(vi)));
-      wsum += wt;
-      wvmax = fmax(wvmax, a);
-      int64_t ix0, iy0, iw0;
-      double yu, yv, yw;
-      if (place_vis(u, v, w, f, g, &ix0, &yu, &iy0, &yv, &iw0, &yw)) {
-        key = (uint32_t)tile_key(ix0, iy0, iw0, g);
-        if (vis_class) vis_class[i] = (uint8_t)((((unsigned)ix0 % kTile) * P + (unsigned)iy0 % kTile) & 31u);
-      } else {
-        bad = true;
-        if (vis_class) vis_class[i] = 0;
-      }
-    }
+    const int64_t rl = valid ? r : 0, cl = valid ? c : 0;
+    // position loads first: the visibility load of a PSF call is a branch,
+    // and the wait inside it then covers every load (one memory round trip)
+    const double u = uvw[3 * rl], v = uvw[3 * rl + 1], w = uvw[3 * rl + 2], f = fx[cl];
+    const double wt = load_weight<WK>(wgt, il);
+    double vr, vi;
+#if CIP_PLACE_ABL == 1
+    vr = 1.0; vi = 0.0;
+#else
+    load_vis(vis, il, vr, vi);
+#endif
+    // zero-weight visibilities are skipped by the scatter, whatever they hold
+    const bool counted = valid & (wt != 0.0);
+    const double a = counted ? fabs(wt) * fmax(fabs(vr), fabs(vi)) : 0.0;
+    nonfinite = nonfinite | (counted && !(isfinite(wt) && isfinite(vr) && isfinite(vi)));
+    wsum = valid ? wsum + wt : wsum;
+    wvmax = fmax(wvmax, a);
+    int ix0, iy0;
+    int64_t iw0;
+    const bool ok = place_origin(u, v, w, f, g, &ix0, &iy0, &iw0);
+    // the tile key modulo 2^32 (keys are < 2^32 - 1)
+    const uint32_t key = (valid & ok) ? (((uint32_t)iw0 * (uint32_t)g.nty + (uint32_t)iy0 / (uint32_t)kTile) *
+                                             (uint32_t)g.ntx + (uint32_t)ix0 / (uint32_t)kTile)
+                                      : kNoKey;
+    const bool bad = valid & !ok;
+#if CIP_PLACE_ABL != 3
+    if (vis_class && valid)
+      vis_class[i] = ok ? (uint8_t)((((unsigned)ix0 % kTile) * P + (unsigned)iy0 % kTile) & 31u) : (uint8_t)0;
+#endif
     if (__ballot(bad) != 0ull && lane == 0) atomicOr(err_flag, 1u);
     const uint32_t prev = __shfl_up(key, 1, 64);
     const uint32_t prev_r = __shfl_up((uint32_t)r, 1, 64);  // rows < 2^32
@@ -276,7 +287,11 @@ __global__ __launch_bounds__(256, CIP_PLACE_WAVES) void plan_place_kernel(const 
     unsigned wbase = 0;
     if (lane == 0 && emits) wbase = atomicAdd(&s_nruns, (unsigned)__popcll(emits));
     wbase = __shfl(wbase, 0, 64);
+#if CIP_PLACE_ABL == 2
+    if (emit && key == 0x7fffffffu) {
+#else
     if (emit) {
+#endif
       const unsigned long long above = starts & ~((2ull << lane) - 1ull);  // lane 63: 2 << 63 == 0
       const int next = above ? (__ffsll((long long)above) - 1) : nvalid;
       const int64_t slot = (int64_t)blockIdx.x * kPlaceSegs * 64 + wbase + __popcll(emits & ((1ull << lane) - 1ull));
