@@ -176,11 +176,13 @@ def main():
             pending[k].wait()
         dirty, sumw = bufs[k]
         # sync=False (CIP_ASYNC): the call returns once its work is queued, so
-        # the host prepares step k + 1 while the GPU finishes step k
+        # the host prepares step k + 1 while the GPU finishes step k; the
+        # inputs are resident and unchanged (CIP_PIPELINE), so step k + 1's
+        # planner runs beside step k's scatter and FFT
         gridder.device_ms2dirty(uvw_d, freq_d, vis_d, wgt_d, npix, npix, px, px, support=args.support,
                                 do_wstacking=args.wstacking, out=dirty, sum_weights=sumw,
                                 single_precision_accumulation=args.single, normalise=world == 1,
-                                synchronize=sync)
+                                synchronize=sync, resident_inputs=not sync)
         # RCCL reduce of the partial images + weights to rank 0, normalised there
         # (one GPU: the image is already normalised in the FFT epilogue)
         pending[k] = reduce_images(dirty, sumw, dst=0, async_op=True, normalise=world > 1)

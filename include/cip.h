@@ -62,6 +62,16 @@ extern "C" {
                           * planner's two readbacks still synchronise mid-call).
                           * dirty_out / sum_wgt_out are valid when the stream
                           * reaches this point. Ignored while profiling is on. */
+#define CIP_PIPELINE 32  /* with CIP_ASYNC (cip_ms2dirty): the caller promises
+                          * that uvw, freq, vis and wgt were complete before the
+                          * previous CIP_ASYNC call of this thread returned and
+                          * stay unchanged (resident inputs, e.g. re-imaging the
+                          * same chunk): the planner then runs on the
+                          * workspace's own stream beside the previous calls'
+                          * scatter and FFT instead of after everything queued
+                          * on hip_stream. Without it, CIP_ASYNC work starts in
+                          * hip_stream order. Outputs are in stream order
+                          * either way. */
 #define CIP_ACC_SINGLE 2 /* complex64 only: single-precision accumulation
                           * class, the reference's ducc0 float gridding (re/im
                           * packed in one 64-bit fixed-point LDS cell, W^2

@@ -284,10 +284,23 @@ struct Workspace {
   // scatter of call k - 1 (ev_scattered[parity]), the caller's stream waits
   // for it (ev_planned).
   hipStream_t plan_stream = nullptr;
-  hipEvent_t ev_scattered[2] = {nullptr, nullptr}, ev_planned = nullptr;
+  hipEvent_t ev_scattered[2] = {nullptr, nullptr}, ev_planned = nullptr, ev_entry = nullptr;
   int parity = 0;
   bool parity_scope = false;
+  // a planner ran on a caller's stream (parity-0 buffer names) since the last
+  // pipelined call: the next pipelined planner waits for that stream
+  bool plan_unscoped = false;
+  // the stream of the last CIP_ASYNC call, whose work may still be queued: a
+  // call on another stream first waits for it (the workspace is shared)
+  hipStream_t async_stream = nullptr;
 };
+
+static int settle_async(Workspace* ws, hipStream_t s) {
+  hipStream_t prev = ws->async_stream;
+  ws->async_stream = nullptr;
+  if (prev && prev != s) CIP_HIP_CHECK(hipStreamSynchronize(prev));
+  return CIP_OK;
+}
 
 // Zero `bytes` at `p` on the workspace's side stream, ordered after the work
 // already queued on s; join_side() makes s wait for it.
@@ -345,6 +358,7 @@ static void destroy_workspace(Workspace* ws) {
   for (hipEvent_t e : ws->ev_scattered)
     if (e) (void)hipEventDestroy(e);
   if (ws->ev_planned) (void)hipEventDestroy(ws->ev_planned);
+  if (ws->ev_entry) (void)hipEventDestroy(ws->ev_entry);
   delete ws;
 }
 
@@ -696,6 +710,7 @@ static int prepare(Workspace* ws, const double* uvw, int64_t nrow, const double*
                    double px, double py, double epsilon, int support, int do_wstacking, bool packed,
                    const cip_gridder_params* given, hipStream_t s, Prepared* out, double** grid_out = nullptr,
                    const RaggedRows* ragged = nullptr) {
+  if (!ws->parity_scope) ws->plan_unscoped = true;
   if (!vis_dtype_ok(vis_dtype)) return set_error(CIP_EINVAL, "vis dtype must be complex64 or complex128");
   if (!wgt_dtype_ok(wgt_dtype)) return set_error(CIP_EINVAL, "wgt dtype must be float32, float64 or none");
   if (wgt == nullptr) wgt_dtype = CIP_NONE;
@@ -992,6 +1007,7 @@ static int grid_accumulate(const double* uvw, int64_t nrow, const double* freq, 
   hipStream_t s = (hipStream_t)hip_stream;
   Workspace* ws = workspace();
   if (!ws) return set_error(CIP_EHIP, "no HIP device");
+  if (const int sr = settle_async(ws, s); sr != CIP_OK) return sr;
   g_prof.reset();
   hipEvent_t t_start = g_prof.mark(s);
   Prepared pp;
@@ -1034,7 +1050,7 @@ int cip_ms2dirty(const double* uvw, int64_t nrow, const double* freq, int64_t nc
                  double pixsize_y, double epsilon, int support, int flags, void* hip_stream,
                  double* dirty_out, double* sum_wgt_out, cip_gridder_params* params_out) {
   g_last_error.clear();
-  if (flags & ~(CIP_WSTACKING | CIP_ACC_SINGLE | CIP_PSF | CIP_NORMALISE | CIP_ASYNC))
+  if (flags & ~(CIP_WSTACKING | CIP_ACC_SINGLE | CIP_PSF | CIP_NORMALISE | CIP_ASYNC | CIP_PIPELINE))
     return set_error(CIP_EINVAL, "unknown flags");
   const int do_wstacking = (flags & CIP_WSTACKING) ? 1 : 0;
   const bool normalise = (flags & CIP_NORMALISE) != 0;
@@ -1048,23 +1064,33 @@ int cip_ms2dirty(const double* uvw, int64_t nrow, const double* freq, int64_t nc
   hipStream_t s = (hipStream_t)hip_stream;
   Workspace* ws = workspace();
   if (!ws) return set_error(CIP_EHIP, "no HIP device");
+  if (const int sr = settle_async(ws, s); sr != CIP_OK) return sr;
   g_prof.reset();
   hipEvent_t t_start = g_prof.mark(s);
-  // CIP_ASYNC: the planner on the workspace's plan stream with this call's
-  // parity of planner buffers, after the last scatter of the call before the
-  // previous one (the last user of those buffers) - it then runs beside the
-  // previous call's scatter and FFT on s
-  const bool pipelined = (flags & CIP_ASYNC) && !g_prof.on;
+  // CIP_ASYNC | CIP_PIPELINE (resident inputs): the planner on the
+  // workspace's plan stream with this call's parity of planner buffers, after
+  // the last scatter of the call before the previous one (the last user of
+  // those buffers) - it then runs beside the previous call's scatter and FFT
+  // on s. It does not wait for s: the caller promised the inputs are complete.
+  const bool pipelined = (flags & CIP_ASYNC) && (flags & CIP_PIPELINE) && !g_prof.on;
   hipStream_t ps = s;
   if (pipelined) {
     if (!ws->plan_stream) {
       CIP_HIP_CHECK(hipStreamCreateWithFlags(&ws->plan_stream, hipStreamNonBlocking));
       CIP_HIP_CHECK(hipEventCreateWithFlags(&ws->ev_planned, hipEventDisableTiming));
+      CIP_HIP_CHECK(hipEventCreateWithFlags(&ws->ev_entry, hipEventDisableTiming));
       for (hipEvent_t& e : ws->ev_scattered) {
         CIP_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         // the first pipelined calls: the planner starts after the work already on s
         CIP_HIP_CHECK(hipEventRecord(e, s));
       }
+    }
+    if (ws->plan_unscoped) {
+      // a planner ran on s since the last pipelined call: its buffers (parity
+      // 0) may still be read there
+      CIP_HIP_CHECK(hipEventRecord(ws->ev_entry, s));
+      CIP_HIP_CHECK(hipStreamWaitEvent(ws->plan_stream, ws->ev_entry, 0));
+      ws->plan_unscoped = false;
     }
     ws->parity ^= 1;
     CIP_HIP_CHECK(hipStreamWaitEvent(ws->plan_stream, ws->ev_scattered[ws->parity], 0));
@@ -1139,6 +1165,7 @@ int cip_ms2dirty(const double* uvw, int64_t nrow, const double* freq, int64_t nc
   // of this thread in stream order, so nothing on the host waits for it; the
   // grid-clean mark holds in stream order too
   if (!(flags & CIP_ASYNC) || g_prof.on) CIP_HIP_CHECK(hipStreamSynchronize(s));
+  else ws->async_stream = s;
   if (clean) ws->grid_clean = grid;
   g_prof.finish();
   return CIP_OK;
@@ -1179,6 +1206,7 @@ int cip_grid_to_dirty(double* grids, const cip_gridder_params* params, int64_t n
   hipStream_t s = (hipStream_t)hip_stream;
   Workspace* ws = workspace();
   if (!ws) return set_error(CIP_EHIP, "no HIP device");
+  if (const int sr = settle_async(ws, s); sr != CIP_OK) return sr;
   g_prof.reset();
   hipEvent_t t_start = g_prof.mark(s);
   const GridGeometry g = geometry(*params, pixsize_x, pixsize_y);
@@ -1208,6 +1236,7 @@ int cip_grid_plane(const double* uvw, int64_t nrow, const double* freq, int64_t 
   hipStream_t s = (hipStream_t)hip_stream;
   Workspace* ws = workspace();
   if (!ws) return set_error(CIP_EHIP, "no HIP device");
+  if (const int sr = settle_async(ws, s); sr != CIP_OK) return sr;
   g_prof.reset();
   hipEvent_t t_start = g_prof.mark(s);
   Prepared pp;
@@ -1231,6 +1260,7 @@ int cip_tile_runs(const double* uvw, int64_t nrow, const double* freq, int64_t n
   hipStream_t s = (hipStream_t)hip_stream;
   Workspace* ws = workspace();
   if (!ws) return set_error(CIP_EHIP, "no HIP device");
+  if (const int sr = settle_async(ws, s); sr != CIP_OK) return sr;
   if (nrow == 0) {
     *n_runs = 0;
     return CIP_OK;
@@ -1292,6 +1322,7 @@ int cip_facet_rephase(const double* uvw, int64_t nrow, const double* freq, int64
   hipStream_t s = (hipStream_t)hip_stream;
   Workspace* ws = workspace();
   if (!ws) return set_error(CIP_EHIP, "no HIP device");
+  if (const int sr = settle_async(ws, s); sr != CIP_OK) return sr;
   CIP_ALLOC(delay, double, "facet_delay", nrow)
   // Q: the minimal rotation taking z = (0, 0, 1) to s0 (Rodrigues about z x s0)
   const double n0 = std::sqrt(1.0 - l0 * l0 - m0 * m0);

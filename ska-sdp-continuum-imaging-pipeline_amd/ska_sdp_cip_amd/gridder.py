@@ -72,6 +72,7 @@ def device_ms2dirty(
     psf: bool = False,
     normalise: bool = False,
     synchronize: bool = True,
+    resident_inputs: bool = False,
 ) -> tuple["torch.Tensor", _lib.GridderParams]:
     """
     Device-resident ms2dirty: all tensors already in HBM on the current device.
@@ -91,7 +92,14 @@ def device_ms2dirty(
     current stream: `out` / `sum_weights` are valid in stream order (the next
     kernel or copy on that stream sees them; the host must synchronise before
     reading them). The planner's two mid-call readbacks still wait.
+    `resident_inputs=True` (CIP_PIPELINE, with `synchronize=False` only)
+    promises that uvw / freq / vis / wgt were complete before the previous
+    asynchronous call returned and stay unchanged (resident data, as in the
+    benchmark): the planner of this call then runs beside the previous call's
+    scatter and FFT instead of after all work queued on the stream.
     """
+    if resident_inputs and synchronize:
+        raise ValueError("resident_inputs=True needs synchronize=False")
     vis_codes, wgt_codes = _codes()
     if psf:
         vis = None  # never read
@@ -128,7 +136,7 @@ def device_ms2dirty(
         stream = torch.cuda.current_stream(uvw.device).cuda_stream
         rc = _ms2dirty_call(uvw, freq, vis, wgt, vis_codes, wgt_codes, npix_x, npix_y, pixsize_x, pixsize_y,
                             epsilon, support, do_wstacking, single_precision_accumulation, psf, normalise,
-                            stream, out, sum_weights, params, synchronize)
+                            stream, out, sum_weights, params, synchronize, resident_inputs)
     _lib.check(rc)
     return out, params
 
@@ -144,7 +152,7 @@ def _check_device_tensor(t, device, what):
 
 def _ms2dirty_call(uvw, freq, vis, wgt, vis_codes, wgt_codes, npix_x, npix_y, pixsize_x, pixsize_y, epsilon,
                    support, do_wstacking, single_precision_accumulation, psf, normalise, stream, out,
-                   sum_weights, params, synchronize=True):
+                   sum_weights, params, synchronize=True, resident_inputs=False):
     nrow = uvw.shape[0]
     nchan = freq.shape[0]
     return _lib.lib().cip_ms2dirty(
@@ -158,7 +166,8 @@ def _ms2dirty_call(uvw, freq, vis, wgt, vis_codes, wgt_codes, npix_x, npix_y, pi
         | (_lib.CIP_ACC_SINGLE if single_precision_accumulation else 0)
         | (_lib.CIP_PSF if psf else 0)
         | (_lib.CIP_NORMALISE if normalise else 0)
-        | (0 if synchronize else _lib.CIP_ASYNC),
+        | (0 if synchronize else _lib.CIP_ASYNC)
+        | (_lib.CIP_PIPELINE if resident_inputs else 0),
         stream, out.data_ptr(),
         sum_weights.data_ptr() if sum_weights is not None else None, params)
 

@@ -109,12 +109,13 @@ def test_workspace_release_and_thread_exit(gpu_device):
     assert torch.cuda.mem_get_info()[0] > free1 - 32 * 1024 * 1024
 
 
-@pytest.mark.parametrize("wstack", [False, True])
-def test_async_call_matches_synchronous(gpu_device, wstack):
-    """synchronize=False (CIP_ASYNC) queues the whole invert and returns, its
-    planner on the workspace's plan stream overlapping the previous call's FFT;
-    in stream order each image and weight sum equal the synchronous call's,
-    also for back-to-back pipelined calls (alternating planner buffers)."""
+@pytest.mark.parametrize("wstack,resident", [(False, True), (True, True), (False, False)])
+def test_async_call_matches_synchronous(gpu_device, wstack, resident):
+    """synchronize=False (CIP_ASYNC) queues the whole invert and returns; with
+    resident_inputs=True (CIP_PIPELINE) its planner runs on the workspace's plan
+    stream beside the previous calls' scatter and FFT. In stream order each
+    image and weight sum equal the synchronous call's, also for back-to-back
+    pipelined calls (alternating planner buffers)."""
     import torch
 
     args = _inputs(512)
@@ -125,9 +126,38 @@ def test_async_call_matches_synchronous(gpu_device, wstack):
         out = torch.empty_like(ref)
         sw = torch.empty(1, dtype=torch.float64, device=ref.device)
         gridder.device_ms2dirty(*args, support=8, normalise=True, out=out, sum_weights=sw, synchronize=False,
-                                do_wstacking=wstack)
+                                resident_inputs=resident, do_wstacking=wstack)
         outs.append((out, sw))
     torch.cuda.synchronize()
     for out, sw in outs:
         assert torch.equal(out, ref)
         assert float(sw.item()) == float(args[3].double().sum().item())
+
+
+def test_async_call_sees_inputs_written_on_the_stream(gpu_device):
+    """Without resident_inputs, an asynchronous call starts in stream order: a
+    kernel that rewrites the visibilities between two calls is seen by the
+    second call (its planner must not run ahead of the stream)."""
+    import torch
+
+    uvw, f, vis, w, nx, ny, px, py = _inputs(512)
+    vis2 = vis * 3.0
+    ref1, _ = gridder.device_ms2dirty(uvw, f, vis, w, nx, ny, px, py, support=8)
+    ref1 = ref1.clone()
+    ref2, _ = gridder.device_ms2dirty(uvw, f, vis2, w, nx, ny, px, py, support=8)
+    ref2 = ref2.clone()
+    torch.cuda.synchronize()
+    work = vis.clone()
+    outs = [torch.empty_like(ref1) for _ in range(4)]
+    for k, out in enumerate(outs):
+        # stream order: the copy runs after the previous call's work is queued
+        work.copy_(vis if k % 2 == 0 else vis2)
+        gridder.device_ms2dirty(uvw, f, work, w, nx, ny, px, py, support=8, out=out, synchronize=False)
+    torch.cuda.synchronize()
+    for k, out in enumerate(outs):
+        assert torch.equal(out, ref1 if k % 2 == 0 else ref2)
+
+
+def test_resident_inputs_needs_async(gpu_device):
+    with pytest.raises(ValueError):
+        gridder.device_ms2dirty(*_inputs(), support=8, synchronize=True, resident_inputs=True)
