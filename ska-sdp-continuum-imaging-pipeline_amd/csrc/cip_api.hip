@@ -280,11 +280,12 @@ struct Workspace {
   // CIP_ASYNC pipelining (cip_ms2dirty): consecutive calls alternate between
   // two sets of planner buffers (parity; buf() appends the parity to buffer
   // names while parity_scope is set), so the planner of call k + 1 runs on
-  // plan_stream beside call k's scatter and FFT; it only waits for the last
-  // scatter of call k - 1 (ev_scattered[parity]), the caller's stream waits
-  // for it (ev_planned).
+  // plan_stream beside call k's scatter and FFT; it only waits for
+  // call k - 1's work on the caller's stream (ev_done[parity]: its scatter
+  // read the plan, its FFT the masks and weight sum); the caller's stream
+  // waits for the plan (ev_planned).
   hipStream_t plan_stream = nullptr;
-  hipEvent_t ev_scattered[2] = {nullptr, nullptr}, ev_planned = nullptr, ev_entry = nullptr;
+  hipEvent_t ev_done[2] = {nullptr, nullptr}, ev_planned = nullptr, ev_entry = nullptr;
   int parity = 0;
   bool parity_scope = false;
   // a planner ran on a caller's stream (parity-0 buffer names) since the last
@@ -355,7 +356,7 @@ static void destroy_workspace(Workspace* ws) {
     (void)hipStreamSynchronize(ws->plan_stream);
     (void)hipStreamDestroy(ws->plan_stream);
   }
-  for (hipEvent_t e : ws->ev_scattered)
+  for (hipEvent_t e : ws->ev_done)
     if (e) (void)hipEventDestroy(e);
   if (ws->ev_planned) (void)hipEventDestroy(ws->ev_planned);
   if (ws->ev_entry) (void)hipEventDestroy(ws->ev_entry);
@@ -1079,7 +1080,7 @@ int cip_ms2dirty(const double* uvw, int64_t nrow, const double* freq, int64_t nc
       CIP_HIP_CHECK(hipStreamCreateWithFlags(&ws->plan_stream, hipStreamNonBlocking));
       CIP_HIP_CHECK(hipEventCreateWithFlags(&ws->ev_planned, hipEventDisableTiming));
       CIP_HIP_CHECK(hipEventCreateWithFlags(&ws->ev_entry, hipEventDisableTiming));
-      for (hipEvent_t& e : ws->ev_scattered) {
+      for (hipEvent_t& e : ws->ev_done) {
         CIP_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         // the first pipelined calls: the planner starts after the work already on s
         CIP_HIP_CHECK(hipEventRecord(e, s));
@@ -1093,23 +1094,23 @@ int cip_ms2dirty(const double* uvw, int64_t nrow, const double* freq, int64_t nc
       ws->plan_unscoped = false;
     }
     ws->parity ^= 1;
-    CIP_HIP_CHECK(hipStreamWaitEvent(ws->plan_stream, ws->ev_scattered[ws->parity], 0));
+    CIP_HIP_CHECK(hipStreamWaitEvent(ws->plan_stream, ws->ev_done[ws->parity], 0));
     ps = ws->plan_stream;
   } else if (ws->parity) {
     // back to the parity-0 buffers: their last pipelined user may still be queued on s
     ws->parity = 0;
   }
-  // whatever happens below, the next pipelined call's planner starts only
-  // after everything this call queued on s so far (an early error return
-  // included); the normal path records the event right after the last scatter
-  struct ScatteredMark {
+  // the next pipelined call with this parity plans only after everything this
+  // call queued on s - the scatter reads the plan, the FFT the dirty-tile
+  // masks and the weight sum (recorded on every return path)
+  struct DoneMark {
     Workspace* ws;
     hipStream_t s;
     bool armed;
-    ~ScatteredMark() {
-      if (armed) (void)hipEventRecord(ws->ev_scattered[ws->parity], s);
+    ~DoneMark() {
+      if (armed) (void)hipEventRecord(ws->ev_done[ws->parity], s);
     }
-  } scattered_mark{ws, s, pipelined};
+  } done_mark{ws, s, pipelined};
   Prepared pp;
   double* grid = nullptr;
   ws->parity_scope = pipelined;
@@ -1144,11 +1145,6 @@ int cip_ms2dirty(const double* uvw, int64_t nrow, const double* freq, int64_t nc
   for (int64_t p = 0; p < g.nplanes; ++p) {
     rc = scatter_plane(pp, p, uvw, vis, vis_dtype, wgt, wgt_dtype, st.fast, grid, s, clean);
     if (rc != CIP_OK) return rc;
-    // the next pipelined call's planner may overwrite the plan from here on
-    if (pipelined && p == g.nplanes - 1) {
-      CIP_HIP_CHECK(hipEventRecord(ws->ev_scattered[ws->parity], s));
-      scattered_mark.armed = false;
-    }
     rc = plane_to_dirty(st, g, p, grid, dirty_out, s, dmask ? dmask + p * (g.ntx * g.nty / 32) : nullptr,
                         normalise ? pp.red : nullptr);
     if (rc != CIP_OK) return rc;

@@ -118,20 +118,27 @@ def test_async_call_matches_synchronous(gpu_device, wstack, resident):
     pipelined calls (alternating planner buffers)."""
     import torch
 
-    args = _inputs(512)
-    ref, _ = gridder.device_ms2dirty(*args, support=8, normalise=True, do_wstacking=wstack)
-    ref = ref.clone()
+    a = _inputs(512)
+    # a second resident input set (other visibilities and weights): calls
+    # alternate between the two, so consecutive plans, dirty-tile masks and
+    # weight sums differ
+    b = (a[0], a[1], a[2] * (0.5 - 2.0j), a[3] * 0.25 + 1.0) + a[4:]
+    sets = [a, b]
+    refs = []
+    for args in sets:
+        ref, _ = gridder.device_ms2dirty(*args, support=8, normalise=True, do_wstacking=wstack)
+        refs.append(ref.clone())
     outs = []
-    for _ in range(4):
-        out = torch.empty_like(ref)
-        sw = torch.empty(1, dtype=torch.float64, device=ref.device)
-        gridder.device_ms2dirty(*args, support=8, normalise=True, out=out, sum_weights=sw, synchronize=False,
-                                resident_inputs=resident, do_wstacking=wstack)
+    for k in range(6):
+        out = torch.empty_like(refs[0])
+        sw = torch.empty(1, dtype=torch.float64, device=out.device)
+        gridder.device_ms2dirty(*sets[k % 2], support=8, normalise=True, out=out, sum_weights=sw,
+                                synchronize=False, resident_inputs=resident, do_wstacking=wstack)
         outs.append((out, sw))
     torch.cuda.synchronize()
-    for out, sw in outs:
-        assert torch.equal(out, ref)
-        assert float(sw.item()) == float(args[3].double().sum().item())
+    for k, (out, sw) in enumerate(outs):
+        assert torch.equal(out, refs[k % 2])
+        assert float(sw.item()) == float(sets[k % 2][3].double().sum().item())
 
 
 def test_async_call_sees_inputs_written_on_the_stream(gpu_device):
