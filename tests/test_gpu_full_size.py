@@ -59,8 +59,9 @@ def _invert(c, vis=None, **kw):
     return img, prm
 
 
-def _dft_pixels(c, pix):
-    """sum_{r,c} w Re{V exp(2 pi i (f/c) (u l + v m))} at pixels (i, j)."""
+def _dft_pixels(c, pix, apply_w):
+    """sum_{r,c} w Re{V exp(2 pi i (f/c) (u l + v m - w (n - 1)))} / n at
+    pixels (i, j) (2-D: without the w term and n)."""
     import torch
 
     uvw, f, vis, wgt, px, _ = c
@@ -68,26 +69,30 @@ def _dft_pixels(c, pix):
     out = []
     for i, j in pix:
         l, m = (i - NPIX // 2) * px, (j - NPIX // 2) * px
+        e = l * l + m * m
+        nm1 = -e / (math.sqrt(1.0 - e) + 1.0) if apply_w else 0.0
         acc = torch.zeros((), dtype=torch.float64, device=vis.device)
         for r0 in range(0, ROWS, 65_536):
             r1 = min(r0 + 65_536, ROWS)
-            path = uvw[r0:r1, 0] * l + uvw[r0:r1, 1] * m
+            path = uvw[r0:r1, 0] * l + uvw[r0:r1, 1] * m - uvw[r0:r1, 2] * nm1
             ph = (2.0 * math.pi) * path[:, None] * fx[None, :]
             v = vis[r0:r1].to(torch.complex128)
             acc += (wgt[r0:r1].double() * (v.real * torch.cos(ph) - v.imag * torch.sin(ph))).sum()
-        out.append(float(acc.item()))
+        out.append(float(acc.item()) / (nm1 + 1.0))
     return np.array(out)
 
 
-def test_c3_sampled_pixels_equal_dft(c3):
+@pytest.mark.parametrize("wstack", [False, True])
+def test_c3_sampled_pixels_equal_dft(c3, wstack):
     import torch
 
-    img, prm = _invert(c3)
-    assert (prm.nu, prm.nv, prm.nplanes) == (2 * NPIX, 2 * NPIX, 1)
+    img, prm = _invert(c3, do_wstacking=wstack)
+    assert (prm.nu, prm.nv) == (2 * NPIX, 2 * NPIX)
+    assert (prm.nplanes > 1) if wstack else (prm.nplanes == 1)
     rng = np.random.default_rng(3)
     pix = [(NPIX // 2, NPIX // 2), (0, 0), (NPIX - 1, NPIX - 1), (NPIX // 2, 0)]
     pix += [tuple(int(x) for x in rng.integers(0, NPIX, 2)) for _ in range(4)]
-    ref = _dft_pixels(c3, pix)
+    ref = _dft_pixels(c3, pix, wstack)
     got = np.array([float(img[i, j].item()) for i, j in pix])
     sumw = float(c3[3].double().sum().item())
     err = np.abs(got - ref).max() / sumw
