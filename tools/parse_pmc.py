@@ -14,14 +14,11 @@ from pathlib import Path
 
 
 def short(name: str) -> str:
-    name = name.split("(")[0]
-    for key in ("scatter_kernel", "plan_place_kernel", "radix_scatter", "radix_hist", "order_kernel",
-                "fft_rows_kernel", "fft_cols_kernel", "fft_rtc", "transpose_rtc", "crop_correct", "scan_local",
-                "scan_add", "run_lengths", "tile_vis", "tile_offsets", "chunk_emit", "chunk_counts",
-                "prep_final", "fillBuffer"):
-        if key in name:
-            return key
-    return name[-60:]
+    """The kernel's unqualified identifier ("cip::radix_scatter_kernel(...)" ->
+    "radix_scatter_kernel"; template arguments dropped). Exact names: a
+    substring match would lump radix_scatter_kernel into scatter_kernel."""
+    base = name.split("(")[0].split("<")[0].strip().split()[-1]
+    return base.split("::")[-1]
 
 
 def main():
