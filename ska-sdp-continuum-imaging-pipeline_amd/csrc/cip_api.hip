@@ -556,6 +556,22 @@ static bool scatter_order() {
   return on;
 }
 
+// sub-blocks per radix workgroup: pass 0 (place blocks of ~500 runs) and the
+// dense passes (4096 runs); CIP_RADIX_G0 / CIP_RADIX_G1 override (A/B)
+static int radix_group(int pass) {
+  static const int g[2] = {[] {
+                             const char* e = getenv("CIP_RADIX_G0");
+                             const int v = e ? atoi(e) : 0;
+                             return v > 0 ? v : 8;
+                           }(),
+                           [] {
+                             const char* e = getenv("CIP_RADIX_G1");
+                             const int v = e ? atoi(e) : 0;
+                             return v > 0 ? v : 1;
+                           }()};
+  return g[pass ? 1 : 0];
+}
+
 // Also reduces {sum w, max |w V|} into red (device) and returns max |w V| in
 // *maxabs (the place pass reads the visibilities anyway).
 static int make_plan(Workspace* ws, const double* uvw, const double* fx, const RowMap& m,
@@ -583,19 +599,24 @@ static int make_plan(Workspace* ws, const double* uvw, const double* fx, const R
   CIP_ALLOC(park_key, uint32_t, "park_key", (int64_t)nblk * 4096)
   CIP_ALLOC(park_run, uint64_t, "park_run", (int64_t)nblk * 4096)
   CIP_ALLOC(partial, double, "prep_partial", 2 * nblk)
-  // the place pass also writes radix pass 0's histogram; its scan's last entry = runs
-  CIP_ALLOC(hist0, int64_t, "radix_hist0", 256 * (int64_t)nblk + 1)
-  CIP_ALLOC(scan_h0, int64_t, "scan_hist0", scan_tmp_elems(256 * (int64_t)nblk + 1))
+  // the place pass also writes radix pass 0's histogram per place block; summed
+  // per radix group of g0 blocks, its scan's last entry = runs
+  const int g0 = radix_group(0), g1 = radix_group(1);
+  const int64_t ng0 = (nblk + g0 - 1) / g0;
+  CIP_ALLOC(hist0, int64_t, "radix_hist0", 256 * (int64_t)nblk)
+  CIP_ALLOC(hist0g, int64_t, "radix_hist0g", 256 * ng0 + 1)
+  CIP_ALLOC(scan_h0, int64_t, "scan_hist0", scan_tmp_elems(256 * ng0 + 1))
   CIP_HIP_CHECK(launch_plan_place(uvw, fx, m, vis, vis_dtype, wgt, wgt_dtype, g, err, vis_class, blk_cnt, park_key,
                                   park_run, partial, hist0, s));
   CIP_HIP_CHECK(launch_prep_final(partial, nblk, red, s));
   int key_bits = 1;
   while (key_bits < 32 && ((int64_t)1 << key_bits) < ntiles) ++key_bits;
   const int npass = (key_bits + 7) / 8;
-  CIP_HIP_CHECK(exclusive_scan_i64(hist0, 256 * (int64_t)nblk + 1, scan_h0, s));
+  CIP_HIP_CHECK(launch_radix_group_hist(hist0, nblk, g0, hist0g, s));
+  CIP_HIP_CHECK(exclusive_scan_i64(hist0g, 256 * ng0 + 1, scan_h0, s));
   int64_t* h = (int64_t*)pinned(ws, 4 * sizeof(int64_t));
   if (!h) return set_error(CIP_ENOMEM, "hipHostMalloc failed");
-  CIP_HIP_CHECK(hipMemcpyAsync(&h[0], hist0 + 256 * (int64_t)nblk, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+  CIP_HIP_CHECK(hipMemcpyAsync(&h[0], hist0g + 256 * ng0, sizeof(int64_t), hipMemcpyDeviceToHost, s));
   CIP_HIP_CHECK(hipMemcpyAsync(&h[1], err, sizeof(unsigned), hipMemcpyDeviceToHost, s));
   CIP_HIP_CHECK(hipMemcpyAsync(&h[2], red + 1, sizeof(double), hipMemcpyDeviceToHost, s));
   CIP_HIP_CHECK(hipStreamSynchronize(s));
@@ -613,15 +634,16 @@ static int make_plan(Workspace* ws, const double* uvw, const double* fx, const R
   CIP_ALLOC(run_a, uint64_t, "sort_run_a", nruns)
   CIP_ALLOC(run_b, uint64_t, "sort_run_b", nruns)
   const int64_t nbd = radix_blocks(nruns);
-  CIP_ALLOC(hist, int64_t, "radix_hist", 256 * nbd + 1)
-  CIP_ALLOC(scan_h, int64_t, "scan_hist", scan_tmp_elems(256 * nbd + 1))
-  CIP_HIP_CHECK(launch_radix_scatter(park_key, park_run, 0, blk_cnt, nblk, 0, hist0, key_a, run_a, s));
+  const int64_t ng1 = (nbd + g1 - 1) / g1;
+  CIP_ALLOC(hist, int64_t, "radix_hist", 256 * ng1 + 1)
+  CIP_ALLOC(scan_h, int64_t, "scan_hist", scan_tmp_elems(256 * ng1 + 1))
+  CIP_HIP_CHECK(launch_radix_scatter(park_key, park_run, 0, blk_cnt, nblk, g0, 0, hist0g, key_a, run_a, s));
   uint32_t *kin = key_a, *kout = key_b;
   uint64_t *rin = run_a, *rout = run_b;
   for (int p = 1; p < npass; ++p) {
-    CIP_HIP_CHECK(launch_radix_hist(kin, nruns, nullptr, nbd, 8 * p, hist, s));
-    CIP_HIP_CHECK(exclusive_scan_i64(hist, 256 * nbd + 1, scan_h, s));
-    CIP_HIP_CHECK(launch_radix_scatter(kin, rin, nruns, nullptr, nbd, 8 * p, hist, kout, rout, s));
+    CIP_HIP_CHECK(launch_radix_hist(kin, nruns, nullptr, nbd, g1, 8 * p, hist, s));
+    CIP_HIP_CHECK(exclusive_scan_i64(hist, 256 * ng1 + 1, scan_h, s));
+    CIP_HIP_CHECK(launch_radix_scatter(kin, rin, nruns, nullptr, nbd, g1, 8 * p, hist, kout, rout, s));
     std::swap(kin, kout);
     std::swap(rin, rout);
   }

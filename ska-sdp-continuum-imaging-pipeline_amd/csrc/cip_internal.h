@@ -59,10 +59,13 @@ hipError_t launch_ragged_expand(const int64_t* off, const int32_t* c0, int64_t n
 // parked runs (blk_cnt). hist: 256 * nblocks + 1 entries, exclusive-scanned
 // between the two calls (its last entry then holds the item count).
 int64_t radix_blocks(int64_t n);
-hipError_t launch_radix_hist(const uint32_t* keys, int64_t n, const int64_t* blk_cnt, int64_t nblocks, int shift,
+// G: sub-blocks (of <= 4096 items) per workgroup; hist is digit-major per
+// group of G sub-blocks (see cip_plan.hip)
+hipError_t launch_radix_hist(const uint32_t* keys, int64_t n, const int64_t* blk_cnt, int64_t nsub, int G, int shift,
                              int64_t* hist, hipStream_t s);
+hipError_t launch_radix_group_hist(const int64_t* hist0, int64_t nsub, int G, int64_t* hg, hipStream_t s);
 hipError_t launch_radix_scatter(const uint32_t* keys, const uint64_t* vals, int64_t n, const int64_t* blk_cnt,
-                                int64_t nblocks, int shift, const int64_t* hist, uint32_t* keys_out,
+                                int64_t nsub, int G, int shift, const int64_t* hist, uint32_t* keys_out,
                                 uint64_t* vals_out, hipStream_t s);
 hipError_t launch_tile_offsets(const uint32_t* keys, int64_t nruns, int64_t ntiles, int64_t* tile_run_off,
                                hipStream_t s);

@@ -393,20 +393,26 @@ hipError_t launch_ragged_expand(const int64_t* off, const int32_t* c0, int64_t n
 
 // ---------------------------------------------------------- radix sort ----
 // Stable LSD radix sort of (uint32 key, uint64 run) pairs, 8-bit digits.
-// A block owns 4096 input slots; wave w ranks slots [1024 w, 1024 w + 1024)
-// in order, 64 at a time (8 ballots give each lane its digit's peer mask; a
+// Items come in sub-blocks of <= 4096 slots: dense (slots [4096 b, 4096 b +
+// 4096) of n), or the place pass's per-block runs (slots [4096 b, 4096 b +
+// blk_cnt[b])). A workgroup takes a group of G consecutive sub-blocks in
+// order; per sub-block, wave w ranks its contiguous quarter of the items in
+// order, 64 at a time (8 ballots give each lane its digit's peer mask; a
 // wave-private LDS counter per digit carries the rank across steps, read by
 // every lane and then advanced by the digit's first lane - one wave's LDS ops
-// execute in order, so no barrier is needed). One barrier, a per-digit prefix
-// over the 4 waves, and each item lands at base[d] + its rank: the order of a
-// digit's items is the input order (stable). Global bases: the exclusive scan
-// of the digit-major histogram hist[d * nblocks + b] (+1 trailing entry: the
-// item count). Input: dense (slots [4096 b, 4096 b + 4096) of n), or the
-// place pass's per-block runs (slots [4096 b, 4096 b + blk_cnt[b])).
+// execute in order, so no barrier is needed). A per-digit prefix over the 4
+// waves and the group's running digit offsets place each item at its digit's
+// next position: the order of a digit's items is the input order (stable).
+// Global bases: the exclusive scan of the digit-major group histogram
+// hist[d * ngroups + g] (+1 trailing entry: the item count). Grouping pass
+// 0's place blocks (8 of ~500 runs) divides its histogram scan by 8 (C3:
+// 6.2 M -> 0.78 M entries; the kernel's own time is unchanged, ~180 us,
+// latency-bound, and staging a sub-block in LDS for line-coalesced stores did
+// not change it either).
 constexpr int kRadixThreads = 256;
 constexpr int kRadixPer = 16;
 constexpr int64_t kRadixBlock = (int64_t)kRadixThreads * kRadixPer;
-static_assert(kRadixBlock == 64 * 64, "a radix block covers one place block's park region");
+static_assert(kRadixBlock == 64 * 64, "a radix sub-block covers one place block's park region");
 
 __device__ __forceinline__ int64_t radix_count(int64_t b, int64_t n, const int64_t* __restrict__ blk_cnt) {
   if (blk_cnt) return blk_cnt[b];
@@ -415,92 +421,120 @@ __device__ __forceinline__ int64_t radix_count(int64_t b, int64_t n, const int64
 }
 
 __global__ __launch_bounds__(kRadixThreads) void radix_hist_kernel(const uint32_t* __restrict__ keys, int64_t n,
-                                                                   const int64_t* __restrict__ blk_cnt, int shift,
-                                                                   int64_t nblocks, int64_t* __restrict__ hist) {
+                                                                   const int64_t* __restrict__ blk_cnt, int64_t nsub,
+                                                                   int G, int shift, int64_t ngroups,
+                                                                   int64_t* __restrict__ hist) {
   __shared__ unsigned cnt[256];
   cnt[threadIdx.x] = 0u;
   __syncthreads();
-  const int64_t cnt_b = radix_count(blockIdx.x, n, blk_cnt);
-  const uint32_t* kb = keys + (int64_t)blockIdx.x * kRadixBlock;
-  if (cnt_b == kRadixBlock) {
-    // full block: the loads issue back to back (the loop below waits for each)
-    uint32_t kk[kRadixPer];
+  const int64_t b0 = (int64_t)blockIdx.x * G;
+  const int64_t b1 = b0 + G < nsub ? b0 + G : nsub;
+  for (int64_t b = b0; b < b1; ++b) {
+    const int64_t cnt_b = radix_count(b, n, blk_cnt);
+    const uint32_t* kb = keys + b * kRadixBlock;
+    if (cnt_b == kRadixBlock) {
+      // full sub-block: the loads issue back to back (the loop below waits for each)
+      uint32_t kk[kRadixPer];
 #pragma unroll
-    for (int k = 0; k < kRadixPer; ++k) kk[k] = kb[threadIdx.x + k * kRadixThreads];
+      for (int k = 0; k < kRadixPer; ++k) kk[k] = kb[threadIdx.x + k * kRadixThreads];
 #pragma unroll
-    for (int k = 0; k < kRadixPer; ++k) atomicAdd(&cnt[(kk[k] >> shift) & 255u], 1u);
-  } else {
-    for (int64_t i = threadIdx.x; i < cnt_b; i += kRadixThreads) atomicAdd(&cnt[(kb[i] >> shift) & 255u], 1u);
+      for (int k = 0; k < kRadixPer; ++k) atomicAdd(&cnt[(kk[k] >> shift) & 255u], 1u);
+    } else {
+      for (int64_t i = threadIdx.x; i < cnt_b; i += kRadixThreads) atomicAdd(&cnt[(kb[i] >> shift) & 255u], 1u);
+    }
   }
   __syncthreads();
-  hist[(int64_t)threadIdx.x * nblocks + blockIdx.x] = cnt[threadIdx.x];
-  if (blockIdx.x == 0 && threadIdx.x == 0) hist[256 * nblocks] = 0;
+  hist[(int64_t)threadIdx.x * ngroups + blockIdx.x] = cnt[threadIdx.x];
+  if (blockIdx.x == 0 && threadIdx.x == 0) hist[256 * ngroups] = 0;
+}
+
+// hg[d * ngroups + g] = sum of hist0[d * nsub + b] over the G sub-blocks of
+// group g (the place pass's per-block histogram, summed per radix group)
+__global__ void radix_group_hist_kernel(const int64_t* __restrict__ hist0, int64_t nsub, int G, int64_t ngroups,
+                                        int64_t* __restrict__ hg) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t == 0) hg[256 * ngroups] = 0;
+  if (t >= 256 * ngroups) return;
+  const int64_t d = t / ngroups, gi = t - d * ngroups;
+  const int64_t b0 = gi * G, b1 = b0 + G < nsub ? b0 + G : nsub;
+  int64_t sum = 0;
+  for (int64_t b = b0; b < b1; ++b) sum += hist0[d * nsub + b];
+  hg[t] = sum;
 }
 
 __global__ __launch_bounds__(kRadixThreads) void radix_scatter_kernel(
     const uint32_t* __restrict__ keys, const uint64_t* __restrict__ vals, int64_t n,
-    const int64_t* __restrict__ blk_cnt, int shift, int64_t nblocks, const int64_t* __restrict__ hist,
-    uint32_t* __restrict__ keys_out, uint64_t* __restrict__ vals_out) {
+    const int64_t* __restrict__ blk_cnt, int64_t nsub, int G, int shift, int64_t ngroups,
+    const int64_t* __restrict__ hist, uint32_t* __restrict__ keys_out, uint64_t* __restrict__ vals_out) {
   __shared__ unsigned wcnt[4][256];  // per-wave running digit counts
+  __shared__ int64_t dnext[256];     // the group's next position per digit
   __shared__ int64_t woff[4][256];   // global position of each wave's first item per digit
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int64_t cnt_b = radix_count(blockIdx.x, n, blk_cnt);
-  // the block's items are split into 4 contiguous, 64-aligned wave ranges of
-  // q items (q = 1024 for a full block; a parked block holds ~500 runs, which
-  // would otherwise all fall to wave 0); wave ranges in order keep it stable
-  const int steps = (int)((cnt_b + 255) / 256);  // 64-item steps per wave
-  const int q = 64 * steps;
-  const int64_t i0 = (int64_t)blockIdx.x * kRadixBlock + wave * q + lane;
-  const int64_t wlim = (int64_t)blockIdx.x * kRadixBlock + (int64_t)(wave + 1) * q;
-  const int64_t blim = (int64_t)blockIdx.x * kRadixBlock + cnt_b;
-  const int64_t lim = wlim < blim ? wlim : blim;
+  dnext[threadIdx.x] = hist[(int64_t)threadIdx.x * ngroups + blockIdx.x];
+  const int64_t b0 = (int64_t)blockIdx.x * G;
+  const int64_t b1 = b0 + G < nsub ? b0 + G : nsub;
+  for (int64_t b = b0; b < b1; ++b) {
+    const int64_t cnt_b = radix_count(b, n, blk_cnt);
+    // the sub-block's items are split into 4 contiguous, 64-aligned wave
+    // ranges of q items (q = 1024 for a full sub-block; a parked block holds
+    // ~500 runs, which would otherwise all fall to wave 0); wave ranges in
+    // order keep it stable
+    const int steps = (int)((cnt_b + 255) / 256);  // 64-item steps per wave
+    const int q = 64 * steps;
+    const int64_t i0 = b * kRadixBlock + wave * q + lane;
+    const int64_t wlim = b * kRadixBlock + (int64_t)(wave + 1) * q;
+    const int64_t blim = b * kRadixBlock + cnt_b;
+    const int64_t lim = wlim < blim ? wlim : blim;
 #pragma unroll
-  for (int w = 0; w < 4; ++w) wcnt[w][threadIdx.x] = 0u;
-  uint32_t key[kRadixPer];
-  uint64_t val[kRadixPer];
+    for (int w = 0; w < 4; ++w) wcnt[w][threadIdx.x] = 0u;
+    uint32_t key[kRadixPer];
+    uint64_t val[kRadixPer];
 #pragma unroll
-  for (int k = 0; k < kRadixPer; ++k) {
-    const int64_t i = i0 + k * 64;
-    key[k] = i < lim ? keys[i] : 0u;
-    val[k] = i < lim ? vals[i] : 0ull;
-  }
-  __syncthreads();
-  unsigned rank[kRadixPer];
+    for (int k = 0; k < kRadixPer; ++k) {
+      const int64_t i = i0 + k * 64;
+      key[k] = (k < steps && i < lim) ? keys[i] : 0u;
+      val[k] = (k < steps && i < lim) ? vals[i] : 0ull;
+    }
+    __syncthreads();
+    unsigned rank[kRadixPer];
 #pragma unroll
-  for (int k = 0; k < kRadixPer; ++k) {
-    if (k < steps) {  // block-uniform
-      const bool valid = i0 + k * 64 < lim;
-      const unsigned d = (key[k] >> shift) & 255u;
-      unsigned long long peers = __ballot(valid);
+    for (int k = 0; k < kRadixPer; ++k) {
+      if (k < steps) {  // block-uniform
+        const bool valid = i0 + k * 64 < lim;
+        const unsigned d = (key[k] >> shift) & 255u;
+        unsigned long long peers = __ballot(valid);
 #pragma unroll
-      for (int b = 0; b < 8; ++b) {
-        const bool bit = (d >> b) & 1u;
-        const unsigned long long m = __ballot(bit);
-        peers &= bit ? m : ~m;
+        for (int bit = 0; bit < 8; ++bit) {
+          const bool on = (d >> bit) & 1u;
+          const unsigned long long m = __ballot(on);
+          peers &= on ? m : ~m;
+        }
+        const unsigned prior = valid ? wcnt[wave][d] : 0u;
+        rank[k] = prior + (unsigned)__popcll(peers & ((1ull << lane) - 1ull));
+        if (valid && (peers & ((1ull << lane) - 1ull)) == 0ull) wcnt[wave][d] = prior + (unsigned)__popcll(peers);
       }
-      const unsigned prior = valid ? wcnt[wave][d] : 0u;
-      rank[k] = prior + (unsigned)__popcll(peers & ((1ull << lane) - 1ull));
-      if (valid && (peers & ((1ull << lane) - 1ull)) == 0ull) wcnt[wave][d] = prior + (unsigned)__popcll(peers);
     }
-  }
-  __syncthreads();
-  {
-    const int d = threadIdx.x;
-    int64_t o = hist[(int64_t)d * nblocks + blockIdx.x];
+    __syncthreads();
+    {
+      const int d = threadIdx.x;
+      int64_t o = dnext[d];
 #pragma unroll
-    for (int w = 0; w < 4; ++w) {
-      woff[w][d] = o;
-      o += wcnt[w][d];
+      for (int w = 0; w < 4; ++w) {
+        woff[w][d] = o;
+        o += wcnt[w][d];
+      }
+      dnext[d] = o;
     }
-  }
-  __syncthreads();
+    __syncthreads();
 #pragma unroll
-  for (int k = 0; k < kRadixPer; ++k)
-    if (i0 + k * 64 < lim) {
-      const int64_t pos = woff[wave][(key[k] >> shift) & 255u] + rank[k];
-      keys_out[pos] = key[k];
-      vals_out[pos] = val[k];
-    }
+    for (int k = 0; k < kRadixPer; ++k)
+      if (k < steps && i0 + k * 64 < lim) {
+        const int64_t pos = woff[wave][(key[k] >> shift) & 255u] + rank[k];
+        keys_out[pos] = key[k];
+        vals_out[pos] = val[k];
+      }
+    __syncthreads();  // wcnt / woff are reused by the next sub-block
+  }
 }
 
 // tile_run_off[t] = first sorted run with key >= t (t in [0, ntiles])
@@ -519,19 +553,30 @@ __global__ void tile_offsets_kernel(const uint32_t* __restrict__ keys, int64_t n
 
 int64_t radix_blocks(int64_t n) { return (n + kRadixBlock - 1) / kRadixBlock; }
 
-hipError_t launch_radix_hist(const uint32_t* keys, int64_t n, const int64_t* blk_cnt, int64_t nblocks, int shift,
+hipError_t launch_radix_hist(const uint32_t* keys, int64_t n, const int64_t* blk_cnt, int64_t nsub, int G, int shift,
                              int64_t* hist, hipStream_t s) {
-  if (nblocks == 0) return hipSuccess;
-  radix_hist_kernel<<<dim3((unsigned)nblocks), dim3(kRadixThreads), 0, s>>>(keys, n, blk_cnt, shift, nblocks, hist);
+  if (nsub == 0) return hipSuccess;
+  const int64_t ngroups = (nsub + G - 1) / G;
+  radix_hist_kernel<<<dim3((unsigned)ngroups), dim3(kRadixThreads), 0, s>>>(keys, n, blk_cnt, nsub, G, shift,
+                                                                          ngroups, hist);
+  return hipGetLastError();
+}
+
+hipError_t launch_radix_group_hist(const int64_t* hist0, int64_t nsub, int G, int64_t* hg, hipStream_t s) {
+  const int64_t ngroups = (nsub + G - 1) / G;
+  const int64_t nt = 256 * ngroups > 0 ? 256 * ngroups : 1;
+  radix_group_hist_kernel<<<dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, s>>>(hist0, nsub, G, ngroups, hg);
   return hipGetLastError();
 }
 
 hipError_t launch_radix_scatter(const uint32_t* keys, const uint64_t* vals, int64_t n, const int64_t* blk_cnt,
-                                int64_t nblocks, int shift, const int64_t* hist, uint32_t* keys_out,
+                                int64_t nsub, int G, int shift, const int64_t* hist, uint32_t* keys_out,
                                 uint64_t* vals_out, hipStream_t s) {
-  if (nblocks == 0) return hipSuccess;
-  radix_scatter_kernel<<<dim3((unsigned)nblocks), dim3(kRadixThreads), 0, s>>>(keys, vals, n, blk_cnt, shift, nblocks,
-                                                                              hist, keys_out, vals_out);
+  if (nsub == 0) return hipSuccess;
+  const int64_t ngroups = (nsub + G - 1) / G;
+  radix_scatter_kernel<<<dim3((unsigned)ngroups), dim3(kRadixThreads), 0, s>>>(keys, vals, n, blk_cnt, nsub, G,
+                                                                              shift, ngroups, hist, keys_out,
+                                                                              vals_out);
   return hipGetLastError();
 }
 
