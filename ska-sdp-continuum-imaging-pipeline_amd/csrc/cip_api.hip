@@ -603,7 +603,7 @@ static int make_plan(Workspace* ws, const double* uvw, const double* fx, const R
   // per radix group of g0 blocks, its scan's last entry = runs
   const int g0 = radix_group(0), g1 = radix_group(1);
   const int64_t ng0 = (nblk + g0 - 1) / g0;
-  CIP_ALLOC(hist0, int64_t, "radix_hist0", 256 * (int64_t)nblk)
+  CIP_ALLOC(hist0, int64_t, "radix_hist0", 256 * (int64_t)nblk + 1)
   CIP_ALLOC(hist0g, int64_t, "radix_hist0g", 256 * ng0 + 1)
   CIP_ALLOC(scan_h0, int64_t, "scan_hist0", scan_tmp_elems(256 * ng0 + 1))
   CIP_HIP_CHECK(launch_plan_place(uvw, fx, m, vis, vis_dtype, wgt, wgt_dtype, g, err, vis_class, blk_cnt, park_key,
