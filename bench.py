@@ -3,7 +3,8 @@
 Benchmark of the invert hot path (BASELINE.json metric): Mvis/s gridded
 (invert) on an 8k^2 grid with kernel support 8, fp64 accumulation.
 
-Workload (default `--config c3`): 390,625 rows x 256
+Workload (default `--config c3`; `--config c4` is one
+GPU's shard of C4, 125M visibilities -> 16384^2 grid): 390,625 rows x 256
 channels = 100M synthetic visibilities per GPU (MeerKAT-like 64-antenna
 earth-rotation uvw tracks, 856-1712 MHz; complex64 visibilities and float32
 weights with 5 % zero (flagged) weights, as the reference passes them to the
@@ -40,6 +41,9 @@ CONFIGS = {
     "c1": dict(rows=10_000, nchan=1, npix=128, n_ant=16, radius=1000.0),
     "c2": dict(rows=156_250, nchan=64, npix=2048, n_ant=64, radius=4000.0),
     "c3": dict(rows=390_625, nchan=256, npix=4096, n_ant=64, radius=4000.0),
+    # C4's per-GPU shard (BASELINE configs[3]: 1G vis -> 16k^2 grid on 8 GPUs):
+    # 3,906,250 / 8 rows x 256 ch = 125M vis/GPU -> 16384^2 grid (8192^2 image)
+    "c4": dict(rows=488_282, nchan=256, npix=8192, n_ant=64, radius=4000.0),
 }
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
@@ -271,7 +275,7 @@ def main():
         roofline["traffic"] = tr.get("hbm_bytes_per_launch")
 
     result = {
-        "metric": "Mvis/s gridded (invert) on 8k^2 grid, support=8",
+        "metric": f"Mvis/s gridded (invert) on {params.nu // 1024}k^2 grid, support={params.support}",
         "value": round(value, 2),
         "unit": "Mvis/s",
         "n_gpus": world,

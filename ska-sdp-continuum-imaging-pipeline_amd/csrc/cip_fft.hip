@@ -1,5 +1,5 @@
 // cip_fft.hip - the dirty image's 2-D FFT as two hand-written pruned passes
-// (SURVEY.md 8(a) a4.5), for power-of-two grids of 1024..8192 cells per axis.
+// (SURVEY.md 8(a) a4.5), for power-of-two grids of 1024..16384 cells per axis.
 //
 // The image keeps only nx x ny of the nu x nv frequencies (a quarter for
 // sigma = 2). The scatter writes the grid transposed (gT[y, x]); pass A
@@ -289,7 +289,7 @@ __global__ __launch_bounds__(N / 16) void fft_cols_kernel(const double2* __restr
     }
 }
 
-static bool fft_len_ok(int64_t n) { return n == 1024 || n == 2048 || n == 4096 || n == 8192; }
+static bool fft_len_ok(int64_t n) { return n == 1024 || n == 2048 || n == 4096 || n == 8192 || n == 16384; }
 
 bool fast_fft_supported(int64_t nu, int64_t nv, int64_t nx, int64_t ny) {
   return fft_len_ok(nu) && fft_len_ok(nv) && nx > 0 && ny > 0 && nx <= nu && ny <= nv && nx % kColBlock == 0 &&
@@ -315,6 +315,7 @@ hipError_t launch_fft_rows(double* gT, int64_t nu, int64_t nv, int64_t nx, const
     ROWS(2048)
     ROWS(4096)
     ROWS(8192)
+    ROWS(16384)
     default: return hipErrorInvalidValue;
   }
 #undef ROWS
@@ -338,6 +339,7 @@ hipError_t launch_fft_cols(const double* H, int64_t nv, int64_t nx, int64_t ny, 
     COLS(2048)
     COLS(4096)
     COLS(8192)
+    COLS(16384)
     default:
       return hipErrorInvalidValue;
   }

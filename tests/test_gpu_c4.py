@@ -1,0 +1,89 @@
+"""
+GPU test at one GPU's share of C4 (BASELINE.json configs[3]: 1G visibilities
+-> 16384^2 grid on 8 GPUs; one rank inverts 488,282 rows x 256 channels =
+125M visibilities onto the full 16384^2 grid, 8192^2 image, W = 8, 2-D, the
+`bench.py --config c4` workload): the 16384-point pruned FFT, 4 GiB grid and
+2 GiB pass-A buffer at full size, checked through properties that need no CPU
+oracle run at that size (the oracle's host FFT alone would be 4 GiB):
+
+* sampled pixels equal the direct fp64 DFT (the definition, evaluated on the
+  GPU in torch fp64 - TEST CODE) within the W = 8 kernel's accuracy
+  (~3e-7 of the weight sum);
+* the normalised image is the raw image divided by the device weight sum,
+  which equals torch's fp64 sum.
+"""
+import math
+
+import numpy as np
+import pytest
+
+from ska_sdp_cip_amd import gridder, synthetic as syn
+
+pytestmark = pytest.mark.gpu
+
+ROWS, NCHAN, NPIX, N_ANT, RADIUS, SEED = 488_282, 256, 8192, 64, 4000.0, 20241008
+SPEED_OF_LIGHT = 299792458.0
+
+
+@pytest.fixture(scope="module")
+def c4(gpu_device):
+    import torch
+
+    dev = torch.device("cuda", 0)
+    uvw = syn.uvw_tracks(ROWS, N_ANT, array_radius_m=RADIUS, seed=SEED)
+    freq = syn.channel_frequencies(NCHAN)
+    px = syn.pixel_size_for_grid(uvw, freq, NPIX, support=8)
+    g = torch.Generator(device=dev)
+    g.manual_seed(SEED)
+    vis = torch.randn((ROWS, NCHAN), dtype=torch.complex64, device=dev, generator=g)
+    wgt = torch.rand((ROWS, NCHAN), dtype=torch.float32, device=dev, generator=g) + 0.5
+    flags = torch.rand((ROWS, NCHAN), dtype=torch.float32, device=dev, generator=g) < 0.05
+    wgt = torch.where(flags, torch.zeros_like(wgt), wgt).contiguous()
+    yield torch.from_numpy(uvw).to(dev), torch.from_numpy(freq).to(dev), vis, wgt, px
+    torch.cuda.empty_cache()
+
+
+def _dft_pixels(c, pix):
+    """sum_{r,c} w Re{V exp(2 pi i (f/c) (u l + v m))} at pixels (i, j) (2-D)."""
+    import torch
+
+    uvw, f, vis, wgt, px = c
+    fx = f / SPEED_OF_LIGHT
+    out = []
+    for i, j in pix:
+        l, m = (i - NPIX // 2) * px, (j - NPIX // 2) * px
+        acc = torch.zeros((), dtype=torch.float64, device=vis.device)
+        for r0 in range(0, ROWS, 65_536):
+            r1 = min(r0 + 65_536, ROWS)
+            ph = (2.0 * math.pi) * (uvw[r0:r1, 0] * l + uvw[r0:r1, 1] * m)[:, None] * fx[None, :]
+            v = vis[r0:r1].to(torch.complex128)
+            acc += (wgt[r0:r1].double() * (v.real * torch.cos(ph) - v.imag * torch.sin(ph))).sum()
+        out.append(float(acc.item()))
+    return np.array(out)
+
+
+def test_c4_shard_sampled_pixels_equal_dft(c4):
+    import torch
+
+    uvw, f, vis, wgt, px = c4
+    img, prm = gridder.device_ms2dirty(uvw, f, vis, wgt, NPIX, NPIX, px, px, support=8)
+    assert (prm.nu, prm.nv, prm.nplanes) == (2 * NPIX, 2 * NPIX, 1)
+    rng = np.random.default_rng(4)
+    pix = [(NPIX // 2, NPIX // 2), (0, 0), (NPIX - 1, NPIX - 1), (NPIX // 2, 0)]
+    pix += [tuple(int(x) for x in rng.integers(0, NPIX, 2)) for _ in range(4)]
+    ref = _dft_pixels(c4, pix)
+    got = np.array([float(img[i, j].item()) for i, j in pix])
+    sumw = float(wgt.double().sum().item())
+    err = np.abs(got - ref).max() / sumw
+    assert err < 2e-6, (err, got, ref)
+
+    # normalised in the pass-B epilogue == raw / device weight sum
+    raw = img.clone()
+    out = torch.empty_like(raw)
+    sw = torch.empty(1, dtype=torch.float64, device=raw.device)
+    gridder.device_ms2dirty(uvw, f, vis, wgt, NPIX, NPIX, px, px, support=8, normalise=True, out=out,
+                            sum_weights=sw)
+    assert abs(float(sw.item()) - sumw) <= 1e-12 * sumw
+    scale = float(raw.abs().max().item()) / sumw
+    assert float((out - raw / sw).abs().max().item()) <= 1e-12 * max(scale, 1e-300)
+    torch.cuda.synchronize()

@@ -1,9 +1,11 @@
 """
 The pruned FFT fast path (csrc/cip_fft.hip row pass + hipFFT column pass on
 the kept half) against the fp64 oracle, at every grid size it serves
-(nv = 1024 .. 8192, i.e. npix = 512 .. 4096 at sigma = 2), in 2-D and
+(nv = 1024 .. 16384, i.e. npix = 512 .. 8192 at sigma = 2), in 2-D and
 w-stacking mode. Other sizes take the full 2-D hipFFT path (covered by
-test_gpu_invert_parity.py at npix <= 256).
+test_gpu_invert_parity.py at npix <= 256). At nv = 16384 (C4's grid) the
+oracle's 4 GiB host FFT is replaced by the definition itself: sampled
+pixels against the direct fp64 DFT at W = 16 (kernel error ~2e-14).
 """
 
 import numpy as np
@@ -51,3 +53,32 @@ def test_pruned_fft_rectangular_image(gpu_device):
     sumw = float(w.astype(np.float64).sum())
     assert prm.nv == 2048
     assert float(np.abs(gpu.cpu().numpy() - ref).max()) / sumw < TIGHT
+
+
+@pytest.mark.parametrize("wstack", [False, True])
+def test_pruned_fft_16k_grid_matches_dft(gpu_device, wstack):
+    # 16384-point passes (one 1024-thread workgroup per CU, 136 KiB LDS)
+    import torch
+
+    uvw, f, vis, w = _case(400, 4, seed=5)
+    npix = 8192
+    px = syn.pixel_size_for_grid(uvw, f, npix, fill=0.4)
+    args = [torch.from_numpy(a).cuda() for a in (uvw, f, vis.astype(np.complex128), w.astype(np.float64))]
+    gpu, prm = gridder.device_ms2dirty(*args, npix, npix, px, px, support=16, do_wstacking=wstack)
+    assert (prm.nu, prm.nv) == (16384, 16384)
+    rng = np.random.default_rng(8)
+    pix = [(npix // 2, npix // 2), (0, 0), (npix - 1, npix - 1), (npix // 2, 17), (3, npix - 2)]
+    pix += [tuple(int(x) for x in rng.integers(0, npix, 2)) for _ in range(11)]
+    ii = np.array([p[0] for p in pix])
+    jj = np.array([p[1] for p in pix])
+    l, m = (ii - npix // 2) * px, (jj - npix // 2) * px
+    if wstack:
+        ref = oracle.dft_directions(uvw, f, vis, w, l, m)
+        ref = ref / np.sqrt(1.0 - l * l - m * m)
+    else:
+        flat = uvw.copy()
+        flat[:, 2] = 0.0
+        ref = oracle.dft_directions(flat, f, vis, w, l, m)
+    got = gpu[torch.from_numpy(ii).cuda(), torch.from_numpy(jj).cuda()].cpu().numpy()
+    sumw = float(w.astype(np.float64).sum())
+    assert float(np.abs(got - ref).max()) / sumw < 1e-10
