@@ -271,7 +271,8 @@ def main():
                               "basis": f"{8 if args.single else 16} B of ds_add_u64 per tap; 8.12 CU-cycles per "
                                        "conflict-free wave-instr"}
     tr = traffic_from_profiles(args.config)
-    if tr and not args.wstacking:
+    # the committed PMC pass is of the default workload (support 8, 2-D, fp64 class)
+    if tr and not args.wstacking and not args.single and args.support == tr.get("support", 8):
         roofline["traffic"] = tr.get("hbm_bytes_per_launch")
 
     result = {

@@ -92,6 +92,10 @@ CIP_HOST_TABLE(10)
 CIP_HOST_TABLE(12)
 CIP_HOST_TABLE(14)
 CIP_HOST_TABLE(16)
+CIP_HOST_TABLE(24)
+CIP_HOST_TABLE(32)
+CIP_HOST_TABLE(48)
+CIP_HOST_TABLE(64)
 #undef CIP_HOST_TABLE
 
 static bool host_kernel(int W, HostKernel* k) {
@@ -100,7 +104,7 @@ static bool host_kernel(int W, HostKernel* k) {
   case WW:                                                                    \
     *k = {WW, CIP_ES_DEGREE_##WW, CIP_ES_BETA_##WW, &host_coef_##WW[0][0]};  \
     return true;
-    CASE(4) CASE(6) CASE(8) CASE(10) CASE(12) CASE(14) CASE(16)
+    CASE(4) CASE(6) CASE(8) CASE(10) CASE(12) CASE(14) CASE(16) CASE(24) CASE(32) CASE(48) CASE(64)
 #undef CASE
     default:
       return false;
@@ -196,8 +200,18 @@ static int choose(int64_t npix_x, int64_t npix_y, double px, double py, double e
     return set_error(CIP_EINVAL, "npix_x and npix_y must be even and >= 2");
   if (!(px > 0.0) || !(py > 0.0)) return set_error(CIP_EINVAL, "pixel sizes must be positive");
   if (support > 0) {
-    if ((support & 1) || support < 4 || support > 16)
-      return set_error(CIP_EINVAL, "support must be an even number in [4, 16]");
+    // W <= 16: lane-per-visibility scatter; 24..64 (BASELINE configs[2]'s
+    // LDS-tile stress case): wave-per-visibility scatter (cip_scatter_large.hip)
+    const bool small = !(support & 1) && support >= 4 && support <= 16;
+    const bool large = support == 24 || support == 32 || support == 48 || support == 64;
+    if (!small && !large)
+      return set_error(CIP_EINVAL, "support must be an even number in [4, 16] or one of 24, 32, 48, 64");
+    // at beta = 2.3 W the kernel transform at the field edge is F(1/4)/F(0) =
+    // 1.6e-4 for W = 64: the u, v and w corrections amplify the fixed-point
+    // quantum at the field corners by ~1e11 (measured 4e-5 of sum w, above the
+    // 1e-6 gate; tests/test_gpu_large_support.py), so w-stacking stops at 48
+    if (do_wstacking && support > 48)
+      return set_error(CIP_EINVAL, "w-stacking supports kernel supports up to 48");
   } else {
     if (!(epsilon > 0.0)) return set_error(CIP_EINVAL, "epsilon must be positive");
     support = support_for_epsilon(epsilon);
@@ -209,6 +223,8 @@ static int choose(int64_t npix_x, int64_t npix_y, double px, double py, double e
   p.sigma = 2.0;
   p.nu = good_size((int64_t)std::ceil(p.sigma * npix_x));
   p.nv = good_size((int64_t)std::ceil(p.sigma * npix_y));
+  // a footprint wraps around the periodic grid at most once
+  if (p.nu < support || p.nv < support) return set_error(CIP_EINVAL, "grid smaller than the kernel support");
   p.support = support;
   p.degree = hk.D;
   p.beta = hk.beta;
@@ -819,6 +835,8 @@ static int prepare(Workspace* ws, const double* uvw, int64_t nrow, const double*
   out->g = geometry(out->p, px, py);
   if (packed && vis_dtype != CIP_C64)
     return set_error(CIP_EINVAL, "single-precision accumulation needs complex64 visibilities");
+  if (packed && out->g.support > 16)
+    return set_error(CIP_EINVAL, "single-precision accumulation supports kernel supports <= 16");
   out->packed = packed;
   out->fixed_scale = 1.0;
   out->fx = fx;

@@ -256,6 +256,17 @@ hipError_t launch_scatter(int support, int vis_dtype, int wgt_dtype, bool packed
     CASE(12)
     CASE(14)
     CASE(16)
+#define LARGE(WW)                                                                                              \
+  case WW:                                                                                                     \
+    /* wave-per-visibility scatter (cip_scatter_large.hip); fp64 class only */                                 \
+    if (packed) return hipErrorInvalidValue;                                                                   \
+    return launch_scatter_large_w<WW>(vis_dtype, wgt_dtype, gd, s, uvw, fx, vis, wgt, m, runs, run_goff, perm, \
+                                      chunks, chunk_begin, g, plane, fixed_scale, grid);
+    LARGE(24)
+    LARGE(32)
+    LARGE(48)
+    LARGE(64)
+#undef LARGE
     default:
       return hipErrorInvalidValue;
   }

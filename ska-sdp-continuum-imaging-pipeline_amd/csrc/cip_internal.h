@@ -100,6 +100,14 @@ hipError_t launch_scatter_w(int vis_dtype, int wgt_dtype, bool pack, dim3 gd, hi
                             const uint64_t* runs, const int64_t* run_goff, const int64_t* tile_run_off,
                             const uint32_t* perm, const Chunk* chunks, int64_t cb, const GridGeometry& g,
                             int64_t plane, double fs, double* grid);
+// the large supports W = 24, 32, 48, 64 (cip_scatter_large.hip, wave per
+// visibility; one translation unit per W)
+template <int W>
+hipError_t launch_scatter_large_w(int vis_dtype, int wgt_dtype, dim3 gd, hipStream_t s, const double* uvw,
+                                  const double* fx, const void* vis, const void* wgt, const RowMap& m,
+                                  const uint64_t* runs, const int64_t* run_goff, const uint32_t* perm,
+                                  const Chunk* chunks, int64_t cb, const GridGeometry& g, int64_t plane, double fs,
+                                  double* grid);
 hipError_t launch_scatter(int support, int vis_dtype, int wgt_dtype, bool packed, const double* uvw,
                           const double* fx, const void* vis, const void* wgt, const RowMap& m, const uint64_t* runs,
                           const int64_t* run_goff, const int64_t* tile_run_off, const uint32_t* perm,

@@ -615,8 +615,8 @@ __global__ void tile_vis_kernel(const int64_t* run_goff, const int64_t* tile_run
 // bytes, zeroed by the caller): tile (tx, ty) of plane p is written by the
 // scatter's flush when a visibility of a tile layer feeding p (w-stacking:
 // layers p - W + 1 .. p; 2-D: the one layer) lands in it or, through the
-// (T + W - 1)^2 sub-grid's halo (W - 1 < T cells), in its -x, -y or -x-y
-// neighbour (periodic grid).
+// (T + W - 1)^2 sub-grid's halo, in one of its -x, -y or -x-y neighbours
+// within the halo's reach (periodic grid).
 __global__ void dirty_mask_kernel(const int64_t* __restrict__ tile_vis, int64_t ntx, int64_t nty, int64_t ntw,
                                   int support, int64_t nplanes, uint8_t* __restrict__ mask) {
   const int64_t id = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -632,12 +632,14 @@ __global__ void dirty_mask_kernel(const int64_t* __restrict__ tile_vis, int64_t 
   for (int64_t w = lo; w <= hi && !touched; ++w) touched = tile_vis[w * nt + t] > 0;
   if (!touched) return;
   const int64_t tx = t % ntx, ty = t / ntx;
-  const int64_t tx1 = tx + 1 < ntx ? tx + 1 : 0, ty1 = ty + 1 < nty ? ty + 1 : 0;
   uint8_t* m = mask + p * nt;
-  m[ty * ntx + tx] = 1;  // idempotent stores: no atomics needed
-  m[ty * ntx + tx1] = 1;
-  m[ty1 * ntx + tx] = 1;
-  m[ty1 * ntx + tx1] = 1;
+  // the sub-grid's cells reach T + W - 2 past the tile origin: h more tiles
+  // per axis (1 for W <= T + 1, 2 for the large supports up to 64)
+  const int h = (kTile + support - 2) / kTile;
+  for (int dy = 0; dy <= h; ++dy) {
+    const int64_t yy = (ty + dy) % nty;
+    for (int dx = 0; dx <= h; ++dx) m[yy * ntx + (tx + dx) % ntx] = 1;  // idempotent stores: no atomics needed
+  }
 }
 
 // bit-pack the byte mask: bit tx % 32 of word ty * (ntx / 32) + tx / 32

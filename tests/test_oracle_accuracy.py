@@ -47,3 +47,22 @@ def test_oracle_wraps_periodic_uv_exactly(wstack):
     dft = oracle.dft_dirty(uvw, f, vis, w, npix, npix, px, px, apply_w=wstack)
     img = oracle.ms2dirty(uvw, f, vis, w, npix, npix, px, px, support=12, do_wstacking=wstack)
     assert np.abs(img - dft).max() / w.astype(np.float64).sum() < 1e-10
+
+
+# max |image - DFT| / sum(w) bounds of the large supports. At beta = 2.3 W the
+# kernel's transform at the image edge falls as exp(-0.138 W): F(1/4)/F(0) =
+# 0.12 (W = 16), 1.3e-2 (32), 1.6e-4 (64), so the grid correction amplifies
+# rounding there, and w-stacking multiplies the u, v and w corrections at the
+# field corners (W = 64: ~1e11). 2-D stays at ~1e-11 up to W = 64; w-stacking
+# reaches 3e-10 at W = 48 and 2e-7 at W = 64 (still inside the 1e-6 gate).
+LARGE_BOUND = {(False, 24): 1e-11, (False, 32): 1e-11, (False, 48): 1e-10, (False, 64): 1e-9,
+               (True, 24): 1e-11, (True, 32): 1e-10, (True, 48): 2e-9, (True, 64): 1e-6}
+
+
+@pytest.mark.parametrize("support", [24, 32, 48, 64])
+@pytest.mark.parametrize("wstack", [False, True])
+def test_oracle_large_supports_vs_dft(case, support, wstack):
+    uvw, f, vis, w, npix, px, dft = case
+    img = oracle.ms2dirty(uvw, f, vis, w, npix, npix, px, px, support=support, do_wstacking=wstack)
+    err = np.abs(img - dft[wstack]).max() / w.astype(np.float64).sum()
+    assert err < LARGE_BOUND[(wstack, support)], err
