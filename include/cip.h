@@ -81,8 +81,10 @@ extern "C" {
 
 typedef struct cip_gridder_params {
   int64_t nu, nv;      /* oversampled grid size (cells), even, 2/3/5/7-smooth */
-  int32_t support;     /* kernel support W (even, 4..16) */
-  int32_t degree;      /* polynomial degree of each kernel piece (W + 3) */
+  int32_t support;     /* kernel support W: even 4..16, or 24/32/48/64 (2-D;
+                          w-stacking up to 48) */
+  int32_t degree;      /* polynomial degree of each kernel piece (W + 3;
+                          15 for the large supports) */
   double beta;         /* ES shape parameter (2.3 W) */
   double sigma;        /* oversampling factor (2.0) */
   int32_t do_wstacking;/* 1: w-stacking planes; 0: 2-D (w ignored) */
@@ -93,7 +95,9 @@ typedef struct cip_gridder_params {
 } cip_gridder_params;
 
 /* Grid/kernel/w-plane parameters for an image of npix_x x npix_y pixels of
- * pixsize (radians, sin-projected). support <= 0 selects W from epsilon.
+ * pixsize (radians, sin-projected). support <= 0 selects W from epsilon
+ * (4..16); an explicit support may also be 24, 32, 48 or 64 (the
+ * wave-per-visibility scatter; fp64 class only; w-stacking up to 48).
  * wmin/wmax: range of w in wavelengths (only used when do_wstacking). */
 int cip_choose_params(int64_t npix_x, int64_t npix_y, double pixsize_x,
                       double pixsize_y, double epsilon, int support,
