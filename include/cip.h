@@ -72,6 +72,17 @@ extern "C" {
                           * on hip_stream. Without it, CIP_ASYNC work starts in
                           * hip_stream order. Outputs are in stream order
                           * either way. */
+#define CIP_REUSE_PLAN 64 /* cip_ms2dirty only, not with CIP_PIPELINE: the caller
+                          * promises that uvw, freq and the row layout are those
+                          * of this thread's previous planned call (e.g. the
+                          * Stokes parameters and PSF of one facet): when the
+                          * previous call's geometry (nrow, nchan, npix, pixel
+                          * sizes, epsilon / support, w-stacking, accumulation
+                          * class) matches, its tile plan (bucket, chunks,
+                          * bank-class order, dirty-tile masks) is used again
+                          * and only the weight sum and max |w V| are reduced;
+                          * otherwise the call plans as usual. Images are
+                          * identical to a planned call's. */
 #define CIP_ACC_SINGLE 2 /* complex64 only: single-precision accumulation
                           * class, the reference's ducc0 float gridding (re/im
                           * packed in one 64-bit fixed-point LDS cell, W^2

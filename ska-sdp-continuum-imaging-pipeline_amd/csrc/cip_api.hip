@@ -278,6 +278,17 @@ struct FftPlan {
   int64_t nu, nv;
 };
 
+struct PlanResult {
+  int64_t nruns = 0, ntiles = 0, nchunks = 0;
+  std::vector<int64_t> plane_chunk_off;  // chunk offset of tile layer iw (ntw + 1)
+  uint64_t* runs = nullptr;
+  int64_t* run_goff = nullptr;
+  int64_t* tile_run_off = nullptr;
+  Chunk* chunks = nullptr;
+  uint32_t* perm = nullptr;  // bank-class ordered visibility stream, or NULL
+  uint32_t* dmask = nullptr;  // grid tiles the scatter writes, per plane (bit-packed, ntx / 32 words per tile row)
+};
+
 struct Workspace {
   std::map<std::string, DevBuf> bufs;
   std::vector<FftPlan> plans;
@@ -310,6 +321,14 @@ struct Workspace {
   // the stream of the last CIP_ASYNC call, whose work may still be queued: a
   // call on another stream first waits for it (the workspace is shared)
   hipStream_t async_stream = nullptr;
+  // the last complete plan (its buffers stay untouched until the next planner
+  // runs) and the geometry it was made for: CIP_REUSE_PLAN calls with the
+  // same key grid through it. Cleared when a planner starts; never set for
+  // ragged rows (their row map lives in per-call buffers).
+  bool saved_valid = false;
+  std::vector<double> saved_key;
+  cip_gridder_params saved_p;
+  PlanResult saved_plan;
 };
 
 static int settle_async(Workspace* ws, hipStream_t s) {
@@ -421,6 +440,7 @@ static T* buf(Workspace* ws, const char* name, int64_t count) {
   DevBuf& b = ws->bufs[(ws->parity_scope && ws->parity) ? std::string(name) + "~1" : std::string(name)];
   if (b.bytes < bytes) {
     if (b.ptr && b.ptr == (void*)ws->grid_clean) ws->grid_clean = nullptr;  // a new buffer is not known zero
+    if (b.ptr) ws->saved_valid = false;  // the saved plan may point into it
     if (b.ptr) (void)hipFree(b.ptr);
     b.ptr = nullptr;
     b.bytes = 0;
@@ -503,16 +523,6 @@ static int64_t chunk_vis(bool packed) {
   return (env >= kOrderWindow && env < cap) ? env / kOrderWindow * kOrderWindow : cap;
 }
 
-struct PlanResult {
-  int64_t nruns = 0, ntiles = 0, nchunks = 0;
-  std::vector<int64_t> plane_chunk_off;  // chunk offset of tile layer iw (ntw + 1)
-  uint64_t* runs = nullptr;
-  int64_t* run_goff = nullptr;
-  int64_t* tile_run_off = nullptr;
-  Chunk* chunks = nullptr;
-  uint32_t* perm = nullptr;  // bank-class ordered visibility stream, or NULL
-  uint32_t* dmask = nullptr;  // grid tiles the scatter writes, per plane (bit-packed, ntx / 32 words per tile row)
-};
 
 // CIP_FFT_PRUNED=0 selects the full 2-D hipFFT transform (A/B experiments)
 static bool fft_pruned() {
@@ -748,7 +758,7 @@ static int prepare(Workspace* ws, const double* uvw, int64_t nrow, const double*
                    const void* vis, int vis_dtype, const void* wgt, int wgt_dtype, int64_t npix_x, int64_t npix_y,
                    double px, double py, double epsilon, int support, int do_wstacking, bool packed,
                    const cip_gridder_params* given, hipStream_t s, Prepared* out, double** grid_out = nullptr,
-                   const RaggedRows* ragged = nullptr) {
+                   const RaggedRows* ragged = nullptr, bool reuse = false) {
   if (!ws->parity_scope) ws->plan_unscoped = true;
   if (!vis_dtype_ok(vis_dtype)) return set_error(CIP_EINVAL, "vis dtype must be complex64 or complex128");
   if (!wgt_dtype_ok(wgt_dtype)) return set_error(CIP_EINVAL, "wgt dtype must be float32, float64 or none");
@@ -810,6 +820,14 @@ static int prepare(Workspace* ws, const double* uvw, int64_t nrow, const double*
       m.vis_row = vis_row;
     }
   }
+  // CIP_REUSE_PLAN: the previous plan, if it was made for this geometry (its
+  // parameters then also stand in for the w range: same uvw by the caller's
+  // promise)
+  const std::vector<double> key = {(double)nrow, (double)nchan, (double)npix_x, (double)npix_y, px, py, epsilon,
+                                   (double)support, (double)do_wstacking, (double)packed,
+                                   given ? 1.0 : 0.0};
+  const bool reusing = reuse && !ragged && given == nullptr && ws->saved_valid && ws->saved_key == key;
+  if (reusing) given = &ws->saved_p;
   double wmin = 0.0, wmax = 0.0;
   if (do_wstacking && nrow > 0 && given == nullptr) {
     const int nb = 256;
@@ -867,8 +885,35 @@ static int prepare(Workspace* ws, const double* uvw, int64_t nrow, const double*
     out->plan.plane_chunk_off.assign(out->g.ntw + 1, 0);
     return CIP_OK;
   }
-  const int rc = make_plan(ws, uvw, fx, m, vis, vis_dtype, wgt, wgt_dtype, red, out->g, chunk_vis(packed),
-                           s, &out->plan, &maxabs);
+  int rc;
+  if (reusing) {
+    // the plan's buffers are read-only here; only the weight reduction runs
+    const int nblk = plan_place_blocks(m.nvis);
+    CIP_ALLOC(partial, double, "prep_partial_reuse", 2 * nblk)
+    CIP_HIP_CHECK(launch_prep_reduce(m, vis, vis_dtype, wgt, wgt_dtype, out->g, err, partial, s));
+    CIP_HIP_CHECK(launch_prep_final(partial, nblk, red, s));
+    unsigned* h = (unsigned*)pinned(ws, 4 * sizeof(double));
+    if (!h) return set_error(CIP_ENOMEM, "hipHostMalloc failed");
+    CIP_HIP_CHECK(hipMemcpyAsync(h, err, sizeof(unsigned), hipMemcpyDeviceToHost, s));
+    CIP_HIP_CHECK(hipMemcpyAsync((double*)h + 1, red + 1, sizeof(double), hipMemcpyDeviceToHost, s));
+    CIP_HIP_CHECK(hipStreamSynchronize(s));
+    const unsigned errbits = h[0];
+    std::memcpy(&maxabs, (double*)h + 1, sizeof(double));
+    if (errbits & 4u) return set_error(CIP_EINVAL, "channel frequencies must be positive");
+    if (errbits & 2u) return set_error(CIP_EINVAL, "non-finite visibility or weight");
+    out->plan = ws->saved_plan;
+    rc = CIP_OK;
+  } else {
+    ws->saved_valid = false;
+    rc = make_plan(ws, uvw, fx, m, vis, vis_dtype, wgt, wgt_dtype, red, out->g, chunk_vis(packed), s, &out->plan,
+                   &maxabs);
+    if (rc == CIP_OK && !ragged) {
+      ws->saved_key = key;
+      ws->saved_p = out->p;
+      ws->saved_plan = out->plan;
+      ws->saved_valid = true;
+    }
+  }
   g_prof.span(1, e_prep, g_prof.mark(s));
   if (rc != CIP_OK) return rc;
   if (!std::isfinite(maxabs)) return set_error(CIP_EINVAL, "non-finite visibility or weight");
@@ -1091,8 +1136,10 @@ int cip_ms2dirty(const double* uvw, int64_t nrow, const double* freq, int64_t nc
                  double pixsize_y, double epsilon, int support, int flags, void* hip_stream,
                  double* dirty_out, double* sum_wgt_out, cip_gridder_params* params_out) {
   g_last_error.clear();
-  if (flags & ~(CIP_WSTACKING | CIP_ACC_SINGLE | CIP_PSF | CIP_NORMALISE | CIP_ASYNC | CIP_PIPELINE))
+  if (flags & ~(CIP_WSTACKING | CIP_ACC_SINGLE | CIP_PSF | CIP_NORMALISE | CIP_ASYNC | CIP_PIPELINE | CIP_REUSE_PLAN))
     return set_error(CIP_EINVAL, "unknown flags");
+  if ((flags & CIP_REUSE_PLAN) && (flags & CIP_PIPELINE))
+    return set_error(CIP_EINVAL, "CIP_REUSE_PLAN cannot be combined with CIP_PIPELINE");
   const int do_wstacking = (flags & CIP_WSTACKING) ? 1 : 0;
   const bool normalise = (flags & CIP_NORMALISE) != 0;
   const bool packed = (flags & CIP_ACC_SINGLE) != 0;
@@ -1156,7 +1203,7 @@ int cip_ms2dirty(const double* uvw, int64_t nrow, const double* freq, int64_t nc
   ws->parity_scope = pipelined;
   int rc = prepare(ws, uvw, nrow, freq, nchan, vis, vis_dtype, wgt, wgt_dtype, npix_x, npix_y, pixsize_x, pixsize_y,
                    epsilon, support, do_wstacking, packed, nullptr, ps, &pp,
-                   (overlap_zero() && !pipelined) ? &grid : nullptr);
+                   (overlap_zero() && !pipelined) ? &grid : nullptr, nullptr, (flags & CIP_REUSE_PLAN) != 0);
   ws->parity_scope = false;
   if (pipelined) {
     // s continues once the plan exists (also after a failed one: nothing then runs on it)

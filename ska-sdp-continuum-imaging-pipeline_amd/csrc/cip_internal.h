@@ -42,6 +42,10 @@ hipError_t launch_w_range(const double* uvw, int64_t nrow, double fxmin, double 
 // vis_class (optional, nvis bytes): each visibility's LDS bank class.
 // err_flag: bit 0 non-finite uvw / w off the stack, bit 1 non-finite vis or weight.
 int plan_place_blocks(int64_t nvis);
+// the place pass's reduction alone (sum of weights, max |w V|, non-finite
+// check -> partial, err_flag bit 2), in its order: for calls reusing a plan
+hipError_t launch_prep_reduce(const RowMap& m, const void* vis, int vis_dtype, const void* wgt, int wgt_dtype,
+                              const GridGeometry& g, unsigned* err_flag, double* partial, hipStream_t s);
 hipError_t launch_plan_place(const double* uvw, const double* fx, const RowMap& m,
                              const void* vis, int vis_dtype, const void* wgt, int wgt_dtype, const GridGeometry& g,
                              unsigned* err_flag, uint8_t* vis_class, int64_t* blk_cnt, uint32_t* park_key,

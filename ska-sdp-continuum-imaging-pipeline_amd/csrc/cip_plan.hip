@@ -198,7 +198,10 @@ constexpr uint32_t kNoKey = 0xffffffffu;  // visibility off the grid (tile keys 
 #ifndef CIP_PLACE_WAVES
 #define CIP_PLACE_WAVES 1  // min waves per SIMD the place pass is compiled for
 #endif
-template <typename VisT, int WK>
+// PLACE = false: only the fused reduction (sum of weights, max |w V|,
+// non-finite check), in exactly the place pass's order - a call that reuses
+// its predecessor's plan (CIP_REUSE_PLAN) gets the same sums bit for bit.
+template <typename VisT, int WK, bool PLACE = true>
 __global__ __launch_bounds__(256, CIP_PLACE_WAVES) void plan_place_kernel(const double* __restrict__ uvw,
                                                          const double* __restrict__ fx, RowMap m,
                                                          const VisT* __restrict__ vis, const void* __restrict__ wgt,
@@ -249,7 +252,13 @@ __global__ __launch_bounds__(256, CIP_PLACE_WAVES) void plan_place_kernel(const 
     const int64_t rl = valid ? r : 0, cl = valid ? c : 0;
     // position loads first: the visibility load of a PSF call is a branch,
     // and the wait inside it then covers every load (one memory round trip)
-    const double u = uvw[3 * rl], v = uvw[3 * rl + 1], w = uvw[3 * rl + 2], f = fx[cl];
+    double u = 0.0, v = 0.0, w = 0.0, f = 0.0;
+    if constexpr (PLACE) {
+      u = uvw[3 * rl];
+      v = uvw[3 * rl + 1];
+      w = uvw[3 * rl + 2];
+      f = fx[cl];
+    }
     const double wt = load_weight<WK>(wgt, il);
     double vr, vi;
 #if CIP_PLACE_ABL == 1
@@ -263,41 +272,43 @@ __global__ __launch_bounds__(256, CIP_PLACE_WAVES) void plan_place_kernel(const 
     nonfinite = nonfinite | (counted && !(isfinite(wt) && isfinite(vr) && isfinite(vi)));
     wsum = valid ? wsum + wt : wsum;
     wvmax = fmax(wvmax, a);
-    int ix0, iy0;
-    int64_t iw0;
-    const bool ok = place_origin(u, v, w, f, g, &ix0, &iy0, &iw0);
-    // the tile key modulo 2^32 (keys are < 2^32 - 1)
-    const uint32_t key = (valid & ok) ? (((uint32_t)iw0 * (uint32_t)g.nty + (uint32_t)iy0 / (uint32_t)kTile) *
-                                             (uint32_t)g.ntx + (uint32_t)ix0 / (uint32_t)kTile)
-                                      : kNoKey;
-    const bool bad = valid & !ok;
+    if constexpr (PLACE) {
+      int ix0, iy0;
+      int64_t iw0;
+      const bool ok = place_origin(u, v, w, f, g, &ix0, &iy0, &iw0);
+      // the tile key modulo 2^32 (keys are < 2^32 - 1)
+      const uint32_t key = (valid & ok) ? (((uint32_t)iw0 * (uint32_t)g.nty + (uint32_t)iy0 / (uint32_t)kTile) *
+                                               (uint32_t)g.ntx + (uint32_t)ix0 / (uint32_t)kTile)
+                                        : kNoKey;
+      const bool bad = valid & !ok;
 #if CIP_PLACE_ABL != 3
-    if (vis_class && valid)
-      vis_class[i] = ok ? (uint8_t)((((unsigned)ix0 % kTile) * P + (unsigned)iy0 % kTile) & 31u) : (uint8_t)0;
+      if (vis_class && valid)
+        vis_class[i] = ok ? (uint8_t)((((unsigned)ix0 % kTile) * P + (unsigned)iy0 % kTile) & 31u) : (uint8_t)0;
 #endif
-    if (__ballot(bad) != 0ull && lane == 0) atomicOr(err_flag, 1u);
-    const uint32_t prev = __shfl_up(key, 1, 64);
-    const uint32_t prev_r = __shfl_up((uint32_t)r, 1, 64);  // rows < 2^32
-    const bool start = valid && (lane == 0 || (uint32_t)r != prev_r || key != prev);
-    const unsigned long long starts = __ballot(start);
-    const bool emit = start && key != kNoKey;
-    const unsigned long long emits = __ballot(emit);
-    const int nvalid = __popcll(__ballot(valid));  // wave-uniform: outside the branch
-    // the block's runs are parked densely from slot 64 * kPlaceSegs * b on
-    unsigned wbase = 0;
-    if (lane == 0 && emits) wbase = atomicAdd(&s_nruns, (unsigned)__popcll(emits));
-    wbase = __shfl(wbase, 0, 64);
+      if (__ballot(bad) != 0ull && lane == 0) atomicOr(err_flag, 1u);
+      const uint32_t prev = __shfl_up(key, 1, 64);
+      const uint32_t prev_r = __shfl_up((uint32_t)r, 1, 64);  // rows < 2^32
+      const bool start = valid && (lane == 0 || (uint32_t)r != prev_r || key != prev);
+      const unsigned long long starts = __ballot(start);
+      const bool emit = start && key != kNoKey;
+      const unsigned long long emits = __ballot(emit);
+      const int nvalid = __popcll(__ballot(valid));  // wave-uniform: outside the branch
+      // the block's runs are parked densely from slot 64 * kPlaceSegs * b on
+      unsigned wbase = 0;
+      if (lane == 0 && emits) wbase = atomicAdd(&s_nruns, (unsigned)__popcll(emits));
+      wbase = __shfl(wbase, 0, 64);
 #if CIP_PLACE_ABL == 2
-    if (emit && key == 0x7fffffffu) {
+      if (emit && key == 0x7fffffffu) {
 #else
-    if (emit) {
+      if (emit) {
 #endif
-      const unsigned long long above = starts & ~((2ull << lane) - 1ull);  // lane 63: 2 << 63 == 0
-      const int next = above ? (__ffsll((long long)above) - 1) : nvalid;
-      const int64_t slot = (int64_t)blockIdx.x * kPlaceSegs * 64 + wbase + __popcll(emits & ((1ull << lane) - 1ull));
-      park_key[slot] = key;
-      atomicAdd(&s_hist[key & 255u], 1u);
-      park_run[slot] = ((uint64_t)r << 32) | ((uint64_t)c << 16) | (uint64_t)(c + (next - lane));
+        const unsigned long long above = starts & ~((2ull << lane) - 1ull);  // lane 63: 2 << 63 == 0
+        const int next = above ? (__ffsll((long long)above) - 1) : nvalid;
+        const int64_t slot = (int64_t)blockIdx.x * kPlaceSegs * 64 + wbase + __popcll(emits & ((1ull << lane) - 1ull));
+        park_key[slot] = key;
+        atomicAdd(&s_hist[key & 255u], 1u);
+        park_run[slot] = ((uint64_t)r << 32) | ((uint64_t)c << 16) | (uint64_t)(c + (next - lane));
+      }
     }
   }
   if (nonfinite) atomicOr(err_flag, 2u);
@@ -311,12 +322,14 @@ __global__ __launch_bounds__(256, CIP_PLACE_WAVES) void plan_place_kernel(const 
     sm[threadIdx.x >> 6] = wvmax;
   }
   __syncthreads();
-  hist0[(int64_t)threadIdx.x * gridDim.x + blockIdx.x] = s_hist[threadIdx.x];
+  if constexpr (PLACE) hist0[(int64_t)threadIdx.x * gridDim.x + blockIdx.x] = s_hist[threadIdx.x];
   if (threadIdx.x == 0) {
     partial[2 * blockIdx.x] = (ss[0] + ss[1]) + (ss[2] + ss[3]);
     partial[2 * blockIdx.x + 1] = fmax(fmax(sm[0], sm[1]), fmax(sm[2], sm[3]));
-    blk_cnt[blockIdx.x] = s_nruns;
-    if (blockIdx.x == 0) hist0[256 * (int64_t)gridDim.x] = 0;
+    if constexpr (PLACE) {
+      blk_cnt[blockIdx.x] = s_nruns;
+      if (blockIdx.x == 0) hist0[256 * (int64_t)gridDim.x] = 0;
+    }
   }
 }
 
@@ -327,6 +340,26 @@ static unsigned plan_blocks(int64_t nvis) {
 }
 
 int plan_place_blocks(int64_t nvis) { return (int)plan_blocks(nvis); }
+
+hipError_t launch_prep_reduce(const RowMap& m, const void* vis, int vis_dtype, const void* wgt, int wgt_dtype,
+                              const GridGeometry& g, unsigned* err_flag, double* partial, hipStream_t s) {
+  const dim3 gd(plan_blocks(m.nvis));
+#define REDUCE(VT, WKV)                                                                                      \
+  plan_place_kernel<VT, WKV, false><<<gd, dim3(256), 0, s>>>(nullptr, nullptr, m, (const VT*)vis, wgt, g,    \
+                                                            err_flag, nullptr, nullptr, nullptr, nullptr,   \
+                                                            partial, nullptr)
+  if (vis_dtype == CIP_C64) {
+    if (wgt_dtype == CIP_F32) REDUCE(float2, WK_F32);
+    else if (wgt_dtype == CIP_F64) REDUCE(float2, WK_F64);
+    else REDUCE(float2, WK_NONE);
+  } else {
+    if (wgt_dtype == CIP_F32) REDUCE(double2, WK_F32);
+    else if (wgt_dtype == CIP_F64) REDUCE(double2, WK_F64);
+    else REDUCE(double2, WK_NONE);
+  }
+#undef REDUCE
+  return hipGetLastError();
+}
 
 hipError_t launch_plan_place(const double* uvw, const double* fx, const RowMap& m,
                              const void* vis, int vis_dtype, const void* wgt, int wgt_dtype, const GridGeometry& g,

@@ -33,6 +33,7 @@ CIP_PSF = 4
 CIP_NORMALISE = 8
 CIP_ASYNC = 16
 CIP_PIPELINE = 32
+CIP_REUSE_PLAN = 64
 STOKES_CODES = {"I": 0, "Q": 1, "U": 2, "V": 3}
 
 # every symbol declared in include/cip.h

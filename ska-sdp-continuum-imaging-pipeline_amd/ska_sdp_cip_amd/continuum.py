@@ -53,6 +53,7 @@ def continuum_invert(
     do_wstacking: bool = True,
     rank: int = 0,
     world: int = 1,
+    reuse_plans: bool = True,
 ) -> dict:
     """
     Dirty images (normalised by each Stokes parameter's weight sum) and PSFs
@@ -61,6 +62,8 @@ def continuum_invert(
     (nchan,) f64. `facets`: centres (l0, m0) (default: one facet at the phase
     centre). Returns {(name, k): fp64 device tensor (facet_pixels,
     facet_pixels)} with name in `stokes` or "PSF", for this rank's facets k.
+    `reuse_plans`: a facet's later products reuse its first product's tile
+    plan (the same rephased uvw; identical images, one planner per facet).
     """
     _require_gpu()
     pix = pixel_size_lm(pixel_size_asec)
@@ -76,14 +79,19 @@ def continuum_invert(
     for k, (l0, m0) in enumerate(facets):
         if k % world != rank:
             continue
+        # the facet's products share its rephased uvw: the first one plans,
+        # the others reuse that tile plan (CIP_REUSE_PLAN)
+        planned = False
         for s, (vis_s, eff) in per_stokes.items():
             uvw_f, vis_f = device_facet_rephase(uvw, freq, vis_s, l0, m0)
-            img, _ = device_ms2dirty(uvw_f, freq, vis_f, eff, facet_pixels, facet_pixels, pix, pix, **kw)
+            img, _ = device_ms2dirty(uvw_f, freq, vis_f, eff, facet_pixels, facet_pixels, pix, pix,
+                                     reuse_plan=planned and reuse_plans, **kw)
+            planned = True
             out[(s, k)] = img.div_(sums[s])
         if psf:
             uvw_f, _ = device_facet_rephase(uvw, freq, None, l0, m0)
             img, _ = device_ms2dirty(uvw_f, freq, None, wts["I"], facet_pixels, facet_pixels, pix, pix, psf=True,
-                                     **kw)
+                                     reuse_plan=planned and reuse_plans, **kw)
             out[("PSF", k)] = img.div_(sums["I"])
     return out
 

@@ -73,6 +73,7 @@ def device_ms2dirty(
     normalise: bool = False,
     synchronize: bool = True,
     resident_inputs: bool = False,
+    reuse_plan: bool = False,
 ) -> tuple["torch.Tensor", _lib.GridderParams]:
     """
     Device-resident ms2dirty: all tensors already in HBM on the current device.
@@ -97,9 +98,16 @@ def device_ms2dirty(
     asynchronous call returned and stay unchanged (resident data, as in the
     benchmark): the planner of this call then runs beside the previous call's
     scatter and FFT instead of after all work queued on the stream.
+    `reuse_plan=True` (CIP_REUSE_PLAN, not with `resident_inputs`) promises
+    that uvw, freq and the row layout equal those of this thread's previous
+    planned call (e.g. the Stokes parameters and PSF of one facet): if that
+    call's geometry matches, its tile plan is used again and only the weight
+    sum and max |w V| are computed (images identical to a planned call's).
     """
     if resident_inputs and synchronize:
         raise ValueError("resident_inputs=True needs synchronize=False")
+    if reuse_plan and resident_inputs:
+        raise ValueError("reuse_plan=True cannot be combined with resident_inputs=True")
     vis_codes, wgt_codes = _codes()
     if psf:
         vis = None  # never read
@@ -136,7 +144,7 @@ def device_ms2dirty(
         stream = torch.cuda.current_stream(uvw.device).cuda_stream
         rc = _ms2dirty_call(uvw, freq, vis, wgt, vis_codes, wgt_codes, npix_x, npix_y, pixsize_x, pixsize_y,
                             epsilon, support, do_wstacking, single_precision_accumulation, psf, normalise,
-                            stream, out, sum_weights, params, synchronize, resident_inputs)
+                            stream, out, sum_weights, params, synchronize, resident_inputs, reuse_plan)
     _lib.check(rc)
     return out, params
 
@@ -152,7 +160,7 @@ def _check_device_tensor(t, device, what):
 
 def _ms2dirty_call(uvw, freq, vis, wgt, vis_codes, wgt_codes, npix_x, npix_y, pixsize_x, pixsize_y, epsilon,
                    support, do_wstacking, single_precision_accumulation, psf, normalise, stream, out,
-                   sum_weights, params, synchronize=True, resident_inputs=False):
+                   sum_weights, params, synchronize=True, resident_inputs=False, reuse_plan=False):
     nrow = uvw.shape[0]
     nchan = freq.shape[0]
     return _lib.lib().cip_ms2dirty(
@@ -167,7 +175,8 @@ def _ms2dirty_call(uvw, freq, vis, wgt, vis_codes, wgt_codes, npix_x, npix_y, pi
         | (_lib.CIP_PSF if psf else 0)
         | (_lib.CIP_NORMALISE if normalise else 0)
         | (0 if synchronize else _lib.CIP_ASYNC)
-        | (_lib.CIP_PIPELINE if resident_inputs else 0),
+        | (_lib.CIP_PIPELINE if resident_inputs else 0)
+        | (_lib.CIP_REUSE_PLAN if reuse_plan else 0),
         stream, out.data_ptr(),
         sum_weights.data_ptr() if sum_weights is not None else None, params)
 

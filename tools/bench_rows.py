@@ -35,6 +35,7 @@ def main():
     ap.add_argument("--rows-per-chunk", type=int, default=32_768)
     ap.add_argument("--facets", type=int, default=2, help="facets per axis (continuum)")
     ap.add_argument("--repeat", type=int, default=3)
+    ap.add_argument("--no-reuse", action="store_true", help="continuum: plan every product (no CIP_REUSE_PLAN)")
     args = ap.parse_args()
 
     import torch
@@ -72,7 +73,7 @@ def main():
         cols = (t(ms.visibilities()), t(ms.flags(), np.uint8), t(ms.weights()), t(uvw), t(freq))
         facets = facet_centres(args.facets, args.facets, args.npix, px)
         run = lambda: continuum_invert(*cols, args.npix, asec, facets=facets, stokes="IQUV",  # noqa: E731
-                                       psf=True, support=8, do_wstacking=False)
+                                       psf=True, support=8, do_wstacking=False, reuse_plans=not args.no_reuse)
         run()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -83,7 +84,8 @@ def main():
         nimg = len(res)
         out.update(metric="continuum products: Stokes IQUV + PSF per facet (2-D, support 8)",
                    value=round(nimg / dt, 2), unit="images/s", images=nimg, facets=len(facets),
-                   ms_per_call=round(dt * 1e3, 2), mvis_per_s_per_image=round(nvis * nimg / dt / 1e6, 1))
+                   ms_per_call=round(dt * 1e3, 2), mvis_per_s_per_image=round(nvis * nimg / dt / 1e6, 1),
+                   reuse_plans=not args.no_reuse)
     print(json.dumps(out), flush=True)
 
 
