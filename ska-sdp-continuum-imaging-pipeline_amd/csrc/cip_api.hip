@@ -688,34 +688,51 @@ static int make_plan(Workspace* ws, const double* uvw, const double* fx, const R
     pr->dmask = dbits;
   }
   // 2-D: the scatter's work units largest first (one tile layer, so the
-  // plane's chunk range stays contiguous); w-stacking: tile order (each plane
-  // takes the chunks of its tile layers)
-  const int full_first = (g.ntw == 1 && chunks_full_first()) ? 1 : 0;
-  const int64_t nent = full_first ? 2 * ntiles : ntiles;
-  CIP_ALLOC(scan_tmpc, int64_t, "scan_tmp_chunks", scan_tmp_elems(2 * ntiles + 1))
-  CIP_HIP_CHECK(launch_chunk_counts(tile_vis, ntiles, cv, full_first, chunk_off, s));
-  CIP_HIP_CHECK(exclusive_scan_i64(chunk_off, nent + 1, scan_tmpc, s));
-  // chunk offsets of each w tile layer
-  const int64_t layer = full_first ? nent : g.ntx * g.nty;
-  CIP_ALLOC(layer_off, int64_t, "layer_off", g.ntw + 1)
-  CIP_HIP_CHECK(launch_gather_i64(chunk_off, layer, g.ntw + 1, layer_off, s));
-  // bank-class ordering windows: the same split with kOrderWindow
+  // plane's chunk range stays contiguous); w-stacking: per plane, one unit
+  // sequence per uv tile over its layers feeding the plane (tile-major keys
+  // make that a contiguous range), plane after plane
+  const int64_t ntxy = g.ntx * g.nty;
+  const bool per_plane = g.do_wstacking != 0;
+  const int64_t nrange = per_plane ? g.nplanes : 1;  // chunk ranges: per plane, or the one 2-D layer
+  const int full_first = (!per_plane && chunks_full_first()) ? 1 : 0;
+  CIP_ALLOC(layer_off, int64_t, "layer_off", nrange + 1)
+  int64_t* pc_off = nullptr;
+  if (per_plane) {
+    const int64_t nentp = g.nplanes * ntxy;
+    pc_off = buf<int64_t>(ws, "plane_chunk_cnt", nentp + 1);
+    int64_t* scan_tmpp = buf<int64_t>(ws, "scan_tmp_pchunks", scan_tmp_elems(nentp + 1));
+    if (!pc_off || !scan_tmpp) return CIP_ENOMEM;
+    CIP_HIP_CHECK(launch_plane_chunk_counts(tile_vis_off, ntxy, g.ntw, g.nplanes, g.support, cv, pc_off, s));
+    CIP_HIP_CHECK(exclusive_scan_i64(pc_off, nentp + 1, scan_tmpp, s));
+    CIP_HIP_CHECK(launch_gather_i64(pc_off, ntxy, nrange + 1, layer_off, s));
+  } else {
+    const int64_t nent = full_first ? 2 * ntiles : ntiles;
+    CIP_ALLOC(scan_tmpc, int64_t, "scan_tmp_chunks", scan_tmp_elems(2 * ntiles + 1))
+    CIP_HIP_CHECK(launch_chunk_counts(tile_vis, ntiles, cv, full_first, chunk_off, s));
+    CIP_HIP_CHECK(exclusive_scan_i64(chunk_off, nent + 1, scan_tmpc, s));
+    CIP_HIP_CHECK(launch_gather_i64(chunk_off, full_first ? nent : ntiles, nrange + 1, layer_off, s));
+  }
+  // bank-class ordering windows: the same split with kOrderWindow, per tile key
   CIP_ALLOC(win_off, int64_t, "win_off", ntiles + 1)
   if (order) {
     CIP_HIP_CHECK(launch_chunk_counts(tile_vis, ntiles, kOrderWindow, 0, win_off, s));
     CIP_HIP_CHECK(exclusive_scan_i64(win_off, ntiles + 1, scan_tmp, s));
   }
-  int64_t* hl = (int64_t*)pinned(ws, sizeof(int64_t) * (g.ntw + 2));
+  int64_t* hl = (int64_t*)pinned(ws, sizeof(int64_t) * (nrange + 2));
   if (!hl) return set_error(CIP_ENOMEM, "hipHostMalloc failed");
-  CIP_HIP_CHECK(hipMemcpyAsync(hl, layer_off, sizeof(int64_t) * (g.ntw + 1), hipMemcpyDeviceToHost, s));
-  if (order) CIP_HIP_CHECK(hipMemcpyAsync(hl + g.ntw + 1, win_off + ntiles, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+  CIP_HIP_CHECK(hipMemcpyAsync(hl, layer_off, sizeof(int64_t) * (nrange + 1), hipMemcpyDeviceToHost, s));
+  if (order) CIP_HIP_CHECK(hipMemcpyAsync(hl + nrange + 1, win_off + ntiles, sizeof(int64_t), hipMemcpyDeviceToHost, s));
   CIP_HIP_CHECK(hipStreamSynchronize(s));
-  pr->plane_chunk_off.assign(hl, hl + g.ntw + 1);
-  const int64_t nwin = order ? hl[g.ntw + 1] : 0;
+  pr->plane_chunk_off.assign(hl, hl + nrange + 1);
+  const int64_t nwin = order ? hl[nrange + 1] : 0;
   pr->nchunks = pr->plane_chunk_off.back();
   CIP_ALLOC(chunks, Chunk, "chunks", pr->nchunks)
-  CIP_HIP_CHECK(launch_chunk_emit(tile_vis_off, tile_vis, chunk_off, run_goff, tile_runs, ntiles, cv, full_first,
-                                  pr->nchunks, chunks, s));
+  if (per_plane)
+    CIP_HIP_CHECK(launch_plane_chunk_emit(tile_vis_off, pc_off, run_goff, tile_runs, ntxy, g.ntw, g.nplanes, g.support,
+                                          cv, pr->nchunks, chunks, s));
+  else
+    CIP_HIP_CHECK(launch_chunk_emit(tile_vis_off, tile_vis, chunk_off, run_goff, tile_runs, ntiles, cv, full_first,
+                                    pr->nchunks, chunks, s));
   pr->runs = runs;
   pr->run_goff = run_goff;
   pr->tile_run_off = tile_runs;
@@ -875,14 +892,14 @@ static int prepare(Workspace* ws, const double* uvw, int64_t nrow, const double*
   if (nrow == 0) {
     CIP_HIP_CHECK(hipMemsetAsync(red, 0, 2 * sizeof(double), s));
     out->plan = PlanResult();
-    out->plan.plane_chunk_off.assign(out->g.ntw + 1, 0);
+    out->plan.plane_chunk_off.assign((out->g.do_wstacking ? out->g.nplanes : 1) + 1, 0);
     return CIP_OK;
   }
   double maxabs = 0.0;
   if (m.nvis == 0) {
     CIP_HIP_CHECK(hipMemsetAsync(red, 0, 2 * sizeof(double), s));
     out->plan = PlanResult();
-    out->plan.plane_chunk_off.assign(out->g.ntw + 1, 0);
+    out->plan.plane_chunk_off.assign((out->g.do_wstacking ? out->g.nplanes : 1) + 1, 0);
     return CIP_OK;
   }
   int rc;
@@ -938,14 +955,9 @@ static int scatter_plane(const Prepared& pp, int64_t plane, const double* uvw, c
   g.transposed = transposed ? 1 : 0;
   if (!zeroed) CIP_HIP_CHECK(hipMemsetAsync(grid, 0, sizeof(double) * 2 * g.nu * g.nv, s));
   if (pp.plan.nchunks == 0) return CIP_OK;
-  int64_t lo = 0, hi = 0;  // tile layers feeding this plane
-  if (g.do_wstacking) {
-    lo = plane - g.support + 1;
-    if (lo < 0) lo = 0;
-    hi = plane < g.ntw - 1 ? plane : g.ntw - 1;
-    if (hi < lo) return CIP_OK;
-  }
-  const int64_t cb = pp.plan.plane_chunk_off[lo], ce = pp.plan.plane_chunk_off[hi + 1];
+  // the plane's work units (w-stacking: its tiles' layers p - W + 1 .. p)
+  const int64_t k = g.do_wstacking ? plane : 0;
+  const int64_t cb = pp.plan.plane_chunk_off[k], ce = pp.plan.plane_chunk_off[k + 1];
   if (wgt == nullptr) wgt_dtype = CIP_NONE;
   hipEvent_t a = g_prof.mark(s);
   CIP_HIP_CHECK(launch_scatter(g.support, vis_dtype, wgt_dtype, pp.packed, uvw, pp.fx, vis, wgt, pp.m, pp.plan.runs,

@@ -329,9 +329,21 @@ __device__ __forceinline__ void vis_rowchan(const RowMap& m, int64_t i, int64_t*
   }
 }
 
+// Tile key of a footprint origin: tile-major, key = ((iy0 / T) ntx + ix0 / T)
+// ntw + iw0, so the w layers of one uv tile are adjacent in the tile-sorted
+// stream and a w-stacking plane's work units (layers p - W + 1 .. p of a tile)
+// are contiguous ranges (2-D: ntw = 1, key = tile).
 __device__ __forceinline__ int64_t tile_key(int64_t ix0, int64_t iy0, int64_t iw0, const GridGeometry& g) {
   // ix0, iy0 in [0, 2^31) after wrapping: unsigned division
-  return (iw0 * g.nty + (int64_t)((uint32_t)iy0 / (uint32_t)kTile)) * g.ntx + (int64_t)((uint32_t)ix0 / (uint32_t)kTile);
+  return ((int64_t)((uint32_t)iy0 / (uint32_t)kTile) * g.ntx + (int64_t)((uint32_t)ix0 / (uint32_t)kTile)) * g.ntw +
+         iw0;
+}
+
+// Grid origin of a tile key's T x T tile.
+__device__ __forceinline__ void tile_origin(int64_t key, const GridGeometry& g, int64_t* X0, int64_t* Y0) {
+  const int64_t t = key / g.ntw;
+  *X0 = (t % g.ntx) * kTile;
+  *Y0 = ((t / g.ntx) % g.nty) * kTile;
 }
 
 // visibility / weight loads by dtype (CIP_C64 -> float2, CIP_C128 -> double2)

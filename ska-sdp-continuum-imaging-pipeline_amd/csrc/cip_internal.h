@@ -87,6 +87,12 @@ hipError_t launch_chunk_counts(const int64_t* tile_vis, int64_t ntiles, int64_t 
 hipError_t launch_chunk_emit(const int64_t* tile_vis_off, const int64_t* tile_vis, const int64_t* chunk_off,
                              const int64_t* run_goff, const int64_t* tile_run_off, int64_t ntiles,
                              int64_t chunk_vis, int full_first, int64_t nchunks, Chunk* chunks, hipStream_t s);
+// w-stacking: per (plane, uv tile) work units over the tile's merged layer range
+hipError_t launch_plane_chunk_counts(const int64_t* tile_vis_off, int64_t ntxy, int64_t ntw, int64_t nplanes,
+                                     int support, int64_t cv, int64_t* out, hipStream_t s);
+hipError_t launch_plane_chunk_emit(const int64_t* tile_vis_off, const int64_t* chunk_off, const int64_t* run_goff,
+                                   const int64_t* tile_run_off, int64_t ntxy, int64_t ntw, int64_t nplanes,
+                                   int support, int64_t cv, int64_t nchunks, Chunk* chunks, hipStream_t s);
 hipError_t launch_gather_i64(const int64_t* src, int64_t stride, int64_t count, int64_t* dst,
                              hipStream_t s);
 

@@ -223,9 +223,8 @@ __global__ __launch_bounds__(kScatterThreads, CIP_SCATTER_WAVES) void scatter_ke
   __shared__ uint64_t s_run[PERM ? 1 : kRunBatch];
 
   const Chunk ch = chunks[chunk_begin + blockIdx.x];
-  const int64_t t = ch.tile;
-  const int64_t X0 = (t % g.ntx) * T;
-  const int64_t Y0 = ((t / g.ntx) % g.nty) * T;
+  int64_t X0, Y0;
+  tile_origin(ch.tile, g, &X0, &Y0);
   for (int i = threadIdx.x; i < P * P * (PACK ? 1 : 2); i += kScatterThreads) sub[i] = 0ull;
   if constexpr (PACK) {
     fixed_scale *= packed_chunk_gain(ch.g1 - ch.g0);
@@ -262,7 +261,7 @@ __global__ __launch_bounds__(kScatterThreads, CIP_SCATTER_WAVES) void scatter_ke
       pn = pnn;
     }
   } else {
-    const int64_t rb = tile_run_off[t + 1];
+    const int64_t rb = ch.last_run + 1;  // (a w-stacking unit spans several tile keys)
     int64_t r = ch.first_run;
     int64_t v = ch.g0;
     while (v < ch.g1 && r < rb) {

@@ -78,9 +78,8 @@ __global__ __launch_bounds__(kLargeThreads) void scatter_large_kernel(
   constexpr int R = 64 / W;  // footprint rows per wave instruction (2 for W = 24, 32; 1 for 48, 64)
   constexpr int P = T + W - 1, PP = P * P;
   const Chunk ch = chunks[chunk_begin + blockIdx.x];
-  const int64_t t = ch.tile;
-  const int64_t X0 = (t % g.ntx) * T;
-  const int64_t Y0 = ((t / g.ntx) % g.nty) * T;
+  int64_t X0, Y0;
+  tile_origin(ch.tile, g, &X0, &Y0);
   for (int i = threadIdx.x; i < 2 * PP; i += kLargeThreads) sub[i] = 0ull;
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
