@@ -186,8 +186,11 @@ static hipError_t launch_large_one(dim3 gd, hipStream_t s, const double* uvw, co
   constexpr size_t lds = (size_t)2 * P * P * sizeof(unsigned long long);
   static_assert(lds <= 160 * 1024, "sub-grid fits the CU's LDS");
   auto* fn = scatter_large_kernel<W, VisT, WK, WSTACK, PERM>;
-  // more than the default 64 KiB of dynamic LDS (144 KiB at W = 64)
-  hipError_t e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  // more than the default 64 KiB of dynamic LDS (144 KiB at W = 64); set on
+  // every launch (the attribute belongs to the current device's function, and
+  // a host thread may drive several devices; a large-support launch runs for
+  // milliseconds)
+  const hipError_t e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
   fn<<<gd, dim3(kLargeThreads), lds, s>>>(uvw, fx, (const VisT*)vis, wgt, m, runs, run_goff, perm, chunks, cb, g,
                                           plane, fs, 1.0 / fs, grid);

@@ -256,3 +256,17 @@ def test_allreduce_rejects_duplicate_devices():
     assert b"distinct" in L.cip_last_error()
     devs = (ctypes.c_int * 2)(-1, 1)
     assert L.cip_allreduce_grid(grids, devs, 2, 4, -1, None) == _lib.CIP_EINVAL
+
+
+def test_python_constants_match_c_header():
+    # every status / dtype / flag code the ctypes layer passes equals the
+    # #define of include/cip.h (the C ABI is the boundary)
+    header = (Path(__file__).resolve().parents[1] / "include" / "cip.h").read_text()
+    defines = {m.group(1): int(m.group(2)) for m in re.finditer(r"#define (CIP_[A-Z0-9_]+) \(?(-?\d+)\)?", header)}
+    checked = 0
+    for name, value in vars(_lib).items():
+        if name.startswith("CIP_") and isinstance(value, int):
+            assert defines.get(name) == value, name
+            checked += 1
+    assert checked >= 16
+    assert {v: k for k, v in _lib.STOKES_CODES.items()} == {defines[f"CIP_STOKES_{s}"]: s for s in "IQUV"}
