@@ -4,7 +4,7 @@
 // The image keeps only nx x ny of the nu x nv frequencies (a quarter for
 // sigma = 2). The scatter writes the grid transposed (gT[y, x]); pass A
 // transforms each row of gT along u and keeps the nx frequencies i, written
-// in 8-column blocks; pass B transforms each kept column i along v and writes
+// in 4-column blocks; pass B transforms each kept column i along v and writes
 // image row i directly through the crop epilogue (grid correction, or the
 // w-plane screen and accumulation). Each workgroup holds one N-point
 // transform: N/16 threads x 16 complex values in registers, radix-16 (and a
@@ -145,9 +145,12 @@ __device__ __forceinline__ void exchange(double2* v, int t, int ns, double* lds)
   }
 }
 
-// Pass A output block width (columns i per contiguous row of a block).
+// Pass A output block width (columns i per contiguous 16 CIP_FFT_COLBLOCK-byte
+// row of a block). 4 and 8 tie at N = 8192; at N = 16384 (one block per CU)
+// 4 is faster: FFT 3.50 -> 3.23 ms at C4, interleaved A/B
+// (profiles/r02_ab_fft_colblock.txt).
 #ifndef CIP_FFT_COLBLOCK
-#define CIP_FFT_COLBLOCK 8
+#define CIP_FFT_COLBLOCK 4
 #endif
 constexpr int kColBlock = CIP_FFT_COLBLOCK;
 
@@ -182,8 +185,8 @@ __device__ __forceinline__ void fft_core(double2* v, int t, double* lds, const d
 
 // Pass A, along u: row y of the transposed grid gT (nv rows of nu = N cells)
 // -> the nx kept frequencies, i = (k + nx/2) mod N < nx, stored in blocks of
-// 8 columns: H[((i / 8) nv + y) 8 + i % 8] (128-byte rows per block, so pass
-// B's 8 columns of a block read whole lines between them).
+// C = kColBlock columns: H[((i / C) nv + y) C + i % C] (16 C-byte rows per
+// block, so pass B's C columns of a block read whole rows between them).
 // MASKED: only the row's cells in dirty tiles (dmask, kTile-cell segments)
 // are read - the rest of the grid is zero - and those are zeroed after the
 // read, so the next scatter needs no memset of the whole grid.
@@ -234,7 +237,7 @@ __global__ __launch_bounds__(N / 16) void fft_rows_kernel(double2* __restrict__ 
 //   MODE 0 (2-D):      dirty[i, j]  = (-1)^(p+q) Re(.) cx[i] cy[j]
 //   MODE 1 (w plane):  acc[i, j] (+)= (-1)^(p+q) Re(. exp(-2 pi i w (n-1)))
 // p = i - nx/2, q = j - ny/2. Blocks b, b+8, ... share an XCD (round-robin
-// dispatch), so the 8 columns of one H block go to one XCD's L2 together.
+// dispatch), so the kColBlock columns of one H block go to one XCD's L2 together.
 struct ColEpilogue {
   double* out;
   const double* cx;
