@@ -5,28 +5,40 @@ Task dispatch for the dask-shaped API (`dask_invert_measurement_set`,
 dask is not installed in this image; the reference's tasks
 (`client.submit(..., resources={"processing_slots": 1})`, invert.py:256-267,
 reorder.py:68-82) are duck-typed against any client with `submit` and
-`scheduler_info`. `LocalGPUClient` runs each task immediately on one of the
-local GPUs (round robin), which is the single-node form of the
-"dask-task -> HIP-stream" dispatch: a task owns one device and
-enqueues its kernels on that device's current stream. With a real dask
-`Client`, give each GPU worker a `{"gpu": 1}` resource and pin it to one
-device with HIP_VISIBLE_DEVICES.
+`scheduler_info`. `LocalGPUClient` is the single-node form of the
+"dask-task -> HIP-stream" dispatch: every local GPU has one
+worker thread (the reference's `processing_slots=1`: one in-flight invert per
+device), GPU tasks (`resources={"gpu": 1}`) go to the devices in round robin
+and run concurrently across devices, each on its device's current stream with
+the library's per-(device, thread) workspace; other tasks run on a host thread
+pool. Futures passed as arguments are resolved inside the task, so `submit`
+never blocks. `concurrent=False` runs every task at submission instead. With
+a real dask `Client`, give each GPU worker a `{"gpu": 1}` resource and pin it
+to one device with HIP_VISIBLE_DEVICES.
 """
 
 from __future__ import annotations
 
+import concurrent.futures as cf
+import threading
 from typing import Any, Iterable, Optional
 
 
 class LocalFuture:
-    """An already-computed result with the `Future.result()` interface."""
+    """A task's result with the `Future.result()` interface (computed already,
+    or running on one of the client's threads)."""
 
-    def __init__(self, value: Any) -> None:
+    def __init__(self, value: Any = None, future: Optional[cf.Future] = None) -> None:
         self._value = value
+        self._future = future
 
-    def result(self) -> Any:
-        """The task's return value."""
-        return self._value
+    def result(self, timeout: Optional[float] = None) -> Any:
+        """The task's return value (waits for it; re-raises its exception)."""
+        return self._future.result(timeout) if self._future is not None else self._value
+
+    def done(self) -> bool:
+        """True once the result is available."""
+        return self._future is None or self._future.done()
 
 
 def _resolve(obj):
@@ -39,40 +51,102 @@ def _resolve(obj):
     return obj
 
 
-class LocalGPUClient:
-    """Synchronous client that runs tasks on local GPUs in round robin."""
-
-    def __init__(self, devices: Optional[Iterable[int]] = None) -> None:
+def _has_cuda() -> bool:
+    try:
         import torch  # pylint: disable=import-outside-toplevel
+    except ModuleNotFoundError:  # pragma: no cover - torch is in the image
+        return False
+    return torch.cuda.is_available()
 
+
+class LocalGPUClient:
+    """Client that runs GPU tasks on one worker thread per local GPU (round
+    robin, concurrent across devices) and other tasks on a host thread pool."""
+
+    def __init__(self, devices: Optional[Iterable[int]] = None, *, concurrent: bool = True,
+                 host_threads: int = 8) -> None:
         if devices is None:
-            n = torch.cuda.device_count() if torch.cuda.is_available() else 0
+            n = 0
+            if _has_cuda():
+                import torch  # pylint: disable=import-outside-toplevel
+
+                n = torch.cuda.device_count()
             devices = range(max(n, 1))
         self.devices = list(devices)
+        self.concurrent = concurrent
         self._next = 0
+        self._lock = threading.Lock()
+        self._gpu_pools = {}
+        self._host_pool = None
+        if concurrent:
+            self._gpu_pools = {d: cf.ThreadPoolExecutor(1, thread_name_prefix=f"cip-gpu{d}",
+                                                        initializer=self._bind, initargs=(d,))
+                               for d in self.devices}
+            self._host_pool = cf.ThreadPoolExecutor(max(host_threads, 1), thread_name_prefix="cip-host")
+
+    @staticmethod
+    def _bind(device: int) -> None:
+        # the worker thread's current device: the library's workspace and the
+        # stream the task's kernels go to
+        if _has_cuda():
+            import torch  # pylint: disable=import-outside-toplevel
+
+            torch.cuda.set_device(device)
 
     def scheduler_info(self) -> dict:
         """Mimics dask's `Client.scheduler_info()` worker listing."""
         return {"workers": {f"gpu-{d}": {"resources": {"gpu": 1}} for d in self.devices}}
 
-    def submit(self, fn, *args, resources=None, pure=None, **kwargs):  # noqa: ARG002
-        """Run `fn` now; GPU tasks (resources={'gpu': 1}) go to the next device."""
-        args = _resolve(args)
-        kwargs = {k: _resolve(v) for k, v in kwargs.items()}
-        if resources and "gpu" in resources:
-            import torch  # pylint: disable=import-outside-toplevel
-
+    def _pick_device(self) -> int:
+        with self._lock:
             dev = self.devices[self._next % len(self.devices)]
             self._next += 1
-            if torch.cuda.is_available():
+        return dev
+
+    def submit(self, fn, *args, resources=None, pure=None, **kwargs):  # noqa: ARG002
+        """Queue `fn(*args, **kwargs)`; GPU tasks (resources={'gpu': 1}) go to
+        the next device's worker. Returns a LocalFuture."""
+        gpu = bool(resources and "gpu" in resources)
+        dev = self._pick_device() if gpu else None
+
+        def task():
+            a = _resolve(args)
+            kw = {k: _resolve(v) for k, v in kwargs.items()}
+            if dev is not None and _has_cuda():
+                import torch  # pylint: disable=import-outside-toplevel
+
                 with torch.cuda.device(dev):
-                    return LocalFuture(fn(*args, **kwargs))
-        return LocalFuture(fn(*args, **kwargs))
+                    return fn(*a, **kw)
+            return fn(*a, **kw)
+
+        if not self.concurrent:
+            return LocalFuture(task())
+        pool = self._gpu_pools[dev] if gpu else self._host_pool
+        return LocalFuture(future=pool.submit(task))
+
+    def close(self) -> None:
+        """Wait for the queued tasks and stop the worker threads."""
+        for pool in list(self._gpu_pools.values()) + ([self._host_pool] if self._host_pool else []):
+            pool.shutdown(wait=True)
+        self._gpu_pools = {}
+        self._host_pool = None
+        self.concurrent = False
+
+    def __enter__(self) -> "LocalGPUClient":
+        return self
+
+    def __exit__(self, *exc) -> None:
+        self.close()
 
 
 def as_completed(futures: Iterable[LocalFuture]):
-    """dask.distributed.as_completed for LocalFutures (submission order)."""
-    yield from futures
+    """dask.distributed.as_completed for LocalFutures: in completion order."""
+    futures = list(futures)
+    done = [f for f in futures if f._future is None]  # pylint: disable=protected-access
+    yield from done
+    pending = {f._future: f for f in futures if f._future is not None}  # pylint: disable=protected-access
+    for fut in cf.as_completed(pending):
+        yield pending[fut]
 
 
 def get_worker_threads() -> int:

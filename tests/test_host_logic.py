@@ -270,3 +270,41 @@ def test_python_constants_match_c_header():
             checked += 1
     assert checked >= 16
     assert {v: k for k, v in _lib.STOKES_CODES.items()} == {defines[f"CIP_STOKES_{s}"]: s for s in "IQUV"}
+
+
+def test_local_gpu_client_runs_devices_concurrently():
+    # one worker thread per device: two GPU tasks that wait for each other
+    # complete only if they run at the same time (on CPU the device binding is
+    # skipped); futures passed as arguments are resolved inside the task
+    import threading
+
+    from ska_sdp_cip_amd.dispatch import LocalGPUClient, as_completed
+
+    with LocalGPUClient(devices=[0, 1]) as client:
+        assert len(client.scheduler_info()["workers"]) == 2
+        barrier = threading.Barrier(2, timeout=30)
+        names = []
+
+        def task(x):
+            barrier.wait()
+            names.append(threading.current_thread().name)
+            return x
+
+        futs = [client.submit(task, k, resources={"gpu": 1}) for k in (1, 2)]
+        total = client.submit(lambda xs: sum(xs), futs)
+        assert sorted(f.result() for f in as_completed(futs)) == [1, 2]
+        assert total.result() == 3
+        assert sorted(n.split("_")[0] for n in names) == ["cip-gpu0", "cip-gpu1"]
+        bad = client.submit(lambda: 1 / 0, resources={"gpu": 1})
+        with pytest.raises(ZeroDivisionError):
+            bad.result()
+
+
+def test_local_gpu_client_synchronous_mode():
+    from ska_sdp_cip_amd.dispatch import LocalGPUClient, as_completed
+
+    client = LocalGPUClient(devices=[0], concurrent=False)
+    a = client.submit(lambda: 2, resources={"gpu": 1})
+    b = client.submit(lambda x, y: x * y, a, 5)
+    assert a.done() and b.result() == 10
+    assert [f.result() for f in as_completed([a, b])] == [2, 10]
