@@ -512,13 +512,16 @@ static int fft_twiddles(Workspace* ws, int64_t n, hipStream_t s, double** out) {
 // Visibilities per scatter work unit: <= kChunkVis (64-bit fixed point) or
 // kChunkVisPacked (packed class, complex64 input); CIP_CHUNK_VIS lowers it for
 // tuning.
-static int64_t chunk_vis(bool packed) {
+static int64_t chunk_vis(bool packed, int64_t nu) {
   static int64_t env = -2;
   if (env == -2) {
     const char* e = getenv("CIP_CHUNK_VIS");
     env = e ? atoll(e) : -1;
   }
-  const int64_t cap = packed ? kChunkVisPacked : kChunkVis;
+  // grids of 16384+ cells per axis (C4): half-size work units - shorter slices
+  // on finer cells, the scatter's tail matters more (interleaved A/B at C4:
+  // scatter 4.76 vs 4.89 ms, profiles/r02_ab_c4.txt)
+  const int64_t cap = packed ? kChunkVisPacked : (nu >= 16384 ? kChunkVis / 2 : kChunkVis);
   // a multiple of kOrderWindow, so ordering windows never straddle chunks
   return (env >= kOrderWindow && env < cap) ? env / kOrderWindow * kOrderWindow : cap;
 }
@@ -922,7 +925,7 @@ static int prepare(Workspace* ws, const double* uvw, int64_t nrow, const double*
     rc = CIP_OK;
   } else {
     ws->saved_valid = false;
-    rc = make_plan(ws, uvw, fx, m, vis, vis_dtype, wgt, wgt_dtype, red, out->g, chunk_vis(packed), s, &out->plan,
+    rc = make_plan(ws, uvw, fx, m, vis, vis_dtype, wgt, wgt_dtype, red, out->g, chunk_vis(packed, out->g.nu), s, &out->plan,
                    &maxabs);
     if (rc == CIP_OK && !ragged) {
       ws->saved_key = key;
