@@ -8,8 +8,8 @@ cd "$(dirname "$0")/../ska-sdp-continuum-imaging-pipeline_amd/csrc"
 name=$1; shift
 /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -fPIC -munsafe-fp-atomics -I../../include -I. \
   -DCIP_SCATTER_W=8 "$@" -c cip_scatter_w.hip -o build/variant_$name.o
-objs="build/cip_api.o build/cip_plan.o build/cip_grid.o build/cip_tiling.o build/cip_fft.o build/cip_collective.o"
-for w in 4 6 10 12 14 16; do objs="$objs build/cip_scatter_w$w.o"; done
+# every object of the normal build except the W = 8 scatter unit (and other variants)
+objs=$(ls build/*.o | grep -v "build/cip_scatter_w8.o" | grep -v "build/variant_")
 mkdir -p ../../tools/variants
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o ../../tools/variants/libcip_hip_$name.so \
   $objs build/variant_$name.o -L/opt/rocm/lib -lhipfft -lrccl -Wl,-rpath,/opt/rocm/lib
