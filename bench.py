@@ -291,7 +291,8 @@ def main():
         "config": {
             "workload": (f"{args.config.upper()}: {cfg['rows']:,} rows x {cfg['nchan']} ch = {nvis:,} vis/GPU -> "
                          f"{params.nu}x{params.nv} grid ({npix}^2 image), support {params.support}, "
-                         f"{'w-stacking ' + str(P) + ' planes' if args.wstacking else '2-D'}, fp64 accumulate"),
+                         f"{'w-stacking ' + str(P) + ' planes' if args.wstacking else '2-D'}, "
+                         f"{'packed single-precision' if args.single else 'fp64'} accumulate"),
             "rows_per_gpu": cfg["rows"],
             "channels": cfg["nchan"],
             "grid": params.nu,
