@@ -18,8 +18,10 @@ reduced to rank 0 over RCCL (no other collective exists on this path).
 
 Prints ONE JSON line (rank 0). `roofline` is for the dominant kernel (the
 scatter), timed with hipEvents recorded by libcip_hip on the stream it launches
-on; `cpu_baseline` times the CPU oracle (oracle/, fp64 OpenMP restatement) on a
-bounded sample of the same workload.
+on; `cpu_baseline` times a tiled fp64 CPU restatement of ducc0's gridder
+(oracle/cpu_baseline.c) on the whole workload (plus C1, C2 and the numpy
+Stokes-I prep); `max_err` is the dirty image's max |GPU - CPU oracle| / sum w
+on a row subset at the full grid (the metric's second half).
 """
 
 import argparse
@@ -84,50 +86,123 @@ def traffic_from_profiles(config):
         return None
 
 
-def cpu_baseline(uvw, freq, npix, px, nvis_full, support, nthreads, sample_rows):
-    """
-    CPU oracle (oracle/cip_oracle.c, fp64 OpenMP) timed on a bounded sample:
-    gridding of `sample_rows` and 2 x `sample_rows` rows (slope = per-vis cost,
-    intercept = per-call cost), plus one multi-threaded nu x nv FFT; the full
-    workload's time is extrapolated as intercept + slope * N_vis + FFT.
-    """
-    import scipy.fft
+def _cpu_info():
+    """CPU model, os.cpu_count() and the affinity set of this process."""
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo", encoding="ascii", errors="replace") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"cpu_model": model, "cpu_count": os.cpu_count(), "affinity": len(os.sched_getaffinity(0))}
 
+
+def cpu_baseline(cfg_name, uvw_h, freq_h, vis_h, wgt_h, px, support, nthreads):
+    """
+    CPU baseline (BASELINE.md "CPU baseline plan"), timed on this host in this
+    run: oracle/cpu_baseline.c - the tiled fp64 restatement of ducc0's CPU
+    design (ducc0 itself is not importable on the box) - + threaded scipy FFT
+    + crop + correction, i.e. one whole 2-D invert:
+    * C1 and C2 in full on their own synthetic inputs (same generator as the
+      GPU configs), and the benchmark's own workload in full on exactly the
+      GPU run's visibilities (copied to the host);
+    * the reference's numpy Stokes-I / effective-weight prep
+      (StokesIGridderInput, invert.py:78-116, restated in oracle.stokes_i) on
+      C2's (rows, 64, 4) polarisation columns.
+    `value` is the benchmark workload's full-size rate (no extrapolation).
+    """
     import oracle
+    from ska_sdp_cip_amd import synthetic as syn
 
-    nchan = freq.size
-    rng = np.random.default_rng(1)
-    prm = oracle.choose_params(npix, npix, px, px, support=support)
-
-    def grid_time(nr):
-        u = np.ascontiguousarray(uvw[:nr])
-        vis = (rng.standard_normal((nr, nchan)) + 1j * rng.standard_normal((nr, nchan))).astype(np.complex64)
-        w = rng.uniform(0.5, 1.5, (nr, nchan)).astype(np.float32)
+    def run(uvw, freq, vis, wgt, npix, pxx):
+        oracle.baseline_ms2dirty(uvw[:64], freq, vis[:64], wgt[:64], npix, npix, pxx, pxx, support, nthreads)
         t0 = time.perf_counter()
-        oracle.grid_plane(u, freq, vis, w, prm, px, px, 0, nthreads)
+        oracle.baseline_ms2dirty(uvw, freq, vis, wgt, npix, npix, pxx, pxx, support, nthreads)
         return time.perf_counter() - t0
 
-    t1 = grid_time(sample_rows)
-    t2 = grid_time(2 * sample_rows)
-    nv1 = sample_rows * nchan
-    slope = max((t2 - t1) / nv1, 1e-15)
-    intercept = max(t1 - slope * nv1, 0.0)
-    grid = np.zeros((prm["nu"], prm["nv"]), dtype=np.complex128)
-    grid[::7, ::5] = 1.0
+    def synth(name):
+        c = CONFIGS[name]
+        uvw = syn.uvw_tracks(c["rows"], c["n_ant"], array_radius_m=c["radius"])
+        freq = syn.channel_frequencies(c["nchan"])
+        pxx = syn.pixel_size_for_grid(uvw, freq, c["npix"], support=8)
+        rng = np.random.default_rng(1)
+        shape = (c["rows"], c["nchan"])
+        vis = (rng.standard_normal(shape, dtype=np.float32)
+               + 1j * rng.standard_normal(shape, dtype=np.float32)).astype(np.complex64)
+        wgt = rng.uniform(0.5, 1.5, shape).astype(np.float32)
+        wgt[rng.uniform(size=shape) < 0.05] = 0.0
+        return uvw, freq, vis, wgt, pxx
+
+    per = {}
+    for name in ("c1", "c2"):
+        if name == cfg_name:
+            continue
+        uvw, freq, vis, wgt, pxx = synth(name)
+        t = run(uvw, freq, vis, wgt, CONFIGS[name]["npix"], pxx)
+        per[name] = {"mvis_per_s": round(vis.size / t / 1e6, 2), "seconds": round(t, 3), "nvis": int(vis.size)}
+    t = run(uvw_h, freq_h, vis_h, wgt_h, CONFIGS[cfg_name]["npix"], px)
+    per[cfg_name] = {"mvis_per_s": round(vis_h.size / t / 1e6, 2), "seconds": round(t, 3),
+                     "nvis": int(vis_h.size), "inputs": "the GPU run's own visibilities"}
+    # the reference's Stokes-I prep in numpy on C2-shaped polarisation columns
+    c2 = CONFIGS["c2"]
+    rng = np.random.default_rng(2)
+    shape4 = (c2["rows"], c2["nchan"], 4)
+    vis4 = (rng.standard_normal(shape4, dtype=np.float32)
+            + 1j * rng.standard_normal(shape4, dtype=np.float32)).astype(np.complex64)
+    w4 = rng.uniform(0.5, 1.5, shape4).astype(np.float32)
+    f4 = rng.uniform(size=shape4) < 0.05
     t0 = time.perf_counter()
-    scipy.fft.ifft2(grid, workers=nthreads, overwrite_x=True)
-    t_fft = time.perf_counter() - t0
-    t_full = intercept + slope * nvis_full + t_fft
+    oracle.stokes_i(vis4, f4, w4)
+    t_st = time.perf_counter() - t0
+    n_st = c2["rows"] * c2["nchan"]
+    del vis4, w4, f4
     return {
-        "value": nvis_full / t_full / 1e6,
+        "value": per[cfg_name]["mvis_per_s"],
         "unit": "Mvis/s",
         "cores": nthreads,
         "kind": "port",
-        "sample": (f"oracle fp64 gridding of {nv1:,} and {2 * nv1:,} visibilities of the same workload "
-                   f"({t1:.2f} s, {t2:.2f} s -> {slope * 1e9:.1f} ns/vis + {intercept:.2f} s/call) plus one "
-                   f"{prm['nu']}^2 c2c FFT ({t_fft:.2f} s, scipy.fft, {nthreads} workers); full "
-                   f"{nvis_full:,}-vis time extrapolated"),
+        "sample": (f"full {cfg_name.upper()} invert ({vis_h.size:,} vis, 2-D, support {support}) by "
+                   "oracle/cpu_baseline.c: tiled fp64 restatement of ducc0's CPU gridder (ducc0 absent on the box) "
+                   f"+ scipy.fft ({nthreads} workers) + correction; C1/C2 in full on their own inputs"),
+        "configs": per,
+        "stokes_i_prep": {"mvis_per_s": round(n_st / t_st / 1e6, 2), "seconds": round(t_st, 3),
+                          "nvis": n_st, "what": "numpy StokesIGridderInput + effective_weights "
+                                                "(invert.py:78-116) on C2 (rows, 64, 4) columns, 1 thread"},
+        **_cpu_info(),
+        "threads_note": "threads = the box's CPU share for one GPU (OMP_NUM_THREADS), not os.cpu_count()",
     }
+
+
+def max_err_vs_oracle(uvw_h, freq_h, vis_h, wgt_h, npix, px, support, wstacking, single, nthreads, row_step,
+                      device):
+    """
+    Dirty-image max |GPU - CPU oracle| / sum w (BASELINE.json metric, second
+    half) on every `row_step`-th row of the benchmark's own inputs at its full
+    grid: the GPU through the product path (device_ms2dirty), the CPU through
+    the fp64 oracle (oracle/, the parity checker). Outside the timed region.
+    """
+    import torch
+
+    import oracle
+    from ska_sdp_cip_amd import gridder
+
+    uvw = np.ascontiguousarray(uvw_h[::row_step])
+    vis = np.ascontiguousarray(vis_h[::row_step])
+    wgt = np.ascontiguousarray(wgt_h[::row_step])
+    t = lambda a: torch.from_numpy(a).to(device)  # noqa: E731
+    img, _ = gridder.device_ms2dirty(t(uvw), t(freq_h), t(vis), t(wgt), npix, npix, px, px, support=support,
+                                     do_wstacking=wstacking, single_precision_accumulation=single)
+    got = img.cpu().numpy()
+    del img
+    ref = oracle.ms2dirty(uvw, freq_h, vis, wgt, npix, npix, px, px, support=support, do_wstacking=wstacking,
+                          nthreads=nthreads)
+    err = float(np.abs(got - ref).max() / wgt.astype(np.float64).sum())
+    return {"max_err": err, "gate": 1e-6,
+            "sample": f"rows [::{row_step}] of the benchmark inputs ({vis.size:,} vis) at the full "
+                      f"{npix}^2 image, GPU (cip_ms2dirty) vs fp64 CPU oracle, both / sum w"}
 
 
 def main():
@@ -144,7 +219,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--sync", action="store_true",
                     help="synchronous steps (diagnostic: per-kernel times without the pipelined overlap)")
-    ap.add_argument("--cpu-sample-rows", type=int, default=8192)
+    ap.add_argument("--no-max-err", action="store_true", help="skip the GPU-vs-oracle max|err| check")
+    ap.add_argument("--err-row-step", type=int, default=0,
+                    help="max|err| on every k-th row (default: 50 in 2-D, 200 with w-stacking)")
     args = ap.parse_args()
 
     import torch
@@ -217,6 +294,20 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    # the same steps synchronous (each call returns when its image is done; no
+    # planner overlap with the previous call): the single-call rate next to
+    # the pipelined headline
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    for _ in range(args.steps):
+        step(sync=True)
+    drain()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed_sync = time.perf_counter() - t1
     # phase breakdown (hipEvents on the launching stream) from separate
     # profiled steps after the timed region: profiling synchronises each call
     _lib.profile_enable(True)
@@ -228,9 +319,9 @@ def main():
     torch.cuda.synchronize()
     _lib.profile_enable(False)
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        t = torch.tensor([elapsed, elapsed_sync], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        elapsed, elapsed_sync = float(t[0].item()), float(t[1].item())
 
     ms_per_step = elapsed / args.steps * 1e3
     value = world * nvis * args.steps / elapsed / 1e6
@@ -300,17 +391,31 @@ def main():
             "support": params.support,
             "wstacking": bool(args.wstacking),
             "parallelism": f"uvw-shard dp{world} + RCCL image reduce" if world > 1 else "single GPU",
+            "mode": ("sync" if args.sync else
+                     "pipelined: back-to-back CIP_ASYNC|CIP_PIPELINE calls on HBM-resident, unchanged inputs "
+                     "(call k+1's planner overlaps call k's scatter/FFT); value_sync = one call at a time"),
         },
+        "value_sync": round(world * nvis * args.steps / elapsed_sync / 1e6, 2),
+        "ms_per_step_sync": round(elapsed_sync / args.steps * 1e3, 3),
         "roofline": roofline,
         "phases_ms": {k.replace("_ms", ""): round(v, 3) for k, v in avg.items() if k.endswith("_ms")},
         "mean_slice_len": round(avg["visibilities"] / max(runs, 1), 2),
         "gtap_per_s": round(world * nvis * taps * args.steps / elapsed / 1e9, 2),
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.wstacking:
-        nthreads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, len(os.sched_getaffinity(0)))
+    nthreads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, len(os.sched_getaffinity(0)))
+    need_host = rank == 0 and ((world == 1 and not args.no_cpu_baseline) or not args.no_max_err)
+    vis_h = wgt_h = None
+    if need_host:
+        vis_h = vis_d.cpu().numpy()
+        wgt_h = wgt_d.cpu().numpy()
+    if rank == 0 and not args.no_max_err:
+        step_k = args.err_row_step or (200 if args.wstacking else 50)
+        log(f"[bench] max|err| vs the CPU oracle on rows [::{step_k}] ...")
+        result.update(max_err_vs_oracle(uvw_h, freq_h, vis_h, wgt_h, npix, px, args.support, args.wstacking,
+                                        args.single, nthreads, step_k, device))
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.wstacking and args.support <= 16:
         log(f"[bench] cpu baseline with {nthreads} threads ...")
-        result["cpu_baseline"] = cpu_baseline(uvw_h, freq_h, npix, px, nvis, args.support, nthreads,
-                                              args.cpu_sample_rows)
+        result["cpu_baseline"] = cpu_baseline(args.config, uvw_h, freq_h, vis_h, wgt_h, px, args.support, nthreads)
     else:
         result["cpu_baseline"] = None
     if rank == 0:

@@ -43,7 +43,9 @@ import numpy as np
 SPEED_OF_LIGHT = 299792458.0
 HERE = Path(__file__).resolve().parent
 LIB_PATH = HERE / "_build" / "libcip_oracle.so"
+BASELINE_PATH = HERE / "_build" / "libcip_cpu_baseline.so"
 _LIB = None
+_BASE = None
 
 
 def build() -> Path:
@@ -67,6 +69,19 @@ def _lib():
         so.oracle_dft.argtypes = [vp, i64, vp, i64, vp, vp, i64, i64, f64, f64, i32, i32, vp]
         _LIB = so
     return _LIB
+
+
+def _baseline_lib():
+    global _BASE  # pylint: disable=global-statement
+    if _BASE is None:
+        if not BASELINE_PATH.exists():
+            build()
+        so = ctypes.CDLL(str(BASELINE_PATH))
+        vp, i64, f64, i32 = ctypes.c_void_p, ctypes.c_int64, ctypes.c_double, ctypes.c_int
+        so.cpu_grid_tiled.argtypes = [vp, i64, vp, i64, vp, vp, i64, i64, f64, f64, i32, i32, vp]
+        so.cpu_grid_tiled.restype = i64
+        _BASE = so
+    return _BASE
 
 
 # ------------------------------------------------------------- params ----
@@ -161,6 +176,50 @@ def grid_plane(uvw, freq, vis, wgt, params: dict, px: float, py: float, plane: i
     return grid
 
 
+def grid_plane_tiled(uvw, freq, vis, wgt, params: dict, px: float, py: float, nthreads: int = 0) -> np.ndarray:
+    """CPU BASELINE (oracle/cpu_baseline.c, bench.py's cpu_baseline leg): the
+    2-D grid by the tiled restatement of ducc0's CPU design; complex64 vis and
+    float32 weights (or None) are read as given."""
+    uvw = np.ascontiguousarray(uvw, dtype=np.float64)
+    freq = np.ascontiguousarray(freq, dtype=np.float64)
+    vis = np.ascontiguousarray(vis, dtype=np.complex64)
+    wgt = None if wgt is None else np.ascontiguousarray(wgt, dtype=np.float32)
+    nu, nv = params["nu"], params["nv"]
+    grid = np.zeros((nu, nv), dtype=np.complex128)
+    bad = _baseline_lib().cpu_grid_tiled(
+        uvw.ctypes.data, uvw.shape[0], freq.ctypes.data, freq.size, vis.ctypes.data,
+        None if wgt is None else wgt.ctypes.data, nu, nv, px, py, params["support"], int(nthreads),
+        grid.ctypes.data)
+    if bad < 0:
+        raise ValueError("unsupported kernel support")
+    return grid
+
+
+def fft_backward(grid: np.ndarray, workers: int = 0) -> np.ndarray:
+    """Unnormalised backward 2-D FFT (exp(+2 pi i)): scipy.fft with `workers`
+    threads when scipy is present (numpy otherwise; the same fp64 transform)."""
+    nu, nv = grid.shape
+    try:
+        import scipy.fft  # pylint: disable=import-outside-toplevel
+
+        return scipy.fft.ifft2(grid, workers=workers or None) * (nu * nv)
+    except ImportError:  # pragma: no cover - scipy is in the image
+        return np.fft.ifft2(grid) * (nu * nv)
+
+
+def baseline_ms2dirty(uvw, freq, vis, wgt, npix_x, npix_y, px, py, support=8, nthreads=0):
+    """CPU BASELINE dirty image (2-D): tiled gridding + threaded FFT + crop +
+    correction - the work one invert does, timed by bench.py's cpu_baseline."""
+    prm = choose_params(npix_x, npix_y, px, py, support=support)
+    nu, nv, W = prm["nu"], prm["nv"], prm["support"]
+    g = grid_plane_tiled(uvw, freq, vis, wgt, prm, px, py, nthreads)
+    ghat = fft_backward(g, nthreads)
+    del g
+    cx = 1.0 / kernel_ft(W, (np.arange(npix_x) - npix_x // 2) / nu)
+    cy = 1.0 / kernel_ft(W, (np.arange(npix_y) - npix_y // 2) / nv)
+    return _crop(ghat, npix_x, npix_y).real * cx[:, None] * cy[None, :]
+
+
 def _crop(grid_hat: np.ndarray, npix_x: int, npix_y: int) -> np.ndarray:
     """(-1)^(p+q) G^[p mod nu, q mod nv] for p, q in [-npix/2, npix/2)."""
     nu, nv = grid_hat.shape
@@ -189,14 +248,14 @@ def ms2dirty(uvw, freq, vis, wgt, npix_x, npix_y, px, py, epsilon=1e-4, support=
     cy = 1.0 / kernel_ft(W, (np.arange(npix_y) - npix_y // 2) / nv)
     if not do_wstacking:
         g = grid_plane(uvw, freq, vis, wgt, prm, px, py, 0, nthreads)
-        ghat = np.fft.ifft2(g) * (nu * nv)  # backward, unnormalised: exp(+2 pi i)
+        ghat = fft_backward(g, nthreads)  # backward, unnormalised: exp(+2 pi i)
         dirty = _crop(ghat, npix_x, npix_y).real * cx[:, None] * cy[None, :]
     else:
         nm1 = _nm1(npix_x, npix_y, px, py)
         acc = np.zeros((npix_x, npix_y))
         for p in range(prm["nplanes"]):
             g = grid_plane(uvw, freq, vis, wgt, prm, px, py, p, nthreads)
-            ghat = np.fft.ifft2(g) * (nu * nv)
+            ghat = fft_backward(g, nthreads)
             wp = prm["w0"] + p * prm["dw"]
             acc += (_crop(ghat, npix_x, npix_y) * np.exp(-2j * np.pi * wp * nm1)).real
         fw = kernel_ft(W, np.abs(prm["dw"] * nm1).ravel()).reshape(nm1.shape)

@@ -290,6 +290,7 @@ struct PlanResult {
 };
 
 struct Workspace {
+  int device = 0;  // the device every buffer, stream and event belongs to
   std::map<std::string, DevBuf> bufs;
   std::vector<FftPlan> plans;
   void* pinned = nullptr;  // small host staging
@@ -377,6 +378,14 @@ static std::map<std::pair<int, std::thread::id>, Workspace*> g_ws;
 static const std::thread::id g_load_thread = std::this_thread::get_id();
 
 static void destroy_workspace(Workspace* ws) {
+  // the workspace's device current while its buffers go (the reaper may run on
+  // a thread whose current device differs), and a CIP_ASYNC call's work drained
+  // first: its scatter / FFT may still be queued on the caller's stream
+  int prev_dev = -1;
+  (void)hipGetDevice(&prev_dev);
+  if (prev_dev != ws->device) (void)hipSetDevice(ws->device);
+  if (ws->async_stream) (void)hipStreamSynchronize(ws->async_stream);
+  if (ws->plan_stream) (void)hipStreamSynchronize(ws->plan_stream);
   for (auto& kv : ws->bufs)
     if (kv.second.ptr) (void)hipFree(kv.second.ptr);
   for (auto& p : ws->plans) (void)hipfftDestroy(p.h);
@@ -395,7 +404,9 @@ static void destroy_workspace(Workspace* ws) {
     if (e) (void)hipEventDestroy(e);
   if (ws->ev_planned) (void)hipEventDestroy(ws->ev_planned);
   if (ws->ev_entry) (void)hipEventDestroy(ws->ev_entry);
+  const int dev = ws->device;
   delete ws;
+  if (prev_dev >= 0 && prev_dev != dev) (void)hipSetDevice(prev_dev);
 }
 
 // Frees the calling thread's workspaces (every device) when the thread ends.
@@ -429,6 +440,7 @@ static Workspace* workspace() {
   auto it = g_ws.find(key);
   if (it != g_ws.end()) return it->second;
   Workspace* ws = new Workspace();
+  ws->device = dev;
   g_ws[key] = ws;
   return ws;
 }
@@ -522,7 +534,8 @@ static int64_t chunk_vis(bool packed, int64_t nu) {
   // on finer cells, the scatter's tail matters more (interleaved A/B at C4:
   // scatter 4.76 vs 4.89 ms, profiles/r02_ab_c4.txt)
   const int64_t cap = packed ? kChunkVisPacked : (nu >= 16384 ? kChunkVis / 2 : kChunkVis);
-  // a multiple of kOrderWindow, so ordering windows never straddle chunks
+  // a multiple of kOrderWindow, so 2-D ordering windows never straddle chunks
+  // (w-stacking units: see kOrderWindow in cip_common.h)
   return (env >= kOrderWindow && env < cap) ? env / kOrderWindow * kOrderWindow : cap;
 }
 
@@ -871,6 +884,10 @@ static int prepare(Workspace* ws, const double* uvw, int64_t nrow, const double*
     if (rc != CIP_OK) return rc;
   }
   out->g = geometry(out->p, px, py);
+  // tile keys are 32-bit ((iy0 / T) ntx + ix0 / T) ntw + iw0 (cip_plan.hip):
+  // a larger key space would wrap and mis-sort the runs
+  if ((double)out->g.ntx * (double)out->g.nty * (double)out->g.ntw >= 4294967295.0)
+    return set_error(CIP_EINVAL, "grid tiles x w layers exceed the 32-bit tile key space");
   if (packed && vis_dtype != CIP_C64)
     return set_error(CIP_EINVAL, "single-precision accumulation needs complex64 visibilities");
   if (packed && out->g.support > 16)

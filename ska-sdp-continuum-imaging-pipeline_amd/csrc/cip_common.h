@@ -46,7 +46,11 @@ constexpr int kChunkVisPackedLog2 = 12;
 constexpr int kTile = CIP_TILE;
 
 // Visibilities per bank-class ordering window (cip_grid.hip order_kernel);
-// divides kChunkVis and kChunkVisPacked so windows never straddle chunks.
+// divides kChunkVis and kChunkVisPacked so, in 2-D mode, windows never
+// straddle chunks (w-stacking work units start at the first layer of their
+// merged range, not at a window boundary: there a chunk boundary may fall
+// inside a window, which is harmless because perm maps every position to a
+// visibility of the same uv tile, but the invariant does not hold).
 constexpr int kOrderWindow = 1024;
 
 __host__ __device__ inline int64_t floor_div(int64_t a, int64_t b) {

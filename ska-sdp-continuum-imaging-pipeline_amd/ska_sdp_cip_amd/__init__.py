@@ -23,6 +23,19 @@ from .measurement_set import (  # noqa: E402
     UnsupportedMeasurementSetLayout,
 )
 
+# Load libcip_hip.so at import, on the importing thread, when it is built: the
+# library records the thread that loads it as the main thread (whose workspaces
+# are left to process teardown, cip_api.hip), so the first call from a worker
+# thread must not be the one that loads it. A missing library raises at the
+# first call instead (no CPU fallback).
+try:
+    from . import _lib as _cip_lib
+
+    if _cip_lib.LIB_PATH.exists():
+        _cip_lib.lib()
+except OSError:  # pragma: no cover - a broken build raises again at first use
+    pass
+
 __all__ = [
     "__version__",
     "MeasurementSetReader",

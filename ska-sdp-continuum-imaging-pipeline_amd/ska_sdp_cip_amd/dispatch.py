@@ -74,6 +74,14 @@ class LocalGPUClient:
             devices = range(max(n, 1))
         self.devices = list(devices)
         self.concurrent = concurrent
+        # load the HIP library here, on the constructing (main) thread: the
+        # library treats the thread that loaded it as the process's main thread
+        # (its workspaces are left to process teardown), so a GPU worker thread
+        # must never be the first caller (its workspace would outlive it)
+        if _has_cuda():
+            from . import _lib  # pylint: disable=import-outside-toplevel
+
+            _lib.lib()
         self._next = 0
         self._lock = threading.Lock()
         self._gpu_pools = {}

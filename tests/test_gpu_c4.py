@@ -75,7 +75,9 @@ def test_c4_shard_sampled_pixels_equal_dft(c4):
     got = np.array([float(img[i, j].item()) for i, j in pix])
     sumw = float(wgt.double().sum().item())
     err = np.abs(got - ref).max() / sumw
-    assert err < 2e-6, (err, got, ref)
+    print(f"max |GPU - DFT| / sum w = {err:.3e}")
+    # the north-star gate (1e-6); W = 8 measures ~1e-8 on these random visibilities
+    assert err < 1e-6, (err, got, ref)
 
     # normalised in the pass-B epilogue == raw / device weight sum
     raw = img.clone()

@@ -97,7 +97,9 @@ def test_c3_sampled_pixels_equal_dft(c3, wstack):
     sumw = float(c3[3].double().sum().item())
     err = np.abs(got - ref).max() / sumw
     # W = 8: ~3e-7 of the weight sum on point sources
-    assert err < 2e-6, (err, got, ref)
+    print(f"max |GPU - DFT| / sum w = {err:.3e}")
+    # the north-star gate (1e-6); W = 8 measures ~1e-8 on these random visibilities
+    assert err < 1e-6, (err, got, ref)
     torch.cuda.synchronize()
 
 

@@ -66,3 +66,19 @@ def test_oracle_large_supports_vs_dft(case, support, wstack):
     img = oracle.ms2dirty(uvw, f, vis, w, npix, npix, px, px, support=support, do_wstacking=wstack)
     err = np.abs(img - dft[wstack]).max() / w.astype(np.float64).sum()
     assert err < LARGE_BOUND[(wstack, support)], err
+
+
+@pytest.mark.parametrize("support", [6, 8, 12])
+@pytest.mark.parametrize("npix", [64, 66])  # 66: odd tile count (132-cell grid -> 5 tiles): the serial edge phase
+def test_cpu_baseline_equals_oracle(case, support, npix):
+    # bench.py's cpu_baseline times the tiled restatement (oracle/cpu_baseline.c):
+    # it must grid what the oracle grids (same kernel, placement and wrap)
+    uvw, f, vis, w, _, px, _ = case
+    prm = oracle.choose_params(npix, npix, px, px, support=support)
+    ref = oracle.grid_plane(uvw, f, vis, w, prm, px, px, 0, 4)
+    got = oracle.grid_plane_tiled(uvw, f, vis, w, prm, px, px, 4)
+    scale = float(np.abs(w.astype(np.float64) * vis).sum())
+    assert np.abs(got - ref).max() / scale < 1e-12
+    img = oracle.baseline_ms2dirty(uvw, f, vis, w, npix, npix, px, px, support=support, nthreads=4)
+    img_ref = oracle.ms2dirty(uvw, f, vis, w, npix, npix, px, px, support=support, nthreads=4)
+    assert np.abs(img - img_ref).max() / w.astype(np.float64).sum() < 1e-12
