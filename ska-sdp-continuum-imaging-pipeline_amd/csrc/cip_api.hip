@@ -286,7 +286,6 @@ struct PlanResult {
   int64_t* tile_run_off = nullptr;
   Chunk* chunks = nullptr;
   uint32_t* perm = nullptr;  // bank-class ordered visibility stream, or NULL
-  bool grouped = false;  // the grouped scatter (cip_group.hip) grids this plan
   uint32_t* dmask = nullptr;  // grid tiles the scatter writes, per plane (bit-packed, ntx / 32 words per tile row)
 };
 
@@ -599,16 +598,6 @@ static bool scatter_order() {
   return on;
 }
 
-// CIP_GROUPED=0 keeps the lane-per-visibility scatter where the grouped one
-// (register accumulation per origin cell, cip_group.hip) applies (A/B)
-static bool grouped_enabled() {
-  static const bool on = [] {
-    const char* e = getenv("CIP_GROUPED");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
-
 // sub-blocks per radix workgroup: pass 0 (place blocks of ~500 runs) and the
 // dense passes (4096 runs); CIP_RADIX_G0 / CIP_RADIX_G1 override (A/B)
 static int radix_group(int pass) {
@@ -629,8 +618,7 @@ static int radix_group(int pass) {
 // *maxabs (the place pass reads the visibilities anyway).
 static int make_plan(Workspace* ws, const double* uvw, const double* fx, const RowMap& m,
                      const void* vis, int vis_dtype, const void* wgt, int wgt_dtype, double* red,
-                     const GridGeometry& g, int64_t cv, bool packed, hipStream_t s, PlanResult* pr,
-                     double* maxabs) {
+                     const GridGeometry& g, int64_t cv, hipStream_t s, PlanResult* pr, double* maxabs) {
   const int64_t ntiles = g.ntx * g.nty * g.ntw;
   pr->ntiles = ntiles;
   CIP_ALLOC(tile_runs, int64_t, "tile_runs", ntiles + 1)
@@ -644,13 +632,8 @@ static int make_plan(Workspace* ws, const double* uvw, const double* fx, const R
   // the bank-class order needs a 32-bit flattened index (larger inputs grid in
   // plain tile order)
   const bool order = scatter_order() && nvis < ((int64_t)1 << 32);
-  // the grouped scatter (2-D, W = 4, 6, 8, fp64 class) replaces the bank-class
-  // order by its own per-work-unit grouping of the origin cells
-  const bool grouped = order && grouped_enabled() && !g.do_wstacking && !packed && group_supported(g.support) &&
-                       cv <= kChunkVis;
   uint8_t* vis_class = nullptr;
-  uint16_t* vis_cell = nullptr;
-  if (!grouped && order && order_gather()) {
+  if (order && order_gather()) {
     vis_class = buf<uint8_t>(ws, "vis_class", nvis);
     if (!vis_class) return CIP_ENOMEM;
   }
@@ -665,8 +648,8 @@ static int make_plan(Workspace* ws, const double* uvw, const double* fx, const R
   CIP_ALLOC(hist0, int64_t, "radix_hist0", 256 * (int64_t)nblk + 1)
   CIP_ALLOC(hist0g, int64_t, "radix_hist0g", 256 * ng0 + 1)
   CIP_ALLOC(scan_h0, int64_t, "scan_hist0", scan_tmp_elems(256 * ng0 + 1))
-  CIP_HIP_CHECK(launch_plan_place(uvw, fx, m, vis, vis_dtype, wgt, wgt_dtype, g, err, vis_class, vis_cell, blk_cnt,
-                                  park_key, park_run, partial, hist0, s));
+  CIP_HIP_CHECK(launch_plan_place(uvw, fx, m, vis, vis_dtype, wgt, wgt_dtype, g, err, vis_class, blk_cnt, park_key,
+                                  park_run, partial, hist0, s));
   CIP_HIP_CHECK(launch_prep_final(partial, nblk, red, s));
   int key_bits = 1;
   while (key_bits < 32 && ((int64_t)1 << key_bits) < ntiles) ++key_bits;
@@ -747,18 +730,17 @@ static int make_plan(Workspace* ws, const double* uvw, const double* fx, const R
   }
   // bank-class ordering windows: the same split with kOrderWindow, per tile key
   CIP_ALLOC(win_off, int64_t, "win_off", ntiles + 1)
-  if (order && !grouped) {
+  if (order) {
     CIP_HIP_CHECK(launch_chunk_counts(tile_vis, ntiles, kOrderWindow, 0, win_off, s));
     CIP_HIP_CHECK(exclusive_scan_i64(win_off, ntiles + 1, scan_tmp, s));
   }
   int64_t* hl = (int64_t*)pinned(ws, sizeof(int64_t) * (nrange + 2));
   if (!hl) return set_error(CIP_ENOMEM, "hipHostMalloc failed");
   CIP_HIP_CHECK(hipMemcpyAsync(hl, layer_off, sizeof(int64_t) * (nrange + 1), hipMemcpyDeviceToHost, s));
-  if (order && !grouped)
-    CIP_HIP_CHECK(hipMemcpyAsync(hl + nrange + 1, win_off + ntiles, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+  if (order) CIP_HIP_CHECK(hipMemcpyAsync(hl + nrange + 1, win_off + ntiles, sizeof(int64_t), hipMemcpyDeviceToHost, s));
   CIP_HIP_CHECK(hipStreamSynchronize(s));
   pr->plane_chunk_off.assign(hl, hl + nrange + 1);
-  const int64_t nwin = (order && !grouped) ? hl[nrange + 1] : 0;
+  const int64_t nwin = order ? hl[nrange + 1] : 0;
   pr->nchunks = pr->plane_chunk_off.back();
   CIP_ALLOC(chunks, Chunk, "chunks", pr->nchunks)
   if (per_plane)
@@ -771,8 +753,7 @@ static int make_plan(Workspace* ws, const double* uvw, const double* fx, const R
   pr->run_goff = run_goff;
   pr->tile_run_off = tile_runs;
   pr->chunks = chunks;
-  pr->grouped = grouped;
-  if (order && !grouped && nwin > 0) {
+  if (order && nwin > 0) {
     CIP_ALLOC(windows, Chunk, "windows", nwin)
     CIP_HIP_CHECK(launch_chunk_emit(tile_vis_off, tile_vis, win_off, run_goff, tile_runs, ntiles, kOrderWindow, 0, nwin,
                                     windows, s));
@@ -961,7 +942,7 @@ static int prepare(Workspace* ws, const double* uvw, int64_t nrow, const double*
     rc = CIP_OK;
   } else {
     ws->saved_valid = false;
-    rc = make_plan(ws, uvw, fx, m, vis, vis_dtype, wgt, wgt_dtype, red, out->g, chunk_vis(packed, out->g.nu), packed, s,
+    rc = make_plan(ws, uvw, fx, m, vis, vis_dtype, wgt, wgt_dtype, red, out->g, chunk_vis(packed, out->g.nu), s,
                    &out->plan, &maxabs);
     if (rc == CIP_OK && !ragged) {
       ws->saved_key = key;
@@ -999,13 +980,9 @@ static int scatter_plane(const Prepared& pp, int64_t plane, const double* uvw, c
   const int64_t cb = pp.plan.plane_chunk_off[k], ce = pp.plan.plane_chunk_off[k + 1];
   if (wgt == nullptr) wgt_dtype = CIP_NONE;
   hipEvent_t a = g_prof.mark(s);
-  if (pp.plan.grouped)
-    CIP_HIP_CHECK(launch_group_scatter(g.support, vis_dtype, wgt_dtype, uvw, pp.fx, vis, wgt, pp.m, pp.plan.runs,
-                                       pp.plan.run_goff, pp.plan.chunks, cb, ce - cb, g, pp.fixed_scale, grid, s));
-  else
-    CIP_HIP_CHECK(launch_scatter(g.support, vis_dtype, wgt_dtype, pp.packed, uvw, pp.fx, vis, wgt, pp.m,
-                                 pp.plan.runs, pp.plan.run_goff, pp.plan.tile_run_off, pp.plan.perm, pp.plan.chunks,
-                                 cb, ce - cb, g, plane, pp.fixed_scale, grid, s));
+  CIP_HIP_CHECK(launch_scatter(g.support, vis_dtype, wgt_dtype, pp.packed, uvw, pp.fx, vis, wgt, pp.m, pp.plan.runs,
+                               pp.plan.run_goff, pp.plan.tile_run_off, pp.plan.perm, pp.plan.chunks, cb, ce - cb,
+                               g, plane, pp.fixed_scale, grid, s));
   g_prof.span(2, a, g_prof.mark(s));
   if (ce > cb) g_prof.counts[4] += 1;
   return CIP_OK;

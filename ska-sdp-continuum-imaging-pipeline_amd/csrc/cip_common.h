@@ -53,12 +53,6 @@ constexpr int kTile = CIP_TILE;
 // visibility of the same uv tile, but the invariant does not hold).
 constexpr int kOrderWindow = 1024;
 
-// Grouped scatter (cip_group.hip): the visibilities of a work unit's windows
-// are grouped by footprint origin cell into items of <= kGroupCap visibilities
-// accumulated in registers; a window's items form <= kGroupMaxRounds rounds.
-constexpr int kGroupCap = 16;
-constexpr int kGroupMaxRounds = 64;
-
 __host__ __device__ inline int64_t floor_div(int64_t a, int64_t b) {
   int64_t q = a / b;
   return (q * b > a) ? q - 1 : q;

@@ -48,9 +48,8 @@ hipError_t launch_prep_reduce(const RowMap& m, const void* vis, int vis_dtype, c
                               const GridGeometry& g, unsigned* err_flag, double* partial, hipStream_t s);
 hipError_t launch_plan_place(const double* uvw, const double* fx, const RowMap& m,
                              const void* vis, int vis_dtype, const void* wgt, int wgt_dtype, const GridGeometry& g,
-                             unsigned* err_flag, uint8_t* vis_class, uint16_t* vis_cell, int64_t* blk_cnt,
-                             uint32_t* park_key, uint64_t* park_run, double* partial, int64_t* hist0,
-                             hipStream_t s);
+                             unsigned* err_flag, uint8_t* vis_class, int64_t* blk_cnt, uint32_t* park_key,
+                             uint64_t* park_run, double* partial, int64_t* hist0, hipStream_t s);
 // ragged rows: out[r] = chan_stop[r] - chan_start[r] (out[nrow] = 0; err bit
 // set for a range outside [0, nchan)); after the exclusive scan (off[r] = row
 // r's first visibility), launch_ragged_expand writes delta[r] = off[r] -
@@ -140,15 +139,6 @@ hipError_t launch_wplane_accumulate(const double* grid, const GridGeometry& g, i
 hipError_t launch_wfinal_correct(double* acc, int64_t npix_x, int64_t npix_y, double pixsize_x, double pixsize_y,
                                  const double* cx, const double* cy, const double* fw_table, int64_t fw_n,
                                  double fw_dnu, double dw, hipStream_t s);
-
-// ---- grouped scatter (cip_group.hip) -------------------------------------
-// supports W = 4, 6, 8 (2-D, fp64 class); one workgroup per work unit, the
-// unit's visibilities found through the tile-sorted row slices (runs, run_goff)
-bool group_supported(int support);
-hipError_t launch_group_scatter(int support, int vis_dtype, int wgt_dtype, const double* uvw, const double* fx,
-                                const void* vis, const void* wgt, const RowMap& m, const uint64_t* runs,
-                                const int64_t* run_goff, const Chunk* chunks, int64_t chunk_begin, int64_t nchunks,
-                                const GridGeometry& g, double fixed_scale, double* grid, hipStream_t s);
 
 // ---- pruned 2-D FFT (cip_fft.hip) -----------------------------------------
 // gT: the grid transposed (nv rows of nu cells); H: (nx / 8) x nv x 8 complex;

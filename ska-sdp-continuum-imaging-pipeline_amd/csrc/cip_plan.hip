@@ -207,7 +207,6 @@ __global__ __launch_bounds__(256, CIP_PLACE_WAVES) void plan_place_kernel(const 
                                                          const VisT* __restrict__ vis, const void* __restrict__ wgt,
                                                          GridGeometry g, unsigned* err_flag,
                                                          uint8_t* __restrict__ vis_class,
-                                                         uint16_t* __restrict__ vis_cell,
                                                          int64_t* __restrict__ blk_cnt,
                                                          uint32_t* __restrict__ park_key,
                                                          uint64_t* __restrict__ park_run, double* partial,
@@ -288,9 +287,6 @@ __global__ __launch_bounds__(256, CIP_PLACE_WAVES) void plan_place_kernel(const 
 #if CIP_PLACE_ABL != 3
       if (vis_class && valid)
         vis_class[i] = ok ? (uint8_t)((((unsigned)ix0 % kTile) * P + (unsigned)iy0 % kTile) & 31u) : (uint8_t)0;
-      // the origin cell within its tile (grouped scatter, cip_group.hip)
-      if (vis_cell && valid)
-        vis_cell[i] = ok ? (uint16_t)(((unsigned)ix0 % kTile) * kTile + (unsigned)iy0 % kTile) : (uint16_t)0;
 #endif
       if (__ballot(bad) != 0ull && lane == 0) atomicOr(err_flag, 1u);
       const uint32_t prev = __shfl_up(key, 1, 64);
@@ -354,7 +350,7 @@ hipError_t launch_prep_reduce(const RowMap& m, const void* vis, int vis_dtype, c
 #define REDUCE(VT, WKV)                                                                                      \
   plan_place_kernel<VT, WKV, false><<<gd, dim3(256), 0, s>>>(nullptr, nullptr, m, (const VT*)vis, wgt, g,    \
                                                             err_flag, nullptr, nullptr, nullptr, nullptr,   \
-                                                            nullptr, partial, nullptr)
+                                                            partial, nullptr)
   if (vis_dtype == CIP_C64) {
     if (wgt_dtype == CIP_F32) REDUCE(float2, WK_F32);
     else if (wgt_dtype == CIP_F64) REDUCE(float2, WK_F64);
@@ -370,14 +366,12 @@ hipError_t launch_prep_reduce(const RowMap& m, const void* vis, int vis_dtype, c
 
 hipError_t launch_plan_place(const double* uvw, const double* fx, const RowMap& m,
                              const void* vis, int vis_dtype, const void* wgt, int wgt_dtype, const GridGeometry& g,
-                             unsigned* err_flag, uint8_t* vis_class, uint16_t* vis_cell, int64_t* blk_cnt,
-                             uint32_t* park_key, uint64_t* park_run, double* partial, int64_t* hist0,
-                             hipStream_t s) {
+                             unsigned* err_flag, uint8_t* vis_class, int64_t* blk_cnt, uint32_t* park_key,
+                             uint64_t* park_run, double* partial, int64_t* hist0, hipStream_t s) {
   const dim3 gd(plan_blocks(m.nvis));
 #define PLACE(VT, WKV)                                                                                           \
   plan_place_kernel<VT, WKV><<<gd, dim3(256), 0, s>>>(uvw, fx, m, (const VT*)vis, wgt, g, err_flag,       \
-                                                      vis_class, vis_cell, blk_cnt, park_key, park_run, partial, \
-                                                      hist0)
+                                                      vis_class, blk_cnt, park_key, park_run, partial, hist0)
   if (vis_dtype == CIP_C64) {
     if (wgt_dtype == CIP_F32) PLACE(float2, WK_F32);
     else if (wgt_dtype == CIP_F64) PLACE(float2, WK_F64);
