@@ -205,6 +205,116 @@ def max_err_vs_oracle(uvw_h, freq_h, vis_h, wgt_h, npix, px, support, wstacking,
                       f"{npix}^2 image, GPU (cip_ms2dirty) vs fp64 CPU oracle, both / sum w"}
 
 
+def run_strong(args, world, rank, device):
+    """
+    `--strong`: the north star's C4 split (BASELINE configs[3]) - ONE dirty
+    image of 3,906,250 rows x 256 channels = 1,000,000,000 visibilities on a
+    16384^2 grid (8192^2 image) shared by all ranks (strong scaling: the total
+    work is fixed). Rank r grids the visibilities whose footprints start in
+    its balanced uv strip of grid rows, sends its W - 1 halo rows to rank
+    r + 1 (RCCL point-to-point), runs pass A of the FFT on its rows, one
+    all-to-all hands every rank its image rows' columns, pass B + correction
+    run per image-row strip and the rows are gathered on rank 0
+    (ska_sdp_cip_amd.strips). One step = that whole distributed
+    invert on HBM-resident strip data; value = 1G vis x steps / time.
+    """
+    import torch
+    import torch.distributed as dist
+
+    from ska_sdp_cip_amd import _lib, strips
+    from ska_sdp_cip_amd import synthetic as syn
+
+    seed = 20241008
+    rows, nchan, npix = 3_906_250, 256, 8192
+    uvw_h = syn.uvw_tracks(rows, 64, array_radius_m=4000.0, seed=seed)
+    freq_h = syn.channel_frequencies(nchan)
+    px = syn.pixel_size_for_grid(uvw_h, freq_h, npix, support=8)
+    uvw = torch.from_numpy(uvw_h).to(device)
+    freq = torch.from_numpy(freq_h).to(device)
+    params = _lib.choose_params(npix, npix, px, px, 1e-4, args.support)
+    t0 = time.perf_counter()
+    layout = strips.plan_strips(uvw, freq, params, px, npix, npix, world)
+    rws, c0, c1 = strips.strip_slices(uvw, freq, params, px, *layout.rows(rank))
+    t_plan = time.perf_counter() - t0
+    lengths = (c1 - c0)
+    nvis = int(lengths.sum())
+    g = torch.Generator(device=device)
+    g.manual_seed(seed + rank)
+    vis = torch.randn(nvis, dtype=torch.complex64, device=device, generator=g)
+    wgt = torch.rand(nvis, dtype=torch.float32, device=device, generator=g) + 0.5
+    wgt = torch.where(torch.rand(nvis, device=device, generator=g) < 0.05, torch.zeros_like(wgt), wgt).contiguous()
+    data = strips.StripData(uvw[rws].contiguous(), c0.to(torch.int32), c1.to(torch.int32), vis, wgt, rws)
+    del uvw
+    backend = strips.HipStripBackend(params, px, px, npix, npix, device=device)
+    y0, y1 = layout.rows(rank)
+    log(f"[bench --strong] rank {rank}/{world}: strip rows [{y0}, {y1}) of {params.nv}, {nvis:,} vis "
+        f"({data.slice_uvw.shape[0]:,} slices), plan {t_plan:.2f} s")
+
+    def step(stages=None):
+        return strips.invert_strips(data, freq, layout, backend, dst=0, stages=stages)
+
+    for _ in range(args.warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    stages = {}
+    nprof = max(2, min(args.steps, 5))
+    for _ in range(nprof):
+        step(stages)
+    nv_all = torch.tensor([float(nvis)], dtype=torch.float64, device=device)
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        per_rank = [torch.zeros_like(nv_all) for _ in range(world)]
+        dist.all_gather(per_rank, nv_all)
+        per_rank = [int(x.item()) for x in per_rank]
+    else:
+        per_rank = [nvis]
+    total = sum(per_rank)
+    ms_per_step = elapsed / args.steps * 1e3
+    result = {
+        "metric": f"Mvis/s gridded (invert) on {params.nu // 1024}k^2 grid, support={params.support}",
+        "value": round(total * args.steps / elapsed / 1e6, 2),
+        "unit": "Mvis/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 3),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (seeded MeerKAT-like uvw tracks, random complex64 vis, float32 weights, 5% flagged)",
+        "config": {
+            "workload": (f"C4 (BASELINE configs[3]): {rows:,} rows x {nchan} ch = {rows * nchan:,} vis, ONE "
+                         f"{params.nu}x{params.nv} grid ({npix}^2 image), support {params.support}, 2-D, fp64 "
+                         "accumulate"),
+            "parallelism": (f"uv strips x{world}: balanced grid-row strips + {params.support - 1}-row halo "
+                            "send/recv, strip pass A, all-to-all of pass-A blocks, pass B per image-row strip, "
+                            "gather of image rows" if world > 1 else "uv strips x1 (whole C4 on one GPU)"),
+            "strip_rows": [layout.rows(r) for r in range(world)],
+            "strip_vis": per_rank,
+        },
+        "stages_ms_rank0": {k: round(v / nprof * 1e3, 3) for k, v in stages.items()},
+        "roofline": None,
+        "cpu_baseline": None,
+    }
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser(description=__doc__.splitlines()[1])
     ap.add_argument("--gpus", type=int, default=1)
@@ -222,6 +332,9 @@ def main():
     ap.add_argument("--no-max-err", action="store_true", help="skip the GPU-vs-oracle max|err| check")
     ap.add_argument("--err-row-step", type=int, default=0,
                     help="max|err| on every k-th row (default: 50 in 2-D, 200 with w-stacking)")
+    ap.add_argument("--strong", action="store_true",
+                    help="strong scaling of ONE C4 image (1G vis, 16k^2 grid) over the ranks: uv strips + halo "
+                         "exchange + distributed FFT (DESIGN.md 7); --config is ignored")
     args = ap.parse_args()
 
     import torch
@@ -238,6 +351,9 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
     device = torch.device("cuda", local_rank)
     torch.cuda.set_device(device)
+    if args.strong:
+        run_strong(args, world, rank, device)
+        return
     cfg = CONFIGS[args.config]
     nvis = cfg["rows"] * cfg["nchan"]
     npix = cfg["npix"]

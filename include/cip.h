@@ -179,6 +179,27 @@ int cip_grid_to_dirty(double* grids, const cip_gridder_params* params,
                       int64_t npix_x, int64_t npix_y, double pixsize_x,
                       double pixsize_y, void* hip_stream, double* dirty_out);
 
+/* Strips of the dirty-image FFT: the multi-GPU strong-scaling split of one
+ * grid (SURVEY.md 8(e) option 1, the north star's UVW-tile
+ * shards with a partial-grid halo exchange before the FFT). Rank r owns grid
+ * rows [y0, y1) of the transposed 2-D grid (cip_grid_layout == 1, power-of-
+ * two grids) and image rows [i0, i1) (multiples of 4).
+ * cip_strip_rows: pass A over rows [y0, y1) of `grid` (nu x nv complex128 as
+ * gT[y][x]) -> H (device, (npix_x / 4) blocks x (y1 - y0) rows x 4
+ * complex128: row y of block b at ((b (y1 - y0)) + y - y0) 4); the rows read
+ * are zeroed (the grid is left clean for the next call).
+ * cip_strip_cols: pass B for image rows [i0, i1) from H holding blocks
+ * [i0 / 4, i1 / 4), nv rows each (the strips' pass-A outputs exchanged block
+ * by block), written to dirty_rows ((i1 - i0) x npix_y f64) with the crop and
+ * grid correction, divided by *norm (device f64) when norm != NULL. Both
+ * synchronous on hip_stream. */
+int cip_strip_rows(double* grid, const cip_gridder_params* params,
+                   int64_t npix_x, int64_t npix_y, int64_t y0, int64_t y1,
+                   void* hip_stream, double* H);
+int cip_strip_cols(const double* H, const cip_gridder_params* params,
+                   int64_t npix_x, int64_t npix_y, int64_t i0, int64_t i1,
+                   const double* norm, void* hip_stream, double* dirty_rows);
+
 /* Reference-exact UVW tile keys and constant-key channel runs (one run per
  * maximal range of channels with equal (iu, iv, iw) in a row), rows in
  * order, runs in channel order: key = floor(f/c * (uvw / tile) + 0.5) in

@@ -1006,16 +1006,14 @@ static bool grid_is_transposed(const GridGeometry& g, int64_t npix_x, int64_t np
   return fft_pruned() && fast_fft_supported(g.nu, g.nv, npix_x, npix_y);
 }
 
-static int dirty_stage(Workspace* ws, const GridGeometry& g, int64_t npix_x, int64_t npix_y, double px, double py,
-                       hipStream_t s, DirtyStage* st) {
-  st->npix_x = npix_x;
-  st->npix_y = npix_y;
-  st->px = px;
-  st->py = py;
+// the grid-correction vectors cx = 1 / F(p / nu), cy = 1 / F(q / nv) (cached
+// per workspace and geometry)
+static int correction_vectors(Workspace* ws, const GridGeometry& g, int64_t npix_x, int64_t npix_y, hipStream_t s,
+                              double** cx_out, double** cy_out) {
   CIP_ALLOC(cx, double, "cx", npix_x)
   CIP_ALLOC(cy, double, "cy", npix_y)
-  st->cx = cx;
-  st->cy = cy;
+  *cx_out = cx;
+  *cy_out = cy;
   HostKernel hk;
   host_kernel(g.support, &hk);
   KernelFT F(hk);
@@ -1031,6 +1029,16 @@ static int dirty_stage(Workspace* ws, const GridGeometry& g, int64_t npix_x, int
     CIP_HIP_CHECK(hipStreamSynchronize(s));  // host vectors go out of scope
     ws->corr_key = corr_key;
   }
+  return CIP_OK;
+}
+
+static int dirty_stage(Workspace* ws, const GridGeometry& g, int64_t npix_x, int64_t npix_y, double px, double py,
+                       hipStream_t s, DirtyStage* st) {
+  st->npix_x = npix_x;
+  st->npix_y = npix_y;
+  st->px = px;
+  st->py = py;
+  if (const int rc = correction_vectors(ws, g, npix_x, npix_y, s, &st->cx, &st->cy); rc != CIP_OK) return rc;
   // pruned FFT (cip_fft.hip) for power-of-two grids; hipFFT 2-D otherwise
   // (CIP_FFT_PRUNED=0 forces the latter)
   st->fast = grid_is_transposed(g, npix_x, npix_y);
@@ -1362,6 +1370,54 @@ int cip_grid_plane(const double* uvw, int64_t nrow, const double* freq, int64_t 
   g_prof.span(5, t_start, g_prof.mark(s));
   CIP_HIP_CHECK(hipStreamSynchronize(s));
   g_prof.finish();
+  return CIP_OK;
+}
+
+// strips of the pruned FFT (multi-GPU strong scaling)
+static int strip_check(const cip_gridder_params* params, int64_t npix_x, int64_t npix_y, GridGeometry* g) {
+  if (!params) return set_error(CIP_EINVAL, "params is NULL");
+  if (params->do_wstacking) return set_error(CIP_EINVAL, "strips: 2-D grids only");
+  *g = geometry(*params, 1.0, 1.0);
+  if (!grid_is_transposed(*g, npix_x, npix_y))
+    return set_error(CIP_EINVAL, "strips need the pruned-FFT grid layout (power-of-two grids, cip_grid_layout == 1)");
+  return CIP_OK;
+}
+
+int cip_strip_rows(double* grid, const cip_gridder_params* params, int64_t npix_x, int64_t npix_y, int64_t y0,
+                   int64_t y1, void* hip_stream, double* H) {
+  g_last_error.clear();
+  GridGeometry g;
+  if (const int rc = strip_check(params, npix_x, npix_y, &g); rc != CIP_OK) return rc;
+  if (!grid || !H) return set_error(CIP_EINVAL, "NULL grid or H");
+  if (y0 < 0 || y1 > g.nv || y1 <= y0) return set_error(CIP_EINVAL, "row range outside the grid");
+  hipStream_t s = (hipStream_t)hip_stream;
+  Workspace* ws = workspace();
+  if (!ws) return set_error(CIP_EHIP, "no HIP device");
+  if (const int sr = settle_async(ws, s); sr != CIP_OK) return sr;
+  double* tw_u = nullptr;
+  if (const int rc = fft_twiddles(ws, g.nu, s, &tw_u); rc != CIP_OK) return rc;
+  CIP_HIP_CHECK(launch_fft_rows_strip(grid, g.nu, g.nv, npix_x, tw_u, y0, y1, H, s));
+  CIP_HIP_CHECK(hipStreamSynchronize(s));
+  return CIP_OK;
+}
+
+int cip_strip_cols(const double* H, const cip_gridder_params* params, int64_t npix_x, int64_t npix_y, int64_t i0,
+                   int64_t i1, const double* norm, void* hip_stream, double* dirty_rows) {
+  g_last_error.clear();
+  GridGeometry g;
+  if (const int rc = strip_check(params, npix_x, npix_y, &g); rc != CIP_OK) return rc;
+  if (!H || !dirty_rows) return set_error(CIP_EINVAL, "NULL H or dirty_rows");
+  if (i0 < 0 || i1 > npix_x || i1 <= i0 || i0 % 4 || i1 % 4)
+    return set_error(CIP_EINVAL, "image row range must be multiples of 4 inside [0, npix_x]");
+  hipStream_t s = (hipStream_t)hip_stream;
+  Workspace* ws = workspace();
+  if (!ws) return set_error(CIP_EHIP, "no HIP device");
+  if (const int sr = settle_async(ws, s); sr != CIP_OK) return sr;
+  double *tw_v = nullptr, *cx = nullptr, *cy = nullptr;
+  if (const int rc = fft_twiddles(ws, g.nv, s, &tw_v); rc != CIP_OK) return rc;
+  if (const int rc = correction_vectors(ws, g, npix_x, npix_y, s, &cx, &cy); rc != CIP_OK) return rc;
+  CIP_HIP_CHECK(launch_fft_cols_strip(H, g.nv, npix_x, npix_y, tw_v, i0, i1, dirty_rows, cx, cy, norm, s));
+  CIP_HIP_CHECK(hipStreamSynchronize(s));
   return CIP_OK;
 }
 

@@ -189,15 +189,19 @@ __device__ __forceinline__ void fft_core(double2* v, int t, double* lds, const d
 // block, so pass B's C columns of a block read whole rows between them).
 // MASKED: only the row's cells in dirty tiles (dmask, kTile-cell segments)
 // are read - the rest of the grid is zero - and those are zeroed after the
-// read, so the next scatter needs no memset of the whole grid.
-template <int N, bool MASKED>
-__global__ __launch_bounds__(N / 16) void fft_rows_kernel(double2* __restrict__ gT, int64_t nv, int64_t nx,
+// read, so the next scatter needs no memset of the whole grid. Rows
+// y0 + blockIdx.x (a strip of the grid) go to H rows y - hy0 of
+// an H with hrows rows per block (the whole grid: y0 = hy0 = 0, hrows = nv);
+// ZERO (unmasked strips) zeroes every cell read.
+template <int N, bool MASKED, bool ZERO = false>
+__global__ __launch_bounds__(N / 16) void fft_rows_kernel(double2* __restrict__ gT, int64_t hrows, int64_t nx,
                                                           const double2* __restrict__ tw, double2* __restrict__ H,
-                                                          const uint32_t* __restrict__ dmask, int64_t ntx) {
+                                                          const uint32_t* __restrict__ dmask, int64_t ntx,
+                                                          int64_t y0 = 0, int64_t hy0 = 0) {
   using S = FftShape<N>;
   __shared__ double lds[N + N / 16];
   const int t = threadIdx.x;
-  const int64_t y = blockIdx.x;
+  const int64_t y = y0 + blockIdx.x;
   double2* row = gT + y * N;
   double2 v[16];
   if constexpr (MASKED) {
@@ -219,6 +223,10 @@ __global__ __launch_bounds__(N / 16) void fft_rows_kernel(double2* __restrict__ 
   } else {
 #pragma unroll
     for (int r = 0; r < 16; ++r) v[r] = row[t + r * S::T];
+    if constexpr (ZERO) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) row[t + r * S::T] = make_double2(0.0, 0.0);
+    }
   }
   fft_core<N>(v, t, lds, tw);
 #pragma unroll
@@ -227,7 +235,7 @@ __global__ __launch_bounds__(N / 16) void fft_rows_kernel(double2* __restrict__ 
     for (int r = 0; r < S::RF; ++r) {
       const int k = out_pos<N, S::RF>(t, m, r, N / S::RF);
       const int64_t i = (int64_t)((k + (int)(nx / 2)) & (N - 1));
-      if (i < nx) H[((i / kColBlock) * nv + y) * kColBlock + (i % kColBlock)] = v[m * S::RF + r];
+      if (i < nx) H[((i / kColBlock) * hrows + (y - hy0)) * kColBlock + (i % kColBlock)] = v[m * S::RF + r];
     }
 }
 
@@ -247,24 +255,30 @@ struct ColEpilogue {
   const double* norm;  // MODE 0: divide by *norm (the weight sum), NULL = no
 };
 
+// A strip of image rows [i0, i0 + gridDim.x): H holds the
+// blocks from i0 / kColBlock on (i0 a multiple of kColBlock), and image row i
+// goes to ep.out row i - i0. The whole image: i0 = 0.
 template <int N, int MODE>
 __global__ __launch_bounds__(N / 16) void fft_cols_kernel(const double2* __restrict__ H, int64_t nx, int64_t ny,
-                                                          const double2* __restrict__ tw, ColEpilogue ep) {
+                                                          const double2* __restrict__ tw, ColEpilogue ep,
+                                                          int64_t i0 = 0) {
   using S = FftShape<N>;
   __shared__ double lds[N + N / 16];
   const int t = threadIdx.x;
   const int64_t b = blockIdx.x;
-  int64_t i = b;
+  const int64_t nrows = gridDim.x;
+  int64_t il = b;
   // a group of 8 kColBlock consecutive blocks -> one column block per XCD
-  if (nx % (8 * kColBlock) == 0)
-    i = (b / (8 * kColBlock)) * (8 * kColBlock) + (b % 8) * kColBlock + (b / 8) % kColBlock;
-  const double2* col = H + ((i / kColBlock) * N) * kColBlock + (i % kColBlock);
+  if (nrows % (8 * kColBlock) == 0)
+    il = (b / (8 * kColBlock)) * (8 * kColBlock) + (b % 8) * kColBlock + (b / 8) % kColBlock;
+  const int64_t i = i0 + il;
+  const double2* col = H + ((il / kColBlock) * N) * kColBlock + (il % kColBlock);
   double2 v[16];
 #pragma unroll
   for (int r = 0; r < 16; ++r) v[r] = col[(int64_t)(t + r * S::T) * kColBlock];
   fft_core<N>(v, t, lds, tw);
   const int64_t p = i - nx / 2;
-  double* orow = ep.out + i * ny;
+  double* orow = ep.out + il * ny;
   const double cxi = MODE == 0 ? (ep.norm ? ep.cx[i] / *ep.norm : ep.cx[i]) : 0.0;
 #pragma unroll
   for (int m = 0; m < 16 / S::RF; ++m)
@@ -322,6 +336,55 @@ hipError_t launch_fft_rows(double* gT, int64_t nu, int64_t nv, int64_t nx, const
     default: return hipErrorInvalidValue;
   }
 #undef ROWS
+  return hipGetLastError();
+}
+
+hipError_t launch_fft_rows_strip(double* gT, int64_t nu, int64_t nv, int64_t nx, const double* tw_u, int64_t y0,
+                                 int64_t y1, double* H, hipStream_t s) {
+  if (!fft_len_ok(nu) || !fft_len_ok(nv) || nx > nu || y0 < 0 || y1 > nv || y1 <= y0) return hipErrorInvalidValue;
+  const dim3 gd((unsigned)(y1 - y0));
+  double2* g = (double2*)gT;
+  const double2* tw = (const double2*)tw_u;
+  double2* h = (double2*)H;
+#define ROWS(NN)                                                                                          \
+  case NN:                                                                                                \
+    fft_rows_kernel<NN, false, true><<<gd, dim3(NN / 16), 0, s>>>(g, y1 - y0, nx, tw, h, nullptr, 0, y0, y0); \
+    break;
+  switch (nu) {
+    ROWS(1024)
+    ROWS(2048)
+    ROWS(4096)
+    ROWS(8192)
+    ROWS(16384)
+    default: return hipErrorInvalidValue;
+  }
+#undef ROWS
+  return hipGetLastError();
+}
+
+hipError_t launch_fft_cols_strip(const double* H, int64_t nv, int64_t nx, int64_t ny, const double* tw_v, int64_t i0,
+                                 int64_t i1, double* out, const double* cx, const double* cy, const double* norm,
+                                 hipStream_t s) {
+  if (i0 < 0 || i1 > nx || i1 <= i0 || i0 % kColBlock != 0 || (i1 - i0) % kColBlock != 0)
+    return hipErrorInvalidValue;
+  const dim3 gd((unsigned)(i1 - i0));
+  const double2* h = (const double2*)H;
+  const double2* tw = (const double2*)tw_v;
+  const ColEpilogue ep{out, cx, cy, 0.0, 0.0, 0.0, 1, norm};
+#define COLS(NN)                                                                          \
+  case NN:                                                                                \
+    fft_cols_kernel<NN, 0><<<gd, dim3(NN / 16), 0, s>>>(h, nx, ny, tw, ep, i0);           \
+    break;
+  switch (nv) {
+    COLS(1024)
+    COLS(2048)
+    COLS(4096)
+    COLS(8192)
+    COLS(16384)
+    default:
+      return hipErrorInvalidValue;
+  }
+#undef COLS
   return hipGetLastError();
 }
 

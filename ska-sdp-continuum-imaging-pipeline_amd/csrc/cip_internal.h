@@ -154,6 +154,15 @@ hipError_t launch_fft_rows(double* gT, int64_t nu, int64_t nv, int64_t nx, const
 hipError_t launch_fft_cols(const double* H, int64_t nv, int64_t nx, int64_t ny, const double* tw_v, int mode,
                            double* out, const double* cx, const double* cy, double px, double py, double w_plane,
                            int first, const double* norm, hipStream_t s);
+// strips (multi-GPU strong scaling): pass A over rows [y0, y1)
+// of gT (zeroed after reading) into H with y1 - y0 rows per block; pass B for
+// image rows [i0, i1) (multiples of the column block) from an H holding those
+// blocks (nv rows each), out = the strip's rows (2-D epilogue, / *norm if set)
+hipError_t launch_fft_rows_strip(double* gT, int64_t nu, int64_t nv, int64_t nx, const double* tw_u, int64_t y0,
+                                 int64_t y1, double* H, hipStream_t s);
+hipError_t launch_fft_cols_strip(const double* H, int64_t nv, int64_t nx, int64_t ny, const double* tw_v, int64_t i0,
+                                 int64_t i1, double* out, const double* cx, const double* cy, const double* norm,
+                                 hipStream_t s);
 // out[0..n) /= *sumw (device scalar)
 hipError_t launch_scale_inverse(double* out, int64_t n, const double* sumw, hipStream_t s);
 

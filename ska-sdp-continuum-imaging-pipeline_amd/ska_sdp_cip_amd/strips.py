@@ -1,0 +1,381 @@
+"""
+Strong scaling of ONE dirty image over several GPUs: uv strips with a halo
+exchange before the FFT (SURVEY.md 8(e) option 1; the north
+star's "UVW tiles shard naturally across the 8 GPUs ... RCCL reduce over xGMI
+of overlapping partial-grid halos before the FFT-to-dirty-image step").
+
+The uv grid is stored transposed for the pruned FFT (gT[y][x], y along v).
+Rank r owns grid rows [y0_r, y1_r) - contiguous v strips balanced by
+visibility count - and grids the visibilities whose footprint origin row lies
+in its strip (the UVW tiles of that strip: the data layout the reference's
+reorder_by_uvw_tile produces offline, reorder.py:19-111). A footprint reaches
+W - 1 rows past the origin, so rank r's partial grid also holds rows
+[y1_r, y1_r + W - 1) of its successor (mod nv): that halo goes to rank r + 1
+(point-to-point, RCCL over xGMI) and is added there. Then the FFT runs
+distributed: pass A (along u) on each rank's own rows, one all-to-all that
+hands every rank the pass-A columns of its image rows [i0_r, i1_r) (blocks of
+4 kept u frequencies x all v), pass B (along v) + crop + grid correction on
+them, and a gather of the image rows onto the destination rank. The weight sum
+is all-reduced and divided out in pass B's epilogue. Traffic per rank at C4
+(16384^2 grid, 8 ranks): halo 1.8 MB, all-to-all 224 MB, image rows 64 MB -
+against a 4 GiB partial-grid reduce for row (weak) sharding.
+
+The per-rank stages are backend-independent (`HipStripBackend` runs them
+through libcip_hip.so; tests plug in a CPU restatement); `invert_strips` wires
+them with torch.distributed collectives (RCCL, or gloo on CPU tensors), and
+`invert_strips_local` runs all ranks' stages in one process (one device),
+exchanging in memory - the single-GPU check of the decomposition.
+"""
+
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Optional, Sequence
+
+import numpy as np
+
+SPEED_OF_LIGHT = 299792458.0
+COL_BLOCK = 4  # pass-A output block width (cip_fft.hip kColBlock)
+
+try:
+    import torch
+except ModuleNotFoundError:  # pragma: no cover - torch is in the image
+    torch = None
+
+
+@dataclass
+class StripLayout:
+    """Row strips of the grid and image-row strips of the dirty image.
+
+    y_bounds: world + 1 grid-row bounds (0 .. nv); x_bounds: world + 1 image-
+    row bounds (0 .. npix_x, multiples of COL_BLOCK); halo = W - 1 rows.
+    """
+
+    nu: int
+    nv: int
+    npix_x: int
+    npix_y: int
+    support: int
+    y_bounds: list
+    x_bounds: list
+
+    @property
+    def world(self) -> int:
+        return len(self.y_bounds) - 1
+
+    @property
+    def halo(self) -> int:
+        return self.support - 1
+
+    def rows(self, r: int) -> tuple[int, int]:
+        return self.y_bounds[r], self.y_bounds[r + 1]
+
+    def image_rows(self, r: int) -> tuple[int, int]:
+        return self.x_bounds[r], self.x_bounds[r + 1]
+
+
+def origin_rows(v_m, fx, scale_v: float, nv: int, support: int):
+    """Footprint origin row of every (row, channel): iy0 = floor(v f/c nv
+    pixsize_y + nv/2 - W/2) + 1, wrapped into [0, nv) - the gridder's placement
+    arithmetic (cip_common.h place_vis: the same fp64 operations in the same
+    order), so the strip a visibility is assigned to is the one its footprint
+    starts in. v_m (nrow,), fx (nchan,) tensors -> (nrow, nchan) int64."""
+    y = (v_m[:, None] * fx[None, :]) * scale_v + float(nv // 2)
+    iy0 = torch.floor(y - float(support // 2)).to(torch.int64) + 1
+    return torch.remainder(iy0, nv)
+
+
+def _row_chunks(nrow: int, chunk: int = 65536):
+    for a in range(0, nrow, chunk):
+        yield a, min(nrow, a + chunk)
+
+
+def plan_strips(uvw, freq, params, pixsize_y: float, npix_x: int, npix_y: int, world: int) -> StripLayout:
+    """Balanced strips: grid-row bounds splitting the visibilities' origin-row
+    histogram (all visibilities, so every rank computes the same bounds
+    without communication) into `world` near-equal parts, each at least
+    W rows high (the halo then only reaches the next strip); image rows split
+    into near-equal multiples of COL_BLOCK. uvw (nrow, 3), freq (nchan) tensors."""
+    nv, W = int(params.nv), int(params.support)
+    if world < 1:
+        raise ValueError("world must be >= 1")
+    nb = npix_x // COL_BLOCK
+    if npix_x % COL_BLOCK != 0 or nb < world:
+        raise ValueError(f"npix_x must be a multiple of {COL_BLOCK} with at least one block of "
+                         f"{COL_BLOCK} image rows per rank")
+    if nv < W * world:
+        raise ValueError("grid too small for this many strips")
+    fx = freq / SPEED_OF_LIGHT
+    scale_v = float(params.nv) * pixsize_y
+    hist = torch.zeros(nv, dtype=torch.int64, device=uvw.device)
+    for a, b in _row_chunks(uvw.shape[0]):
+        hist += torch.bincount(origin_rows(uvw[a:b, 1], fx, scale_v, nv, W).reshape(-1), minlength=nv)
+    cum = np.cumsum(hist.cpu().numpy())
+    total = int(cum[-1]) if cum.size else 0
+    bounds = [0]
+    for r in range(1, world):
+        target = total * r / world
+        y = int(np.searchsorted(cum, target, side="left")) + 1
+        y = max(y, bounds[-1] + W)
+        y = min(y, nv - W * (world - r))
+        bounds.append(y)
+    bounds.append(nv)
+    return StripLayout(int(params.nu), nv, int(npix_x), int(npix_y), W, bounds,
+                       [COL_BLOCK * (r * nb // world) for r in range(world + 1)])
+
+
+@dataclass
+class StripData:
+    """One strip's visibilities in the Tile layout (reference
+    uvw_tiling/tile.py:14-124): row slices with uvw and channel ranges,
+    visibilities / weights concatenated in slice order."""
+
+    slice_uvw: "torch.Tensor"   # (ns, 3) f64
+    chan_start: "torch.Tensor"  # (ns,) int32
+    chan_stop: "torch.Tensor"   # (ns,) int32
+    vis: "torch.Tensor"         # (nvis,) complex
+    wgt: Optional["torch.Tensor"]  # (nvis,) f32/f64 or None
+    rows: "torch.Tensor"        # (ns,) int64: the MS row of each slice
+
+    @property
+    def nvis(self) -> int:
+        return int(self.vis.shape[0])
+
+
+def strip_slices(uvw, freq, params, pixsize_y: float, y0: int, y1: int):
+    """(rows, c0, c1) int64 tensors: the maximal channel runs of each row whose
+    origin row lies in [y0, y1) (one run per row unless a row's v track wraps
+    or leaves and re-enters the strip)."""
+    nv, W = int(params.nv), int(params.support)
+    fx = freq / SPEED_OF_LIGHT
+    scale_v = float(params.nv) * pixsize_y
+    rows_l, c0_l, c1_l = [], [], []
+    for a, b in _row_chunks(uvw.shape[0]):
+        iy = origin_rows(uvw[a:b, 1], fx, scale_v, nv, W)
+        m = (iy >= y0) & (iy < y1)
+        pad = torch.zeros((m.shape[0], 1), dtype=torch.bool, device=m.device)
+        mp = torch.cat([pad, m, pad], dim=1)
+        starts = torch.nonzero(mp[:, 1:] & ~mp[:, :-1])  # (row, channel) of each run start
+        stops = torch.nonzero(~mp[:, 1:] & mp[:, :-1])   # (row, channel) one past each run's end
+        rows_l.append(starts[:, 0] + a)
+        c0_l.append(starts[:, 1])
+        c1_l.append(stops[:, 1])
+    if not rows_l:
+        e = torch.zeros(0, dtype=torch.int64, device=uvw.device)
+        return e, e, e
+    return torch.cat(rows_l), torch.cat(c0_l), torch.cat(c1_l)
+
+
+def gather_strip(uvw, vis, wgt, rows, c0, c1) -> StripData:
+    """The strip's Tile-layout data from dense (nrow, nchan) columns."""
+    nchan = vis.shape[1]
+    lengths = (c1 - c0)
+    starts = rows * nchan + c0
+    idx = torch.repeat_interleave(starts, lengths)
+    if idx.numel():
+        first = torch.repeat_interleave(torch.cumsum(lengths, 0) - lengths, lengths)
+        idx = idx + (torch.arange(idx.numel(), device=idx.device) - first)
+    return StripData(uvw[rows].contiguous(), c0.to(torch.int32), c1.to(torch.int32),
+                     vis.reshape(-1)[idx].contiguous(), None if wgt is None else wgt.reshape(-1)[idx].contiguous(),
+                     rows)
+
+
+class HipStripBackend:
+    """Per-rank stages on the current GPU through libcip_hip.so: cip_grid_tiles
+    (accumulating gridder) onto a full-size transposed grid that only the
+    strip's rows (+ halo) reach, cip_strip_rows (pass A), cip_strip_cols
+    (pass B + crop + correction). The grid is kept between calls and left
+    clean (pass A zeroes the rows it reads; the halo rows are zeroed after
+    they are sent)."""
+
+    def __init__(self, params, pixsize_x: float, pixsize_y: float, npix_x: int, npix_y: int, device=None):
+        from . import _lib  # pylint: disable=import-outside-toplevel
+        from .gridder import _require_gpu  # pylint: disable=import-outside-toplevel
+
+        _require_gpu()
+        self._lib = _lib
+        self.params = params
+        self.px, self.py = float(pixsize_x), float(pixsize_y)
+        self.npix_x, self.npix_y = int(npix_x), int(npix_y)
+        self.device = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+        if int(params.nplanes) != 1 or not _lib.lib().cip_grid_layout(params, self.npix_x, self.npix_y):
+            raise ValueError("strips need a 2-D (no w-stacking) grid in the pruned-FFT layout "
+                             "(power-of-two grids)")
+        self.grid = torch.zeros((int(params.nv), int(params.nu), 2), dtype=torch.float64, device=self.device)
+
+    def _stream(self):
+        return torch.cuda.current_stream(self.device).cuda_stream
+
+    def grid_strip(self, data: StripData, freq):
+        """Grid the strip's visibilities; returns (grid (nv, nu, 2) f64, weight sum (1,) f64)."""
+        from .gridder import _codes  # pylint: disable=import-outside-toplevel
+
+        vis_codes, wgt_codes = _codes()
+        sumw = torch.zeros(1, dtype=torch.float64, device=self.device)
+        ns = int(data.slice_uvw.shape[0])
+        if ns:
+            self._lib.check(self._lib.lib().cip_grid_tiles(
+                data.slice_uvw.data_ptr(), data.chan_start.data_ptr(), data.chan_stop.data_ptr(), ns,
+                freq.data_ptr(), int(freq.shape[0]), data.vis.data_ptr(), data.nvis, vis_codes[data.vis.dtype],
+                data.wgt.data_ptr() if data.wgt is not None else None,
+                wgt_codes[data.wgt.dtype] if data.wgt is not None else self._lib.CIP_NONE,
+                self.params, self.px, self.py, self.npix_x, self.npix_y, 0, self._stream(),
+                self.grid.data_ptr(), sumw.data_ptr()))
+        return self.grid, sumw
+
+    def pass_rows(self, grid, y0: int, y1: int):
+        """Pass A over grid rows [y0, y1) -> H (npix_x / 4, y1 - y0, 4, 2); zeroes the rows."""
+        H = torch.empty((self.npix_x // COL_BLOCK, y1 - y0, COL_BLOCK, 2), dtype=torch.float64, device=self.device)
+        self._lib.check(self._lib.lib().cip_strip_rows(grid.data_ptr(), self.params, self.npix_x, self.npix_y,
+                                                       int(y0), int(y1), self._stream(), H.data_ptr()))
+        return H
+
+    def pass_cols(self, H, i0: int, i1: int, norm=None):
+        """Pass B for image rows [i0, i1) from H ((i1 - i0) / 4, nv, 4, 2)."""
+        out = torch.empty((i1 - i0, self.npix_y), dtype=torch.float64, device=self.device)
+        self._lib.check(self._lib.lib().cip_strip_cols(H.data_ptr(), self.params, self.npix_x, self.npix_y,
+                                                       int(i0), int(i1), None if norm is None else norm.data_ptr(),
+                                                       self._stream(), out.data_ptr()))
+        return out
+
+
+def _halo_rows(layout: StripLayout, r: int) -> tuple[int, int]:
+    """Grid rows of rank r's halo: [y1, y1 + W - 1) mod nv (contiguous: strips are
+    >= W rows high and only the last one ends at nv)."""
+    _, y1 = layout.rows(r)
+    a = y1 % layout.nv
+    return a, a + layout.halo
+
+
+def _assemble_H(pieces: Sequence, nb: int, layout: StripLayout, device, dtype):
+    """Rank s's pass-B input from every rank's pass-A blocks [i0_s / 4, i1_s / 4)
+    (piece r: (nb, h_r, 4, 2)) -> (nb, nv, 4, 2)."""
+    H = torch.empty((nb, layout.nv, COL_BLOCK, 2), dtype=dtype, device=device)
+    for r, piece in enumerate(pieces):
+        y0, y1 = layout.rows(r)
+        H[:, y0:y1] = piece.reshape(nb, y1 - y0, COL_BLOCK, 2)
+    return H
+
+
+def invert_strips(data: StripData, freq, layout: StripLayout, backend, *, dst: int = 0, group=None,
+                  stages: Optional[dict] = None):
+    """This rank's share of the strip-distributed invert (torch.distributed
+    initialised, one rank per strip). Returns the normalised dirty image
+    (npix_x, npix_y) on `dst`, None elsewhere. Collectives: one point-to-point
+    halo exchange with the ring neighbours, one all-to-all of the pass-A
+    blocks, a scalar all-reduce of the weight sum, a gather of image rows.
+    `stages` (a dict, diagnostic): each stage is synchronised and its seconds
+    added under its name (grid, halo, rows, alltoall, cols, gather)."""
+    import time  # pylint: disable=import-outside-toplevel
+
+    import torch.distributed as dist  # pylint: disable=import-outside-toplevel
+
+    t_last = [time.perf_counter()]
+
+    def mark(name):
+        if stages is not None:
+            if grid.is_cuda:
+                torch.cuda.synchronize(grid.device)
+            t = time.perf_counter()
+            stages[name] = stages.get(name, 0.0) + t - t_last[0]
+            t_last[0] = t
+
+    single = not dist.is_available() or not dist.is_initialized()
+    world = 1 if single else dist.get_world_size(group)
+    rank = 0 if single else dist.get_rank(group)
+    if world != layout.world:
+        raise ValueError("the layout was planned for another number of ranks")
+    y0, y1 = layout.rows(rank)
+    grid, sumw = backend.grid_strip(data, freq)
+    mark("grid")
+    if world > 1:
+        # halo: rows past the strip -> the next rank, added to its first rows
+        ha, hb = _halo_rows(layout, rank)
+        send = grid[ha:hb].contiguous()
+        recv = torch.empty_like(send)
+        ops = [dist.P2POp(dist.isend, send, (rank + 1) % world, group),
+               dist.P2POp(dist.irecv, recv, (rank - 1) % world, group)]
+        for w in dist.batch_isend_irecv(ops):
+            w.wait()
+        grid[ha:hb].zero_()
+        grid[y0:y0 + layout.halo] += recv
+    if world > 1:
+        dist.all_reduce(sumw, group=group)
+    mark("halo")
+    H = backend.pass_rows(grid, y0, y1)
+    mark("rows")
+    h = y1 - y0
+    if world > 1:
+        # all-to-all: rank s receives blocks [i0_s / 4, i1_s / 4) of every rank's rows
+        splits_in = [(layout.image_rows(s)[1] - layout.image_rows(s)[0]) // COL_BLOCK * h * COL_BLOCK * 2
+                     for s in range(world)]
+        i0, i1 = layout.image_rows(rank)
+        nb = (i1 - i0) // COL_BLOCK
+        splits_out = [nb * (layout.rows(r)[1] - layout.rows(r)[0]) * COL_BLOCK * 2 for r in range(world)]
+        recv = torch.empty(sum(splits_out), dtype=H.dtype, device=H.device)
+        dist.all_to_all_single(recv, H.reshape(-1), splits_out, splits_in, group=group)
+        pieces = list(torch.split(recv, splits_out))
+        Hm = _assemble_H(pieces, nb, layout, H.device, H.dtype)
+    else:
+        i0, i1 = layout.image_rows(0)
+        Hm = H
+    mark("alltoall")
+    rows_img = backend.pass_cols(Hm, i0, i1, norm=sumw)
+    mark("cols")
+    if world == 1:
+        return rows_img
+    # gather the image rows (strips padded to the largest: gather needs equal sizes)
+    hmax = max(layout.image_rows(r)[1] - layout.image_rows(r)[0] for r in range(world))
+    if rows_img.shape[0] < hmax:
+        rows_img = torch.cat([rows_img, rows_img.new_zeros((hmax - rows_img.shape[0], rows_img.shape[1]))])
+    gathered = [torch.empty_like(rows_img) for _ in range(world)] if rank == dst else None
+    dist.gather(rows_img, gathered, dst=dst, group=group)
+    mark("gather")
+    if rank != dst:
+        return None
+    return torch.cat([g[:layout.image_rows(r)[1] - layout.image_rows(r)[0]] for r, g in enumerate(gathered)])
+
+
+def invert_strips_local(datas: Sequence[StripData], freq, layout: StripLayout, backend):
+    """All ranks' stages in ONE process on one device, the exchanges done in
+    memory (the single-GPU check of the decomposition and its kernels). The
+    ranks run one after another through the backend's one grid buffer: rank
+    r grids its strip, its halo rows are taken out (-> rank r + 1) and the
+    predecessor's halo is added to its first rows before its pass A; rank 0's
+    rows wait (saved) for the last rank's halo. Returns the normalised dirty
+    image (npix_x, npix_y)."""
+    world = layout.world
+    if len(datas) != world:
+        raise ValueError("one StripData per strip")
+    Hs = [None] * world
+    sumw, prev_halo, rows0 = None, None, None
+    for r in range(world):
+        y0, y1 = layout.rows(r)
+        grid, sw = backend.grid_strip(datas[r], freq)
+        sumw = sw.clone() if sumw is None else sumw + sw
+        if world == 1:
+            Hs[0] = backend.pass_rows(grid, y0, y1)
+            break
+        ha, hb = _halo_rows(layout, r)
+        halo = grid[ha:hb].clone()
+        grid[ha:hb].zero_()
+        if r == 0:
+            rows0 = grid[y0:y1].clone()
+            grid[y0:y1].zero_()
+        else:
+            grid[y0:y0 + layout.halo] += prev_halo
+            Hs[r] = backend.pass_rows(grid, y0, y1)
+        prev_halo = halo
+    if world > 1:
+        y0, y1 = layout.rows(0)
+        grid = backend.grid
+        grid[y0:y1] = rows0
+        grid[y0:y0 + layout.halo] += prev_halo
+        Hs[0] = backend.pass_rows(grid, y0, y1)
+    out = []
+    for s in range(world):
+        i0, i1 = layout.image_rows(s)
+        b0, b1 = i0 // COL_BLOCK, i1 // COL_BLOCK
+        Hm = Hs[0] if world == 1 else _assemble_H([H[b0:b1] for H in Hs], b1 - b0, layout, Hs[0].device, Hs[0].dtype)
+        out.append(backend.pass_cols(Hm.contiguous(), i0, i1, norm=sumw))
+    return torch.cat(out, dim=0)

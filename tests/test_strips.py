@@ -1,0 +1,158 @@
+"""
+Strong-scaling uv-strip decomposition (ska_sdp_cip_amd.strips):
+the strip plan covers every visibility exactly once, the single-process
+emulation of the halo exchange / all-to-all equals the one-shot image, and a
+world-size-2 (and 3) gloo run of the real collectives gives the single-process
+image at 1e-13 - with the CPU restatement of the per-rank stages
+(tests/_strip_np.py) standing in for the GPU. The GPU form of the same checks
+is in test_gpu_strips.py.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import oracle
+from ska_sdp_cip_amd import strips
+from ska_sdp_cip_amd import synthetic as syn
+
+NPIX = 64
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _case(nrow=801, nchan=16, seed=4):
+    ms = syn.make_measurement_set(nrow, nchan, n_ant=12, array_radius_m=800.0, seed=seed)
+    vis, _, _, w = oracle.stokes_i(ms.visibilities(), ms.flags(), ms.weights())
+    uvw, f = ms.uvw(), ms.channel_frequencies()
+    px = syn.pixel_size_for_grid(uvw, f, NPIX)
+    return uvw, f, vis, w, px
+
+
+def _prm(px, W):
+    return oracle.choose_params(NPIX, NPIX, px, px, support=W)
+
+
+class _P:  # the fields plan_strips / strip_slices read from cip_gridder_params
+    def __init__(self, prm):
+        self.nu, self.nv, self.support = prm["nu"], prm["nv"], prm["support"]
+
+
+def _strip_datas(uvw, f, vis, w, px, prm, layout):
+    tu, tf = torch.from_numpy(uvw), torch.from_numpy(f)
+    tv = torch.from_numpy(vis.astype(np.complex128))
+    tw = torch.from_numpy(w.astype(np.float64))
+    out = []
+    for r in range(layout.world):
+        y0, y1 = layout.rows(r)
+        rows, c0, c1 = strips.strip_slices(tu, tf, _P(prm), px, y0, y1)
+        out.append(strips.gather_strip(tu, tv, tw, rows, c0, c1))
+    return out
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 4, 8])
+def test_strip_plan_partitions_visibilities(world):
+    uvw, f, vis, w, px = _case()
+    prm = _prm(px, 8)
+    layout = strips.plan_strips(torch.from_numpy(uvw), torch.from_numpy(f), _P(prm), px, NPIX, NPIX, world)
+    yb = layout.y_bounds
+    assert yb[0] == 0 and yb[-1] == prm["nv"]
+    assert all(b - a >= prm["support"] for a, b in zip(yb, yb[1:]))
+    xb = layout.x_bounds
+    assert xb[0] == 0 and xb[-1] == NPIX and all(x % 4 == 0 and b > a for x, a, b in zip(xb, xb, xb[1:]))
+    count = np.zeros(vis.shape, dtype=np.int64)
+    datas = _strip_datas(uvw, f, vis, w, px, prm, layout)
+    for d in datas:
+        for r, a, b in zip(d.rows.numpy(), d.chan_start.numpy(), d.chan_stop.numpy()):
+            assert a < b
+            count[r, a:b] += 1
+    assert (count == 1).all()
+    sizes = np.array([d.nvis for d in datas])
+    assert sizes.sum() == vis.size
+    if world > 1:  # balanced, up to the granularity of strips at least W rows high
+        iy = strips.origin_rows(torch.from_numpy(uvw[:, 1]), torch.from_numpy(f) / strips.SPEED_OF_LIGHT,
+                                prm["nv"] * px, prm["nv"], prm["support"])
+        hist = np.bincount(iy.numpy().ravel(), minlength=prm["nv"])
+        window = np.convolve(hist, np.ones(2 * prm["support"], dtype=np.int64)).max()
+        assert sizes.max() <= 1.1 * vis.size / world + window
+    # the gathered visibilities are the right ones
+    d = datas[-1]
+    k = 0
+    for r, a, b in zip(d.rows.numpy()[:50], d.chan_start.numpy()[:50], d.chan_stop.numpy()[:50]):
+        np.testing.assert_array_equal(d.vis.numpy()[k:k + b - a], vis[r, a:b])
+        k += b - a
+
+
+def test_strip_plan_rejects_bad_splits():
+    uvw, f, _, _, px = _case(nrow=50, nchan=2)
+    prm = _prm(px, 8)
+    with pytest.raises(ValueError):  # fewer blocks of 4 image rows than ranks
+        strips.plan_strips(torch.from_numpy(uvw), torch.from_numpy(f), _P(prm), px, NPIX, NPIX, 17)
+    with pytest.raises(ValueError):  # strips lower than the kernel support
+        strips.plan_strips(torch.from_numpy(uvw), torch.from_numpy(f), _P(prm), px, NPIX, NPIX, 32)
+
+
+@pytest.mark.parametrize("world,W", [(1, 8), (2, 8), (3, 8), (4, 6), (8, 4)])
+def test_strip_emulation_equals_one_shot(world, W):
+    from _strip_np import NumpyStripBackend
+
+    uvw, f, vis, w, px = _case()
+    prm = _prm(px, W)
+    layout = strips.plan_strips(torch.from_numpy(uvw), torch.from_numpy(f), _P(prm), px, NPIX, NPIX, world)
+    datas = _strip_datas(uvw, f, vis, w, px, prm, layout)
+    be = NumpyStripBackend(prm, px, px, NPIX, NPIX)
+    img = strips.invert_strips_local(datas, torch.from_numpy(f), layout, be).numpy()
+    full = oracle.ms2dirty(uvw, f, vis, w, NPIX, NPIX, px, px, support=W, nthreads=1) / w.astype(np.float64).sum()
+    assert np.abs(img - full).max() < 1e-13 * max(1.0, np.abs(full).max())
+    assert float(be.grid.abs().max()) == 0.0  # the grid is left clean
+
+
+def _worker(rank, world, port, q, W):
+    import sys
+    from pathlib import Path
+
+    root = Path(__file__).resolve().parents[1]
+    sys.path[:0] = [str(root / "ska-sdp-continuum-imaging-pipeline_amd"), str(root / "oracle"), str(root / "tests")]
+    from _strip_np import NumpyStripBackend
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    uvw, f, vis, w, px = _case()
+    prm = _prm(px, W)
+    layout = strips.plan_strips(torch.from_numpy(uvw), torch.from_numpy(f), _P(prm), px, NPIX, NPIX, world)
+    data = _strip_datas(uvw, f, vis, w, px, prm, layout)[rank]  # each rank holds only its strip
+    be = NumpyStripBackend(prm, px, px, NPIX, NPIX)
+    img = strips.invert_strips(data, torch.from_numpy(f), layout, be, dst=0)
+    if rank == 0:
+        full = oracle.ms2dirty(uvw, f, vis, w, NPIX, NPIX, px, px, support=W, nthreads=1) / w.astype(np.float64).sum()
+        q.put((float(np.abs(img.numpy() - full).max()), float(np.abs(full).max()), float(be.grid.abs().max())))
+    else:
+        assert img is None
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,W", [(2, 8), (3, 6)])
+def test_strip_halo_exchange_gloo(world, W):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, W)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=240)
+    assert all(p.exitcode == 0 for p in procs)
+    err, peak, left = q.get(timeout=5)
+    assert err < 1e-13 * max(1.0, peak)
+    assert left == 0.0
