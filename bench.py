@@ -54,6 +54,22 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def make_raw_columns(cfg, rank, device, seed=20241008):
+    """Device-resident raw linear-feed columns of this rank's shard for
+    `--raw`: vis4 (rows, nchan, 4) complex64 XX, XY, YX, YY, wgt4 float32 in
+    [0.5, 1.5) and flags4 uint8 with 5 % of the XX and YY entries flagged (as
+    an MS holds them; the gridder forms Stokes I on load)."""
+    import torch
+
+    g = torch.Generator(device=device)
+    g.manual_seed(seed + 1000 + rank)
+    shape = (cfg["rows"], cfg["nchan"], 4)
+    vis4 = torch.randn(shape, dtype=torch.complex64, device=device, generator=g)
+    wgt4 = torch.rand(shape, dtype=torch.float32, device=device, generator=g) + 0.5
+    flags4 = (torch.rand(shape, dtype=torch.float32, device=device, generator=g) < 0.025).to(torch.uint8)
+    return vis4, flags4, wgt4
+
+
 def make_inputs(cfg, rank, world, device, seed=20241008):
     """Device-resident gridder inputs of this rank's shard."""
     import torch
@@ -332,6 +348,10 @@ def main():
     ap.add_argument("--no-max-err", action="store_true", help="skip the GPU-vs-oracle max|err| check")
     ap.add_argument("--err-row-step", type=int, default=0,
                     help="max|err| on every k-th row (default: 50 in 2-D, 200 with w-stacking)")
+    ap.add_argument("--raw", action="store_true",
+                    help="raw linear-feed columns (rows, nchan, 4) resident in HBM: Stokes I and effective weights "
+                         "formed inside the planner and scatter (cip_ms2dirty_stokes_i) - the reference's whole "
+                         "invert_measurement_set input (secondary measurement)")
     ap.add_argument("--strong", action="store_true",
                     help="strong scaling of ONE C4 image (1G vis, 16k^2 grid) over the ranks: uv strips + halo "
                          "exchange + distributed FFT (DESIGN.md 7); --config is ignored")
@@ -358,6 +378,16 @@ def main():
     nvis = cfg["rows"] * cfg["nchan"]
     npix = cfg["npix"]
     uvw_d, freq_d, vis_d, wgt_d, px, uvw_h, freq_h = make_inputs(cfg, rank, world, device)
+    raw = None
+    if args.raw:
+        del vis_d, wgt_d
+        raw = make_raw_columns(cfg, rank, device)
+        vis_d = wgt_d = None
+
+    def invert(**kw):
+        if raw is not None:
+            return gridder.device_ms2dirty_stokes_i(uvw_d, freq_d, raw[0], raw[1], raw[2], npix, npix, px, px, **kw)
+        return gridder.device_ms2dirty(uvw_d, freq_d, vis_d, wgt_d, npix, npix, px, px, **kw)
     # two image buffers (image + weight sum adjacent: one RCCL reduce each):
     # step k's reduce runs on the communicator's stream while step k + 1
     # inverts into the other buffer; a buffer is rewritten only after its
@@ -376,10 +406,9 @@ def main():
         # the host prepares step k + 1 while the GPU finishes step k; the
         # inputs are resident and unchanged (CIP_PIPELINE), so step k + 1's
         # planner runs beside step k's scatter and FFT
-        gridder.device_ms2dirty(uvw_d, freq_d, vis_d, wgt_d, npix, npix, px, px, support=args.support,
-                                do_wstacking=args.wstacking, out=dirty, sum_weights=sumw,
-                                single_precision_accumulation=args.single, normalise=world == 1,
-                                synchronize=sync, resident_inputs=not sync)
+        invert(support=args.support, do_wstacking=args.wstacking, out=dirty, sum_weights=sumw,
+               single_precision_accumulation=args.single, normalise=world == 1, synchronize=sync,
+               resident_inputs=not sync)
         # RCCL reduce of the partial images + weights to rank 0, normalised there
         # (one GPU: the image is already normalised in the FFT epilogue)
         pending[k] = reduce_images(dirty, sumw, dst=0, async_op=True, normalise=world > 1)
@@ -396,9 +425,8 @@ def main():
         step(sync=args.sync)
     drain()
     dirty, sumw = bufs[0]
-    _, params = gridder.device_ms2dirty(uvw_d, freq_d, vis_d, wgt_d, npix, npix, px, px, support=args.support,
-                                        do_wstacking=args.wstacking, out=dirty, sum_weights=sumw,
-                                        single_precision_accumulation=args.single)
+    _, params = invert(support=args.support, do_wstacking=args.wstacking, out=dirty, sum_weights=sumw,
+                       single_precision_accumulation=args.single)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -453,7 +481,8 @@ def main():
     # plane's grid written once (its read-back belongs to the FFT). The
     # ordered-stream record this design adds (8 B/vis) is not counted.
     vis_per_launch = nvis * (params.support if args.wstacking else 1) / (P if args.wstacking else 1)
-    bytes_launch = vis_per_launch * (8 + 4) + runs / launches * 32 + params.nu * params.nv * 16
+    vis_bytes = 52 if args.raw else 12  # raw: 4 x c64 + 4 x f32 + 4 x u8 per visibility
+    bytes_launch = vis_per_launch * vis_bytes + runs / launches * 32 + params.nu * params.nv * 16
     achieved = bytes_launch / (scatter_ms * 1e-3) / 1e9
     roofline = {
         "bound": "hbm",
@@ -479,7 +508,7 @@ def main():
                                        "conflict-free wave-instr"}
     tr = traffic_from_profiles(args.config)
     # the committed PMC pass is of the default workload (support 8, 2-D, fp64 class)
-    if tr and not args.wstacking and not args.single and args.support == tr.get("support", 8):
+    if tr and not args.wstacking and not args.single and not args.raw and args.support == tr.get("support", 8):
         roofline["traffic"] = tr.get("hbm_bytes_per_launch")
 
     result = {
@@ -494,8 +523,12 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f32-class (packed 2x32-bit)" if args.single else "f64",
-        "data": "synthetic (seeded MeerKAT-like uvw tracks, random complex64 vis, float32 weights, 5% flagged)",
+        "data": ("synthetic (seeded MeerKAT-like uvw tracks, raw (rows, nchan, 4) complex64 correlations, float32 "
+                 "weights, uint8 flags 2.5% per XX/YY entry)" if args.raw else
+                 "synthetic (seeded MeerKAT-like uvw tracks, random complex64 vis, float32 weights, 5% flagged)"),
         "config": {
+            "input": ("raw linear-feed columns, Stokes I formed in the gridder (cip_ms2dirty_stokes_i)" if args.raw
+                      else "Stokes-I visibilities + effective weights (cip_ms2dirty)"),
             "workload": (f"{args.config.upper()}: {cfg['rows']:,} rows x {cfg['nchan']} ch = {nvis:,} vis/GPU -> "
                          f"{params.nu}x{params.nv} grid ({npix}^2 image), support {params.support}, "
                          f"{'w-stacking ' + str(P) + ' planes' if args.wstacking else '2-D'}, "
@@ -521,7 +554,13 @@ def main():
     nthreads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, len(os.sched_getaffinity(0)))
     need_host = rank == 0 and ((world == 1 and not args.no_cpu_baseline) or not args.no_max_err)
     vis_h = wgt_h = None
-    if need_host:
+    if need_host and raw is not None:
+        # the Stokes-I inputs the gridder formed, restated by the oracle's numpy
+        import oracle
+
+        vis_h, _, _, wgt_h = oracle.stokes_i(raw[0].cpu().numpy(), raw[1].cpu().numpy().astype(bool),
+                                             raw[2].cpu().numpy())
+    elif need_host:
         vis_h = vis_d.cpu().numpy()
         wgt_h = wgt_d.cpu().numpy()
     if rank == 0 and not args.no_max_err:

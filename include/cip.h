@@ -130,6 +130,26 @@ int cip_ms2dirty(const double* uvw, int64_t nrow, const double* freq,
                  void* hip_stream, double* dirty_out, double* sum_wgt_out,
                  cip_gridder_params* params_out);
 
+/* cip_ms2dirty on the raw linear-feed columns (the reference's
+ * StokesIGridderInput + effective weights, invert.py:78-116, fused into the
+ * gridder): vis4 (nrow, nchan, 4) complex64 correlations XX, XY, YX, YY,
+ * flags4 (nrow, nchan, 4) uint8 (NULL: none flagged; 4-byte aligned), wgt4
+ * (nrow, nchan, 4) float32, all device pointers. The planner and the scatter
+ * form Stokes I = 0.5 (XX + YY) and the weight !(F_XX | F_YY) * 4 /
+ * (1 / w_XX + 1 / w_YY) in float32 as they load each visibility: the image,
+ * weight sum and parameters equal cip_stokes_i followed by cip_ms2dirty on its
+ * (vis_i, eff_w) bit for bit, without the 12 B/visibility intermediate
+ * columns. Other arguments and flags as cip_ms2dirty (CIP_PSF: unit
+ * visibilities with these weights; CIP_ACC_SINGLE allowed). Replaces
+ * invert.py:170-183's ms2dirty call on StokesIGridderInput's outputs. */
+int cip_ms2dirty_stokes_i(const double* uvw, int64_t nrow, const double* freq,
+                          int64_t nchan, const void* vis4, const uint8_t* flags4,
+                          const float* wgt4, int64_t npix_x, int64_t npix_y,
+                          double pixsize_x, double pixsize_y, double epsilon,
+                          int support, int flags, void* hip_stream,
+                          double* dirty_out, double* sum_wgt_out,
+                          cip_gridder_params* params_out);
+
 /* Uniform-grid ("grid only") variant used by the benchmark and the parity
  * tests: fills grid_out (device, nu x nv complex128, row-major) for w-plane
  * `plane` (0 in 2-D mode) with the gridded visibilities, using params from

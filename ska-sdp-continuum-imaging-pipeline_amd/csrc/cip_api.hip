@@ -764,8 +764,12 @@ static int make_plan(Workspace* ws, const double* uvw, const double* fx, const R
   return CIP_OK;
 }
 
-static bool vis_dtype_ok(int d) { return d == CIP_C64 || d == CIP_C128; }
-static bool wgt_dtype_ok(int d) { return d == CIP_NONE || d == CIP_F32 || d == CIP_F64; }
+// the internal raw linear-feed code is reached through cip_ms2dirty_stokes_i only
+static bool public_dtypes(int vis_dtype, int wgt_dtype) {
+  return vis_dtype != CIP_POL4I && wgt_dtype != CIP_POL4I;
+}
+static bool vis_dtype_ok(int d) { return d == CIP_C64 || d == CIP_C128 || d == CIP_POL4I; }
+static bool wgt_dtype_ok(int d) { return d == CIP_NONE || d == CIP_F32 || d == CIP_F64 || d == CIP_POL4I; }
 
 struct Prepared {
   cip_gridder_params p;
@@ -791,11 +795,14 @@ static int prepare(Workspace* ws, const double* uvw, int64_t nrow, const double*
                    const void* vis, int vis_dtype, const void* wgt, int wgt_dtype, int64_t npix_x, int64_t npix_y,
                    double px, double py, double epsilon, int support, int do_wstacking, bool packed,
                    const cip_gridder_params* given, hipStream_t s, Prepared* out, double** grid_out = nullptr,
-                   const RaggedRows* ragged = nullptr, bool reuse = false) {
+                   const RaggedRows* ragged = nullptr, bool reuse = false, const uint8_t* flags4 = nullptr) {
   if (!ws->parity_scope) ws->plan_unscoped = true;
   if (!vis_dtype_ok(vis_dtype)) return set_error(CIP_EINVAL, "vis dtype must be complex64 or complex128");
   if (!wgt_dtype_ok(wgt_dtype)) return set_error(CIP_EINVAL, "wgt dtype must be float32, float64 or none");
   if (wgt == nullptr) wgt_dtype = CIP_NONE;
+  // raw linear-feed columns: visibilities and weights come as one (internal) pair
+  if ((vis_dtype == CIP_POL4I) != (wgt_dtype == CIP_POL4I))
+    return set_error(CIP_EINVAL, "raw linear-feed visibilities need their raw weights");
   if (nrow < 0 || nchan < 1 || nchan > 65535) return set_error(CIP_EINVAL, "need 1 <= nchan <= 65535, nrow >= 0");
   if (nrow >= ((int64_t)1 << 32)) return set_error(CIP_EINVAL, "nrow must be < 2^32");
   CIP_ALLOC(fx, double, "fx", nchan)
@@ -827,6 +834,7 @@ static int prepare(Workspace* ws, const double* uvw, int64_t nrow, const double*
   m.inv_nchan = 1.0 / (double)nchan;
   m.delta = nullptr;
   m.vis_row = nullptr;
+  m.flags4 = vis_dtype == CIP_POL4I ? flags4 : nullptr;
   m.nvis = nrow * nchan;
   if (ragged) {
     if (ragged->nvis < 0 || ragged->nvis >= ((int64_t)1 << 40)) return set_error(CIP_EINVAL, "bad visibility count");
@@ -888,7 +896,7 @@ static int prepare(Workspace* ws, const double* uvw, int64_t nrow, const double*
   // a larger key space would wrap and mis-sort the runs
   if ((double)out->g.ntx * (double)out->g.nty * (double)out->g.ntw >= 4294967295.0)
     return set_error(CIP_EINVAL, "grid tiles x w layers exceed the 32-bit tile key space");
-  if (packed && vis_dtype != CIP_C64)
+  if (packed && vis_dtype != CIP_C64 && vis_dtype != CIP_POL4I)
     return set_error(CIP_EINVAL, "single-precision accumulation needs complex64 visibilities");
   if (packed && out->g.support > 16)
     return set_error(CIP_EINVAL, "single-precision accumulation supports kernel supports <= 16");
@@ -1124,6 +1132,7 @@ static int grid_accumulate(const double* uvw, int64_t nrow, const double* freq, 
   g_last_error.clear();
   if (flags & ~(CIP_ACC_SINGLE | CIP_PSF)) return set_error(CIP_EINVAL, "unknown flags");
   if (!params || !grids) return set_error(CIP_EINVAL, "NULL params or grids");
+  if (!public_dtypes(vis_dtype, wgt_dtype)) return set_error(CIP_EINVAL, "vis dtype must be complex64 or complex128");
   if (flags & CIP_PSF) {
     vis = nullptr;
     vis_dtype = CIP_C64;
@@ -1170,11 +1179,13 @@ int cip_choose_params(int64_t npix_x, int64_t npix_y, double pixsize_x, double p
   return choose(npix_x, npix_y, pixsize_x, pixsize_y, epsilon, support, do_wstacking, wmin, wmax, out);
 }
 
-int cip_ms2dirty(const double* uvw, int64_t nrow, const double* freq, int64_t nchan, const void* vis, int vis_dtype,
-                 const void* wgt, int wgt_dtype, int64_t npix_x, int64_t npix_y, double pixsize_x,
-                 double pixsize_y, double epsilon, int support, int flags, void* hip_stream,
-                 double* dirty_out, double* sum_wgt_out, cip_gridder_params* params_out) {
-  g_last_error.clear();
+}  // extern "C"
+
+namespace cip {
+static int ms2dirty_impl(const double* uvw, int64_t nrow, const double* freq, int64_t nchan, const void* vis,
+                         int vis_dtype, const void* wgt, int wgt_dtype, const uint8_t* flags4, int64_t npix_x,
+                         int64_t npix_y, double pixsize_x, double pixsize_y, double epsilon, int support, int flags,
+                         void* hip_stream, double* dirty_out, double* sum_wgt_out, cip_gridder_params* params_out) {
   if (flags & ~(CIP_WSTACKING | CIP_ACC_SINGLE | CIP_PSF | CIP_NORMALISE | CIP_ASYNC | CIP_PIPELINE | CIP_REUSE_PLAN))
     return set_error(CIP_EINVAL, "unknown flags");
   if ((flags & CIP_REUSE_PLAN) && (flags & CIP_PIPELINE))
@@ -1184,7 +1195,7 @@ int cip_ms2dirty(const double* uvw, int64_t nrow, const double* freq, int64_t nc
   const bool packed = (flags & CIP_ACC_SINGLE) != 0;
   if (flags & CIP_PSF) {
     vis = nullptr;
-    vis_dtype = CIP_C64;
+    if (vis_dtype != CIP_POL4I) vis_dtype = CIP_C64;
   }
   if (!dirty_out) return set_error(CIP_EINVAL, "dirty_out is NULL");
   if (nrow > 0 && (!uvw || !freq || (!vis && !(flags & CIP_PSF)))) return set_error(CIP_EINVAL, "NULL input pointer");
@@ -1242,7 +1253,7 @@ int cip_ms2dirty(const double* uvw, int64_t nrow, const double* freq, int64_t nc
   ws->parity_scope = pipelined;
   int rc = prepare(ws, uvw, nrow, freq, nchan, vis, vis_dtype, wgt, wgt_dtype, npix_x, npix_y, pixsize_x, pixsize_y,
                    epsilon, support, do_wstacking, packed, nullptr, ps, &pp,
-                   (overlap_zero() && !pipelined) ? &grid : nullptr, nullptr, (flags & CIP_REUSE_PLAN) != 0);
+                   (overlap_zero() && !pipelined) ? &grid : nullptr, nullptr, (flags & CIP_REUSE_PLAN) != 0, flags4);
   ws->parity_scope = false;
   if (pipelined) {
     // s continues once the plan exists (also after a failed one: nothing then runs on it)
@@ -1291,6 +1302,33 @@ int cip_ms2dirty(const double* uvw, int64_t nrow, const double* freq, int64_t nc
   if (clean) ws->grid_clean = grid;
   g_prof.finish();
   return CIP_OK;
+}
+}  // namespace cip
+
+extern "C" {
+
+int cip_ms2dirty(const double* uvw, int64_t nrow, const double* freq, int64_t nchan, const void* vis, int vis_dtype,
+                 const void* wgt, int wgt_dtype, int64_t npix_x, int64_t npix_y, double pixsize_x,
+                 double pixsize_y, double epsilon, int support, int flags, void* hip_stream,
+                 double* dirty_out, double* sum_wgt_out, cip_gridder_params* params_out) {
+  g_last_error.clear();
+  if (vis_dtype != CIP_C64 && vis_dtype != CIP_C128 && !(flags & CIP_PSF))
+    return set_error(CIP_EINVAL, "vis dtype must be complex64 or complex128");
+  if (wgt_dtype != CIP_NONE && wgt_dtype != CIP_F32 && wgt_dtype != CIP_F64)
+    return set_error(CIP_EINVAL, "wgt dtype must be float32, float64 or none");
+  return ms2dirty_impl(uvw, nrow, freq, nchan, vis, vis_dtype, wgt, wgt_dtype, nullptr, npix_x, npix_y, pixsize_x,
+                       pixsize_y, epsilon, support, flags, hip_stream, dirty_out, sum_wgt_out, params_out);
+}
+
+int cip_ms2dirty_stokes_i(const double* uvw, int64_t nrow, const double* freq, int64_t nchan, const void* vis4,
+                          const uint8_t* flags4, const float* wgt4, int64_t npix_x, int64_t npix_y,
+                          double pixsize_x, double pixsize_y, double epsilon, int support, int flags,
+                          void* hip_stream, double* dirty_out, double* sum_wgt_out, cip_gridder_params* params_out) {
+  g_last_error.clear();
+  if (nrow > 0 && (!wgt4 || (!vis4 && !(flags & CIP_PSF)))) return set_error(CIP_EINVAL, "NULL vis4 or wgt4");
+  if (((uintptr_t)flags4 & 3u) != 0u) return set_error(CIP_EINVAL, "flags4 must be 4-byte aligned");
+  return ms2dirty_impl(uvw, nrow, freq, nchan, vis4, CIP_POL4I, wgt4, CIP_POL4I, flags4, npix_x, npix_y, pixsize_x,
+                       pixsize_y, epsilon, support, flags, hip_stream, dirty_out, sum_wgt_out, params_out);
 }
 
 int cip_grid_layout(const cip_gridder_params* params, int64_t npix_x, int64_t npix_y) {
@@ -1355,6 +1393,7 @@ int cip_grid_plane(const double* uvw, int64_t nrow, const double* freq, int64_t 
   if (flags & ~CIP_ACC_SINGLE) return set_error(CIP_EINVAL, "unknown flags");
   if (!params || !grid_out) return set_error(CIP_EINVAL, "NULL params or grid_out");
   if (plane < 0 || plane >= params->nplanes) return set_error(CIP_EINVAL, "plane out of range");
+  if (!public_dtypes(vis_dtype, wgt_dtype)) return set_error(CIP_EINVAL, "vis dtype must be complex64 or complex128");
   hipStream_t s = (hipStream_t)hip_stream;
   Workspace* ws = workspace();
   if (!ws) return set_error(CIP_EHIP, "no HIP device");

@@ -317,6 +317,7 @@ struct RowMap {
   double inv_nchan;         // 1 / nchan
   const int64_t* delta;     // ragged: per-row index offset; NULL = dense
   const uint32_t* vis_row;  // ragged: row of each visibility
+  const uint8_t* flags4;    // raw linear-feed input (WK_POL4I): (nvis, 4) flags, or NULL = none flagged
 };
 
 __device__ __forceinline__ int64_t vis_index(const RowMap& m, int64_t r, int64_t c) {
@@ -350,13 +351,41 @@ __device__ __forceinline__ void tile_origin(int64_t key, const GridGeometry& g, 
   *Y0 = ((t / g.ntx) % g.nty) * kTile;
 }
 
-// visibility / weight loads by dtype (CIP_C64 -> float2, CIP_C128 -> double2)
-enum { WK_NONE = 0, WK_F32 = 1, WK_F64 = 2 };
+// visibility / weight loads by dtype (CIP_C64 -> float2, CIP_C128 -> double2;
+// raw linear-feed columns -> Pol4 + WK_POL4I, Stokes I formed on load)
+enum { WK_NONE = 0, WK_F32 = 1, WK_F64 = 2, WK_POL4I = 3 };
+// internal vis / wgt dtype code of the raw linear-feed input (not in cip.h:
+// reached through cip_ms2dirty_stokes_i only)
+constexpr int CIP_POL4I = 0x100;
+
+// One visibility's linear-feed correlations (XX, XY, YX, YY) in complex64:
+// the raw (nrow, nchan, 4) MS column (cip_ms2dirty_stokes_i).
+struct Pol4 {
+  float2 c[4];
+};
+
+// Stokes I of the raw columns in the reference's numpy float32 arithmetic
+// (invert.py:86-116, :72-76; bit-identical to cip_stokes_i, cip_tiling.hip):
+// V = 0.5 (XX + YY) in complex64; effective weight = !(F_XX | F_YY) *
+// 4 / (1 / w_XX + 1 / w_YY) in float32 (a zero weight gives 4 / inf = 0).
+__device__ __forceinline__ float2 stokes_i_vis(float2 a, float2 d) {
+  return make_float2(0.5f * (a.x + d.x), 0.5f * (a.y + d.y));
+}
+__device__ __forceinline__ float stokes_i_weight(float wa, float wb, uint32_t flags_word) {
+  const bool fl = (flags_word & 0xff0000ffu) != 0u;  // bytes 0 (XX) and 3 (YY)
+  const float w = 4.0f / (1.0f / wa + 1.0f / wb);
+  return (fl ? 0.0f : 1.0f) * w;
+}
 
 template <int WK>
-__device__ __forceinline__ double load_weight(const void* __restrict__ w, int64_t i) {
+__device__ __forceinline__ double load_weight(const void* __restrict__ w, const RowMap& m, int64_t i) {
   if constexpr (WK == WK_F32) return (double)((const float*)w)[i];
   if constexpr (WK == WK_F64) return ((const double*)w)[i];
+  if constexpr (WK == WK_POL4I) {
+    const float* w4 = (const float*)w + 4 * i;
+    const uint32_t fw = m.flags4 ? ((const uint32_t*)m.flags4)[i] : 0u;
+    return (double)stokes_i_weight(w4[0], w4[3], fw);
+  }
   return 1.0;
 }
 
@@ -373,6 +402,16 @@ __device__ __forceinline__ void load_vis(const float2* __restrict__ p, int64_t i
 }
 __device__ __forceinline__ void load_vis(const double2* __restrict__ p, int64_t i, double& re, double& im) {
   const double2 v = p[i];
+  re = v.x;
+  im = v.y;
+}
+__device__ __forceinline__ void load_vis(const Pol4* __restrict__ p, int64_t i, double& re, double& im) {
+  if (p == nullptr) {
+    re = 1.0;
+    im = 0.0;
+    return;
+  }
+  const float2 v = stokes_i_vis(p[i].c[0], p[i].c[3]);
   re = v.x;
   im = v.y;
 }

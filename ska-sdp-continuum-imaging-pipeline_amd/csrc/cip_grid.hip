@@ -242,7 +242,7 @@ hipError_t launch_scatter(int support, int vis_dtype, int wgt_dtype, bool packed
                           const Chunk* chunks, int64_t chunk_begin, int64_t nchunks, const GridGeometry& g,
                           int64_t plane, double fixed_scale, double* grid, hipStream_t s) {
   if (nchunks <= 0) return hipSuccess;
-  if (packed && vis_dtype != CIP_C64) return hipErrorInvalidValue;
+  if (packed && vis_dtype != CIP_C64 && vis_dtype != CIP_POL4I) return hipErrorInvalidValue;
   const dim3 gd((unsigned)nchunks);
 #define CASE(WW)                                                                                             \
   case WW:                                                                                                   \

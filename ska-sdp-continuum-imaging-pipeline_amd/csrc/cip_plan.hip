@@ -259,7 +259,7 @@ __global__ __launch_bounds__(256, CIP_PLACE_WAVES) void plan_place_kernel(const 
       w = uvw[3 * rl + 2];
       f = fx[cl];
     }
-    const double wt = load_weight<WK>(wgt, il);
+    const double wt = load_weight<WK>(wgt, m, il);
     double vr, vi;
 #if CIP_PLACE_ABL == 1
     vr = 1.0; vi = 0.0;
@@ -351,7 +351,9 @@ hipError_t launch_prep_reduce(const RowMap& m, const void* vis, int vis_dtype, c
   plan_place_kernel<VT, WKV, false><<<gd, dim3(256), 0, s>>>(nullptr, nullptr, m, (const VT*)vis, wgt, g,    \
                                                             err_flag, nullptr, nullptr, nullptr, nullptr,   \
                                                             partial, nullptr)
-  if (vis_dtype == CIP_C64) {
+  if (vis_dtype == CIP_POL4I) {
+    REDUCE(Pol4, WK_POL4I);
+  } else if (vis_dtype == CIP_C64) {
     if (wgt_dtype == CIP_F32) REDUCE(float2, WK_F32);
     else if (wgt_dtype == CIP_F64) REDUCE(float2, WK_F64);
     else REDUCE(float2, WK_NONE);
@@ -372,7 +374,9 @@ hipError_t launch_plan_place(const double* uvw, const double* fx, const RowMap& 
 #define PLACE(VT, WKV)                                                                                           \
   plan_place_kernel<VT, WKV><<<gd, dim3(256), 0, s>>>(uvw, fx, m, (const VT*)vis, wgt, g, err_flag,       \
                                                       vis_class, blk_cnt, park_key, park_run, partial, hist0)
-  if (vis_dtype == CIP_C64) {
+  if (vis_dtype == CIP_POL4I) {
+    PLACE(Pol4, WK_POL4I);
+  } else if (vis_dtype == CIP_C64) {
     if (wgt_dtype == CIP_F32) PLACE(float2, WK_F32);
     else if (wgt_dtype == CIP_F64) PLACE(float2, WK_F64);
     else PLACE(float2, WK_NONE);

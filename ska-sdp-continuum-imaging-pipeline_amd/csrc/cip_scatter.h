@@ -56,18 +56,6 @@ __device__ __forceinline__ void locate_vis(int64_t q, const int64_t* s_voff, con
 }
 
 template <typename VisT, int WK>
-__device__ __forceinline__ void fetch_at(int64_t irow, int64_t c, int64_t idx, const double* __restrict__ uvw,
-                                         const double* __restrict__ fx, const VisT* __restrict__ vis,
-                                         const void* __restrict__ wgt, VisFetch& f) {
-  f.u = uvw[3 * irow];
-  f.v = uvw[3 * irow + 1];
-  f.w = uvw[3 * irow + 2];
-  f.fx = fx[c];
-  load_vis(vis, idx, f.vr, f.vi);
-  f.wt = load_weight<WK>(wgt, idx);
-}
-
-template <typename VisT, int WK>
 __device__ __forceinline__ void fetch_vis(int64_t q, const int64_t* s_voff, const uint64_t* s_run, int nst,
                                           const double* __restrict__ uvw, const double* __restrict__ fx,
                                           const VisT* __restrict__ vis, const void* __restrict__ wgt,
@@ -80,18 +68,27 @@ __device__ __forceinline__ void fetch_vis(int64_t q, const int64_t* s_voff, cons
   f.w = uvw[3 * irow + 2];
   f.fx = fx[c];
   load_vis(vis, idx, f.vr, f.vi);
-  f.wt = load_weight<WK>(wgt, idx);
+  f.wt = load_weight<WK>(wgt, m, idx);
 }
 
 // The same, as loaded (complex64 / float32 kept in their own types): the
 // position-ordered path converts only at use, so nothing waits for a load
 // next to it and the loads of position q + 256 stay in flight while q grids.
+// Raw linear-feed input keeps the two correlations, weights and the flag word
+// of Stokes I (formed at use).
 template <typename VisT, int WK>
 struct RawFetch {
   using WT = typename std::conditional<WK == WK_F64, double, float>::type;
   double u, v, w, fx;
   VisT vis;
   WT wt;
+};
+template <>
+struct RawFetch<Pol4, WK_POL4I> {
+  double u, v, w, fx;
+  float2 a, d;
+  float wa, wb;
+  uint32_t fw;
 };
 
 // Branch-free loads of MS visibility i (lanes with !ok load element 0; a PSF
@@ -101,7 +98,6 @@ __device__ __forceinline__ void fetch_raw(int64_t i, bool ok, const double* __re
                                           const double* __restrict__ fx, const VisT* __restrict__ vis_ld,
                                           bool unit_vis, const void* __restrict__ wgt, const RowMap& m,
                                           RawFetch<VisT, WK>& f) {
-  using WT = typename RawFetch<VisT, WK>::WT;
   const int64_t il = ok ? i : 0;
   int64_t r, c;
   vis_rowchan(m, il, &r, &c);
@@ -109,8 +105,19 @@ __device__ __forceinline__ void fetch_raw(int64_t i, bool ok, const double* __re
   f.v = uvw[3 * r + 1];
   f.w = uvw[3 * r + 2];
   f.fx = fx[c];
-  f.vis = vis_ld[unit_vis ? 0 : il];
-  if constexpr (WK != WK_NONE) f.wt = ((const WT*)wgt)[il];
+  if constexpr (WK == WK_POL4I) {
+    const float2* p = (const float2*)vis_ld;
+    f.a = p[unit_vis ? 0 : 4 * il];
+    f.d = p[unit_vis ? 0 : 4 * il + 3];
+    const float* w4 = (const float*)wgt + 4 * il;
+    f.wa = w4[0];
+    f.wb = w4[3];
+    f.fw = m.flags4 ? ((const uint32_t*)m.flags4)[il] : 0u;
+  } else {
+    using WT = typename RawFetch<VisT, WK>::WT;
+    f.vis = vis_ld[unit_vis ? 0 : il];
+    if constexpr (WK != WK_NONE) f.wt = ((const WT*)wgt)[il];
+  }
 }
 
 template <typename VisT, int WK>
@@ -120,9 +127,16 @@ __device__ __forceinline__ VisFetch from_raw(const RawFetch<VisT, WK>& r, bool u
   f.v = r.v;
   f.w = r.w;
   f.fx = r.fx;
-  f.vr = unit_vis ? 1.0 : (double)r.vis.x;
-  f.vi = unit_vis ? 0.0 : (double)r.vis.y;
-  f.wt = WK == WK_NONE ? 1.0 : (double)r.wt;
+  if constexpr (WK == WK_POL4I) {
+    const float2 s = stokes_i_vis(r.a, r.d);
+    f.vr = unit_vis ? 1.0 : (double)s.x;
+    f.vi = unit_vis ? 0.0 : (double)s.y;
+    f.wt = (double)stokes_i_weight(r.wa, r.wb, r.fw);
+  } else {
+    f.vr = unit_vis ? 1.0 : (double)r.vis.x;
+    f.vi = unit_vis ? 0.0 : (double)r.vis.y;
+    f.wt = WK == WK_NONE ? 1.0 : (double)r.wt;
+  }
   return f;
 }
 
@@ -342,9 +356,9 @@ inline hipError_t scatter_dispatch_ws(bool ws, bool pack, dim3 grid_dim, hipStre
     }                        \
   }
   // the packed single-precision class exists for complex64 input only (the
-  // reference's configuration)
+  // reference's configuration; raw linear-feed columns are complex64 too)
   bool done = false;
-  if constexpr (std::is_same<VisT, float2>::value) {
+  if constexpr (std::is_same<VisT, float2>::value || std::is_same<VisT, Pol4>::value) {
     if (pack) {
       if (perm) {
         LAUNCH_WS(true, true)
@@ -375,6 +389,7 @@ hipError_t launch_scatter_w(int vis_dtype, int wgt_dtype, bool pack, dim3 gd, hi
   const bool ws = g.do_wstacking != 0;
 #define ARGS \
   ws, pack, gd, s, uvw, fx, vis, wgt, m, runs, run_goff, tile_run_off, perm, chunks, cb, g, plane, fs, grid
+  if (vis_dtype == CIP_POL4I) return scatter_dispatch_ws<W, Pol4, WK_POL4I>(ARGS);
   if (vis_dtype == CIP_C64) {
     if (wgt_dtype == CIP_F32) return scatter_dispatch_ws<W, float2, WK_F32>(ARGS);
     if (wgt_dtype == CIP_F64) return scatter_dispatch_ws<W, float2, WK_F64>(ARGS);

@@ -220,6 +220,7 @@ hipError_t launch_scatter_large_w(int vis_dtype, int wgt_dtype, dim3 gd, hipStre
                                   double* grid) {
   if (g.support != W) return hipErrorInvalidValue;
 #define ARGS gd, s, uvw, fx, vis, wgt, m, runs, run_goff, perm, chunks, cb, g, plane, fs, grid
+  if (vis_dtype == CIP_POL4I) return launch_large_vt<W, Pol4, WK_POL4I>(ARGS);
   if (vis_dtype == CIP_C64) {
     if (wgt_dtype == CIP_F32) return launch_large_vt<W, float2, WK_F32>(ARGS);
     if (wgt_dtype == CIP_F64) return launch_large_vt<W, float2, WK_F64>(ARGS);

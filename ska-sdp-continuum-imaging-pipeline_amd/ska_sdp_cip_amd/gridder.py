@@ -181,6 +181,90 @@ def _ms2dirty_call(uvw, freq, vis, wgt, vis_codes, wgt_codes, npix_x, npix_y, pi
         sum_weights.data_ptr() if sum_weights is not None else None, params)
 
 
+def device_ms2dirty_stokes_i(
+    uvw: "torch.Tensor",
+    freq: "torch.Tensor",
+    vis4: Optional["torch.Tensor"],
+    flags4: Optional["torch.Tensor"],
+    wgt4: "torch.Tensor",
+    npix_x: int,
+    npix_y: int,
+    pixsize_x: float,
+    pixsize_y: float,
+    *,
+    epsilon: float = 1e-4,
+    support: Optional[int] = None,
+    do_wstacking: bool = False,
+    out: Optional["torch.Tensor"] = None,
+    sum_weights: Optional["torch.Tensor"] = None,
+    single_precision_accumulation: bool = False,
+    psf: bool = False,
+    normalise: bool = False,
+    synchronize: bool = True,
+    resident_inputs: bool = False,
+    reuse_plan: bool = False,
+) -> tuple["torch.Tensor", _lib.GridderParams]:
+    """
+    device_ms2dirty on the raw linear-feed columns (cip_ms2dirty_stokes_i):
+    vis4 (nrow, nchan, 4) complex64 XX, XY, YX, YY, flags4 (nrow, nchan, 4)
+    bool/uint8 or None, wgt4 (nrow, nchan, 4) float32. Stokes I and the
+    effective weights (reference invert.py:78-116) are formed inside the
+    planner and scatter as each visibility is loaded - no intermediate
+    columns; the image is bit-identical to device_stokes_i + device_ms2dirty.
+    Keyword arguments as device_ms2dirty.
+    """
+    if resident_inputs and synchronize:
+        raise ValueError("resident_inputs=True needs synchronize=False")
+    if reuse_plan and resident_inputs:
+        raise ValueError("reuse_plan=True cannot be combined with resident_inputs=True")
+    nrow, nchan = uvw.shape[0], freq.shape[0]
+    shape = (nrow, nchan, 4)
+    if psf:
+        vis4 = None
+    elif vis4 is None or vis4.dtype != torch.complex64 or tuple(vis4.shape) != shape:
+        raise ValueError(f"vis4 must be complex64 of shape {shape}")
+    if wgt4 is None or wgt4.dtype != torch.float32 or tuple(wgt4.shape) != shape:
+        raise ValueError(f"wgt4 must be float32 of shape {shape}")
+    if flags4 is not None:
+        if tuple(flags4.shape) != shape:
+            raise ValueError(f"flags4 must have shape {shape}")
+        if flags4.dtype == torch.bool:
+            flags4 = flags4.view(torch.uint8)
+        elif flags4.dtype != torch.uint8:
+            raise ValueError("flags4 must be bool or uint8")
+    if tuple(uvw.shape) != (nrow, 3) or uvw.dtype != torch.float64 or freq.dtype != torch.float64:
+        raise ValueError("uvw must be float64 (nrow, 3) and freq float64")
+    for t in (uvw, freq, wgt4) + tuple(x for x in (vis4, flags4) if x is not None):
+        _check_device_tensor(t, uvw.device, "device_ms2dirty_stokes_i inputs")
+    if out is None:
+        out = torch.empty((npix_x, npix_y), dtype=torch.float64, device=uvw.device)
+    elif out.dtype != torch.float64 or tuple(out.shape) != (int(npix_x), int(npix_y)):
+        raise ValueError(f"out must be float64 of shape ({npix_x}, {npix_y})")
+    else:
+        _check_device_tensor(out, uvw.device, "out")
+    if sum_weights is not None:
+        if sum_weights.dtype != torch.float64 or sum_weights.numel() != 1:
+            raise ValueError("sum_weights must be a float64 tensor of one element")
+        _check_device_tensor(sum_weights, uvw.device, "sum_weights")
+    params = _lib.GridderParams()
+    with torch.cuda.device(uvw.device):
+        stream = torch.cuda.current_stream(uvw.device).cuda_stream
+        rc = _lib.lib().cip_ms2dirty_stokes_i(
+            uvw.data_ptr(), nrow, freq.data_ptr(), nchan, None if vis4 is None else vis4.data_ptr(),
+            None if flags4 is None else flags4.data_ptr(), wgt4.data_ptr(), int(npix_x), int(npix_y),
+            float(pixsize_x), float(pixsize_y), float(epsilon), int(support or 0),
+            (_lib.CIP_WSTACKING if do_wstacking else 0)
+            | (_lib.CIP_ACC_SINGLE if single_precision_accumulation else 0)
+            | (_lib.CIP_PSF if psf else 0)
+            | (_lib.CIP_NORMALISE if normalise else 0)
+            | (0 if synchronize else _lib.CIP_ASYNC)
+            | (_lib.CIP_PIPELINE if resident_inputs else 0)
+            | (_lib.CIP_REUSE_PLAN if reuse_plan else 0),
+            stream, out.data_ptr(), sum_weights.data_ptr() if sum_weights is not None else None, params)
+    _lib.check(rc)
+    return out, params
+
+
 def device_stokes(vis4: "torch.Tensor", flags4: "torch.Tensor", wgt4: "torch.Tensor", stokes: str = "I"):
     """
     Stokes parameter `stokes` ("I", "Q", "U", "V") on the device (cip_stokes;

@@ -22,7 +22,7 @@ from typing import Any, Iterable, Optional
 import numpy as np
 from numpy.typing import NDArray
 
-from .gridder import device_ms2dirty, device_stokes_i, ms2dirty
+from .gridder import device_ms2dirty, device_ms2dirty_stokes_i, device_stokes_i, ms2dirty
 
 # Reference call arguments (invert.py:170-183)
 EPSILON = 1e-4
@@ -107,9 +107,10 @@ def invert_measurement_set(
     :119-149): (1 / total_weight) * image, float32 (num_pixels, num_pixels).
     `nthreads` is accepted for signature compatibility (the GPU ignores it).
     `stokes_on_device=True` ships the raw (nrow, nchan, 4) columns to the GPU
-    and forms Stokes I there (`device_invert`) instead of in
-    numpy as the reference does; the total weight is then summed in fp64 on
-    the device (the reference sums float32 in numpy).
+    and forms Stokes I there, inside the gridder (`device_invert`, fused;
+    SURVEY.md 8(f)1) instead of in numpy as the reference does; the total
+    weight is then summed in fp64 on the device (the reference sums float32 in
+    numpy). Device-resident raw columns go to `device_invert` directly.
     """
     if stokes_on_device:
         import torch  # pylint: disable=import-outside-toplevel
@@ -175,21 +176,28 @@ def device_invert(
     epsilon: float = EPSILON,
     do_wstacking: bool = DO_WSTACKING,
     support: Optional[int] = None,
+    fused: bool = True,
 ):
     """
-    Whole invert on device-resident raw columns: Stokes I and
-    effective weights by cip_stokes_i, the dirty image by cip_ms2dirty, the
-    total weight summed on the device, and the normalised fp64 image returned
-    as a device tensor. Arguments: vis4 (nrow, nchan, 4) complex64, flags4
-    bool/uint8, wgt4 float32, uvw (nrow, 3) f64, freq (nchan,) f64.
+    Whole invert on device-resident raw columns, the total
+    weight summed on the device, and the normalised fp64 image returned as a
+    device tensor. `fused=True` (default): Stokes I and the effective weights
+    are formed inside the gridder's planner and scatter as they load each
+    visibility (cip_ms2dirty_stokes_i, no intermediate columns);
+    `fused=False`: cip_stokes_i writes (vis_i, eff_w) first and cip_ms2dirty
+    grids them (same image bit for bit). Arguments: vis4 (nrow, nchan, 4)
+    complex64, flags4 bool/uint8, wgt4 float32, uvw (nrow, 3) f64, freq
+    (nchan,) f64.
     """
-    import torch  # pylint: disable=import-outside-toplevel
-
-    vis_i, eff = device_stokes_i(vis4, flags4, wgt4)
     pix = pixel_size_lm(pixel_size_asec)
-    sumw = torch.zeros(1, dtype=torch.float64, device=vis_i.device)
+    if fused:
+        dirty, _ = device_ms2dirty_stokes_i(uvw, freq, vis4, flags4, wgt4, num_pixels, num_pixels, pix, pix,
+                                            epsilon=epsilon, support=support, do_wstacking=do_wstacking,
+                                            normalise=True)
+        return dirty
+    vis_i, eff = device_stokes_i(vis4, flags4, wgt4)
     dirty, _ = device_ms2dirty(uvw, freq, vis_i, eff, num_pixels, num_pixels, pix, pix, epsilon=epsilon,
-                              support=support, do_wstacking=do_wstacking, sum_weights=sumw, normalise=True)
+                              support=support, do_wstacking=do_wstacking, normalise=True)
     return dirty
 
 
