@@ -179,6 +179,16 @@ int cip_grid_ms(const double* uvw, int64_t nrow, const double* freq,
                 double pixsize_y, int64_t npix_x, int64_t npix_y, int flags,
                 void* hip_stream, double* grids, double* sum_wgt);
 
+/* cip_grid_ms on the raw linear-feed columns (Stokes I formed on load, as
+ * cip_ms2dirty_stokes_i): vis4 / flags4 / wgt4 (nrow, nchan, 4) complex64 /
+ * uint8 (NULL: none flagged; 4-byte aligned) / float32 device pointers. */
+int cip_grid_ms_stokes_i(const double* uvw, int64_t nrow, const double* freq,
+                         int64_t nchan, const void* vis4, const uint8_t* flags4,
+                         const float* wgt4, const cip_gridder_params* params,
+                         double pixsize_x, double pixsize_y, int64_t npix_x,
+                         int64_t npix_y, int flags, void* hip_stream,
+                         double* grids, double* sum_wgt);
+
 /* Tile-sorted chunk (the uvw_tiling Tile layout, reference
  * uvw_tiling/tile.py:14-124, the reorder output): nslices row slices with
  * uvw (nslices,3) f64 metres and channel ranges [chan_start, chan_stop)

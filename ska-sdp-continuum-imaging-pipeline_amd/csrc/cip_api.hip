@@ -1128,14 +1128,14 @@ static int finish_dirty(Workspace* ws, const DirtyStage& st, const cip_gridder_p
 static int grid_accumulate(const double* uvw, int64_t nrow, const double* freq, int64_t nchan, const void* vis,
                            int vis_dtype, const void* wgt, int wgt_dtype, const cip_gridder_params* params,
                            double pixsize_x, double pixsize_y, int64_t npix_x, int64_t npix_y, int flags,
-                           void* hip_stream, double* grids, double* sum_wgt, const RaggedRows* ragged) {
+                           void* hip_stream, double* grids, double* sum_wgt, const RaggedRows* ragged,
+                           const uint8_t* flags4 = nullptr) {
   g_last_error.clear();
   if (flags & ~(CIP_ACC_SINGLE | CIP_PSF)) return set_error(CIP_EINVAL, "unknown flags");
   if (!params || !grids) return set_error(CIP_EINVAL, "NULL params or grids");
-  if (!public_dtypes(vis_dtype, wgt_dtype)) return set_error(CIP_EINVAL, "vis dtype must be complex64 or complex128");
   if (flags & CIP_PSF) {
     vis = nullptr;
-    vis_dtype = CIP_C64;
+    if (vis_dtype != CIP_POL4I) vis_dtype = CIP_C64;
   }
   if (nrow > 0 && (!uvw || !freq || (!vis && !(flags & CIP_PSF)))) return set_error(CIP_EINVAL, "NULL input pointer");
   hipStream_t s = (hipStream_t)hip_stream;
@@ -1147,7 +1147,7 @@ static int grid_accumulate(const double* uvw, int64_t nrow, const double* freq, 
   Prepared pp;
   int rc = prepare(ws, uvw, nrow, freq, nchan, vis, vis_dtype, wgt, wgt_dtype, 2, 2, pixsize_x, pixsize_y, 0.0,
                    params->support, params->do_wstacking, (flags & CIP_ACC_SINGLE) != 0, params, s, &pp, nullptr,
-                   ragged);
+                   ragged, false, flags4);
   if (rc != CIP_OK) return rc;
   const GridGeometry& g = pp.g;
   const bool transposed = grid_is_transposed(g, npix_x, npix_y);
@@ -1341,8 +1341,20 @@ int cip_grid_ms(const double* uvw, int64_t nrow, const double* freq, int64_t nch
                 const void* wgt, int wgt_dtype, const cip_gridder_params* params, double pixsize_x, double pixsize_y,
                 int64_t npix_x, int64_t npix_y, int flags, void* hip_stream, double* grids, double* sum_wgt) {
   if (nrow < 0) return set_error(CIP_EINVAL, "nrow must be >= 0");
+  if (!public_dtypes(vis_dtype, wgt_dtype)) return set_error(CIP_EINVAL, "vis dtype must be complex64 or complex128");
   return grid_accumulate(uvw, nrow, freq, nchan, vis, vis_dtype, wgt, wgt_dtype, params, pixsize_x, pixsize_y,
                          npix_x, npix_y, flags, hip_stream, grids, sum_wgt, nullptr);
+}
+
+int cip_grid_ms_stokes_i(const double* uvw, int64_t nrow, const double* freq, int64_t nchan, const void* vis4,
+                         const uint8_t* flags4, const float* wgt4, const cip_gridder_params* params,
+                         double pixsize_x, double pixsize_y, int64_t npix_x, int64_t npix_y, int flags,
+                         void* hip_stream, double* grids, double* sum_wgt) {
+  if (nrow < 0) return set_error(CIP_EINVAL, "nrow must be >= 0");
+  if (nrow > 0 && (!wgt4 || (!vis4 && !(flags & CIP_PSF)))) return set_error(CIP_EINVAL, "NULL vis4 or wgt4");
+  if (((uintptr_t)flags4 & 3u) != 0u) return set_error(CIP_EINVAL, "flags4 must be 4-byte aligned");
+  return grid_accumulate(uvw, nrow, freq, nchan, vis4, CIP_POL4I, wgt4, CIP_POL4I, params, pixsize_x, pixsize_y,
+                         npix_x, npix_y, flags, hip_stream, grids, sum_wgt, nullptr, flags4);
 }
 
 int cip_grid_tiles(const double* slice_uvw, const int32_t* chan_start, const int32_t* chan_stop, int64_t nslices,
@@ -1352,6 +1364,7 @@ int cip_grid_tiles(const double* slice_uvw, const int32_t* chan_start, const int
   if (nslices < 0 || nvis < 0) return set_error(CIP_EINVAL, "nslices and nvis must be >= 0");
   if (nslices > 0 && (!chan_start || !chan_stop)) return set_error(CIP_EINVAL, "NULL channel ranges");
   if (nslices >= ((int64_t)1 << 32) - 1) return set_error(CIP_EINVAL, "nslices must be < 2^32 - 1");
+  if (!public_dtypes(vis_dtype, wgt_dtype)) return set_error(CIP_EINVAL, "vis dtype must be complex64 or complex128");
   const RaggedRows rr{chan_start, chan_stop, nvis};
   return grid_accumulate(slice_uvw, nslices, freq, nchan, vis, vis_dtype, wgt, wgt_dtype, params, pixsize_x,
                          pixsize_y, npix_x, npix_y, flags, hip_stream, grids, sum_wgt, &rr);

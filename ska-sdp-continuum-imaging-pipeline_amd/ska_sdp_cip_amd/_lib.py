@@ -44,6 +44,7 @@ EXPORTED_SYMBOLS = (
     "cip_grid_plane",
     "cip_grid_layout",
     "cip_grid_ms",
+    "cip_grid_ms_stokes_i",
     "cip_grid_tiles",
     "cip_grid_to_dirty",
     "cip_strip_rows",
@@ -120,6 +121,8 @@ def lib() -> ctypes.CDLL:
     so.cip_grid_layout.argtypes = [ctypes.POINTER(GridderParams), _i64, _i64]
     so.cip_grid_ms.argtypes = [_vp, _i64, _vp, _i64, _vp, _i32, _vp, _i32, ctypes.POINTER(GridderParams),
                                _f64, _f64, _i64, _i64, _i32, _vp, _vp, _vp]
+    so.cip_grid_ms_stokes_i.argtypes = [_vp, _i64, _vp, _i64, _vp, _vp, _vp, ctypes.POINTER(GridderParams),
+                                        _f64, _f64, _i64, _i64, _i32, _vp, _vp, _vp]
     so.cip_grid_tiles.argtypes = [_vp, _vp, _vp, _i64, _vp, _i64, _vp, _i64, _i32, _vp, _i32,
                                   ctypes.POINTER(GridderParams), _f64, _f64, _i64, _i64, _i32, _vp, _vp, _vp]
     so.cip_grid_to_dirty.argtypes = [_vp, ctypes.POINTER(GridderParams), _i64, _i64, _f64, _f64, _vp, _vp]
@@ -135,7 +138,7 @@ def lib() -> ctypes.CDLL:
     so.cip_profile_last.argtypes = [_vp, _vp]
     so.cip_last_error.restype = ctypes.c_char_p
     so.cip_build_info.restype = ctypes.c_char_p
-    for name in ("cip_choose_params", "cip_ms2dirty", "cip_ms2dirty_stokes_i", "cip_grid_plane", "cip_grid_layout", "cip_grid_ms",
+    for name in ("cip_choose_params", "cip_ms2dirty", "cip_ms2dirty_stokes_i", "cip_grid_plane", "cip_grid_layout", "cip_grid_ms", "cip_grid_ms_stokes_i",
                  "cip_grid_tiles", "cip_grid_to_dirty", "cip_strip_rows", "cip_strip_cols", "cip_tile_runs",
                  "cip_stokes_i", "cip_stokes", "cip_facet_rephase", "cip_allreduce_grid", "cip_release_collectives",
                  "cip_release_workspace", "cip_profile_enable", "cip_profile_last"):

@@ -120,6 +120,28 @@ class GridAccumulator:
                 self.planes.data_ptr(), self.sum_weights.data_ptr()))
         self.num_visibilities += nrow * nchan
 
+    def add_ms_stokes_i(self, uvw, freq, vis4, flags4, wgt4) -> None:
+        """Add MS rows given as raw linear-feed columns (cip_grid_ms_stokes_i:
+        Stokes I and effective weights formed on load, reference
+        invert.py:78-116): vis4 (nrow, nchan, 4) complex64, flags4 uint8/bool
+        or None, wgt4 float32."""
+        self._check(uvw, freq, vis4, flags4, wgt4)
+        nrow, nchan = uvw.shape[0], freq.shape[0]
+        shape = (nrow, nchan, 4)
+        if vis4.dtype != torch.complex64 or wgt4.dtype != torch.float32 or tuple(vis4.shape) != shape or \
+                tuple(wgt4.shape) != shape or (flags4 is not None and tuple(flags4.shape) != shape):
+            raise ValueError(f"vis4 complex64, wgt4 float32 and flags4 must have shape {shape}")
+        if flags4 is not None and flags4.dtype == torch.bool:
+            flags4 = flags4.view(torch.uint8)
+        with torch.cuda.device(self.device):
+            stream = torch.cuda.current_stream(self.device).cuda_stream
+            _lib.check(_lib.lib().cip_grid_ms_stokes_i(
+                uvw.data_ptr(), nrow, freq.data_ptr(), nchan, vis4.data_ptr(),
+                None if flags4 is None else flags4.data_ptr(), wgt4.data_ptr(), self.params, self.pixsize_x,
+                self.pixsize_y, self.npix_x, self.npix_y, self.flags, stream, self.planes.data_ptr(),
+                self.sum_weights.data_ptr()))
+        self.num_visibilities += nrow * nchan
+
     def add_tile(self, slice_uvw, chan_start, chan_stop, freq, vis, wgt=None) -> None:
         """Add one tile chunk (Tile layout): slice_uvw (ns, 3) f64, chan_start /
         chan_stop (ns) int32, freq (nchan) f64, vis (nvis) complex, wgt (nvis)

@@ -244,6 +244,33 @@ class InMemoryMeasurementSet(_BoundedReader):
         data = self._weights[self._rows()]
         return np.repeat(data[:, None, :], self.num_channels, axis=1)
 
+    def read_into(self, out: dict, row0: int = 0, row1: Optional[int] = None) -> None:
+        """
+        Copy rows [row0, row1) of this (bounded) set's columns straight into
+        caller-owned arrays - e.g. pinned staging buffers - instead of
+        returning fresh ones (the streaming path; a casacore
+        reader does the same with `getcolnp(column, out, startrow, nrow)`).
+        `out` holds any of "uvw" (n, 3) float64, "vis4" (n, nchan, 4)
+        complex64, "flags4" (n, nchan, 4) uint8 or bool, "wgt4" (n, nchan, 4)
+        float32 with n = row1 - row0 rows. Called on disjoint row ranges from
+        several threads at once (numpy releases the GIL for the copies).
+        """
+        row1 = self.num_data_rows if row1 is None else row1
+        a, b = self.row_start + row0, self.row_start + row1
+        ch = self._chans()
+        if "uvw" in out:
+            np.copyto(out["uvw"], self._uvw[a:b])
+        if "vis4" in out:
+            np.copyto(out["vis4"], self._vis[a:b, ch])
+        if "flags4" in out:
+            dst = out["flags4"]
+            np.copyto(dst.view(np.bool_) if dst.dtype == np.uint8 else dst, self._flags[a:b, ch])
+        if "wgt4" in out:
+            if self._weights.ndim == 3:
+                np.copyto(out["wgt4"], self._weights[a:b, ch])
+            else:
+                np.copyto(out["wgt4"], self._weights[a:b, None, :])
+
 
 class MeasurementSetReader(_BoundedReader):
     """

@@ -8,13 +8,13 @@ Two sources, one pipeline:
   reorder output of reference uvw_tiling/reorder.py:19-111, optional
   `weights` key), gridded slice-wise by `cip_grid_tiles`;
 * `invert_measurement_set_streamed` - row blocks of a measurement set reader
-  (raw (rows, chans, 4) columns; Stokes I formed on the device by
-  `cip_stokes_i`), gridded by `cip_grid_ms`.
+  (raw (rows, chans, 4) columns read straight into pinned slots by the
+  reader's `read_into`; Stokes I formed inside the gridder,
+  `cip_grid_ms_stokes_i`), `RowStreamer`.
 
 Pipeline: while chunk k is gridded on the compute stream onto the resident
-planes of a `GridAccumulator`, a worker thread reads chunk k + 1 (disk /
-reader), copies it into its pinned staging slot and sends it to HBM on a
-dedicated copy stream (two slots). One FFT at the end.
+planes of a `GridAccumulator`, later chunks are read into pinned staging
+slots and sent to HBM on a dedicated copy stream. One FFT at the end.
 """
 
 from __future__ import annotations
@@ -26,7 +26,7 @@ from typing import Callable, Iterable, Optional, Sequence
 import numpy as np
 
 from .accumulate import GridAccumulator, merge_w_ranges, w_range_rows, w_range_slices
-from .gridder import _require_gpu, device_stokes_i
+from .gridder import _require_gpu
 from .invert import EPSILON, pixel_size_lm
 from .uvw_tiling.tile import Tile
 
@@ -212,6 +212,88 @@ def invert_tile_files(
     return image
 
 
+class RowStreamer:
+    """
+    Raw MS rows host -> HBM at link speed: the reader fills
+    pinned staging slots directly (`read_into`, several threads on disjoint
+    row blocks - no fresh arrays, no second host copy), a copy stream moves
+    each filled slot to a device slot, and the caller grids it from there.
+
+    Three pinned slots and two device slots: while chunk k grids on the
+    compute stream (synchronous gridder call), chunk k + 1's H2D copy is in
+    flight and chunks k + 2, k + 3 are being filled; a pinned slot is refilled
+    once its previous H2D copy completed (event waited on by the filling
+    thread), a device slot is rewritten only after the gridding call that read
+    it returned. The slots persist across calls (pinned allocation is slow).
+    """
+
+    _cache = {}
+    COLUMNS = (("uvw", np.float64, (3,)), ("vis4", np.complex64, ("c", 4)), ("flags4", np.uint8, ("c", 4)),
+               ("wgt4", np.float32, ("c", 4)))
+
+    def __init__(self, device, rows: int, nchan: int, fill_threads: int = 16, nhost: int = 3, ndev: int = 2):
+        self.device = torch.device(device)
+        self.rows, self.nchan = int(rows), int(nchan)
+        self.copy_stream = torch.cuda.Stream(device=self.device)
+        self.host, self.dev = [], []
+        for _ in range(nhost):
+            self.host.append({n: torch.empty(self._shape(sh), dtype=_torch_dtype(dt), pin_memory=True)
+                              for n, dt, sh in self.COLUMNS})
+        for _ in range(ndev):
+            self.dev.append({n: torch.empty(self._shape(sh), dtype=_torch_dtype(dt), device=self.device)
+                             for n, dt, sh in self.COLUMNS})
+        self.h2d_done = [None] * nhost
+        self.pool = cf.ThreadPoolExecutor(max_workers=max(1, fill_threads))
+        self.fill_threads = max(1, fill_threads)
+        self.bytes_staged = 0
+
+    def _shape(self, sh):
+        return (self.rows,) + tuple(self.nchan if d == "c" else d for d in sh)
+
+    @classmethod
+    def get(cls, device, rows: int, nchan: int) -> "RowStreamer":
+        key = (str(torch.device(device)), int(rows), int(nchan))
+        st = cls._cache.get(key)
+        if st is None:
+            cls._cache.clear()  # one set of slots at a time
+            st = cls._cache[key] = cls(device, rows, nchan)
+        return st
+
+    def fill(self, slot: int, reader, row0: int, row1: int) -> int:
+        """Fill pinned slot `slot` with reader rows [row0, row1) (blocking;
+        parallel over row blocks). Waits for the slot's previous H2D copy."""
+        ev = self.h2d_done[slot]
+        if ev is not None:
+            ev.synchronize()
+        n = row1 - row0
+        views = {name: t.numpy()[:n] for name, t in self.host[slot].items()}
+        step = max(256, -(-n // self.fill_threads))
+        jobs = [self.pool.submit(reader.read_into, {k: v[a:min(n, a + step)] for k, v in views.items()},
+                                 row0 + a, row0 + min(n, a + step)) for a in range(0, n, step)]
+        for j in jobs:
+            j.result()
+        return n
+
+    def send(self, hslot: int, dslot: int, n: int) -> dict:
+        """H2D copy of the first n rows of pinned slot hslot into device slot
+        dslot on the copy stream; returns the device views (valid for work on
+        the current stream once `wait` is called)."""
+        out = {}
+        with torch.cuda.stream(self.copy_stream):
+            for name, h in self.host[hslot].items():
+                d = self.dev[dslot][name][:n]
+                d.copy_(h[:n], non_blocking=True)
+                out[name] = d
+                self.bytes_staged += h[:n].numel() * h.element_size()
+            ev = torch.cuda.Event()
+            ev.record(self.copy_stream)
+        self.h2d_done[hslot] = ev
+        return out
+
+    def wait(self, hslot: int) -> None:
+        torch.cuda.current_stream(self.device).wait_event(self.h2d_done[hslot])
+
+
 def invert_measurement_set_streamed(
     ms_reader,
     num_pixels: int,
@@ -226,40 +308,68 @@ def invert_measurement_set_streamed(
     """
     `invert_measurement_set` (reference invert.py:119-149) for measurement
     sets larger than one transfer: the raw (rows, chans, 4) columns are read
-    `rows_per_chunk` rows at a time, staged through pinned memory to HBM on a
-    copy stream, turned into Stokes I + effective weights on the device and
-    gridded onto one set of resident planes. Returns the normalised image as
-    float32 numpy (N, N), like the reference.
+    `rows_per_chunk` rows at a time straight into pinned staging slots (the
+    reader's `read_into`; readers without it are copied from their returned
+    arrays), sent to HBM on a copy stream and gridded onto one set of resident
+    planes with Stokes I formed inside the gridder (`add_ms_stokes_i`).
+    Returns the normalised image as float32 numpy (N, N), like the reference.
     """
     _require_gpu()
     dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
     freq = np.asarray(ms_reader.channel_frequencies(), dtype=np.float64)
     nrow = ms_reader.num_data_rows
-    nchunks = max(1, -(-nrow // max(int(rows_per_chunk), 1)))
+    nchan = freq.size
     w_range = w_range_rows(ms_reader.uvw(), freq) if do_wstacking else (0.0, 0.0)
     pix = pixel_size_lm(pixel_size_asec)
     acc = GridAccumulator(num_pixels, num_pixels, pix, pix, epsilon=epsilon, support=support,
                           do_wstacking=do_wstacking, w_range=w_range, device=dev)
     freq_d = torch.from_numpy(freq).to(dev)
-    chunks = list(ms_reader.partition(nchunks, 1)) if nrow > 0 else []
-
-    def loader(chunk):
-        def load():
-            return {"uvw": np.asarray(chunk.uvw(), dtype=np.float64),
-                    "vis4": np.asarray(chunk.visibilities(), dtype=np.complex64),
-                    "flags4": np.asarray(chunk.flags(), dtype=np.bool_),
-                    "wgt4": np.asarray(chunk.weights(), dtype=np.float32)}
-        return load
-
-    def consume(c):
-        vis_i, eff = device_stokes_i(c["vis4"], c["flags4"], c["wgt4"])
-        acc.add_ms(c["uvw"], freq_d, vis_i, eff)
-
+    rpc = max(1, min(int(rows_per_chunk), max(nrow, 1)))
+    bounds = [(a, min(nrow, a + rpc)) for a in range(0, nrow, rpc)]
+    reader = ms_reader if hasattr(ms_reader, "read_into") else _CopyingReader(ms_reader)
     with torch.cuda.device(dev):
-        _pipeline([loader(ch) for ch in chunks], ChunkStager(dev), consume)
+        if bounds:
+            st = RowStreamer.get(dev, rpc, nchan)
+            H, D = len(st.host), len(st.dev)
+            fills = {}
+
+            def submit_fill(k):
+                if k < len(bounds) and k not in fills:
+                    fills[k] = _FILL_POOL.submit(st.fill, k % H, reader, *bounds[k])
+
+            for k in range(min(H, len(bounds))):
+                submit_fill(k)
+            staged = {0: st.send(0, 0, fills.pop(0).result())}
+            for k in range(len(bounds)):
+                if k + 1 < len(bounds):
+                    # the device slot of chunk k + 1 was last read by chunk k - 1's (returned) call
+                    staged[k + 1] = st.send((k + 1) % H, (k + 1) % D, fills.pop(k + 1).result())
+                submit_fill(k + H)  # into chunk k's pinned slot, once its H2D copy is done
+                c = staged.pop(k)
+                st.wait(k % H)
+                acc.add_ms_stokes_i(c["uvw"], freq_d, c["vis4"], c["flags4"], c["wgt4"])
         dirty, sumw = acc.dirty()
         image = (dirty / sumw).to(torch.float32).cpu().numpy()
     return image
 
 
-__all__ = ["ChunkStager", "invert_measurement_set_streamed", "invert_tile_files"]
+class _CopyingReader:
+    """read_into for readers that only return fresh arrays (the reference's
+    reader protocol, measurement_set.py:281-358): one extra host copy."""
+
+    def __init__(self, reader):
+        self.reader = reader
+
+    def read_into(self, out: dict, row0: int, row1: int) -> None:
+        r = self.reader.partition(1, 1)[0] if hasattr(self.reader, "partition") else self.reader
+        r.set_row_bounds(self.reader.row_start + row0, self.reader.row_start + row1)
+        cols = {"uvw": r.uvw, "vis4": r.visibilities, "flags4": r.flags, "wgt4": r.weights}
+        for name, dst in out.items():
+            src = cols[name]()
+            np.copyto(dst.view(np.bool_) if name == "flags4" and dst.dtype == np.uint8 else dst, src)
+
+
+_FILL_POOL = cf.ThreadPoolExecutor(max_workers=4)
+
+
+__all__ = ["ChunkStager", "RowStreamer", "invert_measurement_set_streamed", "invert_tile_files"]
