@@ -93,19 +93,23 @@ constexpr int kOrderBatch = kOrderThreads * kOrderPer;
 static_assert(kOrderBatch == kOrderWindow, "one order block per window");
 
 // Bank class of a visibility's footprint origin in its tile's LDS sub-grid,
-// recomputed from (u, v, f/c) with place_vis's arithmetic (fp contraction off,
-// so it matches the scatter bit for bit; a mismatch would only cost a bank
-// conflict, never a wrong sum).
-__device__ __forceinline__ unsigned origin_class(double u_m, double v_m, double fx, const GridGeometry& g) {
-#pragma clang fp contract(off)
+// recomputed in fp32 from the row's pre-scaled (u scale_u, v scale_v) and
+// f/c. The class only decides the ORDER of a window's visibilities (bank
+// spreading); the scatter places every visibility with its own fp64
+// arithmetic whatever position it gets, so a class that differs from the
+// exact one near a cell edge (fp32: ~1e-3 cells at |x| = 8192) costs at most a
+// bank conflict, never a different sum.
+__device__ __forceinline__ unsigned origin_class_f32(float us, float vs, float f, const GridGeometry& g) {
   const int hw = g.support / 2;
   const int P = kTile + g.support - 1;
-  const double x = (u_m * fx) * g.scale_u + (double)(g.nu / 2);
-  const double y = (v_m * fx) * g.scale_v + (double)(g.nv / 2);
-  int64_t ix0, iy0;
-  double t0, t1;
-  uv_origin(x, y, hw, g, &ix0, &t0, &iy0, &t1);
-  return (unsigned)((((int)ix0 % kTile) * P + (int)iy0 % kTile) & 31);  // ix0, iy0 in [0, 2^31)
+  const float x = fmaf(us, f, (float)(g.nu / 2) - (float)hw);
+  const float y = fmaf(vs, f, (float)(g.nv / 2) - (float)hw);
+  int ix0 = (int)floorf(x) + 1, iy0 = (int)floorf(y) + 1;
+  ix0 += ix0 < 0 ? (int)g.nu : 0;
+  ix0 -= ix0 >= (int)g.nu ? (int)g.nu : 0;
+  iy0 += iy0 < 0 ? (int)g.nv : 0;
+  iy0 -= iy0 >= (int)g.nv ? (int)g.nv : 0;
+  return (unsigned)(((ix0 % kTile) * P + iy0 % kTile) & 31);  // ix0, iy0 in [0, nu), [0, nv)
 }
 
 // One block per window (<= kOrderWindow consecutive tile-order positions).
@@ -130,7 +134,7 @@ __global__ __launch_bounds__(kOrderThreads, 8) void order_kernel(const double* _
   // tables reuse their space
   __shared__ union {
     struct {
-      double2 uv[GATHER ? 1 : kOrderBatch];  // (u, v) of each slice's row (recompute only)
+      float2 uv[GATHER ? 1 : kOrderBatch];  // (u scale_u, v scale_v) of each slice's row (recompute only)
       uint64_t rec[kOrderBatch];
       int off[kOrderBatch + 1];  // slice starts relative to the window start
       uint16_t idx[kOrderBatch];  // slice of each position
@@ -139,7 +143,7 @@ __global__ __launch_bounds__(kOrderThreads, 8) void order_kernel(const double* _
       unsigned S[kOrderBatch], M[kOrderBatch];
     } b;
   } sh;
-  double2* const s_uv = sh.a.uv;
+  float2* const s_uv = sh.a.uv;
   uint64_t* const s_rec = sh.a.rec;
   int* const s_off = sh.a.off;
   uint16_t* const s_idx = sh.a.idx;
@@ -156,7 +160,7 @@ __global__ __launch_bounds__(kOrderThreads, 8) void order_kernel(const double* _
     s_rec[k] = rec;
     if constexpr (!GATHER) {
       const int64_t row = (int64_t)(rec >> 32);
-      s_uv[k] = make_double2(uvw[3 * row], uvw[3 * row + 1]);
+      s_uv[k] = make_float2((float)(uvw[3 * row] * g.scale_u), (float)(uvw[3 * row + 1] * g.scale_v));
     }
   }
   if (threadIdx.x < 32) s_cnt[threadIdx.x] = 0u;
@@ -194,8 +198,8 @@ __global__ __launch_bounds__(kOrderThreads, 8) void order_kernel(const double* _
       if constexpr (GATHER) {
         cls[k] = vis_class[packed[k]];
       } else {
-        const double2 uv = s_uv[slice[k]];
-        cls[k] = origin_class(uv.x, uv.y, fx[chan[k]], g);
+        const float2 uv = s_uv[slice[k]];
+        cls[k] = origin_class_f32(uv.x, uv.y, (float)fx[chan[k]], g);
       }
     }
   }

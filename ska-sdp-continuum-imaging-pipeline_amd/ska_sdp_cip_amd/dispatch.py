@@ -20,7 +20,10 @@ to one device with HIP_VISIBLE_DEVICES.
 from __future__ import annotations
 
 import concurrent.futures as cf
+import contextlib
+import itertools
 import threading
+import time
 from typing import Any, Iterable, Optional
 
 
@@ -84,6 +87,8 @@ class LocalGPUClient:
             _lib.lib()
         self._next = 0
         self._lock = threading.Lock()
+        self._streams = []  # active task-stream recorders (get_task_stream)
+        self._ids = itertools.count()
         self._gpu_pools = {}
         self._host_pool = None
         if concurrent:
@@ -117,20 +122,60 @@ class LocalGPUClient:
         gpu = bool(resources and "gpu" in resources)
         dev = self._pick_device() if gpu else None
 
-        def task():
+        key = f"{getattr(fn, '__name__', 'task')}-{next(self._ids):08x}"
+
+        def run():
             a = _resolve(args)
             kw = {k: _resolve(v) for k, v in kwargs.items()}
             if dev is not None and _has_cuda():
                 import torch  # pylint: disable=import-outside-toplevel
 
                 with torch.cuda.device(dev):
-                    return fn(*a, **kw)
+                    out = fn(*a, **kw)
+                    torch.cuda.current_stream(dev).synchronize()  # the task ends when its GPU work does
+                    return out
             return fn(*a, **kw)
+
+        def task():
+            t0 = time.time()
+            status = "OK"
+            try:
+                return run()
+            except BaseException:
+                status = "error"
+                raise
+            finally:
+                self._record(key, dev, status, t0, time.time())
 
         if not self.concurrent:
             return LocalFuture(task())
         pool = self._gpu_pools[dev] if gpu else self._host_pool
         return LocalFuture(future=pool.submit(task))
+
+    def _record(self, key: str, dev: Optional[int], status: str, start: float, stop: float) -> None:
+        if not self._streams:
+            return
+        entry = {"key": key, "worker": f"gpu-{dev}" if dev is not None else "host", "status": status,
+                 "startstops": ({"action": "compute", "start": start, "stop": stop},)}
+        if dev is not None:
+            entry["device"] = dev
+        with self._lock:
+            for rec in self._streams:
+                rec.data.append(entry)
+
+    @contextlib.contextmanager
+    def get_task_stream(self):
+        """Record the tasks that finish inside the block, in dask's
+        `get_task_stream()` format (`.data`: {key, worker, status,
+        startstops[, device]} per task), for `task_metrics.TaskMetrics`."""
+        rec = _TaskStream()
+        with self._lock:
+            self._streams.append(rec)
+        try:
+            yield rec
+        finally:
+            with self._lock:
+                self._streams.remove(rec)
 
     def close(self) -> None:
         """Wait for the queued tasks and stop the worker threads."""
@@ -145,6 +190,13 @@ class LocalGPUClient:
 
     def __exit__(self, *exc) -> None:
         self.close()
+
+
+class _TaskStream:
+    """Recorded task stream (`data`: list of dask-format entries)."""
+
+    def __init__(self) -> None:
+        self.data = []
 
 
 def as_completed(futures: Iterable[LocalFuture]):

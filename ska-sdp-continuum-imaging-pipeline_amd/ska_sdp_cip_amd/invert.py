@@ -216,6 +216,37 @@ def worker_ducc_invert(
     return ducc_invert(gridder_input, num_pixels, pixel_size_asec, nthreads=1, **kwargs)
 
 
+def worker_device_invert(
+    chunk_reader,
+    num_pixels: int,
+    pixel_size_asec: float,
+    *,
+    epsilon: float = EPSILON,
+    do_wstacking: bool = DO_WSTACKING,
+    support: Optional[int] = None,
+) -> tuple[NDArray, float]:
+    """
+    GPU task of `dask_invert_measurement_set(..., stokes_on_device=True)`:
+    the chunk's raw (rows, chans, 4) columns go to the task's device as they
+    are read, Stokes I and the effective weights are formed inside the gridder
+    (cip_ms2dirty_stokes_i) and the unnormalised float32 image is returned
+    with its weight sum (fp64, summed on the device), the pair that
+    `integrate_weighted_images` reduces (reference :187-209 shape).
+    """
+    import torch  # pylint: disable=import-outside-toplevel
+
+    dev = torch.device("cuda", torch.cuda.current_device())
+    t = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a, dtype=dt)).to(dev)  # noqa: E731
+    pix = pixel_size_lm(pixel_size_asec)
+    sumw = torch.zeros(1, dtype=torch.float64, device=dev)
+    image, _ = device_ms2dirty_stokes_i(
+        t(chunk_reader.uvw(), np.float64), t(chunk_reader.channel_frequencies(), np.float64),
+        t(chunk_reader.visibilities(), np.complex64), t(chunk_reader.flags(), np.uint8),
+        t(chunk_reader.weights(), np.float32), num_pixels, num_pixels, pix, pix, epsilon=epsilon,
+        support=support, do_wstacking=do_wstacking, sum_weights=sumw)
+    return image.to(torch.float32).cpu().numpy(), float(sumw.item())
+
+
 def integrate_weighted_images(
     weighted_images: Iterable[tuple[NDArray, float]]
 ) -> NDArray:
@@ -240,6 +271,7 @@ def dask_invert_measurement_set(
     *,
     row_chunks: Optional[int] = 1,
     freq_chunks: Optional[int] = None,
+    stokes_on_device: bool = False,
     **kwargs,
 ) -> NDArray:
     """
@@ -249,6 +281,10 @@ def dask_invert_measurement_set(
     `ska_sdp_cip_amd.dispatch.LocalGPUClient`. Default `freq_chunks` is one per
     worker (the reference's `len(client.scheduler_info())` counts the keys of
     the info dict; the worker count is used here).
+    `stokes_on_device=True`: each GPU task takes its chunk's raw columns and
+    forms Stokes I inside the gridder (`worker_device_invert`) instead of a
+    host task building `StokesIGridderInput` first (one task per chunk, the
+    weight sums in fp64).
     """
     row_chunks = max(row_chunks or 1, 1)
     if not freq_chunks:
@@ -256,6 +292,10 @@ def dask_invert_measurement_set(
 
     weighted_images = []
     for chunk in ms_reader.partition(row_chunks, freq_chunks):
+        if stokes_on_device:
+            weighted_images.append(client.submit(worker_device_invert, chunk, num_pixels, pixel_size_asec,
+                                                 resources={"gpu": 1}, **kwargs))
+            continue
         gridder_input = client.submit(
             StokesIGridderInput.from_measurement_set_reader, chunk
         )
@@ -281,5 +321,6 @@ __all__ = [
     "invert_measurement_set",
     "pixel_size_lm",
     "set_env",
+    "worker_device_invert",
     "worker_ducc_invert",
 ]

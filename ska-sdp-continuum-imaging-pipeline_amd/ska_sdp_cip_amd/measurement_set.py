@@ -201,6 +201,20 @@ class InMemoryMeasurementSet(_BoundedReader):
         self._total_channels = nchan
         self._init_bounds()
 
+    _NPZ_KEYS = ("uvw", "visibilities", "flags", "weights", "channel_frequencies")
+
+    def save_npz(self, path: Union[str, os.PathLike]) -> None:
+        """Write the whole set's columns to an .npz file (a stand-in for an MS
+        directory where python-casacore is absent; `open_measurement_set`)."""
+        np.savez(path, uvw=self._uvw, visibilities=self._vis, flags=self._flags, weights=self._weights,
+                 channel_frequencies=self._freqs)
+
+    @classmethod
+    def load_npz(cls, path: Union[str, os.PathLike]) -> "InMemoryMeasurementSet":
+        """Read a set written by `save_npz` (plain arrays, no pickles)."""
+        with np.load(path, allow_pickle=False) as z:
+            return cls(*(z[k] for k in cls._NPZ_KEYS))
+
     def _clone_unbounded(self) -> "InMemoryMeasurementSet":
         clone = object.__new__(InMemoryMeasurementSet)
         clone.__dict__.update(self.__dict__)
@@ -270,6 +284,16 @@ class InMemoryMeasurementSet(_BoundedReader):
                 np.copyto(out["wgt4"], self._weights[a:b, ch])
             else:
                 np.copyto(out["wgt4"], self._weights[a:b, None, :])
+
+
+def open_measurement_set(path: Union[str, os.PathLike]) -> _BoundedReader:
+    """A reader for `path`: an .npz column file (`InMemoryMeasurementSet.
+    save_npz`) or a MeasurementSet v2 directory (`MeasurementSetReader`,
+    which needs python-casacore)."""
+    p = Path(path)
+    if p.suffix == ".npz":
+        return InMemoryMeasurementSet.load_npz(p)
+    return MeasurementSetReader(p)
 
 
 class MeasurementSetReader(_BoundedReader):
