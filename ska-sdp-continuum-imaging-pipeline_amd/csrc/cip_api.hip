@@ -287,10 +287,6 @@ struct PlanResult {
   Chunk* chunks = nullptr;
   uint32_t* perm = nullptr;  // bank-class ordered visibility stream, or NULL
   uint32_t* dmask = nullptr;  // grid tiles the scatter writes, per plane (bit-packed, ntx / 32 words per tile row)
-  // w-stacking, layer-major: one chunk range over all (uv tile, w layer) keys,
-  // gridded onto all resident planes by one scatter_layers launch (else
-  // plane_chunk_off holds one chunk range per plane)
-  bool layers = false;
 };
 
 struct Workspace {
@@ -309,10 +305,6 @@ struct Workspace {
   // the "grid" buffer when it is known all-zero (the masked FFT pass A zeroes
   // what the scatter wrote), else NULL
   double* grid_clean = nullptr;
-  // the "grid_planes" buffer (layer-major w-stacking) when all its planes are
-  // known zero, and how many doubles of it
-  double* planes_clean = nullptr;
-  int64_t planes_clean_elems = 0;
   // CIP_ASYNC pipelining (cip_ms2dirty): consecutive calls alternate between
   // two sets of planner buffers (parity; buf() appends the parity to buffer
   // names while parity_scope is set), so the planner of call k + 1 runs on
@@ -460,7 +452,6 @@ static T* buf(Workspace* ws, const char* name, int64_t count) {
   DevBuf& b = ws->bufs[(ws->parity_scope && ws->parity) ? std::string(name) + "~1" : std::string(name)];
   if (b.bytes < bytes) {
     if (b.ptr && b.ptr == (void*)ws->grid_clean) ws->grid_clean = nullptr;  // a new buffer is not known zero
-    if (b.ptr && b.ptr == (void*)ws->planes_clean) ws->planes_clean = nullptr;
     if (b.ptr) ws->saved_valid = false;  // the saved plan may point into it
     if (b.ptr) (void)hipFree(b.ptr);
     b.ptr = nullptr;
@@ -627,8 +618,7 @@ static int radix_group(int pass) {
 // *maxabs (the place pass reads the visibilities anyway).
 static int make_plan(Workspace* ws, const double* uvw, const double* fx, const RowMap& m,
                      const void* vis, int vis_dtype, const void* wgt, int wgt_dtype, double* red,
-                     const GridGeometry& g, int64_t cv, hipStream_t s, PlanResult* pr, double* maxabs,
-                     bool layers = false) {
+                     const GridGeometry& g, int64_t cv, hipStream_t s, PlanResult* pr, double* maxabs) {
   const int64_t ntiles = g.ntx * g.nty * g.ntw;
   pr->ntiles = ntiles;
   CIP_ALLOC(tile_runs, int64_t, "tile_runs", ntiles + 1)
@@ -718,8 +708,7 @@ static int make_plan(Workspace* ws, const double* uvw, const double* fx, const R
   // sequence per uv tile over its layers feeding the plane (tile-major keys
   // make that a contiguous range), plane after plane
   const int64_t ntxy = g.ntx * g.nty;
-  const bool per_plane = g.do_wstacking != 0 && !layers;
-  pr->layers = g.do_wstacking != 0 && layers;
+  const bool per_plane = g.do_wstacking != 0;
   const int64_t nrange = per_plane ? g.nplanes : 1;  // chunk ranges: per plane, or the one 2-D layer
   const int full_first = (!per_plane && chunks_full_first()) ? 1 : 0;
   CIP_ALLOC(layer_off, int64_t, "layer_off", nrange + 1)
@@ -782,19 +771,6 @@ static bool public_dtypes(int vis_dtype, int wgt_dtype) {
 static bool vis_dtype_ok(int d) { return d == CIP_C64 || d == CIP_C128 || d == CIP_POL4I; }
 static bool wgt_dtype_ok(int d) { return d == CIP_NONE || d == CIP_F32 || d == CIP_F64 || d == CIP_POL4I; }
 
-// Layer-major w-stacking (one scatter over all planes a visibility feeds,
-// scatter_layers_kernel) for supports <= 16 when all planes fit in HBM next to
-// everything else (<= 64 GiB of planes); CIP_WSTACK_LAYERS=0 keeps the
-// per-plane scatter (A/B).
-static bool use_layers(const GridGeometry& g) {
-  static const bool on = [] {
-    const char* e = getenv("CIP_WSTACK_LAYERS");
-    return !(e && std::strcmp(e, "0") == 0);
-  }();
-  const double bytes = (double)g.nplanes * (double)g.nu * (double)g.nv * 16.0;
-  return on && g.do_wstacking && g.support <= 16 && bytes <= 64.0 * (1ull << 30);
-}
-
 struct Prepared {
   cip_gridder_params p;
   GridGeometry g;
@@ -819,8 +795,7 @@ static int prepare(Workspace* ws, const double* uvw, int64_t nrow, const double*
                    const void* vis, int vis_dtype, const void* wgt, int wgt_dtype, int64_t npix_x, int64_t npix_y,
                    double px, double py, double epsilon, int support, int do_wstacking, bool packed,
                    const cip_gridder_params* given, hipStream_t s, Prepared* out, double** grid_out = nullptr,
-                   const RaggedRows* ragged = nullptr, bool reuse = false, const uint8_t* flags4 = nullptr,
-                   bool want_layers = false) {
+                   const RaggedRows* ragged = nullptr, bool reuse = false, const uint8_t* flags4 = nullptr) {
   if (!ws->parity_scope) ws->plan_unscoped = true;
   if (!vis_dtype_ok(vis_dtype)) return set_error(CIP_EINVAL, "vis dtype must be complex64 or complex128");
   if (!wgt_dtype_ok(wgt_dtype)) return set_error(CIP_EINVAL, "wgt dtype must be float32, float64 or none");
@@ -891,7 +866,7 @@ static int prepare(Workspace* ws, const double* uvw, int64_t nrow, const double*
   // promise)
   const std::vector<double> key = {(double)nrow, (double)nchan, (double)npix_x, (double)npix_y, px, py, epsilon,
                                    (double)support, (double)do_wstacking, (double)packed,
-                                   given ? 1.0 : 0.0, want_layers ? 1.0 : 0.0};
+                                   given ? 1.0 : 0.0};
   const bool reusing = reuse && !ragged && given == nullptr && ws->saved_valid && ws->saved_key == key;
   if (reusing) given = &ws->saved_p;
   double wmin = 0.0, wmax = 0.0;
@@ -976,7 +951,7 @@ static int prepare(Workspace* ws, const double* uvw, int64_t nrow, const double*
   } else {
     ws->saved_valid = false;
     rc = make_plan(ws, uvw, fx, m, vis, vis_dtype, wgt, wgt_dtype, red, out->g, chunk_vis(packed, out->g.nu), s,
-                   &out->plan, &maxabs, want_layers && use_layers(out->g));
+                   &out->plan, &maxabs);
     if (rc == CIP_OK && !ragged) {
       ws->saved_key = key;
       ws->saved_p = out->p;
@@ -997,22 +972,6 @@ static int prepare(Workspace* ws, const double* uvw, int64_t nrow, const double*
   g_prof.counts[2] = out->plan.nchunks;
   g_prof.counts[3] = out->g.nplanes;
   return rc;
-}
-
-// every plane of a layer-major plan: grids[p * 2 nu nv] (zero or accumulating)
-static int scatter_layers(const Prepared& pp, const double* uvw, const void* vis, int vis_dtype, const void* wgt,
-                          int wgt_dtype, bool transposed, double* grids, hipStream_t s) {
-  GridGeometry g = pp.g;
-  g.transposed = transposed ? 1 : 0;
-  if (pp.plan.nchunks == 0) return CIP_OK;
-  if (wgt == nullptr) wgt_dtype = CIP_NONE;
-  hipEvent_t a = g_prof.mark(s);
-  CIP_HIP_CHECK(launch_scatter_layers(g.support, vis_dtype, wgt_dtype, pp.packed, uvw, pp.fx, vis, wgt, pp.m,
-                                      pp.plan.runs, pp.plan.run_goff, pp.plan.perm, pp.plan.chunks, 0,
-                                      pp.plan.nchunks, g, pp.fixed_scale, grids, 2 * g.nu * g.nv, s));
-  g_prof.span(2, a, g_prof.mark(s));
-  g_prof.counts[4] += 1;
-  return CIP_OK;
 }
 
 // transposed: store the grid as gT[y, x] (input layout of the pruned FFT)
@@ -1188,19 +1147,14 @@ static int grid_accumulate(const double* uvw, int64_t nrow, const double* freq, 
   Prepared pp;
   int rc = prepare(ws, uvw, nrow, freq, nchan, vis, vis_dtype, wgt, wgt_dtype, 2, 2, pixsize_x, pixsize_y, 0.0,
                    params->support, params->do_wstacking, (flags & CIP_ACC_SINGLE) != 0, params, s, &pp, nullptr,
-                   ragged, false, flags4, true);
+                   ragged, false, flags4);
   if (rc != CIP_OK) return rc;
   const GridGeometry& g = pp.g;
   const bool transposed = grid_is_transposed(g, npix_x, npix_y);
   const int64_t plane_elems = 2 * g.nu * g.nv;
-  if (pp.plan.layers) {
-    rc = scatter_layers(pp, uvw, vis, vis_dtype, wgt, wgt_dtype, transposed, grids, s);
+  for (int64_t p = 0; p < g.nplanes; ++p) {
+    rc = scatter_plane(pp, p, uvw, vis, vis_dtype, wgt, wgt_dtype, transposed, grids + p * plane_elems, s, true);
     if (rc != CIP_OK) return rc;
-  } else {
-    for (int64_t p = 0; p < g.nplanes; ++p) {
-      rc = scatter_plane(pp, p, uvw, vis, vis_dtype, wgt, wgt_dtype, transposed, grids + p * plane_elems, s, true);
-      if (rc != CIP_OK) return rc;
-    }
   }
   if (sum_wgt) CIP_HIP_CHECK(launch_add_scalar(pp.red, sum_wgt, s));
   g_prof.span(5, t_start, g_prof.mark(s));
@@ -1299,8 +1253,7 @@ static int ms2dirty_impl(const double* uvw, int64_t nrow, const double* freq, in
   ws->parity_scope = pipelined;
   int rc = prepare(ws, uvw, nrow, freq, nchan, vis, vis_dtype, wgt, wgt_dtype, npix_x, npix_y, pixsize_x, pixsize_y,
                    epsilon, support, do_wstacking, packed, nullptr, ps, &pp,
-                   (overlap_zero() && !pipelined) ? &grid : nullptr, nullptr, (flags & CIP_REUSE_PLAN) != 0, flags4,
-                   true);
+                   (overlap_zero() && !pipelined) ? &grid : nullptr, nullptr, (flags & CIP_REUSE_PLAN) != 0, flags4);
   ws->parity_scope = false;
   if (pipelined) {
     // s continues once the plan exists (also after a failed one: nothing then runs on it)
@@ -1326,35 +1279,13 @@ static int ms2dirty_impl(const double* uvw, int64_t nrow, const double* freq, in
   if (rc != CIP_OK) return rc;
   ws->grid_clean = nullptr;  // dirty until a masked pass A has consumed every written tile
   const uint32_t* dmask = st.fast ? pp.plan.dmask : nullptr;
-  if (pp.plan.layers) {
-    // every plane resident: one scatter over all of them, then plane after
-    // plane to the image (a masked pass A leaves each plane zero again)
-    const int64_t plane_elems = 2 * g.nu * g.nv, nel = g.nplanes * plane_elems;
-    double* planes = buf<double>(ws, "grid_planes", nel);
-    if (!planes) return CIP_ENOMEM;
-    if (!(ws->planes_clean == planes && ws->planes_clean_elems >= nel))
-      CIP_HIP_CHECK(hipMemsetAsync(planes, 0, sizeof(double) * nel, s));
-    ws->planes_clean = nullptr;
-    rc = scatter_layers(pp, uvw, vis, vis_dtype, wgt, wgt_dtype, st.fast, planes, s);
+  for (int64_t p = 0; p < g.nplanes; ++p) {
+    rc = scatter_plane(pp, p, uvw, vis, vis_dtype, wgt, wgt_dtype, st.fast, grid, s, clean);
     if (rc != CIP_OK) return rc;
-    for (int64_t p = 0; p < g.nplanes; ++p) {
-      rc = plane_to_dirty(st, g, p, planes + p * plane_elems, dirty_out, s,
-                          dmask ? dmask + p * (g.ntx * g.nty / 32) : nullptr, nullptr);
-      if (rc != CIP_OK) return rc;
-    }
-    if (dmask) {
-      ws->planes_clean = planes;
-      ws->planes_clean_elems = nel;
-    }
-  } else {
-    for (int64_t p = 0; p < g.nplanes; ++p) {
-      rc = scatter_plane(pp, p, uvw, vis, vis_dtype, wgt, wgt_dtype, st.fast, grid, s, clean);
-      if (rc != CIP_OK) return rc;
-      rc = plane_to_dirty(st, g, p, grid, dirty_out, s, dmask ? dmask + p * (g.ntx * g.nty / 32) : nullptr,
-                          normalise ? pp.red : nullptr);
-      if (rc != CIP_OK) return rc;
-      clean = dmask != nullptr;
-    }
+    rc = plane_to_dirty(st, g, p, grid, dirty_out, s, dmask ? dmask + p * (g.ntx * g.nty / 32) : nullptr,
+                        normalise ? pp.red : nullptr);
+    if (rc != CIP_OK) return rc;
+    clean = dmask != nullptr;
   }
   rc = finish_dirty(ws, st, pp.p, g, dirty_out, s);
   if (rc != CIP_OK) return rc;

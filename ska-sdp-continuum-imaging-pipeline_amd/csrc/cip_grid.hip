@@ -240,33 +240,6 @@ hipError_t launch_order(const double* uvw, const double* fx, const uint8_t* vis_
   return hipGetLastError();
 }
 
-hipError_t launch_scatter_layers(int support, int vis_dtype, int wgt_dtype, bool packed, const double* uvw,
-                                 const double* fx, const void* vis, const void* wgt, const RowMap& m,
-                                 const uint64_t* runs, const int64_t* run_goff, const uint32_t* perm,
-                                 const Chunk* chunks, int64_t chunk_begin, int64_t nchunks, const GridGeometry& g,
-                                 double fixed_scale, double* grids, int64_t plane_elems, hipStream_t s) {
-  if (nchunks <= 0) return hipSuccess;
-  if (packed && vis_dtype != CIP_C64 && vis_dtype != CIP_POL4I) return hipErrorInvalidValue;
-  if (nchunks >= ((int64_t)1 << 31)) return hipErrorInvalidValue;
-#define LCASE(WW)                                                                                             \
-  case WW:                                                                                                    \
-    return launch_scatter_layers_w<WW>(vis_dtype, wgt_dtype, packed, (unsigned)nchunks, s, uvw, fx, vis, wgt, m, \
-                                       runs, run_goff, perm, chunks, chunk_begin, g, fixed_scale, grids,         \
-                                       plane_elems);
-  switch (support) {
-    LCASE(4)
-    LCASE(6)
-    LCASE(8)
-    LCASE(10)
-    LCASE(12)
-    LCASE(14)
-    LCASE(16)
-    default:
-      return hipErrorInvalidValue;
-  }
-#undef LCASE
-}
-
 hipError_t launch_scatter(int support, int vis_dtype, int wgt_dtype, bool packed, const double* uvw,
                           const double* fx, const void* vis, const void* wgt, const RowMap& m, const uint64_t* runs,
                           const int64_t* run_goff, const int64_t* tile_run_off, const uint32_t* perm,

@@ -118,20 +118,6 @@ hipError_t launch_scatter_large_w(int vis_dtype, int wgt_dtype, dim3 gd, hipStre
                                   const uint64_t* runs, const int64_t* run_goff, const uint32_t* perm,
                                   const Chunk* chunks, int64_t cb, const GridGeometry& g, int64_t plane, double fs,
                                   double* grid);
-// layer-major w-stacking (cip_scatter.h scatter_layers_kernel): every chunk of
-// the plan (one (uv tile, w layer) key each) onto the G planes of each of its
-// plane groups at once; grids = nplanes resident planes, plane_elems apart
-template <int W>
-hipError_t launch_scatter_layers_w(int vis_dtype, int wgt_dtype, bool pack, unsigned nchunks, hipStream_t s,
-                                   const double* uvw, const double* fx, const void* vis, const void* wgt,
-                                   const RowMap& m, const uint64_t* runs, const int64_t* run_goff,
-                                   const uint32_t* perm, const Chunk* chunks, int64_t cb, const GridGeometry& g,
-                                   double fs, double* grids, int64_t plane_elems);
-hipError_t launch_scatter_layers(int support, int vis_dtype, int wgt_dtype, bool packed, const double* uvw,
-                                 const double* fx, const void* vis, const void* wgt, const RowMap& m,
-                                 const uint64_t* runs, const int64_t* run_goff, const uint32_t* perm,
-                                 const Chunk* chunks, int64_t chunk_begin, int64_t nchunks, const GridGeometry& g,
-                                 double fixed_scale, double* grids, int64_t plane_elems, hipStream_t s);
 hipError_t launch_scatter(int support, int vis_dtype, int wgt_dtype, bool packed, const double* uvw,
                           const double* fx, const void* vis, const void* wgt, const RowMap& m, const uint64_t* runs,
                           const int64_t* run_goff, const int64_t* tile_run_off, const uint32_t* perm,

@@ -337,241 +337,6 @@ __global__ __launch_bounds__(kScatterThreads, CIP_SCATTER_WAVES) void scatter_ke
   }
 }
 
-// ------------------------------------------------ layer-major w-stacking ----
-// One work unit = one (uv tile, w layer iw0) key of the tile-sorted stream: its
-// visibilities feed planes iw0 .. iw0 + W - 1, all resident in HBM. A block
-// holds G of those planes' (T+W-1)^2 sub-grids in LDS (blockIdx.y = plane
-// group) and places each visibility, and evaluates its u, v and w kernel
-// values, once for all G planes - the per-plane path (scatter_kernel with
-// WSTACK) re-places a visibility for each of the W planes it feeds. The taps
-// and atomics per plane are the same; the flush goes to each plane's grid.
-constexpr int kLayerThreads = 1024;
-constexpr int kLayerLdsBudget = 150 * 1024;  // bytes of LDS a layer block may hold (160 KB per CU)
-
-template <int W, bool PACK>
-constexpr int layer_group() {
-  constexpr int P = kTile + W - 1;
-  constexpr int per = P * P * (PACK ? 8 : 16);
-  constexpr int g = kLayerLdsBudget / per;
-  return g >= W ? W : (g >= (W + 1) / 2 ? (W + 1) / 2 : (g >= (W + 2) / 3 ? (W + 2) / 3 : 1));
-}
-
-template <int W, int G, bool PACK>
-__device__ __forceinline__ void grid_fetched_layers(const VisFetch& f, const GridGeometry& g, int64_t layer, int k0,
-                                                    int64_t X0, int64_t Y0, double fixed_scale,
-                                                    unsigned long long* sub) {
-  constexpr int T = kTile;
-  constexpr int P = T + W - 1;
-  constexpr int S = P * P * (PACK ? 1 : 2);  // u64 per plane sub-grid
-  if (f.wt == 0.0) return;
-  int64_t ix0, iy0, iw0;
-  double yu, yv, yw;
-  if (!place_vis(f.u, f.v, f.w, f.fx, g, &ix0, &yu, &iy0, &yv, &iw0, &yw)) return;
-  const int64_t lx = ix0 - X0, ly = iy0 - Y0;
-  if (lx < 0 || lx >= T || ly < 0 || ly >= T || iw0 != layer) return;  // never for a consistent plan
-  double kwv[W], ku[W], kv[W];
-  eval_kernel<W>(yw, kwv);
-  eval_kernel<W>(yu, ku);
-  eval_kernel<W>(yv, kv);
-  const double sc0 = f.wt * fixed_scale;
-  unsigned long long* base = sub + (lx * P + ly);
-#pragma unroll
-  for (int k = 0; k < G; ++k) {
-    if (k0 + k >= W) break;  // block-uniform (last group)
-    double kw = 0.0;
-#pragma unroll
-    for (int q = 0; q < W; ++q) kw = (q == k0 + k) ? kwv[q] : kw;
-    const double sc = sc0 * kw;
-    const double vr = f.vr * sc, vi = f.vi * sc;
-    double kr[W], ki[W];
-#pragma unroll
-    for (int j = 0; j < W; ++j) {
-      kr[j] = kv[j] * vr;
-      ki[j] = kv[j] * vi;
-    }
-    unsigned long long* bk = base + k * S;
-#pragma unroll
-    for (int i = 0; i < W; ++i) {
-#pragma unroll
-      for (int j = 0; j < W; ++j) {
-        const double qr = fma(ku[i], kr[j], kMagic);
-        const double qi = fma(ku[i], ki[j], kMagic);
-        const unsigned long long br = (unsigned long long)__double_as_longlong(qr);
-        const unsigned long long bi = (unsigned long long)__double_as_longlong(qi);
-        if constexpr (PACK) {
-          unsigned hi;
-          asm("v_add3_u32 %0, %1, %2, %3" : "=v"(hi) : "v"((unsigned)br), "v"((unsigned)(bi >> 32)),
-              "s"(0u - kMagicHi));
-          atomicAdd(bk + (i * P + j), __builtin_bit_cast(unsigned long long, make_uint2((unsigned)bi, hi)));
-        } else {
-          atomicAdd(bk + (i * P + j), br - 0x4338000000000000ull);
-          atomicAdd(bk + P * P + (i * P + j), bi - 0x4338000000000000ull);
-        }
-      }
-    }
-  }
-}
-
-template <int W, int G, typename VisT, int WK, bool PERM, bool PACK>
-__global__ __launch_bounds__(kLayerThreads, 1) void scatter_layers_kernel(
-    const double* __restrict__ uvw, const double* __restrict__ fx, const VisT* __restrict__ vis,
-    const void* __restrict__ wgt, RowMap m, const uint64_t* __restrict__ runs,
-    const int64_t* __restrict__ run_goff, const uint32_t* __restrict__ perm, const Chunk* __restrict__ chunks,
-    int64_t chunk_begin, GridGeometry g, double fixed_scale, double inv_scale, double* __restrict__ grids,
-    int64_t plane_elems) {
-  constexpr int T = kTile;
-  constexpr int P = T + W - 1;
-  constexpr int S = P * P * (PACK ? 1 : 2);
-  constexpr int NT = kLayerThreads;
-  __shared__ unsigned long long sub[G * S];
-  __shared__ int64_t s_voff[PERM ? 1 : kRunBatch + 1];
-  __shared__ uint64_t s_run[PERM ? 1 : kRunBatch];
-
-  const Chunk ch = chunks[chunk_begin + blockIdx.x];
-  const int k0 = (int)blockIdx.y * G;
-  const int64_t layer = ch.tile % g.ntw;
-  int64_t X0, Y0;
-  tile_origin(ch.tile, g, &X0, &Y0);
-  for (int i = threadIdx.x; i < G * S; i += NT) sub[i] = 0ull;
-  if constexpr (PACK) {
-    fixed_scale *= packed_chunk_gain(ch.g1 - ch.g0);
-    inv_scale = 1.0 / fixed_scale;
-  }
-  if constexpr (PERM) {
-    __syncthreads();
-    const bool unit_vis = vis == nullptr;
-    const VisT* vis_ld = unit_vis ? (const VisT*)uvw : vis;
-    int64_t q = ch.g0 + threadIdx.x;
-    bool have = q < ch.g1;
-    RawFetch<VisT, WK> cur;
-    int64_t qn = q + NT;
-    bool hn = qn < ch.g1;
-    uint32_t pn = 0;
-    if (have) {
-      fetch_raw<VisT, WK>((int64_t)perm[q], true, uvw, fx, vis_ld, unit_vis, wgt, m, cur);
-      pn = perm[hn ? qn : q];
-    }
-    while (have) {
-      const int64_t qnn = qn + NT;
-      const bool hnn = qnn < ch.g1;
-      const uint32_t pnn = perm[hnn ? qnn : q];
-      RawFetch<VisT, WK> nxt;
-      fetch_raw<VisT, WK>((int64_t)pn, hn, uvw, fx, vis_ld, unit_vis, wgt, m, nxt);
-      grid_fetched_layers<W, G, PACK>(from_raw<VisT, WK>(cur, unit_vis), g, layer, k0, X0, Y0, fixed_scale, sub);
-      cur = nxt;
-      q = qn;
-      have = hn;
-      qn = qnn;
-      hn = hnn;
-      pn = pnn;
-    }
-  } else {
-    const int64_t rb = ch.last_run + 1;
-    int64_t r = ch.first_run;
-    int64_t v = ch.g0;
-    while (v < ch.g1 && r < rb) {
-      const int nst = (int)((rb - r) < kRunBatch ? (rb - r) : kRunBatch);
-      __syncthreads();
-      for (int k = threadIdx.x; k <= nst; k += NT) {
-        s_voff[k] = run_goff[r + k];
-        if (k < nst) s_run[k] = runs[r + k];
-      }
-      __syncthreads();
-      const int64_t bend = ch.g1 < s_voff[nst] ? ch.g1 : s_voff[nst];
-      int64_t q = v + threadIdx.x;
-      bool have = q < bend;
-      VisFetch cur;
-      if (have) fetch_vis<VisT, WK>(q, s_voff, s_run, nst, uvw, fx, vis, wgt, m, cur);
-      while (have) {
-        const int64_t qn = q + NT;
-        const bool hn = qn < bend;
-        VisFetch nxt;
-        if (hn) fetch_vis<VisT, WK>(qn, s_voff, s_run, nst, uvw, fx, vis, wgt, m, nxt);
-        grid_fetched_layers<W, G, PACK>(cur, g, layer, k0, X0, Y0, fixed_scale, sub);
-        cur = nxt;
-        q = qn;
-        have = hn;
-      }
-      v = bend;
-      r += nst;
-    }
-  }
-  __syncthreads();
-  // flush each plane's touched cells (planes layer + k0 + k < nplanes always)
-  for (int k = 0; k < G && k0 + k < W; ++k) {
-    double* grid = grids + (layer + k0 + k) * plane_elems;
-    const unsigned long long* sk = sub + k * S;
-    for (int cell = threadIdx.x; cell < P * P; cell += NT) {
-      const int lcell = g.transposed ? (cell % P) * P + cell / P : cell;
-      long long re, im;
-      if constexpr (PACK) {
-        const unsigned long long sv = sk[lcell];
-        im = (long long)(int)(unsigned)sv;
-        re = (long long)(int)(unsigned)((sv - (unsigned long long)im) >> 32);
-      } else {
-        re = (long long)sk[lcell];
-        im = (long long)sk[P * P + lcell];
-      }
-      if ((re | im) != 0) {
-        int64_t gx = X0 + lcell / P, gy = Y0 + lcell % P;
-        gx -= (gx >= g.nu) ? g.nu : 0;
-        gy -= (gy >= g.nv) ? g.nv : 0;
-        double* dst = grid + 2 * (g.transposed ? gy * g.nu + gx : gx * g.nv + gy);
-        unsafeAtomicAdd(dst, (double)re * inv_scale);
-        unsafeAtomicAdd(dst + 1, (double)im * inv_scale);
-      }
-    }
-  }
-}
-
-template <int W, typename VisT, int WK>
-inline hipError_t scatter_layers_dispatch(bool pack, unsigned nchunks, hipStream_t s, const double* uvw,
-                                          const double* fx, const void* vis, const void* wgt, const RowMap& m,
-                                          const uint64_t* runs, const int64_t* run_goff, const uint32_t* perm,
-                                          const Chunk* chunks, int64_t chunk_begin, const GridGeometry& g,
-                                          double fs, double* grids, int64_t plane_elems) {
-#define LAUNCH_L(PRM, PK)                                                                                     \
-  {                                                                                                           \
-    constexpr int G = layer_group<W, PK>();                                                                   \
-    scatter_layers_kernel<W, G, VisT, WK, PRM, PK><<<dim3(nchunks, (W + G - 1) / G), dim3(kLayerThreads), 0, s>>>( \
-        uvw, fx, (const VisT*)vis, wgt, m, runs, run_goff, perm, chunks, chunk_begin, g, fs, 1.0 / fs, grids,     \
-        plane_elems);                                                                                         \
-  }
-  bool done = false;
-  if constexpr (std::is_same<VisT, float2>::value || std::is_same<VisT, Pol4>::value) {
-    if (pack) {
-      if (perm) LAUNCH_L(true, true) else LAUNCH_L(false, true)
-      done = true;
-    }
-  }
-  if (!done) {
-    if (perm) LAUNCH_L(true, false) else LAUNCH_L(false, false)
-  }
-#undef LAUNCH_L
-  return hipGetLastError();
-}
-
-// all chunks [cb, cb + nchunks) of a layer-major w-stacking plan onto the
-// resident planes grids[p * plane_elems]
-template <int W>
-hipError_t launch_scatter_layers_w(int vis_dtype, int wgt_dtype, bool pack, unsigned nchunks, hipStream_t s,
-                                   const double* uvw, const double* fx, const void* vis, const void* wgt,
-                                   const RowMap& m, const uint64_t* runs, const int64_t* run_goff,
-                                   const uint32_t* perm, const Chunk* chunks, int64_t cb, const GridGeometry& g,
-                                   double fs, double* grids, int64_t plane_elems) {
-#define ARGS pack, nchunks, s, uvw, fx, vis, wgt, m, runs, run_goff, perm, chunks, cb, g, fs, grids, plane_elems
-  if (vis_dtype == CIP_POL4I) return scatter_layers_dispatch<W, Pol4, WK_POL4I>(ARGS);
-  if (vis_dtype == CIP_C64) {
-    if (wgt_dtype == CIP_F32) return scatter_layers_dispatch<W, float2, WK_F32>(ARGS);
-    if (wgt_dtype == CIP_F64) return scatter_layers_dispatch<W, float2, WK_F64>(ARGS);
-    return scatter_layers_dispatch<W, float2, WK_NONE>(ARGS);
-  }
-  if (wgt_dtype == CIP_F32) return scatter_layers_dispatch<W, double2, WK_F32>(ARGS);
-  if (wgt_dtype == CIP_F64) return scatter_layers_dispatch<W, double2, WK_F64>(ARGS);
-  return scatter_layers_dispatch<W, double2, WK_NONE>(ARGS);
-#undef ARGS
-}
-
 template <int W, typename VisT, int WK>
 inline hipError_t scatter_dispatch_ws(bool ws, bool pack, dim3 grid_dim, hipStream_t s, const double* uvw,
                                       const double* fx, const void* vis, const void* wgt, const RowMap& m,

@@ -13,9 +13,4 @@ template hipError_t launch_scatter_w<CIP_SCATTER_W>(int, int, bool, dim3, hipStr
                                                     const int64_t*, const int64_t*, const uint32_t*,
                                                     const Chunk*, int64_t, const GridGeometry&, int64_t, double,
                                                     double*);
-template hipError_t launch_scatter_layers_w<CIP_SCATTER_W>(int, int, bool, unsigned, hipStream_t, const double*,
-                                                           const double*, const void*, const void*, const RowMap&,
-                                                           const uint64_t*, const int64_t*, const uint32_t*,
-                                                           const Chunk*, int64_t, const GridGeometry&, double,
-                                                           double*, int64_t);
 }  // namespace cip
