@@ -285,7 +285,7 @@ struct PlanResult {
   int64_t* run_goff = nullptr;
   int64_t* tile_run_off = nullptr;
   Chunk* chunks = nullptr;
-  uint32_t* perm = nullptr;  // bank-class ordered visibility stream, or NULL
+  void* perm = nullptr;  // bank-class ordered visibility stream (perm_encode entries), or NULL
   uint32_t* dmask = nullptr;  // grid tiles the scatter writes, per plane (bit-packed, ntx / 32 words per tile row)
 };
 
@@ -629,9 +629,11 @@ static int make_plan(Workspace* ws, const double* uvw, const double* fx, const R
   CIP_ALLOC(scan_tmp, int64_t, "scan_tmp", scan_tmp_elems(ntiles + 1))
   const int64_t nvis = m.nvis;
   const int nblk = plan_place_blocks(nvis);
-  // the bank-class order needs a 32-bit flattened index (larger inputs grid in
-  // plain tile order)
-  const bool order = scatter_order() && nvis < ((int64_t)1 << 32);
+  // the bank-class order of dense rows stores 32-bit flattened indices (larger
+  // inputs grid in plain tile order); ragged row slices store 64-bit
+  // (row, channel) entries
+  const bool ragged = m.delta != nullptr;
+  const bool order = scatter_order() && (ragged || nvis < ((int64_t)1 << 32));
   uint8_t* vis_class = nullptr;
   if (order && order_gather()) {
     vis_class = buf<uint8_t>(ws, "vis_class", nvis);
@@ -757,7 +759,7 @@ static int make_plan(Workspace* ws, const double* uvw, const double* fx, const R
     CIP_ALLOC(windows, Chunk, "windows", nwin)
     CIP_HIP_CHECK(launch_chunk_emit(tile_vis_off, tile_vis, win_off, run_goff, tile_runs, ntiles, kOrderWindow, 0, nwin,
                                     windows, s));
-    CIP_ALLOC(perm, uint32_t, "perm", nvis)
+    CIP_ALLOC(perm, uint32_t, "perm", ragged ? 2 * nvis : nvis)
     CIP_HIP_CHECK(launch_order(uvw, fx, vis_class, g, m, runs, run_goff, tile_runs, windows, nwin, perm, s));
     pr->perm = perm;
   }

@@ -334,6 +334,50 @@ __device__ __forceinline__ void vis_rowchan(const RowMap& m, int64_t i, int64_t*
   }
 }
 
+// Entries of the bank-class ordered stream (perm, cip_grid.hip order_kernel):
+// dense rows store the flattened MS index (u32; (row, channel) by one fp64
+// multiply); ragged row slices store (row << 16) | channel (u64), so the
+// scatter finds a visibility's row without a per-visibility row lookup
+// (index = delta[row] + channel, delta a per-row, mostly cached array).
+__device__ __forceinline__ uint64_t perm_entry(const void* perm, const RowMap& m, int64_t q) {
+  return m.delta ? ((const uint64_t*)perm)[q] : (uint64_t)((const uint32_t*)perm)[q];
+}
+__device__ __forceinline__ uint64_t perm_encode(const RowMap& m, int64_t r, int64_t c) {
+  return m.delta ? (((uint64_t)r << 16) | (uint64_t)c) : (uint64_t)(r * m.nchan + c);
+}
+__device__ __forceinline__ void perm_store(void* perm, const RowMap& m, int64_t pos, uint64_t e) {
+  if (m.delta) ((uint64_t*)perm)[pos] = e;
+  else ((uint32_t*)perm)[pos] = (uint32_t)e;
+}
+// compile-time forms (WIDE: ragged row slices) for the hot kernels
+template <bool WIDE>
+__device__ __forceinline__ uint64_t perm_entry_t(const void* perm, int64_t q) {
+  if constexpr (WIDE) return ((const uint64_t*)perm)[q];
+  return (uint64_t)((const uint32_t*)perm)[q];
+}
+template <bool WIDE>
+__device__ __forceinline__ void perm_decode_t(uint64_t e, const RowMap& m, int64_t* il, int64_t* r, int64_t* c) {
+  if constexpr (WIDE) {
+    *r = (int64_t)(e >> 16);
+    *c = (int64_t)(e & 0xffffu);
+    *il = m.delta[*r] + *c;
+  } else {
+    *il = (int64_t)e;
+    split_index64((int64_t)e, m.nchan, m.inv_nchan, r, c);
+  }
+}
+// -> (visibility index, row, channel)
+__device__ __forceinline__ void perm_decode(uint64_t e, const RowMap& m, int64_t* il, int64_t* r, int64_t* c) {
+  if (m.delta) {
+    *r = (int64_t)(e >> 16);
+    *c = (int64_t)(e & 0xffffu);
+    *il = m.delta[*r] + *c;
+  } else {
+    *il = (int64_t)e;
+    split_index64((int64_t)e, m.nchan, m.inv_nchan, r, c);
+  }
+}
+
 // Tile key of a footprint origin: tile-major, key = ((iy0 / T) ntx + ix0 / T)
 // ntw + iw0, so the w layers of one uv tile are adjacent in the tile-sorted
 // stream and a w-stacking plane's work units (layers p - W + 1 .. p of a tile)

@@ -1,6 +1,8 @@
 // cip_grid.hip - the planner's order pass (bank-class order, SURVEY.md 8(a)
 // a4.3), the support dispatch of the scatter (cip_scatter.h, a4.4) and the
 // post-FFT crop / grid-correction / w-screen kernels (a4.5, a4.6).
+#include <type_traits>
+
 #include "cip_internal.h"
 
 namespace cip {
@@ -85,7 +87,9 @@ hipError_t launch_add_scalar(const double* src, double* dst, hipStream_t s) {
 // lower classes of equal rank), so any 32 consecutive positions of a level
 // have distinct classes and the scatter's waves (64 consecutive positions)
 // issue conflict-free atomics. Level tables: S[r] = sum_c min(cnt[c], r),
-// M[r] = {c : cnt[c] > r}. perm[g] = (row << 16) | channel. Atomic ranks make
+// M[r] = {c : cnt[c] > r}. perm[g] = the visibility's perm_encode entry
+// (cip_common.h: flattened index, or (row << 16) | channel for ragged row
+// slices). Atomic ranks make
 // the order within a class run-to-run variable; the integer sums are not.
 constexpr int kOrderThreads = 256;
 constexpr int kOrderPer = 4;
@@ -119,8 +123,8 @@ __device__ __forceinline__ unsigned origin_class_f32(float us, float vs, float f
 // search, recomputes the bank class of each visibility (no per-visibility
 // class array: a gathered byte per visibility cost more HBM lines than the
 // whole perm stream) and the window is counting-sorted into level-major
-// order: perm[g] = row * nchan + channel (32-bit flattened MS index).
-template <bool GATHER>
+// order: perm[g] = perm_encode(row, channel).
+template <bool GATHER, bool WIDE>
 __global__ __launch_bounds__(kOrderThreads, 8) void order_kernel(const double* __restrict__ uvw,
                                                               const double* __restrict__ fx,
                                                               const uint8_t* __restrict__ vis_class, GridGeometry g,
@@ -128,7 +132,7 @@ __global__ __launch_bounds__(kOrderThreads, 8) void order_kernel(const double* _
                                                               const int64_t* __restrict__ run_goff,
                                                               const int64_t* __restrict__ tile_run_off,
                                                               const Chunk* __restrict__ windows, int64_t nwindows,
-                                                              uint32_t* __restrict__ perm) {
+                                                              void* __restrict__ perm) {
   __shared__ __attribute__((aligned(16))) unsigned s_cnt[32];
   // the staged slices are dead once every position has its class: the level
   // tables reuse their space
@@ -172,7 +176,8 @@ __global__ __launch_bounds__(kOrderThreads, 8) void order_kernel(const double* _
     for (int p = a; p < b; ++p) s_idx[p] = (uint16_t)k;
   }
   __syncthreads();
-  uint32_t packed[kOrderPer];
+  using Entry = typename std::conditional<WIDE, uint64_t, uint32_t>::type;
+  Entry packed[kOrderPer];
   unsigned cls[kOrderPer], rk[kOrderPer];
   int slice[kOrderPer];
   int64_t chan[kOrderPer];
@@ -186,7 +191,7 @@ __global__ __launch_bounds__(kOrderThreads, 8) void order_kernel(const double* _
       const uint64_t rec = s_rec[lo];
       const int64_t row = (int64_t)(rec >> 32);
       const int64_t c = (int64_t)((rec >> 16) & 0xffff) + (qi - s_off[lo]);
-      packed[k] = (uint32_t)vis_index(m, row, c);
+      packed[k] = WIDE ? (Entry)(((uint64_t)row << 16) | (uint64_t)c) : (Entry)(row * m.nchan + c);
       slice[k] = lo;
       chan[k] = c;
     }
@@ -196,7 +201,7 @@ __global__ __launch_bounds__(kOrderThreads, 8) void order_kernel(const double* _
     cls[k] = 32u;
     if (threadIdx.x + k * kOrderThreads < nsb) {
       if constexpr (GATHER) {
-        cls[k] = vis_class[packed[k]];
+        cls[k] = vis_class[WIDE ? vis_index(m, (int64_t)(s_rec[slice[k]] >> 32), chan[k]) : (int64_t)packed[k]];
       } else {
         const float2 uv = s_uv[slice[k]];
         cls[k] = origin_class_f32(uv.x, uv.y, (float)fx[chan[k]], g);
@@ -224,25 +229,31 @@ __global__ __launch_bounds__(kOrderThreads, 8) void order_kernel(const double* _
   __syncthreads();
 #pragma unroll
   for (int k = 0; k < kOrderPer; ++k)
-    if (cls[k] < 32u) perm[sb + s_S[rk[k]] + __popc(s_M[rk[k]] & ((1u << cls[k]) - 1u))] = packed[k];
+    if (cls[k] < 32u) ((Entry*)perm)[sb + s_S[rk[k]] + __popc(s_M[rk[k]] & ((1u << cls[k]) - 1u))] = packed[k];
 }
 
 hipError_t launch_order(const double* uvw, const double* fx, const uint8_t* vis_class, const GridGeometry& g,
                         const RowMap& m, const uint64_t* runs, const int64_t* run_goff, const int64_t* tile_run_off,
-                        const Chunk* windows, int64_t nwindows, uint32_t* perm, hipStream_t s) {
+                        const Chunk* windows, int64_t nwindows, void* perm, hipStream_t s) {
   if (nwindows <= 0) return hipSuccess;
-  if (vis_class)
-    order_kernel<true><<<dim3((unsigned)nwindows), dim3(kOrderThreads), 0, s>>>(
-        uvw, fx, vis_class, g, m, runs, run_goff, tile_run_off, windows, nwindows, perm);
-  else
-    order_kernel<false><<<dim3((unsigned)nwindows), dim3(kOrderThreads), 0, s>>>(
-        uvw, fx, vis_class, g, m, runs, run_goff, tile_run_off, windows, nwindows, perm);
+#define ORDER(GA, WI)                                                              \
+  order_kernel<GA, WI><<<dim3((unsigned)nwindows), dim3(kOrderThreads), 0, s>>>( \
+      uvw, fx, vis_class, g, m, runs, run_goff, tile_run_off, windows, nwindows, perm)
+  const bool wide = m.delta != nullptr;  // ragged row slices: u64 entries
+  if (vis_class) {
+    if (wide) ORDER(true, true);
+    else ORDER(true, false);
+  } else {
+    if (wide) ORDER(false, true);
+    else ORDER(false, false);
+  }
+#undef ORDER
   return hipGetLastError();
 }
 
 hipError_t launch_scatter(int support, int vis_dtype, int wgt_dtype, bool packed, const double* uvw,
                           const double* fx, const void* vis, const void* wgt, const RowMap& m, const uint64_t* runs,
-                          const int64_t* run_goff, const int64_t* tile_run_off, const uint32_t* perm,
+                          const int64_t* run_goff, const int64_t* tile_run_off, const void* perm,
                           const Chunk* chunks, int64_t chunk_begin, int64_t nchunks, const GridGeometry& g,
                           int64_t plane, double fixed_scale, double* grid, hipStream_t s) {
   if (nchunks <= 0) return hipSuccess;

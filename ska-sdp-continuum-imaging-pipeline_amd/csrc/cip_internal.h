@@ -108,19 +108,19 @@ template <int W>
 hipError_t launch_scatter_w(int vis_dtype, int wgt_dtype, bool pack, dim3 gd, hipStream_t s, const double* uvw,
                             const double* fx, const void* vis, const void* wgt, const RowMap& m,
                             const uint64_t* runs, const int64_t* run_goff, const int64_t* tile_run_off,
-                            const uint32_t* perm, const Chunk* chunks, int64_t cb, const GridGeometry& g,
+                            const void* perm, const Chunk* chunks, int64_t cb, const GridGeometry& g,
                             int64_t plane, double fs, double* grid);
 // the large supports W = 24, 32, 48, 64 (cip_scatter_large.hip, wave per
 // visibility; one translation unit per W)
 template <int W>
 hipError_t launch_scatter_large_w(int vis_dtype, int wgt_dtype, dim3 gd, hipStream_t s, const double* uvw,
                                   const double* fx, const void* vis, const void* wgt, const RowMap& m,
-                                  const uint64_t* runs, const int64_t* run_goff, const uint32_t* perm,
+                                  const uint64_t* runs, const int64_t* run_goff, const void* perm,
                                   const Chunk* chunks, int64_t cb, const GridGeometry& g, int64_t plane, double fs,
                                   double* grid);
 hipError_t launch_scatter(int support, int vis_dtype, int wgt_dtype, bool packed, const double* uvw,
                           const double* fx, const void* vis, const void* wgt, const RowMap& m, const uint64_t* runs,
-                          const int64_t* run_goff, const int64_t* tile_run_off, const uint32_t* perm,
+                          const int64_t* run_goff, const int64_t* tile_run_off, const void* perm,
                           const Chunk* chunks, int64_t chunk_begin, int64_t nchunks, const GridGeometry& g,
                           int64_t plane, double fixed_scale, double* grid, hipStream_t s);
 // perm (nvis 32-bit records, nvis < 2^32): the tile-order visibilities as
@@ -130,7 +130,7 @@ hipError_t launch_scatter(int support, int vis_dtype, int wgt_dtype, bool packed
 hipError_t launch_order(const double* uvw, const double* fx, const uint8_t* vis_class, const GridGeometry& g,
                         const RowMap& m,
                         const uint64_t* runs, const int64_t* run_goff, const int64_t* tile_run_off,
-                        const Chunk* windows, int64_t nwindows, uint32_t* perm, hipStream_t s);
+                        const Chunk* windows, int64_t nwindows, void* perm, hipStream_t s);
 hipError_t launch_crop_correct_2d(const double* grid, const GridGeometry& g, int64_t npix_x, int64_t npix_y,
                                   const double* cx, const double* cy, double* dirty, hipStream_t s);
 hipError_t launch_wplane_accumulate(const double* grid, const GridGeometry& g, int64_t npix_x, int64_t npix_y,

@@ -91,16 +91,19 @@ struct RawFetch<Pol4, WK_POL4I> {
   uint32_t fw;
 };
 
-// Branch-free loads of MS visibility i (lanes with !ok load element 0; a PSF
-// call, vis == NULL, reads its ignored visibility from uvw[0..1]).
-template <typename VisT, int WK>
-__device__ __forceinline__ void fetch_raw(int64_t i, bool ok, const double* __restrict__ uvw,
+// Branch-free loads of the visibility of ordered-stream entry e (callers pass
+// a valid entry for every lane - out-of-range lanes repeat one - and mask the
+// result; a PSF call, vis == NULL, reads its ignored visibility from
+// uvw[0..1]).
+// WIDE = 0 / 1: dense / ragged entries (compile time); -1: decided by m.delta
+template <typename VisT, int WK, int WIDE = -1>
+__device__ __forceinline__ void fetch_raw(uint64_t e, const double* __restrict__ uvw,
                                           const double* __restrict__ fx, const VisT* __restrict__ vis_ld,
                                           bool unit_vis, const void* __restrict__ wgt, const RowMap& m,
                                           RawFetch<VisT, WK>& f) {
-  const int64_t il = ok ? i : 0;
-  int64_t r, c;
-  vis_rowchan(m, il, &r, &c);
+  int64_t il, r, c;
+  if constexpr (WIDE < 0) perm_decode(e, m, &il, &r, &c);
+  else perm_decode_t<WIDE == 1>(e, m, &il, &r, &c);
   f.u = uvw[3 * r];
   f.v = uvw[3 * r + 1];
   f.w = uvw[3 * r + 2];
@@ -223,18 +226,21 @@ __device__ __forceinline__ void grid_fetched(const VisFetch& f, const GridGeomet
 #endif
 }
 
-template <int W, typename VisT, int WK, bool WSTACK, bool PERM, bool PACK>
+// PERM: 0 = tile order through the row slices, 1 / 2 = the bank-class ordered
+// stream of dense (u32) / ragged (u64) entries
+template <int W, typename VisT, int WK, bool WSTACK, int PERM, bool PACK>
 __global__ __launch_bounds__(kScatterThreads, CIP_SCATTER_WAVES) void scatter_kernel(
     const double* __restrict__ uvw, const double* __restrict__ fx, const VisT* __restrict__ vis,
     const void* __restrict__ wgt, RowMap m, const uint64_t* __restrict__ runs,
     const int64_t* __restrict__ run_goff, const int64_t* __restrict__ tile_run_off,
-    const uint32_t* __restrict__ perm, const Chunk* __restrict__ chunks, int64_t chunk_begin, GridGeometry g,
+    const void* __restrict__ perm, const Chunk* __restrict__ chunks, int64_t chunk_begin, GridGeometry g,
     int64_t plane, double fixed_scale, double inv_scale, double* __restrict__ grid) {
   constexpr int T = kTile;
   constexpr int P = T + W - 1;
   __shared__ unsigned long long sub[P * P * (PACK ? 1 : 2)];
   __shared__ int64_t s_voff[PERM ? 1 : kRunBatch + 1];
   __shared__ uint64_t s_run[PERM ? 1 : kRunBatch];
+  constexpr bool kWide = PERM == 2;
 
   const Chunk ch = chunks[chunk_begin + blockIdx.x];
   int64_t X0, Y0;
@@ -255,17 +261,17 @@ __global__ __launch_bounds__(kScatterThreads, CIP_SCATTER_WAVES) void scatter_ke
     RawFetch<VisT, WK> cur;
     int64_t qn = q + kScatterThreads;
     bool hn = qn < ch.g1;
-    uint32_t pn = 0;
+    uint64_t pn = 0;
     if (have) {
-      fetch_raw<VisT, WK>((int64_t)perm[q], true, uvw, fx, vis_ld, unit_vis, wgt, m, cur);
-      pn = perm[hn ? qn : q];
+      fetch_raw<VisT, WK, kWide>(perm_entry_t<kWide>(perm, q), uvw, fx, vis_ld, unit_vis, wgt, m, cur);
+      pn = perm_entry_t<kWide>(perm, hn ? qn : q);
     }
     while (have) {
       const int64_t qnn = qn + kScatterThreads;
       const bool hnn = qnn < ch.g1;
-      const uint32_t pnn = perm[hnn ? qnn : q];
+      const uint64_t pnn = perm_entry_t<kWide>(perm, hnn ? qnn : q);
       RawFetch<VisT, WK> nxt;
-      fetch_raw<VisT, WK>((int64_t)pn, hn, uvw, fx, vis_ld, unit_vis, wgt, m, nxt);
+      fetch_raw<VisT, WK, kWide>(pn, uvw, fx, vis_ld, unit_vis, wgt, m, nxt);
       grid_fetched<W, WSTACK, PACK>(from_raw<VisT, WK>(cur, unit_vis), g, plane, X0, Y0, fixed_scale, sub);
       cur = nxt;
       q = qn;
@@ -341,7 +347,7 @@ template <int W, typename VisT, int WK>
 inline hipError_t scatter_dispatch_ws(bool ws, bool pack, dim3 grid_dim, hipStream_t s, const double* uvw,
                                       const double* fx, const void* vis, const void* wgt, const RowMap& m,
                                       const uint64_t* runs, const int64_t* run_goff, const int64_t* tile_run_off,
-                                      const uint32_t* perm, const Chunk* chunks, int64_t chunk_begin,
+                                      const void* perm, const Chunk* chunks, int64_t chunk_begin,
                                       const GridGeometry& g, int64_t plane, double fs, double* grid) {
 #define LAUNCH(WSV, PRM, PK)                                                                               \
   scatter_kernel<W, VisT, WK, WSV, PRM, PK><<<grid_dim, dim3(kScatterThreads), 0, s>>>(                    \
@@ -358,21 +364,26 @@ inline hipError_t scatter_dispatch_ws(bool ws, bool pack, dim3 grid_dim, hipStre
   // the packed single-precision class exists for complex64 input only (the
   // reference's configuration; raw linear-feed columns are complex64 too)
   bool done = false;
+  const bool wide = m.delta != nullptr;  // ragged row slices: u64 entries
   if constexpr (std::is_same<VisT, float2>::value || std::is_same<VisT, Pol4>::value) {
     if (pack) {
-      if (perm) {
-        LAUNCH_WS(true, true)
+      if (perm && wide) {
+        LAUNCH_WS(2, true)
+      } else if (perm) {
+        LAUNCH_WS(1, true)
       } else {
-        LAUNCH_WS(false, true)
+        LAUNCH_WS(0, true)
       }
       done = true;
     }
   }
   if (!done) {
-    if (perm) {
-      LAUNCH_WS(true, false)
+    if (perm && wide) {
+      LAUNCH_WS(2, false)
+    } else if (perm) {
+      LAUNCH_WS(1, false)
     } else {
-      LAUNCH_WS(false, false)
+      LAUNCH_WS(0, false)
     }
   }
 #undef LAUNCH_WS
@@ -384,7 +395,7 @@ template <int W>
 hipError_t launch_scatter_w(int vis_dtype, int wgt_dtype, bool pack, dim3 gd, hipStream_t s,
                                      const double* uvw, const double* fx, const void* vis, const void* wgt,
                                      const RowMap& m, const uint64_t* runs, const int64_t* run_goff,
-                                     const int64_t* tile_run_off, const uint32_t* perm, const Chunk* chunks,
+                                     const int64_t* tile_run_off, const void* perm, const Chunk* chunks,
                                      int64_t cb, const GridGeometry& g, int64_t plane, double fs, double* grid) {
   const bool ws = g.do_wstacking != 0;
 #define ARGS \

@@ -71,7 +71,7 @@ template <int W, typename VisT, int WK, bool WSTACK, bool PERM>
 __global__ __launch_bounds__(kLargeThreads) void scatter_large_kernel(
     const double* __restrict__ uvw, const double* __restrict__ fx, const VisT* __restrict__ vis,
     const void* __restrict__ wgt, RowMap m, const uint64_t* __restrict__ runs, const int64_t* __restrict__ run_goff,
-    const uint32_t* __restrict__ perm, const Chunk* __restrict__ chunks, int64_t chunk_begin, GridGeometry g,
+    const void* __restrict__ perm, const Chunk* __restrict__ chunks, int64_t chunk_begin, GridGeometry g,
     int64_t plane, double fixed_scale, double inv_scale, double* __restrict__ grid) {
   extern __shared__ unsigned long long sub[];  // re plane, then im plane: 2 P^2 cells
   constexpr int T = kTile;
@@ -98,9 +98,9 @@ __global__ __launch_bounds__(kLargeThreads) void scatter_large_kernel(
   for (int64_t q0 = ch.g0 + (int64_t)wave * 64; q0 < ch.g1; q0 += kLargeThreads) {
     const int64_t q = q0 + lane;
     const bool ok = q < ch.g1;
-    int64_t idx;
+    uint64_t idx;  // ordered-stream entry (perm_encode form)
     if constexpr (PERM) {
-      idx = (int64_t)perm[ok ? q : ch.g0];
+      idx = perm_entry(perm, m, ok ? q : ch.g0);
     } else {
       // the chunk's row slices [first_run, last_run]: last slice starting at or before q
       const int64_t qq = ok ? q : ch.g0;
@@ -111,10 +111,10 @@ __global__ __launch_bounds__(kLargeThreads) void scatter_large_kernel(
         else hi = mid - 1;
       }
       const uint64_t rec = runs[lo];
-      idx = vis_index(m, (int64_t)(rec >> 32), (int64_t)((rec >> 16) & 0xffff) + (qq - run_goff[lo]));
+      idx = perm_encode(m, (int64_t)(rec >> 32), (int64_t)((rec >> 16) & 0xffff) + (qq - run_goff[lo]));
     }
     RawFetch<VisT, WK> raw;
-    fetch_raw<VisT, WK>(idx, ok, uvw, fx, vis_ld, unit_vis, wgt, m, raw);
+    fetch_raw<VisT, WK>(idx, uvw, fx, vis_ld, unit_vis, wgt, m, raw);
     const VisFetch f = from_raw<VisT, WK>(raw, unit_vis);
     int64_t ix0, iy0, iw0;
     double yu, yv, yw;
@@ -180,7 +180,7 @@ __global__ __launch_bounds__(kLargeThreads) void scatter_large_kernel(
 template <int W, typename VisT, int WK, bool WSTACK, bool PERM>
 static hipError_t launch_large_one(dim3 gd, hipStream_t s, const double* uvw, const double* fx, const void* vis,
                                    const void* wgt, const RowMap& m, const uint64_t* runs, const int64_t* run_goff,
-                                   const uint32_t* perm, const Chunk* chunks, int64_t cb, const GridGeometry& g,
+                                   const void* perm, const Chunk* chunks, int64_t cb, const GridGeometry& g,
                                    int64_t plane, double fs, double* grid) {
   constexpr int P = kTile + W - 1;
   constexpr size_t lds = (size_t)2 * P * P * sizeof(unsigned long long);
@@ -200,7 +200,7 @@ static hipError_t launch_large_one(dim3 gd, hipStream_t s, const double* uvw, co
 template <int W, typename VisT, int WK>
 static hipError_t launch_large_vt(dim3 gd, hipStream_t s, const double* uvw, const double* fx, const void* vis,
                                   const void* wgt, const RowMap& m, const uint64_t* runs, const int64_t* run_goff,
-                                  const uint32_t* perm, const Chunk* chunks, int64_t cb, const GridGeometry& g,
+                                  const void* perm, const Chunk* chunks, int64_t cb, const GridGeometry& g,
                                   int64_t plane, double fs, double* grid) {
 #define ARGS gd, s, uvw, fx, vis, wgt, m, runs, run_goff, perm, chunks, cb, g, plane, fs, grid
   if (g.do_wstacking) {
@@ -215,7 +215,7 @@ static hipError_t launch_large_vt(dim3 gd, hipStream_t s, const double* uvw, con
 template <int W>
 hipError_t launch_scatter_large_w(int vis_dtype, int wgt_dtype, dim3 gd, hipStream_t s, const double* uvw,
                                   const double* fx, const void* vis, const void* wgt, const RowMap& m,
-                                  const uint64_t* runs, const int64_t* run_goff, const uint32_t* perm,
+                                  const uint64_t* runs, const int64_t* run_goff, const void* perm,
                                   const Chunk* chunks, int64_t cb, const GridGeometry& g, int64_t plane, double fs,
                                   double* grid) {
   if (g.support != W) return hipErrorInvalidValue;
@@ -234,7 +234,7 @@ hipError_t launch_scatter_large_w(int vis_dtype, int wgt_dtype, dim3 gd, hipStre
 
 template hipError_t launch_scatter_large_w<CIP_LARGE_W>(int, int, dim3, hipStream_t, const double*, const double*,
                                                         const void*, const void*, const RowMap&, const uint64_t*,
-                                                        const int64_t*, const uint32_t*, const Chunk*, int64_t,
+                                                        const int64_t*, const void*, const Chunk*, int64_t,
                                                         const GridGeometry&, int64_t, double, double*);
 
 }  // namespace cip
