@@ -280,7 +280,8 @@ struct FftPlan {
 
 struct PlanResult {
   int64_t nruns = 0, ntiles = 0, nchunks = 0;
-  std::vector<int64_t> plane_chunk_off;  // chunk offset of tile layer iw (ntw + 1)
+  std::vector<int64_t> plane_chunk_off;  // chunk offset of each range: w plane group q (ngroups + 1), or the 2-D layer
+  int group = 1;                         // w planes per work unit (w-stacking plane groups)
   uint64_t* runs = nullptr;
   int64_t* run_goff = nullptr;
   int64_t* tile_run_off = nullptr;
@@ -305,6 +306,7 @@ struct Workspace {
   // the "grid" buffer when it is known all-zero (the masked FFT pass A zeroes
   // what the scatter wrote), else NULL
   double* grid_clean = nullptr;
+  int64_t grid_clean_planes = 0;  // how many of its leading planes are known zero
   // CIP_ASYNC pipelining (cip_ms2dirty): consecutive calls alternate between
   // two sets of planner buffers (parity; buf() appends the parity to buffer
   // names while parity_scope is set), so the planner of call k + 1 runs on
@@ -618,7 +620,8 @@ static int radix_group(int pass) {
 // *maxabs (the place pass reads the visibilities anyway).
 static int make_plan(Workspace* ws, const double* uvw, const double* fx, const RowMap& m,
                      const void* vis, int vis_dtype, const void* wgt, int wgt_dtype, double* red,
-                     const GridGeometry& g, int64_t cv, hipStream_t s, PlanResult* pr, double* maxabs) {
+                     const GridGeometry& g, int64_t cv, hipStream_t s, PlanResult* pr, double* maxabs,
+                     int group = 1) {
   const int64_t ntiles = g.ntx * g.nty * g.ntw;
   pr->ntiles = ntiles;
   CIP_ALLOC(tile_runs, int64_t, "tile_runs", ntiles + 1)
@@ -711,16 +714,18 @@ static int make_plan(Workspace* ws, const double* uvw, const double* fx, const R
   // make that a contiguous range), plane after plane
   const int64_t ntxy = g.ntx * g.nty;
   const bool per_plane = g.do_wstacking != 0;
-  const int64_t nrange = per_plane ? g.nplanes : 1;  // chunk ranges: per plane, or the one 2-D layer
+  pr->group = per_plane ? group : 1;
+  const int64_t ngroups = per_plane ? (g.nplanes + group - 1) / group : 1;
+  const int64_t nrange = ngroups;  // chunk ranges: per plane group, or the one 2-D layer
   const int full_first = (!per_plane && chunks_full_first()) ? 1 : 0;
   CIP_ALLOC(layer_off, int64_t, "layer_off", nrange + 1)
   int64_t* pc_off = nullptr;
   if (per_plane) {
-    const int64_t nentp = g.nplanes * ntxy;
+    const int64_t nentp = ngroups * ntxy;
     pc_off = buf<int64_t>(ws, "plane_chunk_cnt", nentp + 1);
     int64_t* scan_tmpp = buf<int64_t>(ws, "scan_tmp_pchunks", scan_tmp_elems(nentp + 1));
     if (!pc_off || !scan_tmpp) return CIP_ENOMEM;
-    CIP_HIP_CHECK(launch_plane_chunk_counts(tile_vis_off, ntxy, g.ntw, g.nplanes, g.support, cv, pc_off, s));
+    CIP_HIP_CHECK(launch_plane_chunk_counts(tile_vis_off, ntxy, g.ntw, ngroups, group, g.support, cv, pc_off, s));
     CIP_HIP_CHECK(exclusive_scan_i64(pc_off, nentp + 1, scan_tmpp, s));
     CIP_HIP_CHECK(launch_gather_i64(pc_off, ntxy, nrange + 1, layer_off, s));
   } else {
@@ -746,8 +751,8 @@ static int make_plan(Workspace* ws, const double* uvw, const double* fx, const R
   pr->nchunks = pr->plane_chunk_off.back();
   CIP_ALLOC(chunks, Chunk, "chunks", pr->nchunks)
   if (per_plane)
-    CIP_HIP_CHECK(launch_plane_chunk_emit(tile_vis_off, pc_off, run_goff, tile_runs, ntxy, g.ntw, g.nplanes, g.support,
-                                          cv, pr->nchunks, chunks, s));
+    CIP_HIP_CHECK(launch_plane_chunk_emit(tile_vis_off, pc_off, run_goff, tile_runs, ntxy, g.ntw, ngroups, group,
+                                          g.support, cv, pr->nchunks, chunks, s));
   else
     CIP_HIP_CHECK(launch_chunk_emit(tile_vis_off, tile_vis, chunk_off, run_goff, tile_runs, ntiles, cv, full_first,
                                     pr->nchunks, chunks, s));
@@ -773,6 +778,25 @@ static bool public_dtypes(int vis_dtype, int wgt_dtype) {
 static bool vis_dtype_ok(int d) { return d == CIP_C64 || d == CIP_C128 || d == CIP_POL4I; }
 static bool wgt_dtype_ok(int d) { return d == CIP_NONE || d == CIP_F32 || d == CIP_F64 || d == CIP_POL4I; }
 
+// w planes per scatter work unit in w-stacking mode: 2 (a visibility placed
+// and its u, v, w kernels evaluated once for two planes; the unit holds two
+// sub-grids in 512-thread blocks) for the lane-per-visibility supports,
+// CIP_WSTACK_GROUP=1 one plane per unit (A/B); the large supports always 1.
+static int wstack_group(const GridGeometry& g) {
+  static const int env = [] {
+    const char* e = getenv("CIP_WSTACK_GROUP");
+    const int v = e ? atoi(e) : 2;
+    return v < 1 ? 1 : (v > 3 ? 3 : v);
+  }();
+  if (!g.do_wstacking || g.support > 16 || g.nplanes < 2) return 1;
+  // two 512-thread blocks per CU must fit their G sub-grids in 160 KB of LDS
+  const int64_t P = kTile + g.support - 1;
+  const int64_t per_plane = P * P * 16;
+  int G = env;
+  while (G > 1 && 2 * G * per_plane > 160 * 1024) --G;
+  return G;
+}
+
 struct Prepared {
   cip_gridder_params p;
   GridGeometry g;
@@ -797,7 +821,8 @@ static int prepare(Workspace* ws, const double* uvw, int64_t nrow, const double*
                    const void* vis, int vis_dtype, const void* wgt, int wgt_dtype, int64_t npix_x, int64_t npix_y,
                    double px, double py, double epsilon, int support, int do_wstacking, bool packed,
                    const cip_gridder_params* given, hipStream_t s, Prepared* out, double** grid_out = nullptr,
-                   const RaggedRows* ragged = nullptr, bool reuse = false, const uint8_t* flags4 = nullptr) {
+                   const RaggedRows* ragged = nullptr, bool reuse = false, const uint8_t* flags4 = nullptr,
+                   bool want_group = true) {
   if (!ws->parity_scope) ws->plan_unscoped = true;
   if (!vis_dtype_ok(vis_dtype)) return set_error(CIP_EINVAL, "vis dtype must be complex64 or complex128");
   if (!wgt_dtype_ok(wgt_dtype)) return set_error(CIP_EINVAL, "wgt dtype must be float32, float64 or none");
@@ -868,7 +893,7 @@ static int prepare(Workspace* ws, const double* uvw, int64_t nrow, const double*
   // promise)
   const std::vector<double> key = {(double)nrow, (double)nchan, (double)npix_x, (double)npix_y, px, py, epsilon,
                                    (double)support, (double)do_wstacking, (double)packed,
-                                   given ? 1.0 : 0.0};
+                                   given ? 1.0 : 0.0, want_group ? 1.0 : 0.0};
   const bool reusing = reuse && !ragged && given == nullptr && ws->saved_valid && ws->saved_key == key;
   if (reusing) given = &ws->saved_p;
   double wmin = 0.0, wmax = 0.0;
@@ -907,11 +932,12 @@ static int prepare(Workspace* ws, const double* uvw, int64_t nrow, const double*
   out->fx = fx;
   out->red = red;
   if (grid_out) {
-    // the grid is known now: zero its first plane beside the planner
-    const size_t gbytes = sizeof(double) * 2 * out->g.nu * out->g.nv;
-    double* grid = buf<double>(ws, "grid", 2 * out->g.nu * out->g.nv);
+    // the grid is known now: zero its first plane group beside the planner
+    const int64_t gplanes = want_group ? wstack_group(out->g) : 1;
+    const size_t gbytes = sizeof(double) * 2 * out->g.nu * out->g.nv * gplanes;
+    double* grid = buf<double>(ws, "grid", 2 * out->g.nu * out->g.nv * gplanes);
     if (!grid) return CIP_ENOMEM;
-    if (ws->grid_clean != grid) {
+    if (ws->grid_clean != grid || ws->grid_clean_planes < gplanes) {
       const int zr = zero_on_side(ws, grid, gbytes, s);
       if (zr != CIP_OK) return zr;
     }
@@ -922,14 +948,14 @@ static int prepare(Workspace* ws, const double* uvw, int64_t nrow, const double*
   if (nrow == 0) {
     CIP_HIP_CHECK(hipMemsetAsync(red, 0, 2 * sizeof(double), s));
     out->plan = PlanResult();
-    out->plan.plane_chunk_off.assign((out->g.do_wstacking ? out->g.nplanes : 1) + 1, 0);
+    out->plan.plane_chunk_off.assign((out->g.do_wstacking ? out->g.nplanes : 1) + 1, 0);  // group 1
     return CIP_OK;
   }
   double maxabs = 0.0;
   if (m.nvis == 0) {
     CIP_HIP_CHECK(hipMemsetAsync(red, 0, 2 * sizeof(double), s));
     out->plan = PlanResult();
-    out->plan.plane_chunk_off.assign((out->g.do_wstacking ? out->g.nplanes : 1) + 1, 0);
+    out->plan.plane_chunk_off.assign((out->g.do_wstacking ? out->g.nplanes : 1) + 1, 0);  // group 1
     return CIP_OK;
   }
   int rc;
@@ -953,7 +979,7 @@ static int prepare(Workspace* ws, const double* uvw, int64_t nrow, const double*
   } else {
     ws->saved_valid = false;
     rc = make_plan(ws, uvw, fx, m, vis, vis_dtype, wgt, wgt_dtype, red, out->g, chunk_vis(packed, out->g.nu), s,
-                   &out->plan, &maxabs);
+                   &out->plan, &maxabs, want_group ? wstack_group(out->g) : 1);
     if (rc == CIP_OK && !ragged) {
       ws->saved_key = key;
       ws->saved_p = out->p;
@@ -976,23 +1002,27 @@ static int prepare(Workspace* ws, const double* uvw, int64_t nrow, const double*
   return rc;
 }
 
+// Work-unit range q of the plan (w-stacking: plane group q = planes
+// [q G, q G + G), written to grid + k planes for plane q G + k; 2-D: q = 0).
 // transposed: store the grid as gT[y, x] (input layout of the pruned FFT)
-// zeroed: the grid was zeroed already (side stream, joined by the caller)
-static int scatter_plane(const Prepared& pp, int64_t plane, const double* uvw, const void* vis, int vis_dtype,
+// zeroed: the group's planes were zeroed already (side stream, joined by the caller)
+static int scatter_plane(const Prepared& pp, int64_t q, const double* uvw, const void* vis, int vis_dtype,
                          const void* wgt, int wgt_dtype, bool transposed, double* grid,
                          hipStream_t s, bool zeroed = false) {
   GridGeometry g = pp.g;
   g.transposed = transposed ? 1 : 0;
-  if (!zeroed) CIP_HIP_CHECK(hipMemsetAsync(grid, 0, sizeof(double) * 2 * g.nu * g.nv, s));
+  const int G = pp.plan.group;
+  const int64_t p0 = g.do_wstacking ? q * G : 0;
+  const int64_t np = g.do_wstacking ? std::min<int64_t>(G, g.nplanes - p0) : 1;
+  if (!zeroed) CIP_HIP_CHECK(hipMemsetAsync(grid, 0, sizeof(double) * 2 * g.nu * g.nv * np, s));
   if (pp.plan.nchunks == 0) return CIP_OK;
-  // the plane's work units (w-stacking: its tiles' layers p - W + 1 .. p)
-  const int64_t k = g.do_wstacking ? plane : 0;
+  const int64_t k = g.do_wstacking ? q : 0;
   const int64_t cb = pp.plan.plane_chunk_off[k], ce = pp.plan.plane_chunk_off[k + 1];
   if (wgt == nullptr) wgt_dtype = CIP_NONE;
   hipEvent_t a = g_prof.mark(s);
-  CIP_HIP_CHECK(launch_scatter(g.support, vis_dtype, wgt_dtype, pp.packed, uvw, pp.fx, vis, wgt, pp.m, pp.plan.runs,
-                               pp.plan.run_goff, pp.plan.tile_run_off, pp.plan.perm, pp.plan.chunks, cb, ce - cb,
-                               g, plane, pp.fixed_scale, grid, s));
+  CIP_HIP_CHECK(launch_scatter(g.support, vis_dtype, wgt_dtype, pp.packed, G, uvw, pp.fx, vis, wgt, pp.m,
+                               pp.plan.runs, pp.plan.run_goff, pp.plan.tile_run_off, pp.plan.perm, pp.plan.chunks, cb,
+                               ce - cb, g, p0, pp.fixed_scale, grid, s));
   g_prof.span(2, a, g_prof.mark(s));
   if (ce > cb) g_prof.counts[4] += 1;
   return CIP_OK;
@@ -1154,8 +1184,9 @@ static int grid_accumulate(const double* uvw, int64_t nrow, const double* freq, 
   const GridGeometry& g = pp.g;
   const bool transposed = grid_is_transposed(g, npix_x, npix_y);
   const int64_t plane_elems = 2 * g.nu * g.nv;
-  for (int64_t p = 0; p < g.nplanes; ++p) {
-    rc = scatter_plane(pp, p, uvw, vis, vis_dtype, wgt, wgt_dtype, transposed, grids + p * plane_elems, s, true);
+  const int G = pp.plan.group;
+  for (int64_t q = 0; q * G < g.nplanes; ++q) {
+    rc = scatter_plane(pp, q, uvw, vis, vis_dtype, wgt, wgt_dtype, transposed, grids + q * G * plane_elems, s, true);
     if (rc != CIP_OK) return rc;
   }
   if (sum_wgt) CIP_HIP_CHECK(launch_add_scalar(pp.red, sum_wgt, s));
@@ -1273,20 +1304,25 @@ static int ms2dirty_impl(const double* uvw, int64_t nrow, const double* freq, in
   const GridGeometry& g = pp.g;
   // zeroed beside the planner, or left all-zero by the previous call
   bool clean = grid != nullptr;
-  if (!grid) grid = buf<double>(ws, "grid", 2 * g.nu * g.nv);
+  const int G = pp.plan.group;
+  const int64_t plane_elems = 2 * g.nu * g.nv;
+  if (!grid) grid = buf<double>(ws, "grid", plane_elems * G);
   if (!grid) return CIP_ENOMEM;
-  clean = clean || ws->grid_clean == grid;
+  const int64_t prev_clean = ws->grid_clean == grid ? ws->grid_clean_planes : 0;
+  clean = clean || prev_clean >= G;
   DirtyStage st;
   rc = dirty_stage(ws, g, npix_x, npix_y, pixsize_x, pixsize_y, s, &st);
   if (rc != CIP_OK) return rc;
   ws->grid_clean = nullptr;  // dirty until a masked pass A has consumed every written tile
   const uint32_t* dmask = st.fast ? pp.plan.dmask : nullptr;
-  for (int64_t p = 0; p < g.nplanes; ++p) {
-    rc = scatter_plane(pp, p, uvw, vis, vis_dtype, wgt, wgt_dtype, st.fast, grid, s, clean);
+  for (int64_t q = 0; q * G < g.nplanes; ++q) {
+    rc = scatter_plane(pp, q, uvw, vis, vis_dtype, wgt, wgt_dtype, st.fast, grid, s, clean);
     if (rc != CIP_OK) return rc;
-    rc = plane_to_dirty(st, g, p, grid, dirty_out, s, dmask ? dmask + p * (g.ntx * g.nty / 32) : nullptr,
-                        normalise ? pp.red : nullptr);
-    if (rc != CIP_OK) return rc;
+    for (int64_t p = q * G; p < std::min<int64_t>(q * G + G, g.nplanes); ++p) {
+      rc = plane_to_dirty(st, g, p, grid + (p - q * G) * plane_elems, dirty_out, s,
+                          dmask ? dmask + p * (g.ntx * g.nty / 32) : nullptr, normalise ? pp.red : nullptr);
+      if (rc != CIP_OK) return rc;
+    }
     clean = dmask != nullptr;
   }
   rc = finish_dirty(ws, st, pp.p, g, dirty_out, s);
@@ -1301,7 +1337,10 @@ static int ms2dirty_impl(const double* uvw, int64_t nrow, const double* freq, in
   // grid-clean mark holds in stream order too
   if (!(flags & CIP_ASYNC) || g_prof.on) CIP_HIP_CHECK(hipStreamSynchronize(s));
   else ws->async_stream = s;
-  if (clean) ws->grid_clean = grid;
+  if (clean) {
+    ws->grid_clean = grid;
+    ws->grid_clean_planes = std::max<int64_t>(prev_clean, G);
+  }
   g_prof.finish();
   return CIP_OK;
 }
@@ -1417,7 +1456,8 @@ int cip_grid_plane(const double* uvw, int64_t nrow, const double* freq, int64_t 
   hipEvent_t t_start = g_prof.mark(s);
   Prepared pp;
   int rc = prepare(ws, uvw, nrow, freq, nchan, vis, vis_dtype, wgt, wgt_dtype, 2, 2, pixsize_x, pixsize_y, 0.0,
-                   params->support, params->do_wstacking, (flags & CIP_ACC_SINGLE) != 0, params, s, &pp);
+                   params->support, params->do_wstacking, (flags & CIP_ACC_SINGLE) != 0, params, s, &pp, nullptr,
+                   nullptr, false, nullptr, false);
   if (rc != CIP_OK) return rc;
   rc = scatter_plane(pp, plane, uvw, vis, vis_dtype, wgt, wgt_dtype, false, grid_out, s);
   if (rc != CIP_OK) return rc;

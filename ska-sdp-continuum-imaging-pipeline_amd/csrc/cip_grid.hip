@@ -251,7 +251,7 @@ hipError_t launch_order(const double* uvw, const double* fx, const uint8_t* vis_
   return hipGetLastError();
 }
 
-hipError_t launch_scatter(int support, int vis_dtype, int wgt_dtype, bool packed, const double* uvw,
+hipError_t launch_scatter(int support, int vis_dtype, int wgt_dtype, bool packed, int group, const double* uvw,
                           const double* fx, const void* vis, const void* wgt, const RowMap& m, const uint64_t* runs,
                           const int64_t* run_goff, const int64_t* tile_run_off, const void* perm,
                           const Chunk* chunks, int64_t chunk_begin, int64_t nchunks, const GridGeometry& g,
@@ -261,7 +261,7 @@ hipError_t launch_scatter(int support, int vis_dtype, int wgt_dtype, bool packed
   const dim3 gd((unsigned)nchunks);
 #define CASE(WW)                                                                                             \
   case WW:                                                                                                   \
-    return launch_scatter_w<WW>(vis_dtype, wgt_dtype, packed, gd, s, uvw, fx, vis, wgt, m, runs,           \
+    return launch_scatter_w<WW>(vis_dtype, wgt_dtype, packed, group, gd, s, uvw, fx, vis, wgt, m, runs,    \
                                   run_goff, tile_run_off, perm, chunks, chunk_begin, g, plane, fixed_scale, grid);
   switch (support) {
     CASE(4)
@@ -273,8 +273,8 @@ hipError_t launch_scatter(int support, int vis_dtype, int wgt_dtype, bool packed
     CASE(16)
 #define LARGE(WW)                                                                                              \
   case WW:                                                                                                     \
-    /* wave-per-visibility scatter (cip_scatter_large.hip); fp64 class only */                                 \
-    if (packed) return hipErrorInvalidValue;                                                                   \
+    /* wave-per-visibility scatter (cip_scatter_large.hip); fp64 class, one plane per unit */                  \
+    if (packed || group != 1) return hipErrorInvalidValue;                                                     \
     return launch_scatter_large_w<WW>(vis_dtype, wgt_dtype, gd, s, uvw, fx, vis, wgt, m, runs, run_goff, perm, \
                                       chunks, chunk_begin, g, plane, fixed_scale, grid);
     LARGE(24)

@@ -88,11 +88,12 @@ hipError_t launch_chunk_emit(const int64_t* tile_vis_off, const int64_t* tile_vi
                              const int64_t* run_goff, const int64_t* tile_run_off, int64_t ntiles,
                              int64_t chunk_vis, int full_first, int64_t nchunks, Chunk* chunks, hipStream_t s);
 // w-stacking: per (plane, uv tile) work units over the tile's merged layer range
-hipError_t launch_plane_chunk_counts(const int64_t* tile_vis_off, int64_t ntxy, int64_t ntw, int64_t nplanes,
-                                     int support, int64_t cv, int64_t* out, hipStream_t s);
+// per plane group (planes [q G, q G + G), ngroups groups): its work units per uv tile
+hipError_t launch_plane_chunk_counts(const int64_t* tile_vis_off, int64_t ntxy, int64_t ntw, int64_t ngroups,
+                                     int group, int support, int64_t cv, int64_t* out, hipStream_t s);
 hipError_t launch_plane_chunk_emit(const int64_t* tile_vis_off, const int64_t* chunk_off, const int64_t* run_goff,
-                                   const int64_t* tile_run_off, int64_t ntxy, int64_t ntw, int64_t nplanes,
-                                   int support, int64_t cv, int64_t nchunks, Chunk* chunks, hipStream_t s);
+                                   const int64_t* tile_run_off, int64_t ntxy, int64_t ntw, int64_t ngroups,
+                                   int group, int support, int64_t cv, int64_t nchunks, Chunk* chunks, hipStream_t s);
 hipError_t launch_gather_i64(const int64_t* src, int64_t stride, int64_t count, int64_t* dst,
                              hipStream_t s);
 
@@ -105,7 +106,8 @@ hipError_t launch_prep_final(const double* partial, int nblocks, double* out2, h
 // located through the tile's row slices in tile order).
 // one kernel support W (instantiated in cip_scatter_w.hip for W = 4, 6, ..., 16)
 template <int W>
-hipError_t launch_scatter_w(int vis_dtype, int wgt_dtype, bool pack, dim3 gd, hipStream_t s, const double* uvw,
+hipError_t launch_scatter_w(int vis_dtype, int wgt_dtype, bool pack, int group, dim3 gd, hipStream_t s,
+                            const double* uvw,
                             const double* fx, const void* vis, const void* wgt, const RowMap& m,
                             const uint64_t* runs, const int64_t* run_goff, const int64_t* tile_run_off,
                             const void* perm, const Chunk* chunks, int64_t cb, const GridGeometry& g,
@@ -118,7 +120,9 @@ hipError_t launch_scatter_large_w(int vis_dtype, int wgt_dtype, dim3 gd, hipStre
                                   const uint64_t* runs, const int64_t* run_goff, const void* perm,
                                   const Chunk* chunks, int64_t cb, const GridGeometry& g, int64_t plane, double fs,
                                   double* grid);
-hipError_t launch_scatter(int support, int vis_dtype, int wgt_dtype, bool packed, const double* uvw,
+// group: w planes per work unit (w-stacking plane groups, 1 or 2; grid = the
+// group's planes, 2 nu nv doubles apart)
+hipError_t launch_scatter(int support, int vis_dtype, int wgt_dtype, bool packed, int group, const double* uvw,
                           const double* fx, const void* vis, const void* wgt, const RowMap& m, const uint64_t* runs,
                           const int64_t* run_goff, const int64_t* tile_run_off, const void* perm,
                           const Chunk* chunks, int64_t chunk_begin, int64_t nchunks, const GridGeometry& g,

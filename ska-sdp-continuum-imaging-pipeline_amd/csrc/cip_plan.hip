@@ -799,26 +799,30 @@ hipError_t launch_chunk_emit(const int64_t* tile_vis_off, const int64_t* tile_vi
 // sub-grid zeroing and one flush per tile and plane instead of one per tile
 // layer (C3, 16 planes: 291k instead of 665k work units). Entry p ntxy + t
 // counts ceil(n / cv) units; out[nplanes ntxy] = 0.
+// plane group q = planes [q G, q G + G): the layers feeding them are
+// [q G - W + 1, q G + G - 1] (clipped to [0, ntw))
 __global__ void plane_chunk_counts_kernel(const int64_t* __restrict__ tile_vis_off, int64_t ntxy, int64_t ntw,
-                                          int64_t nplanes, int support, int64_t cv, int64_t* __restrict__ out) {
+                                          int64_t ngroups, int group, int support, int64_t cv,
+                                          int64_t* __restrict__ out) {
   const int64_t id = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t nent = nplanes * ntxy;
+  const int64_t nent = ngroups * ntxy;
   if (id > nent) return;
   if (id == nent) {
     out[id] = 0;
     return;
   }
-  const int64_t p = id / ntxy, t = id - p * ntxy;
-  const int64_t lo = p - support + 1 > 0 ? p - support + 1 : 0, hi = p < ntw - 1 ? p : ntw - 1;
+  const int64_t q = id / ntxy, t = id - q * ntxy;
+  const int64_t p0 = q * group, p1 = p0 + group - 1;
+  const int64_t lo = p0 - support + 1 > 0 ? p0 - support + 1 : 0, hi = p1 < ntw - 1 ? p1 : ntw - 1;
   const int64_t n = hi < lo ? 0 : tile_vis_off[t * ntw + hi + 1] - tile_vis_off[t * ntw + lo];
   out[id] = (n + cv - 1) / cv;
 }
 
-hipError_t launch_plane_chunk_counts(const int64_t* tile_vis_off, int64_t ntxy, int64_t ntw, int64_t nplanes,
-                                     int support, int64_t cv, int64_t* out, hipStream_t s) {
-  const int64_t n = nplanes * ntxy + 1;
-  plane_chunk_counts_kernel<<<dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s>>>(tile_vis_off, ntxy, ntw, nplanes,
-                                                                                    support, cv, out);
+hipError_t launch_plane_chunk_counts(const int64_t* tile_vis_off, int64_t ntxy, int64_t ntw, int64_t ngroups,
+                                     int group, int support, int64_t cv, int64_t* out, hipStream_t s) {
+  const int64_t n = ngroups * ntxy + 1;
+  plane_chunk_counts_kernel<<<dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s>>>(tile_vis_off, ntxy, ntw, ngroups,
+                                                                                    group, support, cv, out);
   return hipGetLastError();
 }
 
@@ -828,19 +832,20 @@ hipError_t launch_plane_chunk_counts(const int64_t* tile_vis_off, int64_t ntxy, 
 // grid origin, tile_origin), first and last run by binary search.
 __global__ void plane_chunk_emit_kernel(const int64_t* __restrict__ tile_vis_off, const int64_t* __restrict__ chunk_off,
                                         const int64_t* __restrict__ run_goff, const int64_t* __restrict__ tile_run_off,
-                                        int64_t ntxy, int64_t ntw, int64_t nplanes, int support, int64_t cv,
-                                        int64_t nchunks, Chunk* __restrict__ chunks) {
+                                        int64_t ntxy, int64_t ntw, int64_t ngroups, int group, int support,
+                                        int64_t cv, int64_t nchunks, Chunk* __restrict__ chunks) {
   const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= nchunks) return;
-  int64_t lo = 0, hi = nplanes * ntxy - 1;
+  int64_t lo = 0, hi = ngroups * ntxy - 1;
   while (lo < hi) {
     const int64_t mid = (lo + hi + 1) >> 1;
     if (chunk_off[mid] <= j) lo = mid;
     else hi = mid - 1;
   }
   const int64_t e = lo;
-  const int64_t p = e / ntxy, t = e - p * ntxy;
-  const int64_t l0 = p - support + 1 > 0 ? p - support + 1 : 0, l1 = p < ntw - 1 ? p : ntw - 1;
+  const int64_t q = e / ntxy, t = e - q * ntxy;
+  const int64_t p0 = q * group, p1 = p0 + group - 1;
+  const int64_t l0 = p0 - support + 1 > 0 ? p0 - support + 1 : 0, l1 = p1 < ntw - 1 ? p1 : ntw - 1;
   const int64_t k = j - chunk_off[e];
   const int64_t a = tile_vis_off[t * ntw + l0], b = tile_vis_off[t * ntw + l1 + 1];
   Chunk ch;
@@ -865,11 +870,12 @@ __global__ void plane_chunk_emit_kernel(const int64_t* __restrict__ tile_vis_off
 }
 
 hipError_t launch_plane_chunk_emit(const int64_t* tile_vis_off, const int64_t* chunk_off, const int64_t* run_goff,
-                                   const int64_t* tile_run_off, int64_t ntxy, int64_t ntw, int64_t nplanes,
-                                   int support, int64_t cv, int64_t nchunks, Chunk* chunks, hipStream_t s) {
+                                   const int64_t* tile_run_off, int64_t ntxy, int64_t ntw, int64_t ngroups,
+                                   int group, int support, int64_t cv, int64_t nchunks, Chunk* chunks,
+                                   hipStream_t s) {
   if (nchunks <= 0) return hipSuccess;
   plane_chunk_emit_kernel<<<dim3((unsigned)((nchunks + 255) / 256)), dim3(256), 0, s>>>(
-      tile_vis_off, chunk_off, run_goff, tile_run_off, ntxy, ntw, nplanes, support, cv, nchunks, chunks);
+      tile_vis_off, chunk_off, run_goff, tile_run_off, ntxy, ntw, ngroups, group, support, cv, nchunks, chunks);
   return hipGetLastError();
 }
 

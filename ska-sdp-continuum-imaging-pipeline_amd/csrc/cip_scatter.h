@@ -143,7 +143,10 @@ __device__ __forceinline__ VisFetch from_raw(const RawFetch<VisT, WK>& r, bool u
   return f;
 }
 
-template <int W, bool WSTACK, bool PACK>
+// One visibility onto the unit's sub-grid(s). G > 1 (w-stacking): the unit
+// grids planes plane .. plane + G - 1 at once (G sub-grids, S u64 apart), the
+// visibility placed and its u, v, w kernels evaluated once for all of them.
+template <int W, bool WSTACK, bool PACK, int G = 1>
 __device__ __forceinline__ void grid_fetched(const VisFetch& f, const GridGeometry& g, int64_t plane, int64_t X0,
                                              int64_t Y0, double fixed_scale, unsigned long long* sub) {
   constexpr int T = kTile;
@@ -154,6 +157,52 @@ __device__ __forceinline__ void grid_fetched(const VisFetch& f, const GridGeomet
   if (!place_vis(f.u, f.v, f.w, f.fx, g, &ix0, &yu, &iy0, &yv, &iw0, &yw)) return;
   const int64_t lx = ix0 - X0, ly = iy0 - Y0;
   if (lx < 0 || lx >= T || ly < 0 || ly >= T) return;  // never for a consistent plan
+  if constexpr (G > 1) {
+    constexpr int S = P * P * (PACK ? 1 : 2);
+    double kwv[W], ku[W], kv[W];
+    eval_kernel<W>(yw, kwv);
+    eval_kernel<W>(yu, ku);
+    eval_kernel<W>(yv, kv);
+    const double sc0 = f.wt * fixed_scale;
+    unsigned long long* base = sub + (lx * P + ly);
+#pragma unroll
+    for (int k = 0; k < G; ++k) {
+      const int64_t kw = plane + k - iw0;
+      if (kw < 0 || kw >= W) continue;  // the visibility does not feed plane + k
+      double sel = 0.0;
+#pragma unroll
+      for (int q = 0; q < W; ++q) sel = (q == kw) ? kwv[q] : sel;
+      const double sc = sc0 * sel;
+      const double vr = f.vr * sc, vi = f.vi * sc;
+      double kr[W], ki[W];
+#pragma unroll
+      for (int j = 0; j < W; ++j) {
+        kr[j] = kv[j] * vr;
+        ki[j] = kv[j] * vi;
+      }
+      unsigned long long* bk = base + k * S;
+#pragma unroll
+      for (int i = 0; i < W; ++i) {
+#pragma unroll
+        for (int j = 0; j < W; ++j) {
+          const double qr = fma(ku[i], kr[j], kMagic);
+          const double qi = fma(ku[i], ki[j], kMagic);
+          const unsigned long long br = (unsigned long long)__double_as_longlong(qr);
+          const unsigned long long bi = (unsigned long long)__double_as_longlong(qi);
+          if constexpr (PACK) {
+            unsigned hi;
+            asm("v_add3_u32 %0, %1, %2, %3" : "=v"(hi) : "v"((unsigned)br), "v"((unsigned)(bi >> 32)),
+                "s"(0u - kMagicHi));
+            atomicAdd(bk + (i * P + j), __builtin_bit_cast(unsigned long long, make_uint2((unsigned)bi, hi)));
+          } else {
+            atomicAdd(bk + (i * P + j), br - 0x4338000000000000ull);
+            atomicAdd(bk + P * P + (i * P + j), bi - 0x4338000000000000ull);
+          }
+        }
+      }
+    }
+    return;
+  }
   double sc = f.wt * fixed_scale;
   if constexpr (WSTACK) {
     const int64_t kw = plane - iw0;
@@ -227,9 +276,14 @@ __device__ __forceinline__ void grid_fetched(const VisFetch& f, const GridGeomet
 }
 
 // PERM: 0 = tile order through the row slices, 1 / 2 = the bank-class ordered
-// stream of dense (u32) / ragged (u64) entries
-template <int W, typename VisT, int WK, bool WSTACK, int PERM, bool PACK>
-__global__ __launch_bounds__(kScatterThreads, CIP_SCATTER_WAVES) void scatter_kernel(
+// stream of dense (u32) / ragged (u64) entries. G: w planes per work unit
+// (w-stacking plane groups; G > 1 runs 512-thread blocks holding G sub-grids).
+template <int G>
+constexpr int scatter_threads() {
+  return G == 1 ? kScatterThreads : 2 * kScatterThreads;
+}
+template <int W, typename VisT, int WK, bool WSTACK, int PERM, bool PACK, int G = 1>
+__global__ __launch_bounds__(scatter_threads<G>(), CIP_SCATTER_WAVES) void scatter_kernel(
     const double* __restrict__ uvw, const double* __restrict__ fx, const VisT* __restrict__ vis,
     const void* __restrict__ wgt, RowMap m, const uint64_t* __restrict__ runs,
     const int64_t* __restrict__ run_goff, const int64_t* __restrict__ tile_run_off,
@@ -237,7 +291,9 @@ __global__ __launch_bounds__(kScatterThreads, CIP_SCATTER_WAVES) void scatter_ke
     int64_t plane, double fixed_scale, double inv_scale, double* __restrict__ grid) {
   constexpr int T = kTile;
   constexpr int P = T + W - 1;
-  __shared__ unsigned long long sub[P * P * (PACK ? 1 : 2)];
+  constexpr int S = P * P * (PACK ? 1 : 2);
+  constexpr int NT = scatter_threads<G>();
+  __shared__ unsigned long long sub[G * S];
   __shared__ int64_t s_voff[PERM ? 1 : kRunBatch + 1];
   __shared__ uint64_t s_run[PERM ? 1 : kRunBatch];
   constexpr bool kWide = PERM == 2;
@@ -245,7 +301,7 @@ __global__ __launch_bounds__(kScatterThreads, CIP_SCATTER_WAVES) void scatter_ke
   const Chunk ch = chunks[chunk_begin + blockIdx.x];
   int64_t X0, Y0;
   tile_origin(ch.tile, g, &X0, &Y0);
-  for (int i = threadIdx.x; i < P * P * (PACK ? 1 : 2); i += kScatterThreads) sub[i] = 0ull;
+  for (int i = threadIdx.x; i < G * S; i += NT) sub[i] = 0ull;
   if constexpr (PACK) {
     fixed_scale *= packed_chunk_gain(ch.g1 - ch.g0);
     inv_scale = 1.0 / fixed_scale;
@@ -259,7 +315,7 @@ __global__ __launch_bounds__(kScatterThreads, CIP_SCATTER_WAVES) void scatter_ke
     int64_t q = ch.g0 + threadIdx.x;
     bool have = q < ch.g1;
     RawFetch<VisT, WK> cur;
-    int64_t qn = q + kScatterThreads;
+    int64_t qn = q + NT;
     bool hn = qn < ch.g1;
     uint64_t pn = 0;
     if (have) {
@@ -267,12 +323,12 @@ __global__ __launch_bounds__(kScatterThreads, CIP_SCATTER_WAVES) void scatter_ke
       pn = perm_entry_t<kWide>(perm, hn ? qn : q);
     }
     while (have) {
-      const int64_t qnn = qn + kScatterThreads;
+      const int64_t qnn = qn + NT;
       const bool hnn = qnn < ch.g1;
       const uint64_t pnn = perm_entry_t<kWide>(perm, hnn ? qnn : q);
       RawFetch<VisT, WK> nxt;
       fetch_raw<VisT, WK, kWide>(pn, uvw, fx, vis_ld, unit_vis, wgt, m, nxt);
-      grid_fetched<W, WSTACK, PACK>(from_raw<VisT, WK>(cur, unit_vis), g, plane, X0, Y0, fixed_scale, sub);
+      grid_fetched<W, WSTACK, PACK, G>(from_raw<VisT, WK>(cur, unit_vis), g, plane, X0, Y0, fixed_scale, sub);
       cur = nxt;
       q = qn;
       have = hn;
@@ -287,7 +343,7 @@ __global__ __launch_bounds__(kScatterThreads, CIP_SCATTER_WAVES) void scatter_ke
     while (v < ch.g1 && r < rb) {
       const int nst = (int)((rb - r) < kRunBatch ? (rb - r) : kRunBatch);
       __syncthreads();
-      for (int k = threadIdx.x; k <= nst; k += kScatterThreads) {
+      for (int k = threadIdx.x; k <= nst; k += NT) {
         s_voff[k] = run_goff[r + k];
         if (k < nst) s_run[k] = runs[r + k];
       }
@@ -299,11 +355,11 @@ __global__ __launch_bounds__(kScatterThreads, CIP_SCATTER_WAVES) void scatter_ke
       VisFetch cur;
       if (have) fetch_vis<VisT, WK>(q, s_voff, s_run, nst, uvw, fx, vis, wgt, m, cur);
       while (have) {
-        const int64_t qn = q + kScatterThreads;
+        const int64_t qn = q + NT;
         const bool hn = qn < bend;
         VisFetch nxt;
         if (hn) fetch_vis<VisT, WK>(qn, s_voff, s_run, nst, uvw, fx, vis, wgt, m, nxt);
-        grid_fetched<W, WSTACK, PACK>(cur, g, plane, X0, Y0, fixed_scale, sub);
+        grid_fetched<W, WSTACK, PACK, G>(cur, g, plane, X0, Y0, fixed_scale, sub);
         cur = nxt;
         q = qn;
         have = hn;
@@ -313,53 +369,63 @@ __global__ __launch_bounds__(kScatterThreads, CIP_SCATTER_WAVES) void scatter_ke
     }
   }
   __syncthreads();
-  // flush the touched cells of the sub-grid to the fp64 HBM grid
+  // flush the touched cells of the sub-grid(s) to the fp64 HBM grid(s)
   // (lanes walk the HBM grid's contiguous axis: y, or x when it is stored
-  // transposed for the pruned FFT)
-  for (int cell = threadIdx.x; cell < P * P; cell += kScatterThreads) {
-    const int lcell = g.transposed ? (cell % P) * P + cell / P : cell;  // lx * P + ly
-    long long re, im;
-    if constexpr (PACK) {
-      const unsigned long long s = sub[lcell];
-      im = (long long)(int)(unsigned)s;
-      re = (long long)(int)(unsigned)((s - (unsigned long long)im) >> 32);
-    } else {
-      re = (long long)sub[lcell];
-      im = (long long)sub[P * P + lcell];
-    }
+  // transposed for the pruned FFT); plane group: plane + k -> grid + k planes
+#pragma unroll
+  for (int k = 0; k < G; ++k) {
+    if (G > 1 && plane + k >= g.nplanes) break;
+    const unsigned long long* sk = sub + k * S;
+    double* gk = grid + (int64_t)k * 2 * g.nu * g.nv;
+    for (int cell = threadIdx.x; cell < P * P; cell += NT) {
+      const int lcell = g.transposed ? (cell % P) * P + cell / P : cell;  // lx * P + ly
+      long long re, im;
+      if constexpr (PACK) {
+        const unsigned long long sv = sk[lcell];
+        im = (long long)(int)(unsigned)sv;
+        re = (long long)(int)(unsigned)((sv - (unsigned long long)im) >> 32);
+      } else {
+        re = (long long)sk[lcell];
+        im = (long long)sk[P * P + lcell];
+      }
 #if CIP_ABLATE == 4
-    if (((re | im) != 0) && re == 0x123456789ll) {  // ablation: no flush (timing only)
+      if (((re | im) != 0) && re == 0x123456789ll) {  // ablation: no flush (timing only)
 #else
-    if ((re | im) != 0) {
+      if ((re | im) != 0) {
 #endif
-      // the sub-grid of an edge tile wraps around the periodic grid
-      int64_t gx = X0 + lcell / P, gy = Y0 + lcell % P;
-      gx -= (gx >= g.nu) ? g.nu : 0;
-      gy -= (gy >= g.nv) ? g.nv : 0;
-      double* dst = grid + 2 * (g.transposed ? gy * g.nu + gx : gx * g.nv + gy);
-      unsafeAtomicAdd(dst, (double)re * inv_scale);
-      unsafeAtomicAdd(dst + 1, (double)im * inv_scale);
+        // the sub-grid of an edge tile wraps around the periodic grid
+        int64_t gx = X0 + lcell / P, gy = Y0 + lcell % P;
+        gx -= (gx >= g.nu) ? g.nu : 0;
+        gy -= (gy >= g.nv) ? g.nv : 0;
+        double* dst = gk + 2 * (g.transposed ? gy * g.nu + gx : gx * g.nv + gy);
+        unsafeAtomicAdd(dst, (double)re * inv_scale);
+        unsafeAtomicAdd(dst + 1, (double)im * inv_scale);
+      }
     }
   }
 }
 
 template <int W, typename VisT, int WK>
-inline hipError_t scatter_dispatch_ws(bool ws, bool pack, dim3 grid_dim, hipStream_t s, const double* uvw,
+inline hipError_t scatter_dispatch_ws(bool ws, int group, bool pack, dim3 grid_dim, hipStream_t s, const double* uvw,
                                       const double* fx, const void* vis, const void* wgt, const RowMap& m,
                                       const uint64_t* runs, const int64_t* run_goff, const int64_t* tile_run_off,
                                       const void* perm, const Chunk* chunks, int64_t chunk_begin,
                                       const GridGeometry& g, int64_t plane, double fs, double* grid) {
-#define LAUNCH(WSV, PRM, PK)                                                                               \
-  scatter_kernel<W, VisT, WK, WSV, PRM, PK><<<grid_dim, dim3(kScatterThreads), 0, s>>>(                    \
-      uvw, fx, (const VisT*)vis, wgt, m, runs, run_goff, tile_run_off, perm, chunks, chunk_begin, g, plane, \
+#define LAUNCH(WSV, PRM, PK, GG)                                                                            \
+  scatter_kernel<W, VisT, WK, WSV, PRM, PK, GG><<<grid_dim, dim3(scatter_threads<GG>()), 0, s>>>(            \
+      uvw, fx, (const VisT*)vis, wgt, m, runs, run_goff, tile_run_off, perm, chunks, chunk_begin, g, plane,    \
       fs, 1.0 / fs, grid)
-#define LAUNCH_WS(PRM, PK)   \
-  {                          \
-    if (ws) {                \
-      LAUNCH(true, PRM, PK); \
-    } else {                 \
-      LAUNCH(false, PRM, PK);\
-    }                        \
+#define LAUNCH_WS(PRM, PK)            \
+  {                                   \
+    if (ws && group == 3) {           \
+      LAUNCH(true, PRM, PK, 3);       \
+    } else if (ws && group == 2) {    \
+      LAUNCH(true, PRM, PK, 2);       \
+    } else if (ws) {                  \
+      LAUNCH(true, PRM, PK, 1);       \
+    } else {                          \
+      LAUNCH(false, PRM, PK, 1);      \
+    }                                 \
   }
   // the packed single-precision class exists for complex64 input only (the
   // reference's configuration; raw linear-feed columns are complex64 too)
@@ -392,14 +458,14 @@ inline hipError_t scatter_dispatch_ws(bool ws, bool pack, dim3 grid_dim, hipStre
 }
 
 template <int W>
-hipError_t launch_scatter_w(int vis_dtype, int wgt_dtype, bool pack, dim3 gd, hipStream_t s,
+hipError_t launch_scatter_w(int vis_dtype, int wgt_dtype, bool pack, int group, dim3 gd, hipStream_t s,
                                      const double* uvw, const double* fx, const void* vis, const void* wgt,
                                      const RowMap& m, const uint64_t* runs, const int64_t* run_goff,
                                      const int64_t* tile_run_off, const void* perm, const Chunk* chunks,
                                      int64_t cb, const GridGeometry& g, int64_t plane, double fs, double* grid) {
   const bool ws = g.do_wstacking != 0;
 #define ARGS \
-  ws, pack, gd, s, uvw, fx, vis, wgt, m, runs, run_goff, tile_run_off, perm, chunks, cb, g, plane, fs, grid
+  ws, group, pack, gd, s, uvw, fx, vis, wgt, m, runs, run_goff, tile_run_off, perm, chunks, cb, g, plane, fs, grid
   if (vis_dtype == CIP_POL4I) return scatter_dispatch_ws<W, Pol4, WK_POL4I>(ARGS);
   if (vis_dtype == CIP_C64) {
     if (wgt_dtype == CIP_F32) return scatter_dispatch_ws<W, float2, WK_F32>(ARGS);
