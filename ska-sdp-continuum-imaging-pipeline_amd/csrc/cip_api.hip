@@ -778,14 +778,16 @@ static bool public_dtypes(int vis_dtype, int wgt_dtype) {
 static bool vis_dtype_ok(int d) { return d == CIP_C64 || d == CIP_C128 || d == CIP_POL4I; }
 static bool wgt_dtype_ok(int d) { return d == CIP_NONE || d == CIP_F32 || d == CIP_F64 || d == CIP_POL4I; }
 
-// w planes per scatter work unit in w-stacking mode: 2 (a visibility placed
-// and its u, v, w kernels evaluated once for two planes; the unit holds two
-// sub-grids in 512-thread blocks) for the lane-per-visibility supports,
-// CIP_WSTACK_GROUP=1 one plane per unit (A/B); the large supports always 1.
+// w planes per scatter work unit in w-stacking mode: G = 3 (a visibility
+// placed and its u, v, w kernels evaluated once for three planes; the unit
+// holds G sub-grids in 512-thread blocks), fewer where two such blocks would
+// not fit a CU's LDS (W >= 10: 2); CIP_WSTACK_GROUP=1/2 caps it (A/B); the
+// large supports always 1. Refcall C3: G = 1 / 2 / 3 -> 13.4 / 12.2 / 11.8 ms
+// of scatter (profiles/r03_ab_wstack_group*.txt).
 static int wstack_group(const GridGeometry& g) {
   static const int env = [] {
     const char* e = getenv("CIP_WSTACK_GROUP");
-    const int v = e ? atoi(e) : 2;
+    const int v = e ? atoi(e) : 3;
     return v < 1 ? 1 : (v > 3 ? 3 : v);
   }();
   if (!g.do_wstacking || g.support > 16 || g.nplanes < 2) return 1;
