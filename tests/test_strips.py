@@ -156,3 +156,28 @@ def test_strip_halo_exchange_gloo(world, W):
     err, peak, left = q.get(timeout=5)
     assert err < 1e-13 * max(1.0, peak)
     assert left == 0.0
+
+
+def test_strips_with_empty_strips_and_no_data():
+    # a compact array (every footprint in a few grid rows): most strips hold
+    # no visibilities; the decomposition still equals the one-shot image
+    from _strip_np import NumpyStripBackend
+
+    uvw, f, vis, w, px = _case(nrow=300, nchan=4)
+    uvw = uvw * 0.02  # all baselines near the uv origin
+    prm = _prm(px, 8)
+    world = 6
+    layout = strips.plan_strips(torch.from_numpy(uvw), torch.from_numpy(f), _P(prm), px, NPIX, NPIX, world)
+    datas = _strip_datas(uvw, f, vis, w, px, prm, layout)
+    assert sum(d.nvis for d in datas) == vis.size
+    assert sum(d.nvis == 0 for d in datas) >= 2
+    be = NumpyStripBackend(prm, px, px, NPIX, NPIX)
+    img = strips.invert_strips_local(datas, torch.from_numpy(f), layout, be).numpy()
+    full = oracle.ms2dirty(uvw, f, vis, w, NPIX, NPIX, px, px, support=8, nthreads=1) / w.astype(np.float64).sum()
+    assert np.abs(img - full).max() < 1e-13 * max(1.0, np.abs(full).max())
+    # no rows at all: a valid layout, empty strips
+    e = torch.zeros((0, 3), dtype=torch.float64)
+    layout0 = strips.plan_strips(e, torch.from_numpy(f), _P(prm), px, NPIX, NPIX, 4)
+    assert layout0.y_bounds[0] == 0 and layout0.y_bounds[-1] == prm["nv"]
+    rows, c0, c1 = strips.strip_slices(e, torch.from_numpy(f), _P(prm), px, *layout0.rows(1))
+    assert rows.numel() == 0
