@@ -492,6 +492,10 @@ def main():
         "frac": round(achieved / HBM_PEAK_GBS, 5),
         "traffic": None,
         "kernel": "cip::scatter_kernel",
+        # the roof that binds this kernel is LDS atomic bandwidth (lds_atomic
+        # below), not HBM: 1 KiB of LDS read-modify-write per visibility at W = 8
+        # against ~40 B of HBM (SURVEY.md 8(d) asks for HBM as the reported bound)
+        "binding": "lds_atomic",
         "bytes_per_launch_alg": int(bytes_launch),
         "launch_ms": round(scatter_ms, 4),
     }
