@@ -1010,7 +1010,7 @@ static int prepare(Workspace* ws, const double* uvw, int64_t nrow, const double*
 // zeroed: the group's planes were zeroed already (side stream, joined by the caller)
 static int scatter_plane(const Prepared& pp, int64_t q, const double* uvw, const void* vis, int vis_dtype,
                          const void* wgt, int wgt_dtype, bool transposed, double* grid,
-                         hipStream_t s, bool zeroed = false) {
+                         hipStream_t s, bool zeroed = false, bool share_cus = false) {
   GridGeometry g = pp.g;
   g.transposed = transposed ? 1 : 0;
   const int G = pp.plan.group;
@@ -1022,7 +1022,7 @@ static int scatter_plane(const Prepared& pp, int64_t q, const double* uvw, const
   const int64_t cb = pp.plan.plane_chunk_off[k], ce = pp.plan.plane_chunk_off[k + 1];
   if (wgt == nullptr) wgt_dtype = CIP_NONE;
   hipEvent_t a = g_prof.mark(s);
-  CIP_HIP_CHECK(launch_scatter(g.support, vis_dtype, wgt_dtype, pp.packed, G, uvw, pp.fx, vis, wgt, pp.m,
+  CIP_HIP_CHECK(launch_scatter(g.support, vis_dtype, wgt_dtype, pp.packed, G, share_cus, uvw, pp.fx, vis, wgt, pp.m,
                                pp.plan.runs, pp.plan.run_goff, pp.plan.tile_run_off, pp.plan.perm, pp.plan.chunks, cb,
                                ce - cb, g, p0, pp.fixed_scale, grid, s));
   g_prof.span(2, a, g_prof.mark(s));
@@ -1072,6 +1072,15 @@ static int correction_vectors(Workspace* ws, const GridGeometry& g, int64_t npix
     ws->corr_key = corr_key;
   }
   return CIP_OK;
+}
+
+// CIP_SCATTER_SHARE=0: pipelined calls' scatters take every CU slot (A/B)
+static bool share_cus_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("CIP_SCATTER_SHARE");
+    return !(e && std::strcmp(e, "0") == 0);
+  }();
+  return on;
 }
 
 static int dirty_stage(Workspace* ws, const GridGeometry& g, int64_t npix_x, int64_t npix_y, double px, double py,
@@ -1318,7 +1327,9 @@ static int ms2dirty_impl(const double* uvw, int64_t nrow, const double* freq, in
   ws->grid_clean = nullptr;  // dirty until a masked pass A has consumed every written tile
   const uint32_t* dmask = st.fast ? pp.plan.dmask : nullptr;
   for (int64_t q = 0; q * G < g.nplanes; ++q) {
-    rc = scatter_plane(pp, q, uvw, vis, vis_dtype, wgt, wgt_dtype, st.fast, grid, s, clean);
+    // pipelined calls: leave CU slots to the next call's planner (profiles/r03_ab_scatter_share.txt)
+    rc = scatter_plane(pp, q, uvw, vis, vis_dtype, wgt, wgt_dtype, st.fast, grid, s, clean,
+                       pipelined && share_cus_enabled());
     if (rc != CIP_OK) return rc;
     for (int64_t p = q * G; p < std::min<int64_t>(q * G + G, g.nplanes); ++p) {
       rc = plane_to_dirty(st, g, p, grid + (p - q * G) * plane_elems, dirty_out, s,

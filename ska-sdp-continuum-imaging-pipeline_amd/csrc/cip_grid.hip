@@ -251,7 +251,8 @@ hipError_t launch_order(const double* uvw, const double* fx, const uint8_t* vis_
   return hipGetLastError();
 }
 
-hipError_t launch_scatter(int support, int vis_dtype, int wgt_dtype, bool packed, int group, const double* uvw,
+hipError_t launch_scatter(int support, int vis_dtype, int wgt_dtype, bool packed, int group, bool share_cus,
+                          const double* uvw,
                           const double* fx, const void* vis, const void* wgt, const RowMap& m, const uint64_t* runs,
                           const int64_t* run_goff, const int64_t* tile_run_off, const void* perm,
                           const Chunk* chunks, int64_t chunk_begin, int64_t nchunks, const GridGeometry& g,
@@ -259,9 +260,18 @@ hipError_t launch_scatter(int support, int vis_dtype, int wgt_dtype, bool packed
   if (nchunks <= 0) return hipSuccess;
   if (packed && vis_dtype != CIP_C64 && vis_dtype != CIP_POL4I) return hipErrorInvalidValue;
   const dim3 gd((unsigned)nchunks);
+  // three blocks per CU: each needs > 160 KB / 4 of LDS (static sub-grid +
+  // this pad); the 256-thread lane kernels only (plane groups run 512)
+  unsigned pad = 0;
+  if (share_cus && group == 1 && support <= 16) {
+    const unsigned P = (unsigned)(kTile + support - 1);
+    const unsigned stat = P * P * (packed ? 8u : 16u) + 64u;
+    const unsigned need = 160u * 1024u / 4u + 256u;
+    pad = stat < need ? need - stat : 0u;
+  }
 #define CASE(WW)                                                                                             \
   case WW:                                                                                                   \
-    return launch_scatter_w<WW>(vis_dtype, wgt_dtype, packed, group, gd, s, uvw, fx, vis, wgt, m, runs,    \
+    return launch_scatter_w<WW>(vis_dtype, wgt_dtype, packed, group, pad, gd, s, uvw, fx, vis, wgt, m, runs, \
                                   run_goff, tile_run_off, perm, chunks, chunk_begin, g, plane, fixed_scale, grid);
   switch (support) {
     CASE(4)

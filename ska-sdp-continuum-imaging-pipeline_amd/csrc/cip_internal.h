@@ -106,7 +106,8 @@ hipError_t launch_prep_final(const double* partial, int nblocks, double* out2, h
 // located through the tile's row slices in tile order).
 // one kernel support W (instantiated in cip_scatter_w.hip for W = 4, 6, ..., 16)
 template <int W>
-hipError_t launch_scatter_w(int vis_dtype, int wgt_dtype, bool pack, int group, dim3 gd, hipStream_t s,
+hipError_t launch_scatter_w(int vis_dtype, int wgt_dtype, bool pack, int group, unsigned lds_extra, dim3 gd,
+                            hipStream_t s,
                             const double* uvw,
                             const double* fx, const void* vis, const void* wgt, const RowMap& m,
                             const uint64_t* runs, const int64_t* run_goff, const int64_t* tile_run_off,
@@ -122,7 +123,11 @@ hipError_t launch_scatter_large_w(int vis_dtype, int wgt_dtype, dim3 gd, hipStre
                                   double* grid);
 // group: w planes per work unit (w-stacking plane groups, 1 or 2; grid = the
 // group's planes, 2 nu nv doubles apart)
-hipError_t launch_scatter(int support, int vis_dtype, int wgt_dtype, bool packed, int group, const double* uvw,
+// share_cus: cap the scatter at three 256-thread blocks per CU (extra dynamic
+// LDS) so kernels of another stream - the next pipelined call's planner - run
+// beside it
+hipError_t launch_scatter(int support, int vis_dtype, int wgt_dtype, bool packed, int group, bool share_cus,
+                          const double* uvw,
                           const double* fx, const void* vis, const void* wgt, const RowMap& m, const uint64_t* runs,
                           const int64_t* run_goff, const int64_t* tile_run_off, const void* perm,
                           const Chunk* chunks, int64_t chunk_begin, int64_t nchunks, const GridGeometry& g,

@@ -13,6 +13,7 @@
 // to fp64 and added to the HBM grid with global fp64 atomics. No MFMA: this
 // is a scatter.
 #pragma once
+#include <cstdlib>
 #include <type_traits>
 
 #include "cip_internal.h"
@@ -406,13 +407,14 @@ __global__ __launch_bounds__(scatter_threads<G>(), CIP_SCATTER_WAVES) void scatt
 }
 
 template <int W, typename VisT, int WK>
-inline hipError_t scatter_dispatch_ws(bool ws, int group, bool pack, dim3 grid_dim, hipStream_t s, const double* uvw,
+inline hipError_t scatter_dispatch_ws(bool ws, int group, bool pack, unsigned lds_extra, dim3 grid_dim, hipStream_t s,
+                                      const double* uvw,
                                       const double* fx, const void* vis, const void* wgt, const RowMap& m,
                                       const uint64_t* runs, const int64_t* run_goff, const int64_t* tile_run_off,
                                       const void* perm, const Chunk* chunks, int64_t chunk_begin,
                                       const GridGeometry& g, int64_t plane, double fs, double* grid) {
 #define LAUNCH(WSV, PRM, PK, GG)                                                                            \
-  scatter_kernel<W, VisT, WK, WSV, PRM, PK, GG><<<grid_dim, dim3(scatter_threads<GG>()), 0, s>>>(            \
+  scatter_kernel<W, VisT, WK, WSV, PRM, PK, GG><<<grid_dim, dim3(scatter_threads<GG>()), lds_extra, s>>>(   \
       uvw, fx, (const VisT*)vis, wgt, m, runs, run_goff, tile_run_off, perm, chunks, chunk_begin, g, plane,    \
       fs, 1.0 / fs, grid)
 #define LAUNCH_WS(PRM, PK)            \
@@ -458,14 +460,16 @@ inline hipError_t scatter_dispatch_ws(bool ws, int group, bool pack, dim3 grid_d
 }
 
 template <int W>
-hipError_t launch_scatter_w(int vis_dtype, int wgt_dtype, bool pack, int group, dim3 gd, hipStream_t s,
+hipError_t launch_scatter_w(int vis_dtype, int wgt_dtype, bool pack, int group, unsigned lds_extra, dim3 gd,
+                            hipStream_t s,
                                      const double* uvw, const double* fx, const void* vis, const void* wgt,
                                      const RowMap& m, const uint64_t* runs, const int64_t* run_goff,
                                      const int64_t* tile_run_off, const void* perm, const Chunk* chunks,
                                      int64_t cb, const GridGeometry& g, int64_t plane, double fs, double* grid) {
   const bool ws = g.do_wstacking != 0;
 #define ARGS \
-  ws, group, pack, gd, s, uvw, fx, vis, wgt, m, runs, run_goff, tile_run_off, perm, chunks, cb, g, plane, fs, grid
+  ws, group, pack, lds_extra, gd, s, uvw, fx, vis, wgt, m, runs, run_goff, tile_run_off, perm, chunks, cb, g, plane, \
+      fs, grid
   if (vis_dtype == CIP_POL4I) return scatter_dispatch_ws<W, Pol4, WK_POL4I>(ARGS);
   if (vis_dtype == CIP_C64) {
     if (wgt_dtype == CIP_F32) return scatter_dispatch_ws<W, float2, WK_F32>(ARGS);
