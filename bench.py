@@ -345,6 +345,49 @@ def run_strong(args, world, rank, device):
         dist.destroy_process_group()
 
 
+def reference_call_rate(invert, buf, steps, warmup=3):
+    """Pipelined rate of the reference's ms2dirty call (epsilon = 1e-4 ->
+    support 6, w-stacking, packed single-precision class) on the bench's
+    resident inputs, plus its synchronous per-phase times."""
+    import torch
+
+    from ska_sdp_cip_amd import _lib
+
+    dirty, sumw = buf
+    kw = dict(epsilon=1e-4, do_wstacking=True, single_precision_accumulation=True, out=dirty, sum_weights=sumw,
+              normalise=True)
+    for _ in range(warmup):
+        invert(synchronize=False, resident_inputs=True, **kw)
+    torch.cuda.synchronize()
+    nsteps = max(3, min(steps, 10))
+    t0 = time.perf_counter()
+    for _ in range(nsteps):
+        invert(synchronize=False, resident_inputs=True, **kw)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    _lib.profile_enable(True)
+    phases = []
+    for _ in range(3):
+        _, params = invert(**kw)
+        phases.append(_lib.profile_last())
+    torch.cuda.synchronize()
+    _lib.profile_enable(False)
+    nvis = int(phases[0]["visibilities"])
+    avg = {k: float(np.mean([p[k] for p in phases])) for k in phases[0] if k.endswith("_ms")}
+    return {
+        "what": "invert.py:170-183 ms2dirty(epsilon=1e-4, do_wstacking=True) on complex64 vis + float32 weights: "
+                f"support {params.support}, {params.nplanes} w planes, packed single-precision accumulation "
+                "(ducc0's float class for complex64 input), pipelined calls on the same resident inputs",
+        "value": round(nvis * nsteps / elapsed / 1e6, 2),
+        "unit": "Mvis/s",
+        "ms_per_step": round(elapsed / nsteps * 1e3, 3),
+        "steps": nsteps,
+        "support": params.support,
+        "nplanes": params.nplanes,
+        "phases_ms_sync": {k.replace("_ms", ""): round(v, 3) for k, v in avg.items()},
+    }
+
+
 def main():
     ap = argparse.ArgumentParser(description=__doc__.splitlines()[1])
     ap.add_argument("--gpus", type=int, default=1)
@@ -366,6 +409,8 @@ def main():
                     help="raw linear-feed columns (rows, nchan, 4) resident in HBM: Stokes I and effective weights "
                          "formed inside the planner and scatter (cip_ms2dirty_stokes_i) - the reference's whole "
                          "invert_measurement_set input (secondary measurement)")
+    ap.add_argument("--no-secondary", action="store_true",
+                    help="skip the reference-call secondary figure of the default run")
     ap.add_argument("--strong", action="store_true",
                     help="strong scaling of ONE C4 image (1G vis, 16k^2 grid) over the ranks: uv strips + halo "
                          "exchange + distributed FFT (DESIGN.md 7); --config is ignored")
@@ -569,6 +614,12 @@ def main():
         "mean_slice_len": round(avg["visibilities"] / max(runs, 1), 2),
         "gtap_per_s": round(world * nvis * taps * args.steps / elapsed / 1e9, 2),
     }
+    if world == 1 and not args.no_secondary and raw is None and not args.wstacking and not args.single:
+        # the reference's own gridder call on the same resident inputs
+        # (invert.py:170-183: epsilon 1e-4 -> W = 6, do_wstacking=True,
+        # complex64 input -> ducc0's float accumulation class): a secondary
+        # figure beside the f64 metric, so every default run reports it
+        result["secondary"] = {"reference_call": reference_call_rate(invert, bufs[0], args.steps)}
     nthreads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, len(os.sched_getaffinity(0)))
     need_host = rank == 0 and ((world == 1 and not args.no_cpu_baseline) or not args.no_max_err)
     vis_h = wgt_h = None
