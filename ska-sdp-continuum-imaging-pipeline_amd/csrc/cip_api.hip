@@ -703,7 +703,8 @@ static int make_plan(Workspace* ws, const double* uvw, const double* fx, const R
   CIP_HIP_CHECK(launch_tile_vis(run_goff, tile_run_off, ntiles, tile_vis_off, tile_vis, s));
   if (g.ntx % 32 == 0 && grid_mask()) {
     CIP_ALLOC(dmask, uint8_t, "dirty_mask", g.ntx * g.nty * g.nplanes)
-    CIP_ALLOC(dbits, uint32_t, "dirty_bits", g.ntx * g.nty / 32 * g.nplanes)
+    // tile bits, then tile-row bits (row_bits_kernel), per plane
+    CIP_ALLOC(dbits, uint32_t, "dirty_bits", g.ntx * g.nty / 32 * g.nplanes + (g.nty + 31) / 32 * g.nplanes)
     CIP_HIP_CHECK(hipMemsetAsync(dmask, 0, (size_t)(g.ntx * g.nty * g.nplanes), s));
     CIP_HIP_CHECK(launch_dirty_mask(tile_vis, g.ntx, g.nty, g.ntw, g.support, g.nplanes, dmask, dbits, s));
     pr->dmask = dbits;
@@ -1113,11 +1114,23 @@ static int dirty_stage(Workspace* ws, const GridGeometry& g, int64_t npix_x, int
 // rest of the grid is zero, and pass A zeroes the masked tiles after reading
 // norm (pruned 2-D path only, may be NULL): device weight sum the image is
 // divided by in pass B's epilogue (CIP_NORMALISE)
+// CIP_FFT_ROWSKIP=0: pass A transforms (and pass B reads) clean tile rows too (A/B)
+static bool fft_rowskip() {
+  static const bool on = [] {
+    const char* e = getenv("CIP_FFT_ROWSKIP");
+    return !(e && std::strcmp(e, "0") == 0);
+  }();
+  return on;
+}
+
+// rowbits (with dmask): the plane's tile-row bits (row_bits_kernel)
 static int plane_to_dirty(const DirtyStage& st, const GridGeometry& g, int64_t p, double* grid, double* dirty_out,
-                          hipStream_t s, const uint32_t* dmask = nullptr, const double* norm = nullptr) {
+                          hipStream_t s, const uint32_t* dmask = nullptr, const double* norm = nullptr,
+                          const uint32_t* rowbits = nullptr) {
   hipEvent_t f0 = g_prof.mark(s);
   if (st.fast) {
-    CIP_HIP_CHECK(launch_fft_rows(grid, g.nu, g.nv, st.npix_x, st.tw_u, st.fft_h, dmask, g.ntx, s));
+    if (!fft_rowskip()) rowbits = nullptr;
+    CIP_HIP_CHECK(launch_fft_rows(grid, g.nu, g.nv, st.npix_x, st.tw_u, st.fft_h, dmask, g.ntx, rowbits != nullptr, s));
   } else if (hipfftExecZ2Z(st.plan, (hipfftDoubleComplex*)grid, (hipfftDoubleComplex*)grid, HIPFFT_BACKWARD) !=
              HIPFFT_SUCCESS) {
     return set_error(CIP_EHIP, "hipfftExecZ2Z failed");
@@ -1126,7 +1139,8 @@ static int plane_to_dirty(const DirtyStage& st, const GridGeometry& g, int64_t p
   // pass B carries the crop epilogue: it is booked under "fft"
   if (st.fast)
     CIP_HIP_CHECK(launch_fft_cols(st.fft_h, g.nv, st.npix_x, st.npix_y, st.tw_v, g.do_wstacking ? 1 : 0, dirty_out,
-                                  st.cx, st.cy, st.px, st.py, w_plane, p == 0, g.do_wstacking ? nullptr : norm, s));
+                                  st.cx, st.cy, st.px, st.py, w_plane, p == 0, g.do_wstacking ? nullptr : norm,
+                                  dmask ? rowbits : nullptr, s));
   hipEvent_t f1 = g_prof.mark(s);
   g_prof.span(3, f0, f1);
   if (st.fast) {
@@ -1333,7 +1347,8 @@ static int ms2dirty_impl(const double* uvw, int64_t nrow, const double* freq, in
     if (rc != CIP_OK) return rc;
     for (int64_t p = q * G; p < std::min<int64_t>(q * G + G, g.nplanes); ++p) {
       rc = plane_to_dirty(st, g, p, grid + (p - q * G) * plane_elems, dirty_out, s,
-                          dmask ? dmask + p * (g.ntx * g.nty / 32) : nullptr, normalise ? pp.red : nullptr);
+                          dmask ? dmask + p * (g.ntx * g.nty / 32) : nullptr, normalise ? pp.red : nullptr,
+                          dmask ? dmask + g.nplanes * (g.ntx * g.nty / 32) + p * ((g.nty + 31) / 32) : nullptr);
       if (rc != CIP_OK) return rc;
     }
     clean = dmask != nullptr;

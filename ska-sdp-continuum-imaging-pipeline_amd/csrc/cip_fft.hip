@@ -197,7 +197,7 @@ template <int N, bool MASKED, bool ZERO = false>
 __global__ __launch_bounds__(N / 16) void fft_rows_kernel(double2* __restrict__ gT, int64_t hrows, int64_t nx,
                                                           const double2* __restrict__ tw, double2* __restrict__ H,
                                                           const uint32_t* __restrict__ dmask, int64_t ntx,
-                                                          int64_t y0 = 0, int64_t hy0 = 0) {
+                                                          int64_t y0 = 0, int64_t hy0 = 0, bool skip_clean = false) {
   using S = FftShape<N>;
   __shared__ double lds[N + N / 16];
   const int t = threadIdx.x;
@@ -210,10 +210,20 @@ __global__ __launch_bounds__(N / 16) void fft_rows_kernel(double2* __restrict__ 
     // mask words are scalar loads and each lane tests one bit
     static_assert(kTile == 32 && 1024 % S::T == 0, "mask word per element uniform");
     const uint32_t* mrow = dmask + (y / kTile) * (ntx / 32);
+    uint32_t words[16];
+    uint32_t any = 0u;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      words[r] = mrow[(r * S::T) >> 10];
+      any |= words[r];
+    }
+    // a clean tile row (every word of it is read above): nothing to transform
+    // or zero, and pass B reads its H rows as zero (row_bits_kernel)
+    if (skip_clean && any == 0u) return;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int x = t + r * S::T;
-      const uint32_t word = mrow[(r * S::T) >> 10];
+      const uint32_t word = words[r];
       v[r] = make_double2(0.0, 0.0);
       if ((word >> ((x >> 5) & 31)) & 1u) {
         v[r] = row[x];
@@ -258,10 +268,13 @@ struct ColEpilogue {
 // A strip of image rows [i0, i0 + gridDim.x): H holds the
 // blocks from i0 / kColBlock on (i0 a multiple of kColBlock), and image row i
 // goes to ep.out row i - i0. The whole image: i0 = 0.
+// rowbits (may be NULL: every H row is read): bit ty of the plane's tile-row
+// words - H rows y of clean tile rows (y / kTile) were not written by pass A
+// and are zero.
 template <int N, int MODE>
 __global__ __launch_bounds__(N / 16) void fft_cols_kernel(const double2* __restrict__ H, int64_t nx, int64_t ny,
                                                           const double2* __restrict__ tw, ColEpilogue ep,
-                                                          int64_t i0 = 0) {
+                                                          int64_t i0 = 0, const uint32_t* __restrict__ rowbits = nullptr) {
   using S = FftShape<N>;
   __shared__ double lds[N + N / 16];
   const int t = threadIdx.x;
@@ -274,8 +287,21 @@ __global__ __launch_bounds__(N / 16) void fft_cols_kernel(const double2* __restr
   const int64_t i = i0 + il;
   const double2* col = H + ((il / kColBlock) * N) * kColBlock + (il % kColBlock);
   double2 v[16];
+  if (rowbits) {
+    // the row-bit word of element r (rows t + r T, tile rows (t + r T) / 32)
+    // is uniform over the block, as in pass A: scalar loads, one bit per lane
+    static_assert(kTile == 32 && 1024 % S::T == 0, "row word per element uniform");
 #pragma unroll
-  for (int r = 0; r < 16; ++r) v[r] = col[(int64_t)(t + r * S::T) * kColBlock];
+    for (int r = 0; r < 16; ++r) {
+      const int y = t + r * S::T;
+      const uint32_t word = rowbits[(r * S::T) >> 10];
+      v[r] = make_double2(0.0, 0.0);
+      if ((word >> ((y >> 5) & 31)) & 1u) v[r] = col[(int64_t)y * kColBlock];
+    }
+  } else {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v[r] = col[(int64_t)(t + r * S::T) * kColBlock];
+  }
   fft_core<N>(v, t, lds, tw);
   const int64_t p = i - nx / 2;
   double* orow = ep.out + il * ny;
@@ -314,7 +340,7 @@ bool fast_fft_supported(int64_t nu, int64_t nv, int64_t nx, int64_t ny) {
 }
 
 hipError_t launch_fft_rows(double* gT, int64_t nu, int64_t nv, int64_t nx, const double* tw_u, double* H,
-                           const uint32_t* dmask, int64_t ntx, hipStream_t s) {
+                           const uint32_t* dmask, int64_t ntx, bool skip_clean, hipStream_t s) {
   if (!fft_len_ok(nu) || !fft_len_ok(nv) || nx > nu) return hipErrorInvalidValue;
   if (dmask && (nu % kTile != 0 || nv % kTile != 0 || ntx * kTile != nu || ntx % 32 != 0))
     return hipErrorInvalidValue;
@@ -324,7 +350,8 @@ hipError_t launch_fft_rows(double* gT, int64_t nu, int64_t nv, int64_t nx, const
   double2* h = (double2*)H;
 #define ROWS(NN)                                                                                         \
   case NN:                                                                                               \
-    if (dmask) fft_rows_kernel<NN, true><<<gd, dim3(NN / 16), 0, s>>>(g, nv, nx, tw, h, dmask, ntx);    \
+    if (dmask) fft_rows_kernel<NN, true><<<gd, dim3(NN / 16), 0, s>>>(g, nv, nx, tw, h, dmask, ntx, 0, 0,  \
+                                                                      skip_clean);                      \
     else fft_rows_kernel<NN, false><<<gd, dim3(NN / 16), 0, s>>>(g, nv, nx, tw, h, nullptr, 0);         \
     break;
   switch (nu) {
@@ -390,15 +417,15 @@ hipError_t launch_fft_cols_strip(const double* H, int64_t nv, int64_t nx, int64_
 
 hipError_t launch_fft_cols(const double* H, int64_t nv, int64_t nx, int64_t ny, const double* tw_v, int mode,
                            double* out, const double* cx, const double* cy, double px, double py, double w_plane,
-                           int first, const double* norm, hipStream_t s) {
+                           int first, const double* norm, const uint32_t* rowbits, hipStream_t s) {
   const dim3 gd((unsigned)nx);
   const double2* h = (const double2*)H;
   const double2* tw = (const double2*)tw_v;
   const ColEpilogue ep{out, cx, cy, px, py, w_plane, first, norm};
 #define COLS(NN)                                                                    \
   case NN:                                                                          \
-    if (mode == 0) fft_cols_kernel<NN, 0><<<gd, dim3(NN / 16), 0, s>>>(h, nx, ny, tw, ep); \
-    else fft_cols_kernel<NN, 1><<<gd, dim3(NN / 16), 0, s>>>(h, nx, ny, tw, ep);          \
+    if (mode == 0) fft_cols_kernel<NN, 0><<<gd, dim3(NN / 16), 0, s>>>(h, nx, ny, tw, ep, 0, rowbits); \
+    else fft_cols_kernel<NN, 1><<<gd, dim3(NN / 16), 0, s>>>(h, nx, ny, tw, ep, 0, rowbits);          \
     break;
   switch (nv) {
     COLS(1024)

@@ -691,6 +691,30 @@ __global__ void pack_mask_kernel(const uint8_t* __restrict__ mask, int64_t nword
   bits[wd] = b;
 }
 
+// Tile-row bits of the packed mask (one per plane and tile row ty: any dirty
+// tile in the row), nrw = ceil(nty / 32) words per plane. The pruned FFT skips
+// the grid rows of clean tile rows in both passes: pass A neither transforms
+// nor writes them, pass B reads them as zero (C3 w-stacking: 36 % of the
+// rows over the 14 planes; 2-D: 14 %).
+__global__ void row_bits_kernel(const uint32_t* __restrict__ bits, int64_t ntx, int64_t nty, int64_t nplanes,
+                                uint32_t* __restrict__ rows) {
+  const int64_t nrw = (nty + 31) / 32;
+  const int64_t id = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (id >= nrw * nplanes) return;
+  const int64_t p = id / nrw, w = id - p * nrw;
+  const int64_t wpr = ntx / 32;  // mask words per tile row
+  const uint32_t* b = bits + p * (nty * wpr);
+  uint32_t out = 0u;
+  for (int k = 0; k < 32; ++k) {
+    const int64_t ty = w * 32 + k;
+    if (ty >= nty) break;
+    uint32_t any = 0u;
+    for (int64_t j = 0; j < wpr; ++j) any |= b[ty * wpr + j];
+    out |= (any != 0u ? 1u : 0u) << k;
+  }
+  rows[id] = out;
+}
+
 hipError_t launch_dirty_mask(const int64_t* tile_vis, int64_t ntx, int64_t nty, int64_t ntw, int support,
                              int64_t nplanes, uint8_t* mask, uint32_t* bits, hipStream_t s) {
   const int64_t n = ntx * nty * nplanes;
@@ -700,6 +724,9 @@ hipError_t launch_dirty_mask(const int64_t* tile_vis, int64_t ntx, int64_t nty, 
     if (ntx % 32 != 0) return hipErrorInvalidValue;
     const int64_t nw = n / 32;
     pack_mask_kernel<<<dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, s>>>(mask, nw, bits);
+    // the row bits follow the tile bits (dirty_bits_words())
+    const int64_t nr = (nty + 31) / 32 * nplanes;
+    row_bits_kernel<<<dim3((unsigned)((nr + 255) / 256)), dim3(256), 0, s>>>(bits, ntx, nty, nplanes, bits + nw);
   }
   return hipGetLastError();
 }
