@@ -54,6 +54,7 @@ def continuum_invert(
     rank: int = 0,
     world: int = 1,
     reuse_plans: bool = True,
+    single_precision_accumulation: bool = False,
 ) -> dict:
     """
     Dirty images (normalised by each Stokes parameter's weight sum) and PSFs
@@ -64,12 +65,15 @@ def continuum_invert(
     facet_pixels)} with name in `stokes` or "PSF", for this rank's facets k.
     `reuse_plans`: a facet's later products reuse its first product's tile
     plan (the same rephased uvw; identical images, one planner per facet).
+    `single_precision_accumulation`: the packed single-precision class (ducc0's
+    float class of the reference's complex64 call) instead of fp64.
     """
     _require_gpu()
     pix = pixel_size_lm(pixel_size_asec)
     facets = [(0.0, 0.0)] if facets is None else list(facets)
     stokes = list(stokes)
-    kw = dict(epsilon=epsilon, support=support, do_wstacking=do_wstacking)
+    kw = dict(epsilon=epsilon, support=support, do_wstacking=do_wstacking,
+              single_precision_accumulation=single_precision_accumulation)
     per_stokes = {s: device_stokes(vis4, flags4, wgt4, s) for s in stokes}
     wts = {s: eff for s, (_, eff) in per_stokes.items()}
     if psf and "I" not in wts:

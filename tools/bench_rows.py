@@ -34,6 +34,12 @@ def main():
     ap.add_argument("--npix", type=int, default=2048)
     ap.add_argument("--rows-per-chunk", type=int, default=32_768)
     ap.add_argument("--facets", type=int, default=2, help="facets per axis (continuum)")
+    ap.add_argument("--facets-xy", type=int, nargs=2, default=None, help="continuum: facets along x and y")
+    ap.add_argument("--world", type=int, default=1,
+                    help="continuum: time rank 0's share of the facets of a `world`-GPU run (k %% world == 0)")
+    ap.add_argument("--refcall", action="store_true",
+                    help="continuum: the reference's gridder call (epsilon 1e-4, w-stacking, float class) "
+                         "instead of 2-D support 8 fp64")
     ap.add_argument("--repeat", type=int, default=3)
     ap.add_argument("--no-reuse", action="store_true", help="continuum: plan every product (no CIP_REUSE_PLAN)")
     args = ap.parse_args()
@@ -71,9 +77,12 @@ def main():
         dev = torch.device("cuda", 0)
         t = lambda a, dt=None: torch.from_numpy(np.ascontiguousarray(a if dt is None else a.astype(dt))).to(dev)  # noqa
         cols = (t(ms.visibilities()), t(ms.flags(), np.uint8), t(ms.weights()), t(uvw), t(freq))
-        facets = facet_centres(args.facets, args.facets, args.npix, px)
+        fx, fy = args.facets_xy or (args.facets, args.facets)
+        facets = facet_centres(fx, fy, args.npix, px)
+        call = (dict(epsilon=1e-4, do_wstacking=True, single_precision_accumulation=True) if args.refcall else
+                dict(support=8, do_wstacking=False))
         run = lambda: continuum_invert(*cols, args.npix, asec, facets=facets, stokes="IQUV",  # noqa: E731
-                                       psf=True, support=8, do_wstacking=False, reuse_plans=not args.no_reuse)
+                                       psf=True, rank=0, world=args.world, reuse_plans=not args.no_reuse, **call)
         run()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -82,8 +91,11 @@ def main():
         torch.cuda.synchronize()
         dt = (time.perf_counter() - t0) / args.repeat
         nimg = len(res)
-        out.update(metric="continuum products: Stokes IQUV + PSF per facet (2-D, support 8)",
+        mode = ("the reference's call: epsilon 1e-4, w-stacking, float class" if args.refcall else
+                "2-D, support 8, fp64")
+        out.update(metric=f"continuum products: Stokes IQUV + PSF per facet ({mode})", world=args.world,
                    value=round(nimg / dt, 2), unit="images/s", images=nimg, facets=len(facets),
+                   facets_this_rank=nimg // 5,
                    ms_per_call=round(dt * 1e3, 2), mvis_per_s_per_image=round(nvis * nimg / dt / 1e6, 1),
                    reuse_plans=not args.no_reuse)
     print(json.dumps(out), flush=True)
