@@ -276,56 +276,6 @@ __device__ __forceinline__ void grid_fetched(const VisFetch& f, const GridGeomet
 #endif
 }
 
-#if CIP_ABLATE == 5
-// Timing experiment only (wrong images): every lane grids a visibility PAIR -
-// its own and the one D rows later (same channel; the same baseline one dump
-// later in MS order) - with one fixed-point atomic per tap and component for
-// both (fma(ua, ka, fma(ub, kb, magic))), placed at the first one's origin.
-// Measures what a time-pair scatter item costs against a single one.
-#ifndef CIP_PAIR_D
-#define CIP_PAIR_D 2016
-#endif
-template <int W>
-__device__ __forceinline__ void grid_pair(const VisFetch& f, const VisFetch& f2, const GridGeometry& g, int64_t X0,
-                                          int64_t Y0, double fixed_scale, unsigned long long* sub) {
-  constexpr int T = kTile;
-  constexpr int P = T + W - 1;
-  if (f.wt == 0.0) return;
-  int64_t ix0, iy0, iw0, jx0, jy0, jw0;
-  double yu, yv, yw, zu, zv, zw;
-  if (!place_vis(f.u, f.v, f.w, f.fx, g, &ix0, &yu, &iy0, &yv, &iw0, &yw)) return;
-  place_vis(f2.u, f2.v, f2.w, f2.fx, g, &jx0, &zu, &jy0, &zv, &jw0, &zw);
-  const int64_t lx = ix0 - X0, ly = iy0 - Y0;
-  if (lx < 0 || lx >= T || ly < 0 || ly >= T) return;
-  const double sc = f.wt * fixed_scale, sc2 = f2.wt * fixed_scale;
-  const double vr = f.vr * sc, vi = f.vi * sc, vr2 = f2.vr * sc2, vi2 = f2.vi * sc2;
-  double ku[W], kv[W], ku2[W], kv2[W];
-  eval_kernel<W>(yu, ku);
-  eval_kernel<W>(yv, kv);
-  eval_kernel<W>(zu, ku2);
-  eval_kernel<W>(zv, kv2);
-  double kr[W], ki[W], kr2[W], ki2[W];
-#pragma unroll
-  for (int j = 0; j < W; ++j) {
-    kr[j] = kv[j] * vr;
-    ki[j] = kv[j] * vi;
-    kr2[j] = kv2[j] * vr2;
-    ki2[j] = kv2[j] * vi2;
-  }
-  unsigned long long* base = sub + (lx * P + ly);
-#pragma unroll
-  for (int i = 0; i < W; ++i) {
-#pragma unroll
-    for (int j = 0; j < W; ++j) {
-      const double qr = fma(ku[i], kr[j], fma(ku2[i], kr2[j], kMagic));
-      const double qi = fma(ku[i], ki[j], fma(ku2[i], ki2[j], kMagic));
-      atomicAdd(base + (i * P + j), (unsigned long long)__double_as_longlong(qr) - 0x4338000000000000ull);
-      atomicAdd(base + P * P + (i * P + j), (unsigned long long)__double_as_longlong(qi) - 0x4338000000000000ull);
-    }
-  }
-}
-#endif
-
 // PERM: 0 = tile order through the row slices, 1 / 2 = the bank-class ordered
 // stream of dense (u32) / ragged (u64) entries. G: w planes per work unit
 // (w-stacking plane groups; G > 1 runs 512-thread blocks holding G sub-grids).
@@ -369,9 +319,6 @@ __global__ __launch_bounds__(scatter_threads<G>(), CIP_SCATTER_WAVES) void scatt
     int64_t qn = q + NT;
     bool hn = qn < ch.g1;
     uint64_t pn = 0;
-#if CIP_ABLATE == 5
-    uint64_t cur_e = have ? perm_entry_t<kWide>(perm, q) : 0;
-#endif
     if (have) {
       fetch_raw<VisT, WK, kWide>(perm_entry_t<kWide>(perm, q), uvw, fx, vis_ld, unit_vis, wgt, m, cur);
       pn = perm_entry_t<kWide>(perm, hn ? qn : q);
@@ -382,20 +329,7 @@ __global__ __launch_bounds__(scatter_threads<G>(), CIP_SCATTER_WAVES) void scatt
       const uint64_t pnn = perm_entry_t<kWide>(perm, hnn ? qnn : q);
       RawFetch<VisT, WK> nxt;
       fetch_raw<VisT, WK, kWide>(pn, uvw, fx, vis_ld, unit_vis, wgt, m, nxt);
-#if CIP_ABLATE == 5
-      if constexpr (!WSTACK && !PACK && G == 1 && !kWide) {
-        const uint64_t e2 = cur_e + (uint64_t)CIP_PAIR_D * (uint64_t)m.nchan;
-        RawFetch<VisT, WK> par;
-        fetch_raw<VisT, WK, kWide>(e2 < (uint64_t)m.nvis ? e2 : cur_e, uvw, fx, vis_ld, unit_vis, wgt, m, par);
-        grid_pair<W>(from_raw<VisT, WK>(cur, unit_vis), from_raw<VisT, WK>(par, unit_vis), g, X0, Y0, fixed_scale,
-                     sub);
-      } else {
-        grid_fetched<W, WSTACK, PACK, G>(from_raw<VisT, WK>(cur, unit_vis), g, plane, X0, Y0, fixed_scale, sub);
-      }
-      cur_e = pn;
-#else
       grid_fetched<W, WSTACK, PACK, G>(from_raw<VisT, WK>(cur, unit_vis), g, plane, X0, Y0, fixed_scale, sub);
-#endif
       cur = nxt;
       q = qn;
       have = hn;
