@@ -12,5 +12,7 @@ timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 && echo "smoke ok" &&
 timeout -k 10 600 python bench.py > $OUT/bench.json 2> $OUT/bench.err && echo "bench ok" &&
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $PWD/$OUT/prof -o $ROUND --output-format csv -- \
-    python3 bench.py --no-cpu-baseline --no-max-err > $OUT/bench_prof.json 2> $OUT/bench_prof.err && echo "prof ok" &&
-python3 tools/trace_summary.py $OUT/prof/${ROUND}_kernel_trace.csv 10 $OUT/${ROUND}_kernel_summary.md > /dev/null
+    python3 bench.py --no-cpu-baseline --no-max-err --no-secondary > $OUT/bench_prof.json 2> $OUT/bench_prof.err && echo "prof ok" &&
+python3 tools/trace_summary.py $OUT/prof/${ROUND}_kernel_trace.csv 10 $OUT/${ROUND}_kernel_summary.md > /dev/null &&
+timeout -k 10 400 python bench.py --config c4 --no-cpu-baseline > $OUT/bench_c4.json 2> $OUT/bench_c4.err && echo "c4 ok" &&
+timeout -k 10 400 python bench.py --strong --no-cpu-baseline > $OUT/bench_strong.json 2> $OUT/bench_strong.err && echo "strong ok"
