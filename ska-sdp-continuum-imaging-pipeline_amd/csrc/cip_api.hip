@@ -1009,9 +1009,24 @@ static int prepare(Workspace* ws, const double* uvw, int64_t nrow, const double*
 // [q G, q G + G), written to grid + k planes for plane q G + k; 2-D: q = 0).
 // transposed: store the grid as gT[y, x] (input layout of the pruned FFT)
 // zeroed: the group's planes were zeroed already (side stream, joined by the caller)
+// Sole-unit private-cell stores in the scatter's flush (cip_scatter.h) on grid
+// planes of >= 16384^2 cells: C4's flush goes to a 4 GiB plane that no cache
+// holds, and stores cut the C4-shard scatter 4.87 -> 4.59 ms; on C3's 8192^2
+// plane they cost 1-3 % (profiles/r03_ab_flush_store.txt). CIP_FLUSH_STORE=0 /
+// 1 forces them off / on for any grid (A/B).
+static bool flush_store_enabled(const GridGeometry& g) {
+  static const int mode = [] {
+    const char* e = getenv("CIP_FLUSH_STORE");
+    return e ? (std::strcmp(e, "0") == 0 ? 0 : 1) : -1;
+  }();
+  return mode < 0 ? g.nu * g.nv >= ((int64_t)1 << 28) : mode == 1;
+}
+
+// zeroed: the planes are already zero (no memset); accumulate: they hold
+// earlier chunks' sums (cip_grid_ms: += onto them), so the flush never stores
 static int scatter_plane(const Prepared& pp, int64_t q, const double* uvw, const void* vis, int vis_dtype,
                          const void* wgt, int wgt_dtype, bool transposed, double* grid,
-                         hipStream_t s, bool zeroed = false, bool share_cus = false) {
+                         hipStream_t s, bool zeroed = false, bool share_cus = false, bool accumulate = false) {
   GridGeometry g = pp.g;
   g.transposed = transposed ? 1 : 0;
   const int G = pp.plan.group;
@@ -1023,7 +1038,8 @@ static int scatter_plane(const Prepared& pp, int64_t q, const double* uvw, const
   const int64_t cb = pp.plan.plane_chunk_off[k], ce = pp.plan.plane_chunk_off[k + 1];
   if (wgt == nullptr) wgt_dtype = CIP_NONE;
   hipEvent_t a = g_prof.mark(s);
-  CIP_HIP_CHECK(launch_scatter(g.support, vis_dtype, wgt_dtype, pp.packed, G, share_cus, uvw, pp.fx, vis, wgt, pp.m,
+  CIP_HIP_CHECK(launch_scatter(g.support, vis_dtype, wgt_dtype, pp.packed, G, share_cus,
+                               !accumulate && flush_store_enabled(g), uvw, pp.fx, vis, wgt, pp.m,
                                pp.plan.runs, pp.plan.run_goff, pp.plan.tile_run_off, pp.plan.perm, pp.plan.chunks, cb,
                                ce - cb, g, p0, pp.fixed_scale, grid, s));
   g_prof.span(2, a, g_prof.mark(s));
@@ -1211,7 +1227,8 @@ static int grid_accumulate(const double* uvw, int64_t nrow, const double* freq, 
   const int64_t plane_elems = 2 * g.nu * g.nv;
   const int G = pp.plan.group;
   for (int64_t q = 0; q * G < g.nplanes; ++q) {
-    rc = scatter_plane(pp, q, uvw, vis, vis_dtype, wgt, wgt_dtype, transposed, grids + q * G * plane_elems, s, true);
+    rc = scatter_plane(pp, q, uvw, vis, vis_dtype, wgt, wgt_dtype, transposed, grids + q * G * plane_elems, s, true,
+                       false, true);
     if (rc != CIP_OK) return rc;
   }
   if (sum_wgt) CIP_HIP_CHECK(launch_add_scalar(pp.red, sum_wgt, s));

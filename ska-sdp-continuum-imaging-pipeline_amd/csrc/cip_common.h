@@ -126,6 +126,8 @@ struct Chunk {
   int64_t tile;
   int64_t first_run;  // first row slice of the tile overlapping [g0, g1)
   int64_t last_run;   // last row slice overlapping [g0, g1)
+  int64_t sole;       // 1: the only work unit of its tile (and plane group) - its private cells
+                      // have no other writer in the launch (scatter flush, cip_scatter.h)
 };
 
 // Everything the planner and the scatter need to place a visibility.

@@ -252,7 +252,7 @@ hipError_t launch_order(const double* uvw, const double* fx, const uint8_t* vis_
 }
 
 hipError_t launch_scatter(int support, int vis_dtype, int wgt_dtype, bool packed, int group, bool share_cus,
-                          const double* uvw,
+                          bool store_private, const double* uvw,
                           const double* fx, const void* vis, const void* wgt, const RowMap& m, const uint64_t* runs,
                           const int64_t* run_goff, const int64_t* tile_run_off, const void* perm,
                           const Chunk* chunks, int64_t chunk_begin, int64_t nchunks, const GridGeometry& g,
@@ -271,7 +271,8 @@ hipError_t launch_scatter(int support, int vis_dtype, int wgt_dtype, bool packed
   }
 #define CASE(WW)                                                                                             \
   case WW:                                                                                                   \
-    return launch_scatter_w<WW>(vis_dtype, wgt_dtype, packed, group, pad, gd, s, uvw, fx, vis, wgt, m, runs, \
+    return launch_scatter_w<WW>(vis_dtype, wgt_dtype, packed, group, pad, store_private ? 1 : 0, gd, s, uvw, fx,  \
+                                vis, wgt, m, runs, \
                                   run_goff, tile_run_off, perm, chunks, chunk_begin, g, plane, fixed_scale, grid);
   switch (support) {
     CASE(4)

@@ -106,8 +106,8 @@ hipError_t launch_prep_final(const double* partial, int nblocks, double* out2, h
 // located through the tile's row slices in tile order).
 // one kernel support W (instantiated in cip_scatter_w.hip for W = 4, 6, ..., 16)
 template <int W>
-hipError_t launch_scatter_w(int vis_dtype, int wgt_dtype, bool pack, int group, unsigned lds_extra, dim3 gd,
-                            hipStream_t s,
+hipError_t launch_scatter_w(int vis_dtype, int wgt_dtype, bool pack, int group, unsigned lds_extra,
+                            int store_private, dim3 gd, hipStream_t s,
                             const double* uvw,
                             const double* fx, const void* vis, const void* wgt, const RowMap& m,
                             const uint64_t* runs, const int64_t* run_goff, const int64_t* tile_run_off,
@@ -126,7 +126,10 @@ hipError_t launch_scatter_large_w(int vis_dtype, int wgt_dtype, dim3 gd, hipStre
 // share_cus: cap the scatter at three 256-thread blocks per CU (extra dynamic
 // LDS) so kernels of another stream - the next pipelined call's planner - run
 // beside it
+// store_private: the grid planes are zero (a cip_ms2dirty plane, not an
+// accumulating one), so a tile's only work unit stores its private cells
 hipError_t launch_scatter(int support, int vis_dtype, int wgt_dtype, bool packed, int group, bool share_cus,
+                          bool store_private,
                           const double* uvw,
                           const double* fx, const void* vis, const void* wgt, const RowMap& m, const uint64_t* runs,
                           const int64_t* run_goff, const int64_t* tile_run_off, const void* perm,

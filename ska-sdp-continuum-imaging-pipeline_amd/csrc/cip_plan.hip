@@ -792,6 +792,7 @@ __global__ void chunk_emit_kernel(const int64_t* __restrict__ tile_vis_off, cons
   ch.g0 = g + k * cv;
   ch.g1 = g + ((k + 1) * cv < nv ? (k + 1) * cv : nv);
   ch.tile = t;
+  ch.sole = nv <= cv ? 1 : 0;
   // first run whose end lies beyond g0 (runs of a tile are consecutive)
   int64_t rl = tile_run_off[t], rh = tile_run_off[t + 1] - 1;
   while (rl < rh) {
@@ -879,6 +880,7 @@ __global__ void plane_chunk_emit_kernel(const int64_t* __restrict__ tile_vis_off
   ch.g0 = a + k * cv;
   ch.g1 = a + (k + 1) * cv < b ? a + (k + 1) * cv : b;
   ch.tile = t * ntw + l0;
+  ch.sole = b - a <= cv ? 1 : 0;
   int64_t rl = tile_run_off[t * ntw + l0], rh = tile_run_off[t * ntw + l1 + 1] - 1;
   while (rl < rh) {
     const int64_t mid = (rl + rh) >> 1;

@@ -8,7 +8,7 @@
 #endif
 
 namespace cip {
-template hipError_t launch_scatter_w<CIP_SCATTER_W>(int, int, bool, int, unsigned, dim3, hipStream_t, const double*, const double*,
+template hipError_t launch_scatter_w<CIP_SCATTER_W>(int, int, bool, int, unsigned, int, dim3, hipStream_t, const double*, const double*,
                                                     const void*, const void*, const RowMap&, const uint64_t*,
                                                     const int64_t*, const int64_t*, const void*,
                                                     const Chunk*, int64_t, const GridGeometry&, int64_t, double,
