@@ -376,9 +376,10 @@ __global__ __launch_bounds__(scatter_threads<G>(), CIP_SCATTER_WAVES) void scatt
   // A tile's cells [W - 1, T)^2 are written by its own units only (the
   // neighbours' sub-grids reach W - 1 cells into it): when this unit is the
   // tile's only one and the grid is zero (store_private: a cip_ms2dirty plane,
-  // not an accumulating one), those cells are stored, not added - one 16-B
-  // store instead of two read-modify-write fp64 atomics at the L2 (C4's
-  // 16384^2 grid: the flush is ~1.1 of the 4.9 ms scatter)
+  // not an accumulating one; set on 16384^2+ planes), those cells are stored,
+  // not added - one 16-B store instead of two read-modify-write fp64 atomics
+  // at the L2 (C4's 16384^2 grid: the flush is ~1.1 of the 4.9 ms scatter,
+  // 0.28 ms less with the stores; profiles/r03_ab_flush_store.txt)
   const bool own = store_private != 0 && ch.sole != 0;
 #pragma unroll
   for (int k = 0; k < G; ++k) {
