@@ -83,6 +83,13 @@ extern "C" {
                           * and only the weight sum and max |w V| are reduced;
                           * otherwise the call plans as usual. Images are
                           * identical to a planned call's. */
+#define CIP_GRID_ZEROED 128 /* cip_grid_ms, cip_grid_ms_stokes_i, cip_grid_tiles:
+                          * the caller promises the planes are all zero (the
+                          * first chunk onto cleared planes, or planes kept
+                          * clean by cip_strip_rows): on planes of >= 16384^2
+                          * cells the scatter then stores the cells only one
+                          * of its work units writes instead of adding them
+                          * with atomics (same values). */
 #define CIP_ACC_SINGLE 2 /* complex64 only: single-precision accumulation
                           * class, the reference's ducc0 float gridding (re/im
                           * packed in one 64-bit fixed-point LDS cell, W^2

@@ -1204,7 +1204,7 @@ static int grid_accumulate(const double* uvw, int64_t nrow, const double* freq, 
                            void* hip_stream, double* grids, double* sum_wgt, const RaggedRows* ragged,
                            const uint8_t* flags4 = nullptr) {
   g_last_error.clear();
-  if (flags & ~(CIP_ACC_SINGLE | CIP_PSF)) return set_error(CIP_EINVAL, "unknown flags");
+  if (flags & ~(CIP_ACC_SINGLE | CIP_PSF | CIP_GRID_ZEROED)) return set_error(CIP_EINVAL, "unknown flags");
   if (!params || !grids) return set_error(CIP_EINVAL, "NULL params or grids");
   if (flags & CIP_PSF) {
     vis = nullptr;
@@ -1228,7 +1228,7 @@ static int grid_accumulate(const double* uvw, int64_t nrow, const double* freq, 
   const int G = pp.plan.group;
   for (int64_t q = 0; q * G < g.nplanes; ++q) {
     rc = scatter_plane(pp, q, uvw, vis, vis_dtype, wgt, wgt_dtype, transposed, grids + q * G * plane_elems, s, true,
-                       false, true);
+                       false, (flags & CIP_GRID_ZEROED) == 0);
     if (rc != CIP_OK) return rc;
   }
   if (sum_wgt) CIP_HIP_CHECK(launch_add_scalar(pp.red, sum_wgt, s));

@@ -34,6 +34,7 @@ CIP_NORMALISE = 8
 CIP_ASYNC = 16
 CIP_PIPELINE = 32
 CIP_REUSE_PLAN = 64
+CIP_GRID_ZEROED = 128
 STOKES_CODES = {"I": 0, "Q": 1, "U": 2, "V": 3}
 
 # every symbol declared in include/cip.h

@@ -219,7 +219,7 @@ class HipStripBackend:
                 freq.data_ptr(), int(freq.shape[0]), data.vis.data_ptr(), data.nvis, vis_codes[data.vis.dtype],
                 data.wgt.data_ptr() if data.wgt is not None else None,
                 wgt_codes[data.wgt.dtype] if data.wgt is not None else self._lib.CIP_NONE,
-                self.params, self.px, self.py, self.npix_x, self.npix_y, 0, self._stream(),
+                self.params, self.px, self.py, self.npix_x, self.npix_y, self._lib.CIP_GRID_ZEROED, self._stream(),
                 self.grid.data_ptr(), sumw.data_ptr()))
         return self.grid, sumw
 
