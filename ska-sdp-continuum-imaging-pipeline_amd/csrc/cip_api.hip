@@ -864,6 +864,7 @@ static int prepare(Workspace* ws, const double* uvw, int64_t nrow, const double*
   m.inv_nchan = 1.0 / (double)nchan;
   m.delta = nullptr;
   m.vis_row = nullptr;
+  m.pk_cbits = m.pk_rbits = 0;
   m.flags4 = vis_dtype == CIP_POL4I ? flags4 : nullptr;
   m.nvis = nrow * nchan;
   if (ragged) {
@@ -889,6 +890,17 @@ static int prepare(Workspace* ws, const double* uvw, int64_t nrow, const double*
       CIP_HIP_CHECK(launch_ragged_expand(off, ragged->chan_start, nrow, delta, vis_row, s));
       m.delta = delta;
       m.vis_row = vis_row;
+      // ordered-stream entries (index, row, channel) when they fit 64 bits
+      auto bits = [](int64_t n) {
+        int b = 1;
+        while (b < 62 && ((int64_t)1 << b) < n) ++b;
+        return b;
+      };
+      const int cb = bits(nchan), rb = bits(nrow), ib = bits(ragged->nvis);
+      if (cb + rb + ib <= 64) {
+        m.pk_cbits = cb;
+        m.pk_rbits = rb;
+      }
     }
   }
   // CIP_REUSE_PLAN: the previous plan, if it was made for this geometry (its

@@ -320,6 +320,10 @@ struct RowMap {
   const int64_t* delta;     // ragged: per-row index offset; NULL = dense
   const uint32_t* vis_row;  // ragged: row of each visibility
   const uint8_t* flags4;    // raw linear-feed input (WK_POL4I): (nvis, 4) flags, or NULL = none flagged
+  // ragged ordered-stream entries packed as (index, row, channel) when their
+  // bit widths fit 64 bits (cbits = channel bits, rbits = row bits; 0 = the
+  // (row << 16) | channel form, index = delta[row] + channel)
+  int pk_cbits, pk_rbits;
 };
 
 __device__ __forceinline__ int64_t vis_index(const RowMap& m, int64_t r, int64_t c) {
@@ -338,14 +342,33 @@ __device__ __forceinline__ void vis_rowchan(const RowMap& m, int64_t i, int64_t*
 
 // Entries of the bank-class ordered stream (perm, cip_grid.hip order_kernel):
 // dense rows store the flattened MS index (u32; (row, channel) by one fp64
-// multiply); ragged row slices store (row << 16) | channel (u64), so the
-// scatter finds a visibility's row without a per-visibility row lookup
-// (index = delta[row] + channel, delta a per-row, mostly cached array).
+// multiply); ragged row slices store (index << (rbits + cbits)) | (row <<
+// cbits) | channel (u64) when the three fit (pk_cbits != 0: C4's 1G
+// visibilities over 3.9M rows x 256 channels take 30 + 22 + 8 bits), so the
+// scatter needs neither a row lookup nor the delta[row] gather; else (row <<
+// 16) | channel and index = delta[row] + channel.
 __device__ __forceinline__ uint64_t perm_entry(const void* perm, const RowMap& m, int64_t q) {
   return m.delta ? ((const uint64_t*)perm)[q] : (uint64_t)((const uint32_t*)perm)[q];
 }
+// ragged entry of visibility il = delta[r] + c (row r, channel c)
+__device__ __forceinline__ uint64_t perm_encode_wide(const RowMap& m, int64_t il, int64_t r, int64_t c) {
+  if (m.pk_cbits)
+    return ((uint64_t)il << (m.pk_cbits + m.pk_rbits)) | ((uint64_t)r << m.pk_cbits) | (uint64_t)c;
+  return ((uint64_t)r << 16) | (uint64_t)c;
+}
+__device__ __forceinline__ void perm_decode_wide(uint64_t e, const RowMap& m, int64_t* il, int64_t* r, int64_t* c) {
+  if (m.pk_cbits) {
+    *c = (int64_t)(e & ((1ull << m.pk_cbits) - 1ull));
+    *r = (int64_t)((e >> m.pk_cbits) & ((1ull << m.pk_rbits) - 1ull));
+    *il = (int64_t)(e >> (m.pk_cbits + m.pk_rbits));
+  } else {
+    *r = (int64_t)(e >> 16);
+    *c = (int64_t)(e & 0xffffu);
+    *il = m.delta[*r] + *c;
+  }
+}
 __device__ __forceinline__ uint64_t perm_encode(const RowMap& m, int64_t r, int64_t c) {
-  return m.delta ? (((uint64_t)r << 16) | (uint64_t)c) : (uint64_t)(r * m.nchan + c);
+  return m.delta ? perm_encode_wide(m, m.delta[r] + c, r, c) : (uint64_t)(r * m.nchan + c);
 }
 __device__ __forceinline__ void perm_store(void* perm, const RowMap& m, int64_t pos, uint64_t e) {
   if (m.delta) ((uint64_t*)perm)[pos] = e;
@@ -360,9 +383,7 @@ __device__ __forceinline__ uint64_t perm_entry_t(const void* perm, int64_t q) {
 template <bool WIDE>
 __device__ __forceinline__ void perm_decode_t(uint64_t e, const RowMap& m, int64_t* il, int64_t* r, int64_t* c) {
   if constexpr (WIDE) {
-    *r = (int64_t)(e >> 16);
-    *c = (int64_t)(e & 0xffffu);
-    *il = m.delta[*r] + *c;
+    perm_decode_wide(e, m, il, r, c);
   } else {
     *il = (int64_t)e;
     split_index64((int64_t)e, m.nchan, m.inv_nchan, r, c);
@@ -371,9 +392,7 @@ __device__ __forceinline__ void perm_decode_t(uint64_t e, const RowMap& m, int64
 // -> (visibility index, row, channel)
 __device__ __forceinline__ void perm_decode(uint64_t e, const RowMap& m, int64_t* il, int64_t* r, int64_t* c) {
   if (m.delta) {
-    *r = (int64_t)(e >> 16);
-    *c = (int64_t)(e & 0xffffu);
-    *il = m.delta[*r] + *c;
+    perm_decode_wide(e, m, il, r, c);
   } else {
     *il = (int64_t)e;
     split_index64((int64_t)e, m.nchan, m.inv_nchan, r, c);

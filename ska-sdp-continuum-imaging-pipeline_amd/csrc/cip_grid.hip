@@ -140,6 +140,7 @@ __global__ __launch_bounds__(kOrderThreads, 8) void order_kernel(const double* _
     struct {
       float2 uv[GATHER ? 1 : kOrderBatch];  // (u scale_u, v scale_v) of each slice's row (recompute only)
       uint64_t rec[kOrderBatch];
+      int64_t delta[WIDE ? kOrderBatch : 1];  // ragged: delta[row] of each slice (index = delta + channel)
       int off[kOrderBatch + 1];  // slice starts relative to the window start
       uint16_t idx[kOrderBatch];  // slice of each position
     } a;
@@ -162,6 +163,7 @@ __global__ __launch_bounds__(kOrderThreads, 8) void order_kernel(const double* _
     s_off[k] = (int)(run_goff[ch.first_run + k] - sb);
     const uint64_t rec = runs[ch.first_run + k];
     s_rec[k] = rec;
+    if constexpr (WIDE) sh.a.delta[k] = m.delta[(int64_t)(rec >> 32)];
     if constexpr (!GATHER) {
       const int64_t row = (int64_t)(rec >> 32);
       s_uv[k] = make_float2((float)(uvw[3 * row] * g.scale_u), (float)(uvw[3 * row + 1] * g.scale_v));
@@ -191,7 +193,8 @@ __global__ __launch_bounds__(kOrderThreads, 8) void order_kernel(const double* _
       const uint64_t rec = s_rec[lo];
       const int64_t row = (int64_t)(rec >> 32);
       const int64_t c = (int64_t)((rec >> 16) & 0xffff) + (qi - s_off[lo]);
-      packed[k] = WIDE ? (Entry)(((uint64_t)row << 16) | (uint64_t)c) : (Entry)(row * m.nchan + c);
+      if constexpr (WIDE) packed[k] = (Entry)perm_encode_wide(m, sh.a.delta[lo] + c, row, c);
+      else packed[k] = (Entry)(row * m.nchan + c);
       slice[k] = lo;
       chan[k] = c;
     }
@@ -201,7 +204,7 @@ __global__ __launch_bounds__(kOrderThreads, 8) void order_kernel(const double* _
     cls[k] = 32u;
     if (threadIdx.x + k * kOrderThreads < nsb) {
       if constexpr (GATHER) {
-        cls[k] = vis_class[WIDE ? vis_index(m, (int64_t)(s_rec[slice[k]] >> 32), chan[k]) : (int64_t)packed[k]];
+        cls[k] = vis_class[WIDE ? sh.a.delta[slice[k]] + chan[k] : (int64_t)packed[k]];
       } else {
         const float2 uv = s_uv[slice[k]];
         cls[k] = origin_class_f32(uv.x, uv.y, (float)fx[chan[k]], g);
