@@ -116,6 +116,14 @@ def _cpu_info():
     return {"cpu_model": model, "cpu_count": os.cpu_count(), "affinity": len(os.sched_getaffinity(0))}
 
 
+def _cgroup_cpu_max():
+    """The process's cgroup-v2 CPU quota ("max 100000" = none), if readable."""
+    try:
+        return Path("/sys/fs/cgroup/cpu.max").read_text().strip()
+    except OSError:
+        return None
+
+
 def cpu_baseline(cfg_name, uvw_h, freq_h, vis_h, wgt_h, px, support, nthreads):
     """
     CPU baseline (BASELINE.md "CPU baseline plan"), timed on this host in this
@@ -133,11 +141,14 @@ def cpu_baseline(cfg_name, uvw_h, freq_h, vis_h, wgt_h, px, support, nthreads):
     import oracle
     from ska_sdp_cip_amd import synthetic as syn
 
-    def run(uvw, freq, vis, wgt, npix, pxx):
-        oracle.baseline_ms2dirty(uvw[:64], freq, vis[:64], wgt[:64], npix, npix, pxx, pxx, support, nthreads)
+    def run_threads(uvw, freq, vis, wgt, npix, pxx, nth):
+        oracle.baseline_ms2dirty(uvw[:64], freq, vis[:64], wgt[:64], npix, npix, pxx, pxx, support, nth)
         t0 = time.perf_counter()
-        oracle.baseline_ms2dirty(uvw, freq, vis, wgt, npix, npix, pxx, pxx, support, nthreads)
+        oracle.baseline_ms2dirty(uvw, freq, vis, wgt, npix, npix, pxx, pxx, support, nth)
         return time.perf_counter() - t0
+
+    def run(uvw, freq, vis, wgt, npix, pxx):
+        return run_threads(uvw, freq, vis, wgt, npix, pxx, nthreads)
 
     def synth(name):
         c = CONFIGS[name]
@@ -162,6 +173,16 @@ def cpu_baseline(cfg_name, uvw_h, freq_h, vis_h, wgt_h, px, support, nthreads):
     t = run(uvw_h, freq_h, vis_h, wgt_h, CONFIGS[cfg_name]["npix"], px)
     per[cfg_name] = {"mvis_per_s": round(vis_h.size / t / 1e6, 2), "seconds": round(t, 3),
                      "nvis": int(vis_h.size), "inputs": "the GPU run's own visibilities"}
+    # BASELINE.md's plan: threads = os.cpu_count(); the headline above uses
+    # the box's CPU share for one GPU (16), this is the same full workload
+    # with every core the OS reports (the cgroup quota, if any, still applies)
+    all_threads = os.cpu_count() or nthreads
+    all_cores = None
+    if all_threads != nthreads:
+        t_all = run_threads(uvw_h, freq_h, vis_h, wgt_h, CONFIGS[cfg_name]["npix"], px, all_threads)
+        all_cores = {"threads": all_threads, "mvis_per_s": round(vis_h.size / t_all / 1e6, 2),
+                     "seconds": round(t_all, 3), "cgroup_cpu_max": _cgroup_cpu_max(),
+                     "what": f"the same full {cfg_name.upper()} invert with os.cpu_count() threads"}
     # the reference's Stokes-I prep in numpy on C2-shaped polarisation columns
     c2 = CONFIGS["c2"]
     rng = np.random.default_rng(2)
@@ -187,8 +208,10 @@ def cpu_baseline(cfg_name, uvw_h, freq_h, vis_h, wgt_h, px, support, nthreads):
         "stokes_i_prep": {"mvis_per_s": round(n_st / t_st / 1e6, 2), "seconds": round(t_st, 3),
                           "nvis": n_st, "what": "numpy StokesIGridderInput + effective_weights "
                                                 "(invert.py:78-116) on C2 (rows, 64, 4) columns, 1 thread"},
+        "all_cores": all_cores,
         **_cpu_info(),
-        "threads_note": "threads = the box's CPU share for one GPU (OMP_NUM_THREADS), not os.cpu_count()",
+        "threads_note": ("value: threads = the box's CPU share for one GPU (OMP_NUM_THREADS); all_cores: the same "
+                         "workload with os.cpu_count() threads (BASELINE.md's plan)"),
     }
 
 
@@ -221,7 +244,7 @@ def max_err_vs_oracle(uvw_h, freq_h, vis_h, wgt_h, npix, px, support, wstacking,
                       f"{npix}^2 image, GPU (cip_ms2dirty) vs fp64 CPU oracle, both / sum w"}
 
 
-def run_strong(args, world, rank, device):
+def run_strong(args, world, rank, device, steps=None, warmup=None):
     """
     `--strong`: the north star's C4 split (BASELINE configs[3]) - ONE dirty
     image of 3,906,250 rows x 256 channels = 1,000,000,000 visibilities on a
@@ -261,7 +284,9 @@ def run_strong(args, world, rank, device):
     wgt = torch.where(torch.rand(nvis, device=device, generator=g) < 0.05, torch.zeros_like(wgt), wgt).contiguous()
     data = strips.StripData(uvw[rws].contiguous(), c0.to(torch.int32), c1.to(torch.int32), vis, wgt, rws)
     del uvw
-    backend = strips.HipStripBackend(params, px, px, npix, npix, device=device)
+    # this rank's strip + W - 1 halo rows only (1/N of the grid per rank)
+    backend = strips.HipStripBackend(params, px, px, npix, npix, device=device,
+                                     rows=strips.strip_buffer_rows(layout, rank))
     y0, y1 = layout.rows(rank)
     log(f"[bench --strong] rank {rank}/{world}: strip rows [{y0}, {y1}) of {params.nv}, {nvis:,} vis "
         f"({data.slice_uvw.shape[0]:,} slices), plan {t_plan:.2f} s")
@@ -269,20 +294,22 @@ def run_strong(args, world, rank, device):
     def step(stages=None):
         return strips.invert_strips(data, freq, layout, backend, dst=0, stages=stages)
 
-    for _ in range(args.warmup):
+    steps = args.steps if steps is None else steps
+    warmup = args.warmup if warmup is None else warmup
+    for _ in range(warmup):
         step()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(steps):
         step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     stages = {}
-    nprof = max(2, min(args.steps, 5))
+    nprof = max(2, min(steps, 5))
     for _ in range(nprof):
         img = step(stages)
     parity = None
@@ -309,14 +336,14 @@ def run_strong(args, world, rank, device):
     else:
         per_rank = [nvis]
     total = sum(per_rank)
-    ms_per_step = elapsed / args.steps * 1e3
+    ms_per_step = elapsed / steps * 1e3
     result = {
         "metric": f"Mvis/s gridded (invert) on {params.nu // 1024}k^2 grid, support={params.support}",
-        "value": round(total * args.steps / elapsed / 1e6, 2),
+        "value": round(total * steps / elapsed / 1e6, 2),
         "unit": "Mvis/s",
         "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
+        "steps": steps,
+        "warmup": warmup,
         "ms_per_step": round(ms_per_step, 3),
         "higher_is_better": True,
         "scaling": "strong",
@@ -332,17 +359,108 @@ def run_strong(args, world, rank, device):
                             "gather of image rows" if world > 1 else "uv strips x1 (whole C4 on one GPU)"),
             "strip_rows": [layout.rows(r) for r in range(world)],
             "strip_vis": per_rank,
+            "grid_rows_per_rank": [strips.strip_buffer_rows(layout, r)[1] for r in range(world)],
         },
         "stages_ms_rank0": {k: round(v / nprof * 1e3, 3) for k, v in stages.items()},
         "parity": parity,
         "roofline": None,
         "cpu_baseline": None,
     }
-    if rank == 0:
-        print(json.dumps(result), flush=True)
+    del backend, data, vis, wgt
+    torch.cuda.empty_cache()
+    return result
+
+
+def run_strong_wplanes(args, world, rank, device):
+    """
+    `--strong --wstacking`: strong scaling of ONE w-stacking image - the
+    reference's gridding mode (invert.py:170-183: epsilon 1e-4 -> W = 6,
+    do_wstacking=True) on the C3 workload (100M visibilities, 8192^2 grid) -
+    by w-plane groups (SURVEY.md 8(e) option 2, ska_sdp_cip_amd.wplanes):
+    every rank holds the visibilities, takes a contiguous range of the plane
+    stack balanced by the plane cost model, grids + FFTs + screens only those
+    planes (cip_ms2dirty_wplanes) and one RCCL reduce of the 4096^2 partial
+    images makes the image on rank 0. value = 100M vis x steps / time.
+    """
+    import torch
+    import torch.distributed as dist
+
+    from ska_sdp_cip_amd import wplanes
+
+    cfg = CONFIGS["c3"]
+    uvw_d, freq_d, vis_d, wgt_d, px, _, _ = make_inputs(cfg, 0, 1, device)  # the same data on every rank
+    npix = cfg["npix"]
+    support = None if args.epsilon_call else args.support
+    be = wplanes.HipWPlaneBackend(uvw_d, freq_d, vis_d, wgt_d, npix, npix, px, px, epsilon=1e-4, support=support,
+                                  single_precision_accumulation=args.single)
+    params = be.params()
+    feeds = wplanes.plane_feeds(uvw_d, freq_d, params)
+    split = wplanes.split_planes(wplanes.plane_cost(feeds, params), world)
+    out = torch.zeros((npix, npix), dtype=torch.float64, device=device)
+    log(f"[bench --strong --wstacking] rank {rank}/{world}: planes {split[rank]} of {params.nplanes}, "
+        f"support {params.support}")
+
+    def step(stages=None):
+        return wplanes.invert_wplanes(be, split, dst=0, stages=stages, out=out)
+
+    for _ in range(args.warmup):
+        step()
     if world > 1:
         dist.barrier()
-        dist.destroy_process_group()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    stages = {}
+    nprof = max(2, min(args.steps, 5))
+    for _ in range(nprof):
+        img = step(stages)
+    parity = None
+    if world == 1:
+        ref, _ = gridder_ms2dirty_ref(uvw_d, freq_d, vis_d, wgt_d, npix, px, params.support, args.single)
+        parity = {"max_abs_diff_vs_one_shot": float((img - ref).abs().max()), "peak": float(ref.abs().max()),
+                  "what": "normalised images: invert_wplanes (1 rank) vs cip_ms2dirty"}
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    nvis = cfg["rows"] * cfg["nchan"]
+    return {
+        "metric": f"Mvis/s gridded (invert) on {params.nu // 1024}k^2 grid, support={params.support}, w-stacking",
+        "value": round(nvis * args.steps / elapsed / 1e6, 2),
+        "unit": "Mvis/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f32-class (packed 2x32-bit)" if args.single else "f64",
+        "data": "synthetic (seeded MeerKAT-like uvw tracks, random complex64 vis, float32 weights, 5% flagged)",
+        "config": {
+            "workload": (f"C3 reference call: {nvis:,} vis -> {params.nu}^2 grid ({npix}^2 image), support "
+                         f"{params.support}, w-stacking {params.nplanes} planes, "
+                         f"{'packed single-precision' if args.single else 'fp64'} accumulate"),
+            "parallelism": f"w-plane groups x{world} + RCCL image reduce (SURVEY 8(e) option 2)",
+            "plane_split": split,
+        },
+        "stages_ms_rank0": {k: round(v / nprof * 1e3, 3) for k, v in stages.items()},
+        "parity": parity,
+        "roofline": None,
+        "cpu_baseline": None,
+    }
+
+
+def gridder_ms2dirty_ref(uvw, freq, vis, wgt, npix, px, support, single):
+    from ska_sdp_cip_amd import gridder
+
+    return gridder.device_ms2dirty(uvw, freq, vis, wgt, npix, npix, px, px, support=support, do_wstacking=True,
+                                   single_precision_accumulation=single, normalise=True)
 
 
 def reference_call_rate(invert, buf, steps, warmup=3):
@@ -413,8 +531,33 @@ def main():
                     help="skip the reference-call secondary figure of the default run")
     ap.add_argument("--strong", action="store_true",
                     help="strong scaling of ONE C4 image (1G vis, 16k^2 grid) over the ranks: uv strips + halo "
-                         "exchange + distributed FFT (DESIGN.md 7); --config is ignored")
+                         "exchange + distributed FFT (DESIGN.md 7); with --wstacking: ONE C3 w-stacking image split "
+                         "by w-plane groups + one image reduce (SURVEY 8(e) option 2); --config is ignored")
+    ap.add_argument("--epsilon-call", action="store_true",
+                    help="with --strong --wstacking: epsilon = 1e-4 picks the support (the reference's call, W = 6) "
+                         "instead of --support")
+    ap.add_argument("--no-strong-secondary", action="store_true",
+                    help="skip the strong-scaling C4 secondary (secondary.strong_c4) of the default run")
     args = ap.parse_args()
+
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # `bench.py --gpus N` outside a launcher: start N rank processes (one
+        # per GPU) through torch.distributed.run BEFORE anything touches the
+        # GPU here, and exit with their status
+        import socket
+        import subprocess
+
+        with socket.socket() as so:
+            so.bind(("127.0.0.1", 0))
+            port = so.getsockname()[1]
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+               "--master-addr", "127.0.0.1", "--master-port", str(port), str(Path(__file__).resolve())] + sys.argv[1:]
+        log(f"[bench] launching {args.gpus} ranks: {' '.join(cmd)}")
+        return subprocess.call(cmd)
+    env_world = int(os.environ.get("WORLD_SIZE", "1"))
+    if env_world != args.gpus:
+        log(f"[bench] WORLD_SIZE={env_world} but --gpus {args.gpus}: refusing to report a mismatched run")
+        return 2
 
     import torch
     import torch.distributed as dist
@@ -425,14 +568,27 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    comm = {"backend": None, "world_size": 1}
     if world > 1:
         torch.cuda.set_device(local_rank)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        # what the communicator reports (RCCL is torch's "nccl" backend on ROCm)
+        comm = {"backend": dist.get_backend(), "world_size": dist.get_world_size(),
+                "rccl_version": ".".join(str(x) for x in torch.cuda.nccl.version())}
+        if comm["world_size"] != args.gpus:
+            raise SystemExit(f"communicator world size {comm['world_size']} != --gpus {args.gpus}")
     device = torch.device("cuda", local_rank)
     torch.cuda.set_device(device)
     if args.strong:
-        run_strong(args, world, rank, device)
-        return
+        result = (run_strong_wplanes(args, world, rank, device) if args.wstacking
+                  else run_strong(args, world, rank, device))
+        result["communicator"] = comm
+        if rank == 0:
+            print(json.dumps(result), flush=True)
+        if world > 1:
+            dist.barrier()
+            dist.destroy_process_group()
+        return 0
     cfg = CONFIGS[args.config]
     nvis = cfg["rows"] * cfg["nchan"]
     npix = cfg["npix"]
@@ -614,12 +770,29 @@ def main():
         "mean_slice_len": round(avg["visibilities"] / max(runs, 1), 2),
         "gtap_per_s": round(world * nvis * taps * args.steps / elapsed / 1e9, 2),
     }
-    if world == 1 and not args.no_secondary and raw is None and not args.wstacking and not args.single:
+    result["communicator"] = comm
+    default_run = raw is None and not args.wstacking and not args.single and args.config == "c3"
+    secondary = {}
+    if world == 1 and not args.no_secondary and default_run:
         # the reference's own gridder call on the same resident inputs
         # (invert.py:170-183: epsilon 1e-4 -> W = 6, do_wstacking=True,
         # complex64 input -> ducc0's float accumulation class): a secondary
         # figure beside the f64 metric, so every default run reports it
-        result["secondary"] = {"reference_call": reference_call_rate(invert, bufs[0], args.steps)}
+        secondary["reference_call"] = reference_call_rate(invert, bufs[0], args.steps)
+    if not args.no_strong_secondary and default_run and args.support == 8:
+        # the north star's strong split beside the weak headline: ONE C4 image
+        # (1G visibilities, 16384^2 grid) over the same ranks (uv strips + halo
+        # exchange + distributed FFT) - at N = 1 the whole C4 on
+        # one GPU, the base of the strong-scaling curve
+        torch.cuda.empty_cache()
+        st = run_strong(args, world, rank, device, steps=max(3, min(args.steps, 10)), warmup=2)
+        secondary["strong_c4"] = {k: st[k] for k in ("metric", "value", "unit", "n_gpus", "steps", "ms_per_step",
+                                                     "scaling", "stages_ms_rank0", "parity")}
+        secondary["strong_c4"]["workload"] = st["config"]["workload"]
+        secondary["strong_c4"]["parallelism"] = st["config"]["parallelism"]
+        secondary["strong_c4"]["grid_rows_per_rank"] = st["config"]["grid_rows_per_rank"]
+    if secondary:
+        result["secondary"] = secondary
     nthreads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, len(os.sched_getaffinity(0)))
     need_host = rank == 0 and ((world == 1 and not args.no_cpu_baseline) or not args.no_max_err)
     vis_h = wgt_h = None
@@ -647,7 +820,8 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

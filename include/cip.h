@@ -89,7 +89,9 @@ extern "C" {
                           * clean by cip_strip_rows): on planes of >= 16384^2
                           * cells the scatter then stores the cells only one
                           * of its work units writes instead of adding them
-                          * with atomics (same values). */
+                          * with atomics (same values). The stores are 16-byte
+                          * cells: planes that are not 16-byte aligned ignore
+                          * the flag (atomic adds, same result). */
 #define CIP_ACC_SINGLE 2 /* complex64 only: single-precision accumulation
                           * class, the reference's ducc0 float gridding (re/im
                           * packed in one 64-bit fixed-point LDS cell, W^2
@@ -136,6 +138,26 @@ int cip_ms2dirty(const double* uvw, int64_t nrow, const double* freq,
                  double epsilon, int support, int flags,
                  void* hip_stream, double* dirty_out, double* sum_wgt_out,
                  cip_gridder_params* params_out);
+
+/* cip_ms2dirty restricted to w planes [plane_begin, plane_end) of the
+ * w-stacking stack (CIP_WSTACKING required): the multi-GPU split of ONE
+ * w-stacking image by plane groups (SURVEY.md 8(e) option 2; ska_sdp_cip_amd
+ * wplanes.py). The planner still reads every visibility (the weight sum and
+ * the stack's parameters are those of the whole call) but keeps only those
+ * feeding a plane of the range; the scatter and the FFT run for those planes
+ * only. dirty_out = that range's share of the image, with the final w and grid
+ * correction (and CIP_NORMALISE) applied - all linear, so the shares of a
+ * partition of [0, nplanes) sum to cip_ms2dirty's image. An empty range gives
+ * zeros; plane_end > nplanes is CIP_EINVAL. No reference counterpart (the
+ * reference's dask tasks split rows, invert.py:248-270). */
+int cip_ms2dirty_wplanes(const double* uvw, int64_t nrow, const double* freq,
+                         int64_t nchan, const void* vis, int vis_dtype,
+                         const void* wgt, int wgt_dtype, int64_t npix_x,
+                         int64_t npix_y, double pixsize_x, double pixsize_y,
+                         double epsilon, int support, int flags,
+                         int64_t plane_begin, int64_t plane_end,
+                         void* hip_stream, double* dirty_out,
+                         double* sum_wgt_out, cip_gridder_params* params_out);
 
 /* cip_ms2dirty on the raw linear-feed columns (the reference's
  * StokesIGridderInput + effective weights, invert.py:78-116, fused into the
@@ -208,6 +230,24 @@ int cip_grid_tiles(const double* slice_uvw, const int32_t* chan_start,
                    const cip_gridder_params* params, double pixsize_x,
                    double pixsize_y, int64_t npix_x, int64_t npix_y, int flags,
                    void* hip_stream, double* grids, double* sum_wgt);
+
+/* cip_grid_tiles onto ONE uv strip's buffer instead of the whole grid (the
+ * strong-scaling ranks of DESIGN.md 7 hold only their strip + halo rows): the
+ * grid must be 2-D in the pruned-FFT layout (cip_grid_layout == 1, stored
+ * gT[y][x]); `strip` holds nrows rows of nu complex128 cells, buffer row k =
+ * grid row (row0 + k) mod nv. Every visibility's footprint must fall inside
+ * those rows (a strip's slices from its footprint-origin rows [y0, y1) need
+ * nrows = y1 - y0 + W - 1): a cell outside is dropped and the call returns
+ * CIP_ERANGE. Flags as cip_grid_tiles (CIP_GRID_ZEROED: buffer all zero).
+ * No reference counterpart (the reference grids whole images per task). */
+int cip_grid_tiles_strip(const double* slice_uvw, const int32_t* chan_start,
+                         const int32_t* chan_stop, int64_t nslices,
+                         const double* freq, int64_t nchan, const void* vis,
+                         int64_t nvis, int vis_dtype, const void* wgt,
+                         int wgt_dtype, const cip_gridder_params* params,
+                         double pixsize_x, double pixsize_y, int64_t npix_x,
+                         int64_t npix_y, int64_t row0, int64_t nrows, int flags,
+                         void* hip_stream, double* strip, double* sum_wgt);
 
 /* The accumulated planes -> dirty image (device (npix_x,npix_y) f64, not
  * normalised): FFT, w-screens and grid correction as in cip_ms2dirty. The

@@ -106,6 +106,35 @@ def support_for_epsilon(eps: float) -> int:
     return 16
 
 
+# The kernel shape rule (tools/gen_es_kernels.py beta_for_support, restated):
+# beta = 2.3 W (Barnett et al.'s sigma = 2 choice) while the ES kernel's edge
+# ratio F(1/4)/F(0) stays >= 0.03; larger supports take the beta at which it
+# equals 0.03 (their grid / w corrections then amplify rounding no more than a
+# W = 24 kernel's, and the aliasing stays at the fp64 floor).
+LARGE_EDGE_RATIO = 0.03
+
+
+def es_edge_ratio(W: int, beta: float, nu: float = 0.25) -> float:
+    """F(nu) / F(0) of the exact ES kernel exp(beta (sqrt(1 - (2d/W)^2) - 1)),
+    |d| < W/2 cells (40-point Gauss-Legendre per cell)."""
+    x, wq = np.polynomial.legendre.leggauss(40)
+    d = (np.arange(W)[:, None] - W / 2.0) + 0.5 * (x[None, :] + 1.0)
+    t = 2.0 * d / W
+    ph = np.where(np.abs(t) < 1.0, np.exp(beta * (np.sqrt(np.clip(1.0 - t * t, 0.0, None)) - 1.0)), 0.0)
+    return float((wq * ph * np.cos(2.0 * math.pi * d * nu)).sum() / (wq * ph).sum())
+
+
+def es_beta(W: int) -> float:
+    """Kernel shape parameter of support W (the rule above; bisection)."""
+    if W <= 16 or es_edge_ratio(W, 2.3 * W) >= LARGE_EDGE_RATIO:
+        return 2.3 * W
+    lo, hi = 2.3 * W, 40.0 * W
+    for _ in range(100):
+        mid = 0.5 * (lo + hi)
+        lo, hi = (mid, hi) if es_edge_ratio(W, mid) < LARGE_EDGE_RATIO else (lo, mid)
+    return 0.5 * (lo + hi)
+
+
 def choose_params(npix_x, npix_y, px, py, epsilon=1e-4, support=None, do_wstacking=False,
                   wmin=0.0, wmax=0.0) -> dict:
     """Grid / kernel / plane parameters (spec: DESIGN.md 'Parameters')."""
@@ -125,7 +154,7 @@ def choose_params(npix_x, npix_y, px, py, epsilon=1e-4, support=None, do_wstacki
     else:
         dw, nplanes, w0 = 1.0, 1, 0.0
     return dict(nu=nu, nv=nv, support=W, sigma=sigma, nplanes=nplanes, w0=w0, dw=dw, nmin=nmin,
-                do_wstacking=bool(do_wstacking))
+                do_wstacking=bool(do_wstacking), beta=es_beta(W))
 
 
 def kernel_ft(W: int, nus) -> np.ndarray:
@@ -238,8 +267,11 @@ def _nm1(npix_x, npix_y, px, py):
 
 
 def ms2dirty(uvw, freq, vis, wgt, npix_x, npix_y, px, py, epsilon=1e-4, support=None,
-             do_wstacking=False, nthreads=0, return_params=False):
-    """fp64 dirty image of the oracle pipeline (same definition as the GPU)."""
+             do_wstacking=False, nthreads=0, return_params=False, planes=None):
+    """fp64 dirty image of the oracle pipeline (same definition as the GPU).
+    planes=(begin, end) (w-stacking): the share of w planes [begin, end) of
+    the stack (cip_ms2dirty_wplanes); the shares of a partition of the stack
+    sum to the image."""
     uvw, freq, vis, wgt = _as_inputs(uvw, freq, vis, wgt)
     wmin, wmax = w_range(uvw, freq) if do_wstacking else (0.0, 0.0)
     prm = choose_params(npix_x, npix_y, px, py, epsilon, support, do_wstacking, wmin, wmax)
@@ -253,7 +285,8 @@ def ms2dirty(uvw, freq, vis, wgt, npix_x, npix_y, px, py, epsilon=1e-4, support=
     else:
         nm1 = _nm1(npix_x, npix_y, px, py)
         acc = np.zeros((npix_x, npix_y))
-        for p in range(prm["nplanes"]):
+        pb, pe = (0, prm["nplanes"]) if planes is None else (int(planes[0]), min(int(planes[1]), prm["nplanes"]))
+        for p in range(pb, pe):
             g = grid_plane(uvw, freq, vis, wgt, prm, px, py, p, nthreads)
             ghat = fft_backward(g, nthreads)
             wp = prm["w0"] + p * prm["dw"]
@@ -306,6 +339,25 @@ def facet_rotation(l0, m0):
     k = axis / s
     kx = np.array([[0.0, -k[2], k[1]], [k[2], 0.0, -k[0]], [-k[1], k[0], 0.0]])
     return np.eye(3) + s * kx + (1.0 - n0) * (kx @ kx)
+
+
+def facet_rephase(uvw, freq, vis, l0, m0):
+    """The facet data (restated from the convention): with
+    b = (u, v, -w), a source at s has delay d(s) = b.s - b.z; the facet frame
+    holds V' = V exp(+2 pi i f/c d(s0)), s0 = (l0, m0, n0), and b' = Q^T b
+    (Q = facet_rotation), stored as (u', v', w') = (b'_0, b'_1, -b'_2).
+    numpy fp64; vis may be None (uvw only). Returns (uvw', vis' complex128)."""
+    uvw = np.asarray(uvw, dtype=np.float64)
+    b = uvw * np.array([1.0, 1.0, -1.0])
+    n0m1 = -(l0 * l0 + m0 * m0) / (math.sqrt(1.0 - l0 * l0 - m0 * m0) + 1.0)
+    delay = b[:, 0] * l0 + b[:, 1] * m0 + b[:, 2] * n0m1
+    bp = b @ facet_rotation(l0, m0)  # rows: (Q^T b)^T = b^T Q
+    uvw_out = np.ascontiguousarray(bp * np.array([1.0, 1.0, -1.0]))
+    if vis is None:
+        return uvw_out, None
+    turns = delay[:, None] * (np.asarray(freq, dtype=np.float64)[None, :] / SPEED_OF_LIGHT)
+    turns -= np.rint(turns)
+    return uvw_out, np.asarray(vis).astype(np.complex128) * np.exp(2j * np.pi * turns)
 
 
 def stokes(vis4, flags4, wgt4, which):

@@ -206,12 +206,9 @@ static int choose(int64_t npix_x, int64_t npix_y, double px, double py, double e
     const bool large = support == 24 || support == 32 || support == 48 || support == 64;
     if (!small && !large)
       return set_error(CIP_EINVAL, "support must be an even number in [4, 16] or one of 24, 32, 48, 64");
-    // at beta = 2.3 W the kernel transform at the field edge is F(1/4)/F(0) =
-    // 1.6e-4 for W = 64: the u, v and w corrections amplify the fixed-point
-    // quantum at the field corners by ~1e11 (measured 4e-5 of sum w, above the
-    // 1e-6 gate; tests/test_gpu_large_support.py), so w-stacking stops at 48
-    if (do_wstacking && support > 48)
-      return set_error(CIP_EINVAL, "w-stacking supports kernel supports up to 48");
+    // (the large supports' shape beta keeps W = 16's edge ratio F(1/4)/F(0),
+    // tools/gen_es_kernels.py, so their grid and w corrections amplify the
+    // fixed-point quantum no more than W = 16's: w-stacking at every support)
   } else {
     if (!(epsilon > 0.0)) return set_error(CIP_EINVAL, "epsilon must be positive");
     support = support_for_epsilon(epsilon);
@@ -264,6 +261,11 @@ static GridGeometry geometry(const cip_gridder_params& p, double px, double py) 
   g.nty = (p.nv + p.tile - 1) / p.tile;
   g.ntw = p.do_wstacking ? (p.nplanes - p.support + 1) : 1;
   g.transposed = 0;
+  g.row0 = 0;
+  g.rows = p.nv;
+  g.oob = nullptr;
+  g.plane_lo = 0;
+  g.plane_hi = p.nplanes;
   return g;
 }
 
@@ -306,7 +308,10 @@ struct Workspace {
   // the "grid" buffer when it is known all-zero (the masked FFT pass A zeroes
   // what the scatter wrote), else NULL
   double* grid_clean = nullptr;
-  int64_t grid_clean_planes = 0;  // how many of its leading planes are known zero
+  // how many of its leading BYTES are known zero: a call on a smaller grid
+  // zeroes (and keeps clean) only its own planes' bytes, so the state is a byte
+  // count, not a plane count (a later larger-geometry call must not trust it)
+  size_t grid_clean_bytes = 0;
   // CIP_ASYNC pipelining (cip_ms2dirty): consecutive calls alternate between
   // two sets of planner buffers (parity; buf() appends the parity to buffer
   // names while parity_scope is set), so the planner of call k + 1 runs on
@@ -825,7 +830,7 @@ static int prepare(Workspace* ws, const double* uvw, int64_t nrow, const double*
                    double px, double py, double epsilon, int support, int do_wstacking, bool packed,
                    const cip_gridder_params* given, hipStream_t s, Prepared* out, double** grid_out = nullptr,
                    const RaggedRows* ragged = nullptr, bool reuse = false, const uint8_t* flags4 = nullptr,
-                   bool want_group = true) {
+                   bool want_group = true, int64_t plane_begin = 0, int64_t plane_end = -1) {
   if (!ws->parity_scope) ws->plan_unscoped = true;
   if (!vis_dtype_ok(vis_dtype)) return set_error(CIP_EINVAL, "vis dtype must be complex64 or complex128");
   if (!wgt_dtype_ok(wgt_dtype)) return set_error(CIP_EINVAL, "wgt dtype must be float32, float64 or none");
@@ -908,7 +913,8 @@ static int prepare(Workspace* ws, const double* uvw, int64_t nrow, const double*
   // promise)
   const std::vector<double> key = {(double)nrow, (double)nchan, (double)npix_x, (double)npix_y, px, py, epsilon,
                                    (double)support, (double)do_wstacking, (double)packed,
-                                   given ? 1.0 : 0.0, want_group ? 1.0 : 0.0};
+                                   given ? 1.0 : 0.0, want_group ? 1.0 : 0.0, (double)plane_begin,
+                                   (double)plane_end};
   const bool reusing = reuse && !ragged && given == nullptr && ws->saved_valid && ws->saved_key == key;
   if (reusing) given = &ws->saved_p;
   double wmin = 0.0, wmax = 0.0;
@@ -934,6 +940,13 @@ static int prepare(Workspace* ws, const double* uvw, int64_t nrow, const double*
     if (rc != CIP_OK) return rc;
   }
   out->g = geometry(out->p, px, py);
+  if (plane_end >= 0) {
+    // a range of the w-plane stack (cip_ms2dirty_wplanes)
+    if (plane_begin < 0 || plane_begin > plane_end || plane_end > out->p.nplanes)
+      return set_error(CIP_EINVAL, "w-plane range outside [0, nplanes]");
+    out->g.plane_lo = plane_begin;
+    out->g.plane_hi = plane_end;
+  }
   // tile keys are 32-bit ((iy0 / T) ntx + ix0 / T) ntw + iw0 (cip_plan.hip):
   // a larger key space would wrap and mis-sort the runs
   if ((double)out->g.ntx * (double)out->g.nty * (double)out->g.ntw >= 4294967295.0)
@@ -952,7 +965,7 @@ static int prepare(Workspace* ws, const double* uvw, int64_t nrow, const double*
     const size_t gbytes = sizeof(double) * 2 * out->g.nu * out->g.nv * gplanes;
     double* grid = buf<double>(ws, "grid", 2 * out->g.nu * out->g.nv * gplanes);
     if (!grid) return CIP_ENOMEM;
-    if (ws->grid_clean != grid || ws->grid_clean_planes < gplanes) {
+    if (ws->grid_clean != grid || ws->grid_clean_bytes < gbytes) {
       const int zr = zero_on_side(ws, grid, gbytes, s);
       if (zr != CIP_OK) return zr;
     }
@@ -1154,7 +1167,8 @@ static bool fft_rowskip() {
 // rowbits (with dmask): the plane's tile-row bits (row_bits_kernel)
 static int plane_to_dirty(const DirtyStage& st, const GridGeometry& g, int64_t p, double* grid, double* dirty_out,
                           hipStream_t s, const uint32_t* dmask = nullptr, const double* norm = nullptr,
-                          const uint32_t* rowbits = nullptr) {
+                          const uint32_t* rowbits = nullptr, int first = -1) {
+  if (first < 0) first = p == 0;  // the first plane overwrites the image, later ones add
   hipEvent_t f0 = g_prof.mark(s);
   if (st.fast) {
     if (!fft_rowskip()) rowbits = nullptr;
@@ -1167,13 +1181,13 @@ static int plane_to_dirty(const DirtyStage& st, const GridGeometry& g, int64_t p
   // pass B carries the crop epilogue: it is booked under "fft"
   if (st.fast)
     CIP_HIP_CHECK(launch_fft_cols(st.fft_h, g.nv, st.npix_x, st.npix_y, st.tw_v, g.do_wstacking ? 1 : 0, dirty_out,
-                                  st.cx, st.cy, st.px, st.py, w_plane, p == 0, g.do_wstacking ? nullptr : norm,
+                                  st.cx, st.cy, st.px, st.py, w_plane, first, g.do_wstacking ? nullptr : norm,
                                   dmask ? rowbits : nullptr, s));
   hipEvent_t f1 = g_prof.mark(s);
   g_prof.span(3, f0, f1);
   if (st.fast) {
   } else if (g.do_wstacking) {
-    CIP_HIP_CHECK(launch_wplane_accumulate(grid, g, st.npix_x, st.npix_y, st.px, st.py, w_plane, p == 0, dirty_out,
+    CIP_HIP_CHECK(launch_wplane_accumulate(grid, g, st.npix_x, st.npix_y, st.px, st.py, w_plane, first, dirty_out,
                                            s));
   } else {
     CIP_HIP_CHECK(launch_crop_correct_2d(grid, g, st.npix_x, st.npix_y, st.cx, st.cy, dirty_out, s));
@@ -1214,10 +1228,13 @@ static int grid_accumulate(const double* uvw, int64_t nrow, const double* freq, 
                            int vis_dtype, const void* wgt, int wgt_dtype, const cip_gridder_params* params,
                            double pixsize_x, double pixsize_y, int64_t npix_x, int64_t npix_y, int flags,
                            void* hip_stream, double* grids, double* sum_wgt, const RaggedRows* ragged,
-                           const uint8_t* flags4 = nullptr) {
+                           const uint8_t* flags4 = nullptr, int64_t row0 = 0, int64_t nrows = 0) {
   g_last_error.clear();
   if (flags & ~(CIP_ACC_SINGLE | CIP_PSF | CIP_GRID_ZEROED)) return set_error(CIP_EINVAL, "unknown flags");
   if (!params || !grids) return set_error(CIP_EINVAL, "NULL params or grids");
+  // the flush's private-cell stores (CIP_GRID_ZEROED) write 16-byte cells:
+  // planes that are only 8-byte aligned take the atomic path instead
+  if (((uintptr_t)grids & 15u) != 0u) flags &= ~CIP_GRID_ZEROED;
   if (flags & CIP_PSF) {
     vis = nullptr;
     if (vis_dtype != CIP_POL4I) vis_dtype = CIP_C64;
@@ -1234,9 +1251,22 @@ static int grid_accumulate(const double* uvw, int64_t nrow, const double* freq, 
                    params->support, params->do_wstacking, (flags & CIP_ACC_SINGLE) != 0, params, s, &pp, nullptr,
                    ragged, false, flags4);
   if (rc != CIP_OK) return rc;
+  const bool transposed = grid_is_transposed(pp.g, npix_x, npix_y);
+  unsigned* oob = nullptr;
+  if (nrows > 0) {
+    // a strip's row window (cip_grid_tiles_strip): rows [row0, row0 + nrows) mod nv
+    if (!transposed || pp.g.nplanes != 1)
+      return set_error(CIP_EINVAL, "strip buffers need a 2-D grid in the pruned-FFT layout");
+    if (row0 < 0 || row0 >= pp.g.nv || nrows > pp.g.nv) return set_error(CIP_EINVAL, "strip rows outside the grid");
+    oob = buf<unsigned>(ws, "strip_oob", 1);
+    if (!oob) return CIP_ENOMEM;
+    CIP_HIP_CHECK(hipMemsetAsync(oob, 0, sizeof(unsigned), s));
+    pp.g.row0 = row0;
+    pp.g.rows = nrows;
+    pp.g.oob = oob;
+  }
   const GridGeometry& g = pp.g;
-  const bool transposed = grid_is_transposed(g, npix_x, npix_y);
-  const int64_t plane_elems = 2 * g.nu * g.nv;
+  const int64_t plane_elems = 2 * g.nu * g.rows;
   const int G = pp.plan.group;
   for (int64_t q = 0; q * G < g.nplanes; ++q) {
     rc = scatter_plane(pp, q, uvw, vis, vis_dtype, wgt, wgt_dtype, transposed, grids + q * G * plane_elems, s, true,
@@ -1245,8 +1275,16 @@ static int grid_accumulate(const double* uvw, int64_t nrow, const double* freq, 
   }
   if (sum_wgt) CIP_HIP_CHECK(launch_add_scalar(pp.red, sum_wgt, s));
   g_prof.span(5, t_start, g_prof.mark(s));
+  unsigned* h_oob = nullptr;
+  if (oob) {
+    h_oob = (unsigned*)pinned(ws, sizeof(unsigned));
+    if (!h_oob) return set_error(CIP_ENOMEM, "hipHostMalloc failed");
+    CIP_HIP_CHECK(hipMemcpyAsync(h_oob, oob, sizeof(unsigned), hipMemcpyDeviceToHost, s));
+  }
   CIP_HIP_CHECK(hipStreamSynchronize(s));
   g_prof.finish();
+  if (h_oob && *h_oob != 0u)
+    return set_error(CIP_ERANGE, "a visibility's footprint leaves the strip's rows (cells dropped)");
   return CIP_OK;
 }
 
@@ -1272,7 +1310,8 @@ namespace cip {
 static int ms2dirty_impl(const double* uvw, int64_t nrow, const double* freq, int64_t nchan, const void* vis,
                          int vis_dtype, const void* wgt, int wgt_dtype, const uint8_t* flags4, int64_t npix_x,
                          int64_t npix_y, double pixsize_x, double pixsize_y, double epsilon, int support, int flags,
-                         void* hip_stream, double* dirty_out, double* sum_wgt_out, cip_gridder_params* params_out) {
+                         void* hip_stream, double* dirty_out, double* sum_wgt_out, cip_gridder_params* params_out,
+                         int64_t plane_begin = 0, int64_t plane_end = -1) {
   if (flags & ~(CIP_WSTACKING | CIP_ACC_SINGLE | CIP_PSF | CIP_NORMALISE | CIP_ASYNC | CIP_PIPELINE | CIP_REUSE_PLAN))
     return set_error(CIP_EINVAL, "unknown flags");
   if ((flags & CIP_REUSE_PLAN) && (flags & CIP_PIPELINE))
@@ -1340,7 +1379,8 @@ static int ms2dirty_impl(const double* uvw, int64_t nrow, const double* freq, in
   ws->parity_scope = pipelined;
   int rc = prepare(ws, uvw, nrow, freq, nchan, vis, vis_dtype, wgt, wgt_dtype, npix_x, npix_y, pixsize_x, pixsize_y,
                    epsilon, support, do_wstacking, packed, nullptr, ps, &pp,
-                   (overlap_zero() && !pipelined) ? &grid : nullptr, nullptr, (flags & CIP_REUSE_PLAN) != 0, flags4);
+                   (overlap_zero() && !pipelined) ? &grid : nullptr, nullptr, (flags & CIP_REUSE_PLAN) != 0, flags4,
+                   true, plane_begin, plane_end);
   ws->parity_scope = false;
   if (pipelined) {
     // s continues once the plan exists (also after a failed one: nothing then runs on it)
@@ -1362,24 +1402,32 @@ static int ms2dirty_impl(const double* uvw, int64_t nrow, const double* freq, in
   const int64_t plane_elems = 2 * g.nu * g.nv;
   if (!grid) grid = buf<double>(ws, "grid", plane_elems * G);
   if (!grid) return CIP_ENOMEM;
-  const int64_t prev_clean = ws->grid_clean == grid ? ws->grid_clean_planes : 0;
-  clean = clean || prev_clean >= G;
+  const size_t group_bytes = sizeof(double) * (size_t)plane_elems * (size_t)G;
+  const size_t prev_clean = ws->grid_clean == grid ? ws->grid_clean_bytes : 0;
+  clean = clean || prev_clean >= group_bytes;
   DirtyStage st;
   rc = dirty_stage(ws, g, npix_x, npix_y, pixsize_x, pixsize_y, s, &st);
   if (rc != CIP_OK) return rc;
   ws->grid_clean = nullptr;  // dirty until a masked pass A has consumed every written tile
   const uint32_t* dmask = st.fast ? pp.plan.dmask : nullptr;
-  for (int64_t q = 0; q * G < g.nplanes; ++q) {
+  // the plane groups holding planes [plane_lo, plane_hi) (the whole stack
+  // unless cip_ms2dirty_wplanes); an empty range leaves a zero image
+  const int64_t p_lo = g.plane_lo, p_hi = g.plane_hi;
+  if (p_lo >= p_hi) CIP_HIP_CHECK(hipMemsetAsync(dirty_out, 0, sizeof(double) * npix_x * npix_y, s));
+  for (int64_t q = p_lo / G; q * G < p_hi; ++q) {
     // pipelined calls: leave CU slots to the next call's planner (profiles/r03_ab_scatter_share.txt)
     rc = scatter_plane(pp, q, uvw, vis, vis_dtype, wgt, wgt_dtype, st.fast, grid, s, clean,
                        pipelined && share_cus_enabled());
     if (rc != CIP_OK) return rc;
-    for (int64_t p = q * G; p < std::min<int64_t>(q * G + G, g.nplanes); ++p) {
+    for (int64_t p = std::max(q * G, p_lo); p < std::min<int64_t>(q * G + G, p_hi); ++p) {
       rc = plane_to_dirty(st, g, p, grid + (p - q * G) * plane_elems, dirty_out, s,
                           dmask ? dmask + p * (g.ntx * g.nty / 32) : nullptr, normalise ? pp.red : nullptr,
-                          dmask ? dmask + g.nplanes * (g.ntx * g.nty / 32) + p * ((g.nty + 31) / 32) : nullptr);
+                          dmask ? dmask + g.nplanes * (g.ntx * g.nty / 32) + p * ((g.nty + 31) / 32) : nullptr,
+                          p == p_lo);
       if (rc != CIP_OK) return rc;
     }
+    // a group's planes outside the range were neither written (the scatter
+    // skips them) nor read, so a masked pass A still leaves the group clean
     clean = dmask != nullptr;
   }
   rc = finish_dirty(ws, st, pp.p, g, dirty_out, s);
@@ -1396,7 +1444,7 @@ static int ms2dirty_impl(const double* uvw, int64_t nrow, const double* freq, in
   else ws->async_stream = s;
   if (clean) {
     ws->grid_clean = grid;
-    ws->grid_clean_planes = std::max<int64_t>(prev_clean, G);
+    ws->grid_clean_bytes = std::max(prev_clean, group_bytes);
   }
   g_prof.finish();
   return CIP_OK;
@@ -1416,6 +1464,23 @@ int cip_ms2dirty(const double* uvw, int64_t nrow, const double* freq, int64_t nc
     return set_error(CIP_EINVAL, "wgt dtype must be float32, float64 or none");
   return ms2dirty_impl(uvw, nrow, freq, nchan, vis, vis_dtype, wgt, wgt_dtype, nullptr, npix_x, npix_y, pixsize_x,
                        pixsize_y, epsilon, support, flags, hip_stream, dirty_out, sum_wgt_out, params_out);
+}
+
+int cip_ms2dirty_wplanes(const double* uvw, int64_t nrow, const double* freq, int64_t nchan, const void* vis,
+                         int vis_dtype, const void* wgt, int wgt_dtype, int64_t npix_x, int64_t npix_y,
+                         double pixsize_x, double pixsize_y, double epsilon, int support, int flags,
+                         int64_t plane_begin, int64_t plane_end, void* hip_stream, double* dirty_out,
+                         double* sum_wgt_out, cip_gridder_params* params_out) {
+  g_last_error.clear();
+  if (!(flags & CIP_WSTACKING)) return set_error(CIP_EINVAL, "a w-plane range needs CIP_WSTACKING");
+  if (plane_begin < 0 || plane_end < plane_begin) return set_error(CIP_EINVAL, "invalid w-plane range");
+  if (vis_dtype != CIP_C64 && vis_dtype != CIP_C128 && !(flags & CIP_PSF))
+    return set_error(CIP_EINVAL, "vis dtype must be complex64 or complex128");
+  if (wgt_dtype != CIP_NONE && wgt_dtype != CIP_F32 && wgt_dtype != CIP_F64)
+    return set_error(CIP_EINVAL, "wgt dtype must be float32, float64 or none");
+  return ms2dirty_impl(uvw, nrow, freq, nchan, vis, vis_dtype, wgt, wgt_dtype, nullptr, npix_x, npix_y, pixsize_x,
+                       pixsize_y, epsilon, support, flags, hip_stream, dirty_out, sum_wgt_out, params_out,
+                       plane_begin, plane_end);
 }
 
 int cip_ms2dirty_stokes_i(const double* uvw, int64_t nrow, const double* freq, int64_t nchan, const void* vis4,
@@ -1466,6 +1531,21 @@ int cip_grid_tiles(const double* slice_uvw, const int32_t* chan_start, const int
   const RaggedRows rr{chan_start, chan_stop, nvis};
   return grid_accumulate(slice_uvw, nslices, freq, nchan, vis, vis_dtype, wgt, wgt_dtype, params, pixsize_x,
                          pixsize_y, npix_x, npix_y, flags, hip_stream, grids, sum_wgt, &rr);
+}
+
+int cip_grid_tiles_strip(const double* slice_uvw, const int32_t* chan_start, const int32_t* chan_stop,
+                         int64_t nslices, const double* freq, int64_t nchan, const void* vis, int64_t nvis,
+                         int vis_dtype, const void* wgt, int wgt_dtype, const cip_gridder_params* params,
+                         double pixsize_x, double pixsize_y, int64_t npix_x, int64_t npix_y, int64_t row0,
+                         int64_t nrows, int flags, void* hip_stream, double* strip, double* sum_wgt) {
+  if (nslices < 0 || nvis < 0) return set_error(CIP_EINVAL, "nslices and nvis must be >= 0");
+  if (nslices > 0 && (!chan_start || !chan_stop)) return set_error(CIP_EINVAL, "NULL channel ranges");
+  if (nslices >= ((int64_t)1 << 32) - 1) return set_error(CIP_EINVAL, "nslices must be < 2^32 - 1");
+  if (nrows < 1) return set_error(CIP_EINVAL, "nrows must be >= 1");
+  if (!public_dtypes(vis_dtype, wgt_dtype)) return set_error(CIP_EINVAL, "vis dtype must be complex64 or complex128");
+  const RaggedRows rr{chan_start, chan_stop, nvis};
+  return grid_accumulate(slice_uvw, nslices, freq, nchan, vis, vis_dtype, wgt, wgt_dtype, params, pixsize_x,
+                         pixsize_y, npix_x, npix_y, flags, hip_stream, strip, sum_wgt, &rr, nullptr, row0, nrows);
 }
 
 int cip_grid_to_dirty(double* grids, const cip_gridder_params* params, int64_t npix_x, int64_t npix_y,

@@ -141,7 +141,26 @@ struct GridGeometry {
   int tile;                 // T
   int64_t ntx, nty, ntw;    // tiles per axis (ntw = nplanes - W + 1, or 1 in 2-D)
   int transposed;           // HBM grid stored as gT[y, x] (pruned FFT), else g[x, y]
+  // row window of the HBM buffer (transposed layout; uv-strip ranks, DESIGN.md
+  // 7): buffer row k holds grid row (row0 + k) mod nv, k < rows. The whole
+  // grid: row0 = 0, rows = nv. A flushed cell outside the window is dropped
+  // and sets *oob (if given) - a plan inconsistent with the strip.
+  int64_t row0, rows;
+  unsigned* oob;
+  // w planes this call grids (w-stacking plane groups split over GPUs,
+  // cip_ms2dirty_wplanes): [plane_lo, plane_hi); the whole stack by default.
+  // The planner drops visibilities feeding no plane of the range.
+  int64_t plane_lo, plane_hi;
 };
+
+// Buffer offset (complex cells) of grid cell (gx, gy) in wrapped coordinates,
+// or -1 outside the buffer's row window.
+__device__ __forceinline__ int64_t grid_cell_offset(const GridGeometry& g, int64_t gx, int64_t gy) {
+  if (!g.transposed) return gx * g.nv + gy;
+  int64_t k = gy - g.row0;
+  k += (k < 0) ? g.nv : 0;
+  return k < g.rows ? k * g.nu + gx : -1;
+}
 
 // Grid coordinate -> footprint origin and kernel variable.
 __device__ __forceinline__ void footprint(double x, int half_w, int64_t* i0, double* y) {

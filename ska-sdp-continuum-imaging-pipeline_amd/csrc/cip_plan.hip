@@ -276,9 +276,12 @@ __global__ __launch_bounds__(256, CIP_PLACE_WAVES) void plan_place_kernel(const 
       int ix0, iy0;
       int64_t iw0;
       const bool ok = place_origin(u, v, w, f, g, &ix0, &iy0, &iw0);
+      // a w layer feeds planes [iw0, iw0 + W): dropped when none is in the
+      // call's plane range (plane groups split over GPUs)
+      const bool feeds = (iw0 + g.support > g.plane_lo) & (iw0 < g.plane_hi);
       // the tile key modulo 2^32 (keys are < 2^32 - 1)
       // tile_key(): tile-major, the w layers of a uv tile adjacent
-      const uint32_t key = (valid & ok) ? ((((uint32_t)iy0 / (uint32_t)kTile) * (uint32_t)g.ntx +
+      const uint32_t key = (valid & ok & feeds) ? ((((uint32_t)iy0 / (uint32_t)kTile) * (uint32_t)g.ntx +
                                             (uint32_t)ix0 / (uint32_t)kTile) *
                                                (uint32_t)g.ntw +
                                            (uint32_t)iw0)

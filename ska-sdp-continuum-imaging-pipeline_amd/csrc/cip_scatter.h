@@ -170,6 +170,7 @@ __device__ __forceinline__ void grid_fetched(const VisFetch& f, const GridGeomet
     for (int k = 0; k < G; ++k) {
       const int64_t kw = plane + k - iw0;
       if (kw < 0 || kw >= W) continue;  // the visibility does not feed plane + k
+      if (plane + k < g.plane_lo || plane + k >= g.plane_hi) continue;  // outside the call's plane range
       double sel = 0.0;
 #pragma unroll
       for (int q = 0; q < W; ++q) sel = (q == kw) ? kwv[q] : sel;
@@ -384,6 +385,7 @@ __global__ __launch_bounds__(scatter_threads<G>(), CIP_SCATTER_WAVES) void scatt
 #pragma unroll
   for (int k = 0; k < G; ++k) {
     if (G > 1 && plane + k >= g.nplanes) break;
+    if (G > 1 && (plane + k < g.plane_lo || plane + k >= g.plane_hi)) continue;
     const unsigned long long* sk = sub + k * S;
     double* gk = grid + (int64_t)k * 2 * g.nu * g.nv;
     for (int cell = threadIdx.x; cell < P * P; cell += NT) {
@@ -406,7 +408,12 @@ __global__ __launch_bounds__(scatter_threads<G>(), CIP_SCATTER_WAVES) void scatt
         int64_t gx = X0 + lcell / P, gy = Y0 + lcell % P;
         gx -= (gx >= g.nu) ? g.nu : 0;
         gy -= (gy >= g.nv) ? g.nv : 0;
-        double* dst = gk + 2 * (g.transposed ? gy * g.nu + gx : gx * g.nv + gy);
+        const int64_t off = grid_cell_offset(g, gx, gy);
+        if (off < 0) {
+          if (g.oob) atomicOr(g.oob, 1u);
+          continue;
+        }
+        double* dst = gk + 2 * off;
         const int lx = lcell / P, ly = lcell % P;
         if (own && lx >= W - 1 && lx < T && ly >= W - 1 && ly < T) {
           *reinterpret_cast<double2*>(dst) = make_double2((double)re * inv_scale, (double)im * inv_scale);

@@ -170,7 +170,12 @@ __global__ __launch_bounds__(kLargeThreads) void scatter_large_kernel(
       int64_t gx = X0 + lcell / P, gy = Y0 + lcell % P;
       gx -= (gx >= g.nu) ? g.nu : 0;
       gy -= (gy >= g.nv) ? g.nv : 0;
-      double* dst = grid + 2 * (g.transposed ? gy * g.nu + gx : gx * g.nv + gy);
+      const int64_t off = grid_cell_offset(g, gx, gy);
+      if (off < 0) {
+        if (g.oob) atomicOr(g.oob, 1u);
+        continue;
+      }
+      double* dst = grid + 2 * off;
       unsafeAtomicAdd(dst, (double)re * inv_scale);
       unsafeAtomicAdd(dst + 1, (double)im * inv_scale);
     }

@@ -74,6 +74,7 @@ def device_ms2dirty(
     synchronize: bool = True,
     resident_inputs: bool = False,
     reuse_plan: bool = False,
+    planes: Optional[tuple] = None,
 ) -> tuple["torch.Tensor", _lib.GridderParams]:
     """
     Device-resident ms2dirty: all tensors already in HBM on the current device.
@@ -103,7 +104,15 @@ def device_ms2dirty(
     planned call (e.g. the Stokes parameters and PSF of one facet): if that
     call's geometry matches, its tile plan is used again and only the weight
     sum and max |w V| are computed (images identical to a planned call's).
+    `planes=(begin, end)` (w-stacking only, cip_ms2dirty_wplanes): the partial
+    image of w planes [begin, end) of the stack - the share of one GPU when the
+    plane groups of ONE image are split over GPUs (SURVEY.md 8(e) option 2,
+    `wplanes.py`); the partial images of a partition of [0, nplanes) sum to
+    the whole image (the final w correction and `normalise` are linear and
+    applied to each part; `sum_weights` is the whole call's weight sum).
     """
+    if planes is not None and not do_wstacking:
+        raise ValueError("planes=(begin, end) needs do_wstacking=True")
     if resident_inputs and synchronize:
         raise ValueError("resident_inputs=True needs synchronize=False")
     if reuse_plan and resident_inputs:
@@ -144,7 +153,7 @@ def device_ms2dirty(
         stream = torch.cuda.current_stream(uvw.device).cuda_stream
         rc = _ms2dirty_call(uvw, freq, vis, wgt, vis_codes, wgt_codes, npix_x, npix_y, pixsize_x, pixsize_y,
                             epsilon, support, do_wstacking, single_precision_accumulation, psf, normalise,
-                            stream, out, sum_weights, params, synchronize, resident_inputs, reuse_plan)
+                            stream, out, sum_weights, params, synchronize, resident_inputs, reuse_plan, planes)
     _lib.check(rc)
     return out, params
 
@@ -160,25 +169,26 @@ def _check_device_tensor(t, device, what):
 
 def _ms2dirty_call(uvw, freq, vis, wgt, vis_codes, wgt_codes, npix_x, npix_y, pixsize_x, pixsize_y, epsilon,
                    support, do_wstacking, single_precision_accumulation, psf, normalise, stream, out,
-                   sum_weights, params, synchronize=True, resident_inputs=False, reuse_plan=False):
+                   sum_weights, params, synchronize=True, resident_inputs=False, reuse_plan=False, planes=None):
     nrow = uvw.shape[0]
     nchan = freq.shape[0]
-    return _lib.lib().cip_ms2dirty(
-        uvw.data_ptr(), nrow, freq.data_ptr(), nchan, None if vis is None else vis.data_ptr(),
-        _lib.CIP_C64 if vis is None else vis_codes[vis.dtype],
-        wgt.data_ptr() if wgt is not None else None,
-        wgt_codes[wgt.dtype] if wgt is not None else _lib.CIP_NONE,
-        int(npix_x), int(npix_y), float(pixsize_x), float(pixsize_y), float(epsilon),
-        int(support or 0),
-        (_lib.CIP_WSTACKING if do_wstacking else 0)
-        | (_lib.CIP_ACC_SINGLE if single_precision_accumulation else 0)
-        | (_lib.CIP_PSF if psf else 0)
-        | (_lib.CIP_NORMALISE if normalise else 0)
-        | (0 if synchronize else _lib.CIP_ASYNC)
-        | (_lib.CIP_PIPELINE if resident_inputs else 0)
-        | (_lib.CIP_REUSE_PLAN if reuse_plan else 0),
-        stream, out.data_ptr(),
-        sum_weights.data_ptr() if sum_weights is not None else None, params)
+    head = (uvw.data_ptr(), nrow, freq.data_ptr(), nchan, None if vis is None else vis.data_ptr(),
+            _lib.CIP_C64 if vis is None else vis_codes[vis.dtype],
+            wgt.data_ptr() if wgt is not None else None,
+            wgt_codes[wgt.dtype] if wgt is not None else _lib.CIP_NONE,
+            int(npix_x), int(npix_y), float(pixsize_x), float(pixsize_y), float(epsilon),
+            int(support or 0),
+            (_lib.CIP_WSTACKING if do_wstacking else 0)
+            | (_lib.CIP_ACC_SINGLE if single_precision_accumulation else 0)
+            | (_lib.CIP_PSF if psf else 0)
+            | (_lib.CIP_NORMALISE if normalise else 0)
+            | (0 if synchronize else _lib.CIP_ASYNC)
+            | (_lib.CIP_PIPELINE if resident_inputs else 0)
+            | (_lib.CIP_REUSE_PLAN if reuse_plan else 0))
+    tail = (stream, out.data_ptr(), sum_weights.data_ptr() if sum_weights is not None else None, params)
+    if planes is not None:
+        return _lib.lib().cip_ms2dirty_wplanes(*head, int(planes[0]), int(planes[1]), *tail)
+    return _lib.lib().cip_ms2dirty(*head, *tail)
 
 
 def device_ms2dirty_stokes_i(

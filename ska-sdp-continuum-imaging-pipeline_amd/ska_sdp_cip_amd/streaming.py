@@ -20,6 +20,7 @@ slots and sent to HBM on a dedicated copy stream. One FFT at the end.
 from __future__ import annotations
 
 import concurrent.futures as cf
+import threading
 from pathlib import Path
 from typing import Callable, Iterable, Optional, Sequence
 
@@ -227,7 +228,8 @@ class RowStreamer:
     it returned. The slots persist across calls (pinned allocation is slow).
     """
 
-    _cache = {}
+    _cache = {}  # (thread id, device) -> ((rows, nchan), RowStreamer)
+    _lock = threading.Lock()
     COLUMNS = (("uvw", np.float64, (3,)), ("vis4", np.complex64, ("c", 4)), ("flags4", np.uint8, ("c", 4)),
                ("wgt4", np.float32, ("c", 4)))
 
@@ -252,11 +254,20 @@ class RowStreamer:
 
     @classmethod
     def get(cls, device, rows: int, nchan: int) -> "RowStreamer":
-        key = (str(torch.device(device)), int(rows), int(nchan))
-        st = cls._cache.get(key)
-        if st is None:
-            cls._cache.clear()  # one set of slots at a time
-            st = cls._cache[key] = cls(device, rows, nchan)
+        """The calling thread's streamer for `device` (one set of slots per
+        (thread, device): concurrent streamed inverts on several GPUs - e.g.
+        LocalGPUClient's per-device worker threads - never evict or share each
+        other's slots). A new shape replaces only this thread's slots."""
+        owner = (threading.get_ident(), str(torch.device(device)))
+        shape = (int(rows), int(nchan))
+        with cls._lock:
+            ent = cls._cache.get(owner)
+            if ent is not None and ent[0] == shape:
+                return ent[1]
+            cls._cache.pop(owner, None)
+        st = cls(device, rows, nchan)
+        with cls._lock:
+            cls._cache[owner] = (shape, st)
         return st
 
     def fill(self, slot: int, reader, row0: int, row1: int) -> int:

@@ -180,15 +180,29 @@ def gather_strip(uvw, vis, wgt, rows, c0, c1) -> StripData:
                      rows)
 
 
-class HipStripBackend:
-    """Per-rank stages on the current GPU through libcip_hip.so: cip_grid_tiles
-    (accumulating gridder) onto a full-size transposed grid that only the
-    strip's rows (+ halo) reach, cip_strip_rows (pass A), cip_strip_cols
-    (pass B + crop + correction). The grid is kept between calls and left
-    clean (pass A zeroes the rows it reads; the halo rows are zeroed after
-    they are sent)."""
+def strip_buffer_rows(layout: StripLayout, r: int) -> tuple[int, int]:
+    """(row0, nrows) of rank r's grid buffer: its strip rows [y0, y1) plus the
+    W - 1 halo rows after them (buffer row k = grid row (y0 + k) mod nv). One
+    strip holding the whole grid: (0, nv), its halo wraps onto its own rows."""
+    y0, y1 = layout.rows(r)
+    if layout.world == 1:
+        return 0, layout.nv
+    return y0, y1 - y0 + layout.halo
 
-    def __init__(self, params, pixsize_x: float, pixsize_y: float, npix_x: int, npix_y: int, device=None):
+
+class HipStripBackend:
+    """Per-rank stages on the current GPU through libcip_hip.so:
+    cip_grid_tiles_strip (accumulating gridder) onto a buffer holding only the
+    rank's strip + halo rows (`bind`: 1/N of the grid plus W - 1 rows instead
+    of a full-size grid per rank), cip_strip_rows (pass A), cip_strip_cols
+    (pass B + crop + correction). The buffer is kept between calls and left
+    clean (pass A zeroes the rows it reads; the halo rows are zeroed after
+    they are sent); an invert that fails in between leaves it marked dirty and
+    the next `grid_strip` zeroes it first instead of trusting CIP_GRID_ZEROED.
+    Unbound (rows=None) the buffer is the whole transposed grid."""
+
+    def __init__(self, params, pixsize_x: float, pixsize_y: float, npix_x: int, npix_y: int, device=None,
+                 rows: Optional[tuple] = None):
         from . import _lib  # pylint: disable=import-outside-toplevel
         from .gridder import _require_gpu  # pylint: disable=import-outside-toplevel
 
@@ -201,30 +215,61 @@ class HipStripBackend:
         if int(params.nplanes) != 1 or not _lib.lib().cip_grid_layout(params, self.npix_x, self.npix_y):
             raise ValueError("strips need a 2-D (no w-stacking) grid in the pruned-FFT layout "
                              "(power-of-two grids)")
-        self.grid = torch.zeros((int(params.nv), int(params.nu), 2), dtype=torch.float64, device=self.device)
+        self.rows = None
+        self.grid = None
+        self.dirty = False
+        self._alloc((0, int(params.nv)) if rows is None else rows)
+
+    def _alloc(self, rows):
+        row0, nrows = int(rows[0]), int(rows[1])
+        if not (0 <= row0 < int(self.params.nv) and 1 <= nrows <= int(self.params.nv)):
+            raise ValueError("strip rows outside the grid")
+        if self.rows != (row0, nrows):
+            self.grid = None  # free the old buffer first
+            self.grid = torch.zeros((nrows, int(self.params.nu), 2), dtype=torch.float64, device=self.device)
+            self.rows = (row0, nrows)
+            self.dirty = False
+
+    def spawn(self) -> "HipStripBackend":
+        """A backend of the same configuration (another rank's, for the
+        single-process emulation)."""
+        return HipStripBackend(self.params, self.px, self.py, self.npix_x, self.npix_y, device=self.device,
+                               rows=self.rows)
+
+    def bind(self, layout: StripLayout, rank: int) -> "HipStripBackend":
+        """Hold rank `rank`'s strip + halo rows of `layout` (reallocates when they change)."""
+        self._alloc(strip_buffer_rows(layout, rank))
+        return self
 
     def _stream(self):
         return torch.cuda.current_stream(self.device).cuda_stream
 
     def grid_strip(self, data: StripData, freq):
-        """Grid the strip's visibilities; returns (grid (nv, nu, 2) f64, weight sum (1,) f64)."""
+        """Grid the strip's visibilities; returns (strip buffer (nrows, nu, 2) f64, weight sum (1,) f64)."""
         from .gridder import _codes  # pylint: disable=import-outside-toplevel
 
+        if self.dirty:  # a previous invert did not finish: the buffer may hold partial sums
+            self.grid.zero_()
+        self.dirty = True
         vis_codes, wgt_codes = _codes()
         sumw = torch.zeros(1, dtype=torch.float64, device=self.device)
         ns = int(data.slice_uvw.shape[0])
         if ns:
-            self._lib.check(self._lib.lib().cip_grid_tiles(
+            self._lib.check(self._lib.lib().cip_grid_tiles_strip(
                 data.slice_uvw.data_ptr(), data.chan_start.data_ptr(), data.chan_stop.data_ptr(), ns,
                 freq.data_ptr(), int(freq.shape[0]), data.vis.data_ptr(), data.nvis, vis_codes[data.vis.dtype],
                 data.wgt.data_ptr() if data.wgt is not None else None,
                 wgt_codes[data.wgt.dtype] if data.wgt is not None else self._lib.CIP_NONE,
-                self.params, self.px, self.py, self.npix_x, self.npix_y, self._lib.CIP_GRID_ZEROED, self._stream(),
-                self.grid.data_ptr(), sumw.data_ptr()))
+                self.params, self.px, self.py, self.npix_x, self.npix_y, self.rows[0], self.rows[1],
+                self._lib.CIP_GRID_ZEROED, self._stream(), self.grid.data_ptr(), sumw.data_ptr()))
         return self.grid, sumw
 
+    def mark_clean(self) -> None:
+        """Pass A consumed the strip rows and the halo rows were zeroed."""
+        self.dirty = False
+
     def pass_rows(self, grid, y0: int, y1: int):
-        """Pass A over grid rows [y0, y1) -> H (npix_x / 4, y1 - y0, 4, 2); zeroes the rows."""
+        """Pass A over buffer rows [y0, y1) -> H (npix_x / 4, y1 - y0, 4, 2); zeroes the rows."""
         H = torch.empty((self.npix_x // COL_BLOCK, y1 - y0, COL_BLOCK, 2), dtype=torch.float64, device=self.device)
         self._lib.check(self._lib.lib().cip_strip_rows(grid.data_ptr(), self.params, self.npix_x, self.npix_y,
                                                        int(y0), int(y1), self._stream(), H.data_ptr()))
@@ -237,14 +282,6 @@ class HipStripBackend:
                                                        int(i0), int(i1), None if norm is None else norm.data_ptr(),
                                                        self._stream(), out.data_ptr()))
         return out
-
-
-def _halo_rows(layout: StripLayout, r: int) -> tuple[int, int]:
-    """Grid rows of rank r's halo: [y1, y1 + W - 1) mod nv (contiguous: strips are
-    >= W rows high and only the last one ends at nv)."""
-    _, y1 = layout.rows(r)
-    a = y1 % layout.nv
-    return a, a + layout.halo
 
 
 def _assemble_H(pieces: Sequence, nb: int, layout: StripLayout, device, dtype):
@@ -264,6 +301,7 @@ def invert_strips(data: StripData, freq, layout: StripLayout, backend, *, dst: i
     (npix_x, npix_y) on `dst`, None elsewhere. Collectives: one point-to-point
     halo exchange with the ring neighbours, one all-to-all of the pass-A
     blocks, a scalar all-reduce of the weight sum, a gather of image rows.
+    The backend is bound to this rank's strip + halo rows (`strip_buffer_rows`).
     `stages` (a dict, diagnostic): each stage is synchronised and its seconds
     added under its name (grid, halo, rows, alltoall, cols, gather)."""
     import time  # pylint: disable=import-outside-toplevel
@@ -271,40 +309,41 @@ def invert_strips(data: StripData, freq, layout: StripLayout, backend, *, dst: i
     import torch.distributed as dist  # pylint: disable=import-outside-toplevel
 
     t_last = [time.perf_counter()]
-
-    def mark(name):
-        if stages is not None:
-            if grid.is_cuda:
-                torch.cuda.synchronize(grid.device)
-            t = time.perf_counter()
-            stages[name] = stages.get(name, 0.0) + t - t_last[0]
-            t_last[0] = t
-
     single = not dist.is_available() or not dist.is_initialized()
     world = 1 if single else dist.get_world_size(group)
     rank = 0 if single else dist.get_rank(group)
     if world != layout.world:
         raise ValueError("the layout was planned for another number of ranks")
+    backend.bind(layout, rank)
     y0, y1 = layout.rows(rank)
-    grid, sumw = backend.grid_strip(data, freq)
+    h = y1 - y0
+    buf, sumw = backend.grid_strip(data, freq)
+
+    def mark(name):
+        if stages is not None:
+            if buf.is_cuda:
+                torch.cuda.synchronize(buf.device)
+            t = time.perf_counter()
+            stages[name] = stages.get(name, 0.0) + t - t_last[0]
+            t_last[0] = t
+
     mark("grid")
     if world > 1:
-        # halo: rows past the strip -> the next rank, added to its first rows
-        ha, hb = _halo_rows(layout, rank)
-        send = grid[ha:hb].contiguous()
+        # halo: buffer rows [h, h + W - 1) = the grid rows past the strip ->
+        # the next rank, added to its first rows
+        send = buf[h:h + layout.halo].contiguous()
         recv = torch.empty_like(send)
         ops = [dist.P2POp(dist.isend, send, (rank + 1) % world, group),
                dist.P2POp(dist.irecv, recv, (rank - 1) % world, group)]
         for w in dist.batch_isend_irecv(ops):
             w.wait()
-        grid[ha:hb].zero_()
-        grid[y0:y0 + layout.halo] += recv
-    if world > 1:
+        buf[h:h + layout.halo].zero_()
+        buf[:layout.halo] += recv
         dist.all_reduce(sumw, group=group)
     mark("halo")
-    H = backend.pass_rows(grid, y0, y1)
+    H = backend.pass_rows(buf, 0, h)
+    backend.mark_clean()
     mark("rows")
-    h = y1 - y0
     if world > 1:
         # all-to-all: rank s receives blocks [i0_s / 4, i1_s / 4) of every rank's rows
         splits_in = [(layout.image_rows(s)[1] - layout.image_rows(s)[0]) // COL_BLOCK * h * COL_BLOCK * 2
@@ -336,46 +375,73 @@ def invert_strips(data: StripData, freq, layout: StripLayout, backend, *, dst: i
     return torch.cat([g[:layout.image_rows(r)[1] - layout.image_rows(r)[0]] for r, g in enumerate(gathered)])
 
 
-def invert_strips_local(datas: Sequence[StripData], freq, layout: StripLayout, backend):
+def invert_strips_local(datas: Sequence[StripData], freq, layout: StripLayout, backend,
+                        stages: Optional[list] = None):
     """All ranks' stages in ONE process on one device, the exchanges done in
-    memory (the single-GPU check of the decomposition and its kernels). The
-    ranks run one after another through the backend's one grid buffer: rank
-    r grids its strip, its halo rows are taken out (-> rank r + 1) and the
-    predecessor's halo is added to its first rows before its pass A; rank 0's
-    rows wait (saved) for the last rank's halo. Returns the normalised dirty
-    image (npix_x, npix_y)."""
+    memory (the single-GPU check of the decomposition and its kernels, and the
+    per-rank cost breakdown of the N-GPU split). Rank r's stages run on its
+    own strip + halo buffer (`backend.spawn()` per rank, kept as
+    `backend.ranks`), in the distributed order: every rank grids its strip,
+    the halos move to the next rank, pass A runs per strip, the pass-A blocks
+    are regrouped per image-row strip (the all-to-all) and pass B runs per
+    image-row strip. `stages` (a list, diagnostic): filled with one dict per
+    rank of synchronised seconds (grid, halo, rows, assemble, cols). Returns
+    the normalised dirty image (npix_x, npix_y)."""
+    import time  # pylint: disable=import-outside-toplevel
+
     world = layout.world
     if len(datas) != world:
         raise ValueError("one StripData per strip")
-    Hs = [None] * world
-    sumw, prev_halo, rows0 = None, None, None
+    if stages is not None:
+        stages[:] = [{} for _ in range(world)]
+    dev = getattr(backend, "device", None)
+    on_gpu = dev is not None and torch.device(dev).type == "cuda"
+
+    def timed(r, name, fn):
+        if stages is None:
+            return fn()
+        if on_gpu:
+            torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        out = fn()
+        if on_gpu:
+            torch.cuda.synchronize(dev)
+        stages[r][name] = stages[r].get(name, 0.0) + time.perf_counter() - t0
+        return out
+
+    ranks = getattr(backend, "ranks", None)
+    if not ranks or len(ranks) != world:
+        ranks = [backend] + [backend.spawn() for _ in range(world - 1)]
+        backend.ranks = ranks
     for r in range(world):
-        y0, y1 = layout.rows(r)
-        grid, sw = backend.grid_strip(datas[r], freq)
-        sumw = sw.clone() if sumw is None else sumw + sw
-        if world == 1:
-            Hs[0] = backend.pass_rows(grid, y0, y1)
-            break
-        ha, hb = _halo_rows(layout, r)
-        halo = grid[ha:hb].clone()
-        grid[ha:hb].zero_()
-        if r == 0:
-            rows0 = grid[y0:y1].clone()
-            grid[y0:y1].zero_()
-        else:
-            grid[y0:y0 + layout.halo] += prev_halo
-            Hs[r] = backend.pass_rows(grid, y0, y1)
-        prev_halo = halo
+        ranks[r].bind(layout, r)
+    bufs, sums = [None] * world, [None] * world
+    for r in range(world):
+        bufs[r], sums[r] = timed(r, "grid", lambda r=r: ranks[r].grid_strip(datas[r], freq))
+    sumw = sums[0].clone()
+    for sw in sums[1:]:
+        sumw = sumw + sw
+    hs = [layout.rows(r)[1] - layout.rows(r)[0] for r in range(world)]
     if world > 1:
-        y0, y1 = layout.rows(0)
-        grid = backend.grid
-        grid[y0:y1] = rows0
-        grid[y0:y0 + layout.halo] += prev_halo
-        Hs[0] = backend.pass_rows(grid, y0, y1)
+        halos = []
+        for r in range(world):
+            halos.append(bufs[r][hs[r]:hs[r] + layout.halo].clone())
+            bufs[r][hs[r]:hs[r] + layout.halo].zero_()
+        for r in range(world):
+            timed(r, "halo", lambda r=r: bufs[r][:layout.halo].add_(halos[(r - 1) % world]))
+    Hs = []
+    for r in range(world):
+        Hs.append(timed(r, "rows", lambda r=r: ranks[r].pass_rows(bufs[r], 0, hs[r])))
+        ranks[r].mark_clean()
     out = []
     for s in range(world):
         i0, i1 = layout.image_rows(s)
         b0, b1 = i0 // COL_BLOCK, i1 // COL_BLOCK
-        Hm = Hs[0] if world == 1 else _assemble_H([H[b0:b1] for H in Hs], b1 - b0, layout, Hs[0].device, Hs[0].dtype)
-        out.append(backend.pass_cols(Hm.contiguous(), i0, i1, norm=sumw))
+        if world == 1:
+            Hm = Hs[0]
+        else:
+            Hm = timed(s, "assemble", lambda b0=b0, b1=b1: _assemble_H([H[b0:b1] for H in Hs], b1 - b0, layout,
+                                                                        Hs[0].device, Hs[0].dtype))
+        out.append(timed(s, "cols", lambda s=s, Hm=Hm, i0=i0, i1=i1: ranks[s].pass_cols(Hm.contiguous(), i0, i1,
+                                                                                         norm=sumw)))
     return torch.cat(out, dim=0)

@@ -11,7 +11,10 @@ dirty-image max |GPU - CPU| / sum w < 1e-6), GPU through the C ABI
 * C3 at its full 8192^2 grid (4096^2 image) on a row subset: every 10th row
   (39,063 rows x 256 channels = 10M visibilities, all hour angles) in 2-D at
   support 8, every 40th row for the reference's w-stacking call (the oracle
-  grids every plane separately).
+  grids every plane separately);
+* configs[2] (support 64 on the 8192^2 grid): every 96th C3 row (1.04M
+  visibilities) in 2-D against the oracle; the whole C3 at support 64, 2-D and
+  w-stacking, is checked against the DFT in test_gpu_full_size.py.
 
 Inputs: the bench's uvw tracks (seed 20241008, 64 antennas, 4 km), complex64
 visibilities and float32 weights with 5 % zero (flagged) weights from numpy's
@@ -101,3 +104,13 @@ def test_c3_grid_row_subset_2d_support8():
 def test_c3_grid_row_subset_reference_call_wstacking():
     uvw, freq, vis, wgt, px = _inputs(390_625, 256, 4096, row_step=40)
     _check(uvw, freq, vis, wgt, 4096, px, epsilon=1e-4, wstack=True, nthreads=min(NTHREADS, 8))
+
+
+def test_c3_grid_row_subset_2d_support64():
+    # BASELINE configs[2]: support 64 on the 8192^2 grid (the LDS-tile stress
+    # case, wave-per-visibility scatter) against the oracle on every 96th row
+    # of the C3 tracks (4,070 rows x 256 channels = 1.04M visibilities, all
+    # hour angles) at the full grid
+    uvw, freq, vis, wgt, px = _inputs(390_625, 256, 4096, row_step=96)
+    assert vis.size >= 1_000_000
+    _check(uvw, freq, vis, wgt, 4096, px, support=64)

@@ -7,7 +7,8 @@ direct fp64 DFT. Covers 2-D and w-stacking, the hipFFT path (npix 128) and the
 pruned FFT path whose dirty-tile mask must follow the two-tile halo of a
 W = 64 sub-grid (npix 512), the dtype / weight variants, unit visibilities
 (PSF), the plain tile-order stream (bank-class order off, in a child process)
-and the argument errors.
+and the argument errors. W = 64 with w-stacking (the reference's gridding
+mode, invert.py:180, at configs[2]'s support) is supported since round 4.
 """
 import os
 import subprocess
@@ -27,16 +28,15 @@ pytestmark = pytest.mark.gpu
 TIGHT = 1e-10
 GATE = 1e-6  # north star: dirty image / sum w, max |GPU - CPU|
 # GPU vs oracle bounds (max |diff| / sum w). Both implement the same kernel and
-# grid correction, but at beta = 2.3 W the kernel's transform at the image
-# edge falls as exp(-0.138 W) per axis (F(1/4)/F(0) = 1.6e-4 at W = 64,
-# tests/test_oracle_accuracy.py LARGE_BOUND), and the correction multiplies
-# the GPU's fixed-point quantum (2^-46 of max |w V| per contribution, vs
-# fp64's relative rounding in the oracle) by up to 1/F^2 at the image corners
-# (1/F^3 with w-stacking). Measured: 2-D W = 48 2e-10, W = 64 2.4e-8;
-# w-stacking W = 48 1.5e-7; w-stacking W = 64 measured 3.8e-5 (1/F^3 ~ 1e11),
-# above the gate, so the library refuses it (CIP_EINVAL).
-TOL = {(False, 24): TIGHT, (False, 32): TIGHT, (False, 48): 1e-9, (False, 64): 1e-7,
-       (True, 32): 1e-9, (True, 48): 5e-7}
+# grid correction; the correction multiplies the GPU's fixed-point quantum
+# (2^-46 of max |w V| per contribution, vs fp64's relative rounding in the
+# oracle) by up to 1/F^2 at the image corners (1/F^3 with w-stacking). The
+# large supports' shape beta keeps F(1/4)/F(0) >= 0.03 (tools/gen_es_kernels.py;
+# at beta = 2.3 W it was 1.6e-4 at W = 64: 3.8e-5 measured with w-stacking, which
+# the library then refused), so every support holds the tight bound in 2-D and
+# 1e-9 with w-stacking (the VERDICT r03 target for W = 64).
+TOL = {(False, 24): TIGHT, (False, 32): TIGHT, (False, 48): TIGHT, (False, 64): TIGHT,
+       (True, 24): 1e-9, (True, 32): 1e-9, (True, 48): 1e-9, (True, 64): 1e-9}
 ROOT = Path(__file__).resolve().parents[1]
 
 
@@ -73,7 +73,7 @@ def test_large_support_2d_parity(gpu_device, support):
         assert _err(gpu, dft, sumw) < 1e-11
 
 
-@pytest.mark.parametrize("support", [32, 48])
+@pytest.mark.parametrize("support", [24, 32, 48, 64])
 def test_large_support_wstacking_parity(gpu_device, support):
     uvw, f, vis, w = _case(1_500, 4, n_ant=24, radius=2000.0, fov=0.05)
     npix = 128
@@ -82,14 +82,16 @@ def test_large_support_wstacking_parity(gpu_device, support):
                                        do_wstacking=True)
     assert prm.nplanes > support
     ref = oracle.ms2dirty(uvw, f, vis, w, npix, npix, px, px, support=support, do_wstacking=True)
-    assert _err(gpu, ref, float(w.astype(np.float64).sum())) < TOL[(True, support)]
+    err = _err(gpu, ref, float(w.astype(np.float64).sum()))
+    print(f"W={support} w-stacking ({prm.nplanes} planes): max|GPU - oracle| / sum w = {err:.2e}")
+    assert err < TOL[(True, support)]
 
 
 @pytest.mark.parametrize("wstack", [False, True])
 def test_large_support_pruned_fft_halo(gpu_device, wstack):
     # npix 512 -> 1024^2 grid: pruned FFT whose pass A reads only the masked
     # tiles; W = 48 and 64 sub-grids reach two tiles past their own
-    W = 48 if wstack else 64
+    W = 64
     uvw, f, vis, w = _case(2_000, 4, n_ant=24, radius=2000.0, fov=0.05 if wstack else 0.01)
     npix = 512
     px = syn.pixel_size_for_grid(uvw, f, npix, fill=0.3 if wstack else 0.4)
@@ -164,7 +166,5 @@ def test_large_support_argument_errors(gpu_device):
         gridder.device_ms2dirty(*args, 64, 64, px, px, support=20)
     with pytest.raises(ValueError):
         gridder.device_ms2dirty(*args, 64, 64, px, px, support=32, single_precision_accumulation=True)
-    with pytest.raises(ValueError):  # w-stacking at W = 64: beyond the fixed-point class's conditioning
-        gridder.device_ms2dirty(*args, 64, 64, px, px, support=64, do_wstacking=True)
     with pytest.raises(ValueError):  # 16 x 16 grid < W = 24
         gridder.device_ms2dirty(*args, 8, 8, px, px, support=24)

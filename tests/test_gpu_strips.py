@@ -71,13 +71,64 @@ def test_strip_decomposition_equals_one_shot(gpu_device, world, W, npix):
         datas.append(strips.gather_strip(tu, tv, tw, rows, c0, c1))
     assert sum(d.nvis for d in datas) == vis.size
     be = strips.HipStripBackend(prm, px, px, npix, npix, device=gpu_device)
-    img = strips.invert_strips_local(datas, tf, layout, be)
+    stages = []
+    img = strips.invert_strips_local(datas, tf, layout, be, stages=stages)
     torch.cuda.synchronize()
     # same visibilities and weights; only the fixed-point quantum of each
     # gridding call differs (2^-46 of each strip's max |w V|)
     peak = float(ref.abs().max())
     assert float((img - ref).abs().max()) < 1e-12 * peak
-    assert float(be.grid.abs().max()) == 0.0
+    # each rank holds only its strip + W - 1 halo rows, left clean
+    for r, b in enumerate(be.ranks):
+        assert b.rows == strips.strip_buffer_rows(layout, r)
+        assert tuple(b.grid.shape) == (b.rows[1], prm.nu, 2)
+        assert float(b.grid.abs().max()) == 0.0 and not b.dirty
+    assert len(stages) == world and all("grid" in st and "rows" in st and "cols" in st for st in stages)
+    # a second call through the same rank buffers gives the same image
+    img2 = strips.invert_strips_local(datas, tf, layout, be)
+    assert torch.equal(img, img2)
+
+
+def test_strip_buffer_rejects_footprints_outside_its_rows(gpu_device):
+    # cip_grid_tiles_strip: a visibility whose footprint leaves the buffer's
+    # row window is an error (CIP_ERANGE), not an out-of-bounds write
+    npix = 512
+    uvw, f, vis, w, px = _case(3000, 8, npix)
+    tu, tf, tv, tw = _to(gpu_device, uvw, f, vis.astype(np.complex64), w.astype(np.float32))
+    prm = _lib.choose_params(npix, npix, px, px, 1e-4, 8)
+    layout = strips.plan_strips(tu, tf, prm, px, npix, npix, 4)
+    rows, c0, c1 = strips.strip_slices(tu, tf, prm, px, *layout.rows(2))
+    data = strips.gather_strip(tu, tv, tw, rows, c0, c1)
+    assert data.nvis > 0
+    be = strips.HipStripBackend(prm, px, px, npix, npix, device=gpu_device)
+    be.bind(layout, 1)  # another rank's rows
+    with pytest.raises(ValueError, match="strip"):
+        be.grid_strip(data, tf)
+    assert be.dirty  # the failed call leaves the buffer marked dirty ...
+    be.bind(layout, 2)  # (rebinding reallocates a clean buffer)
+    buf, sw = be.grid_strip(data, tf)
+    assert float(buf.abs().max()) > 0.0
+    H = be.pass_rows(buf, 0, layout.rows(2)[1] - layout.rows(2)[0])
+    buf[layout.rows(2)[1] - layout.rows(2)[0]:].zero_()
+    be.mark_clean()
+    assert float(buf.abs().max()) == 0.0 and H.shape[1] == layout.rows(2)[1] - layout.rows(2)[0]
+
+
+def test_strip_backend_recovers_from_an_interrupted_invert(gpu_device):
+    # a dirty buffer (an invert that stopped between gridding and pass A) is
+    # zeroed by the next grid_strip instead of being trusted as CIP_GRID_ZEROED
+    npix = 512
+    uvw, f, vis, w, px = _case(3000, 8, npix)
+    tu, tf, tv, tw = _to(gpu_device, uvw, f, vis.astype(np.complex64), w.astype(np.float32))
+    ref, prm = device_ms2dirty(tu, tf, tv, tw, npix, npix, px, px, support=8, normalise=True)
+    layout = strips.plan_strips(tu, tf, prm, px, npix, npix, 1)
+    rows, c0, c1 = strips.strip_slices(tu, tf, prm, px, *layout.rows(0))
+    data = strips.gather_strip(tu, tv, tw, rows, c0, c1)
+    be = strips.HipStripBackend(prm, px, px, npix, npix, device=gpu_device)
+    be.grid_strip(data, tf)  # interrupted: no pass A
+    assert be.dirty
+    img = strips.invert_strips_local([data], tf, layout, be)
+    assert float((img - ref).abs().max()) < 1e-12 * float(ref.abs().max())
 
 
 def test_allreduce_grids_multi_gpu():

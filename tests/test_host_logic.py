@@ -308,3 +308,20 @@ def test_local_gpu_client_synchronous_mode():
     b = client.submit(lambda x, y: x * y, a, 5)
     assert a.done() and b.result() == 10
     assert [f.result() for f in as_completed([a, b])] == [2, 10]
+
+
+def test_bench_refuses_a_world_size_other_than_gpus():
+    # bench.py --gpus N under a launcher whose WORLD_SIZE differs: rc != 0
+    # before anything touches a GPU (the driver must never get an n_gpus that
+    # is not the run's)
+    import os
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    root = Path(__file__).resolve().parents[1]
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    out = subprocess.run([sys.executable, str(root / "bench.py"), "--gpus", "1"], env=env, capture_output=True,
+                         text=True, timeout=120)
+    assert out.returncode == 2, out.stderr[-2000:]
+    assert "WORLD_SIZE=2" in out.stderr

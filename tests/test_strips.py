@@ -114,7 +114,13 @@ def test_strip_emulation_equals_one_shot(world, W):
     img = strips.invert_strips_local(datas, torch.from_numpy(f), layout, be).numpy()
     full = oracle.ms2dirty(uvw, f, vis, w, NPIX, NPIX, px, px, support=W, nthreads=1) / w.astype(np.float64).sum()
     assert np.abs(img - full).max() < 1e-13 * max(1.0, np.abs(full).max())
-    assert float(be.grid.abs().max()) == 0.0  # the grid is left clean
+    # every rank's buffer holds only its strip + halo rows and is left clean
+    assert len(be.ranks) == world
+    for r, b in enumerate(be.ranks):
+        assert b.rows == strips.strip_buffer_rows(layout, r)
+        assert float(b.grid.abs().max()) == 0.0 and not b.dirty
+    if world > 1:
+        assert sum(b.rows[1] for b in be.ranks) == prm["nv"] + world * (W - 1)
 
 
 def _worker(rank, world, port, q, W):
