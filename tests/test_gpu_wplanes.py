@@ -23,7 +23,7 @@ def _case(nrow, nchan, npix, seed=11):
     ms = syn.make_measurement_set(nrow, nchan, n_ant=24, array_radius_m=2000.0, fov_l=0.05, seed=seed)
     vis, _, _, w = oracle.stokes_i(ms.visibilities(), ms.flags(), ms.weights())
     uvw, f = ms.uvw(), ms.channel_frequencies()
-    px = syn.pixel_size_for_grid(uvw, f, npix, fill=0.3)
+    px = 0.2 / npix  # a 0.2 rad field: ~24 w planes at W = 6 (baselines wrap exactly)
     return uvw, f, vis.astype(np.complex64), w.astype(np.float32), px
 
 

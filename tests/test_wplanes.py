@@ -35,7 +35,7 @@ def _case(nrow=600, nchan=8, seed=5):
     ms = syn.make_measurement_set(nrow, nchan, n_ant=12, array_radius_m=1500.0, fov_l=0.05, seed=seed)
     vis, _, _, w = oracle.stokes_i(ms.visibilities(), ms.flags(), ms.weights())
     uvw, f = ms.uvw(), ms.channel_frequencies()
-    px = syn.pixel_size_for_grid(uvw, f, NPIX, fill=0.3)
+    px = 0.2 / NPIX  # a 0.2 rad field: ~20 w planes (baselines wrap exactly)
     return uvw, f, vis, w, px
 
 
