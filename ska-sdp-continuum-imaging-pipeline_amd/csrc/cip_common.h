@@ -37,6 +37,12 @@ constexpr int64_t kChunkVis = 16384;  // 16384 vs 32768: 2 % less scatter tail a
 constexpr int kPackedBits = 18;
 constexpr int64_t kChunkVisPacked = 4096;
 constexpr int kChunkVisPackedLog2 = 12;
+// The packed class rounds each tap in fp32 (cip_scatter.h packed_tap): an fma
+// against 1.5 * 2^23 is an exact integer rounding for |x| < 2^22, so a short
+// chunk's gain over the base scale (contributions < 2^18) is capped at 2^3.
+constexpr float kMagicF = 12582912.0f;  // 1.5 * 2^23
+constexpr uint32_t kMagicFBits = 0x4B400000u;
+constexpr int kPackedGainLog2Max = 3;
 
 // Tile edge (grid cells) of the scatter work decomposition (CIP_TILE
 // overrides it in experiment builds, tools/build_variant_full.sh).
@@ -111,12 +117,40 @@ __device__ __forceinline__ void eval_kernel(double y, double* out) {
   }
 }
 
+// All W kernel values at y in [-1, 1) in fp32 (the packed class): the same
+// polynomial pieces, coefficients rounded to float.
+__device__ __forceinline__ float sgpr_constf(float c) {
+  asm volatile("" : "+s"(c));
+  return c;
+}
+template <int W>
+__device__ __forceinline__ void eval_kernel_f32(float y, float* out) {
+  using K = EsKernel<W>;
+  const float z = y * y;
+#pragma unroll
+  for (int k = 0; k < W / 2; ++k) {
+    constexpr int D = K::D;
+    float e = sgpr_constf((float)K::coef(k, (D & 1) ? D - 1 : D));
+#pragma unroll
+    for (int d = ((D & 1) ? D - 1 : D) - 2; d >= 0; d -= 2) e = fmaf(e, z, sgpr_constf((float)K::coef(k, d)));
+    float o = sgpr_constf((float)K::coef(k, (D & 1) ? D : D - 1));
+#pragma unroll
+    for (int d = ((D & 1) ? D : D - 1) - 2; d >= 1; d -= 2) o = fmaf(o, z, sgpr_constf((float)K::coef(k, d)));
+    out[k] = fmaf(y, o, e);
+    out[W - 1 - k] = fmaf(-y, o, e);
+  }
+}
+
 // Scale of a packed chunk of n visibilities relative to the launch's base
-// scale (which assumes n = kChunkVisPacked): 2^(12 - ceil(lg n)), exact.
+// scale (which assumes n = kChunkVisPacked): 2^min(12 - ceil(lg n), 3), exact
+// (the cap keeps every contribution below 2^22, the fp32 rounding's range;
+// sums stay below 2^30 either way).
 __host__ __device__ inline double packed_chunk_gain(int64_t n) {
   int lg = 0;
   while (((int64_t)1 << lg) < n) ++lg;
-  return (double)((int64_t)1 << (kChunkVisPackedLog2 - (lg < kChunkVisPackedLog2 ? lg : kChunkVisPackedLog2)));
+  int e = kChunkVisPackedLog2 - (lg < kChunkVisPackedLog2 ? lg : kChunkVisPackedLog2);
+  e = e < kPackedGainLog2Max ? e : kPackedGainLog2Max;
+  return (double)((int64_t)1 << e);
 }
 
 // A gridding work unit: the flattened visibilities [g0, g1) of tile `tile`

@@ -144,6 +144,79 @@ __device__ __forceinline__ VisFetch from_raw(const RawFetch<VisT, WK>& r, bool u
   return f;
 }
 
+// One packed single-precision tap (CIP_ACC_SINGLE): the contribution
+// ku * k(r|i) rounded to an integer in fp32 by one fma against 1.5 * 2^23
+// (exact for |x| < 2^22, which packed_chunk_gain guarantees), re and im
+// packed as re * 2^32 + im (two's complement: the high word takes im's sign
+// borrow) for ONE 64-bit LDS add. Two fp32 fmas + three integer ops per tap
+// instead of two fp64 fmas (4x the issue cycles on CDNA4) - the arithmetic
+// class of ducc0's float32 gridding that the reference's complex64 call uses.
+__device__ __forceinline__ unsigned long long packed_tap(float ku, float kr, float ki) {
+  const float qr = fmaf(ku, kr, kMagicF);
+  const float qi = fmaf(ku, ki, kMagicF);
+  const unsigned bi = __float_as_uint(qi);
+  const unsigned im = bi - kMagicFBits;
+  // the borrow is im < 0: qi's mantissa is 2^22 + im, so bit 22 of its bits
+  // is set exactly when im >= 0 (hi = re + bit22 - 1; no wait on im)
+  unsigned hi;
+  asm("v_add3_u32 %0, %1, %2, %3"
+      : "=v"(hi)
+      : "v"(__float_as_uint(qr)), "v"(__builtin_amdgcn_ubfe(bi, 22u, 1u)), "s"(0u - kMagicFBits - 1u));
+  return __builtin_bit_cast(unsigned long long, make_uint2(im, hi));
+}
+
+// The packed class's visibility: fp32 kernel values and tap products (the
+// placement stays fp64, the planner's bit for bit). G > 1: the unit's G
+// planes as in grid_fetched.
+template <int W, bool WSTACK, int G>
+__device__ __forceinline__ void grid_fetched_packed(const VisFetch& f, const GridGeometry& g, int64_t plane,
+                                                    int64_t X0, int64_t Y0, double fixed_scale,
+                                                    unsigned long long* sub) {
+  constexpr int T = kTile;
+  constexpr int P = T + W - 1;
+  constexpr int S = P * P;
+  if (f.wt == 0.0) return;
+  int64_t ix0, iy0, iw0;
+  double yu, yv, yw;
+  if (!place_vis(f.u, f.v, f.w, f.fx, g, &ix0, &yu, &iy0, &yv, &iw0, &yw)) return;
+  const int64_t lx = ix0 - X0, ly = iy0 - Y0;
+  if (lx < 0 || lx >= T || ly < 0 || ly >= T) return;  // never for a consistent plan
+  const double sc0 = f.wt * fixed_scale;
+  const float vr0 = (float)(f.vr * sc0), vi0 = (float)(f.vi * sc0);
+  float ku[W], kv[W];
+  eval_kernel_f32<W>((float)yu, ku);
+  eval_kernel_f32<W>((float)yv, kv);
+  unsigned long long* base = sub + (lx * P + ly);
+  auto taps = [&](unsigned long long* bk, float vr, float vi) {
+    float kr[W], ki[W];
+#pragma unroll
+    for (int j = 0; j < W; ++j) {
+      kr[j] = kv[j] * vr;
+      ki[j] = kv[j] * vi;
+    }
+#pragma unroll
+    for (int i = 0; i < W; ++i)
+#pragma unroll
+      for (int j = 0; j < W; ++j) atomicAdd(bk + (i * P + j), packed_tap(ku[i], kr[j], ki[j]));
+  };
+  if constexpr (!WSTACK) {
+    taps(base, vr0, vi0);
+  } else {
+    float kwv[W];
+    eval_kernel_f32<W>((float)yw, kwv);
+#pragma unroll
+    for (int k = 0; k < G; ++k) {
+      const int64_t kw = plane + k - iw0;
+      if (kw < 0 || kw >= W) continue;  // the visibility does not feed plane + k
+      if (plane + k < g.plane_lo || plane + k >= g.plane_hi) continue;  // outside the call's plane range
+      float sel = 0.0f;
+#pragma unroll
+      for (int q = 0; q < W; ++q) sel = (q == kw) ? kwv[q] : sel;
+      taps(base + k * S, vr0 * sel, vi0 * sel);
+    }
+  }
+}
+
 // One visibility onto the unit's sub-grid(s). G > 1 (w-stacking): the unit
 // grids planes plane .. plane + G - 1 at once (G sub-grids, S u64 apart), the
 // visibility placed and its u, v, w kernels evaluated once for all of them.
@@ -152,6 +225,12 @@ __device__ __forceinline__ void grid_fetched(const VisFetch& f, const GridGeomet
                                              int64_t Y0, double fixed_scale, unsigned long long* sub) {
   constexpr int T = kTile;
   constexpr int P = T + W - 1;
+#if CIP_ABLATE == 0 || CIP_ABLATE == 4
+  if constexpr (PACK) {
+    grid_fetched_packed<W, WSTACK, G>(f, g, plane, X0, Y0, fixed_scale, sub);
+    return;
+  }
+#endif
   if (f.wt == 0.0) return;
   int64_t ix0, iy0, iw0;
   double yu, yv, yw;

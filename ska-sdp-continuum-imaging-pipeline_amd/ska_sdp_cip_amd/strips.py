@@ -90,12 +90,47 @@ def _row_chunks(nrow: int, chunk: int = 65536):
         yield a, min(nrow, a + chunk)
 
 
-def plan_strips(uvw, freq, params, pixsize_y: float, npix_x: int, npix_y: int, world: int) -> StripLayout:
-    """Balanced strips: grid-row bounds splitting the visibilities' origin-row
-    histogram (all visibilities, so every rank computes the same bounds
-    without communication) into `world` near-equal parts, each at least
-    W rows high (the halo then only reaches the next strip); image rows split
-    into near-equal multiples of COL_BLOCK. uvw (nrow, 3), freq (nchan) tensors."""
+# Per-rank cost model of a strip (measured on MI355X, profiles/
+# r04_strong_model_c4_n8.json: the 8 strips of C4 balanced by visibility count
+# took 6.7-9.5 ms to grid, linear in their row slices): gridding costs
+# ~36.9 ps per visibility + ~112 ps per row slice (the planner's runs and the
+# scatter's per-slice loads), pass A ~8.9 ps per grid cell of the strip's rows.
+COST_PS_PER_VIS = 36.9
+COST_PS_PER_SLICE = 112.0
+COST_PS_PER_CELL = 8.9
+
+
+def row_costs(uvw, freq, params, pixsize_x: float, pixsize_y: float):
+    """Modelled cost (ps) of each grid row as a strip member: its visibilities
+    (by footprint-origin row), the row slices starting there (a slice starts
+    at each row's first channel and wherever the origin's 32-cell tile changes
+    along the channels) and its pass-A cells."""
+    nu, nv, W = int(params.nu), int(params.nv), int(params.support)
+    fx = freq / SPEED_OF_LIGHT
+    vis = torch.zeros(nv, dtype=torch.int64, device=uvw.device)
+    runs = torch.zeros(nv, dtype=torch.int64, device=uvw.device)
+    for a, b in _row_chunks(uvw.shape[0]):
+        iy = origin_rows(uvw[a:b, 1], fx, float(params.nv) * pixsize_y, nv, W)
+        ix = origin_rows(uvw[a:b, 0], fx, float(params.nu) * pixsize_x, nu, W)
+        key = torch.div(iy, 32, rounding_mode="floor") * (nu // 32 + 1) + torch.div(ix, 32, rounding_mode="floor")
+        start = torch.ones_like(key, dtype=torch.bool)
+        start[:, 1:] = key[:, 1:] != key[:, :-1]
+        vis += torch.bincount(iy.reshape(-1), minlength=nv)
+        runs += torch.bincount(iy[start], minlength=nv)
+    cost = (COST_PS_PER_VIS * vis.double() + COST_PS_PER_SLICE * runs.double() + COST_PS_PER_CELL * nu)
+    return cost.cpu().numpy()
+
+
+def plan_strips(uvw, freq, params, pixsize_y: float, npix_x: int, npix_y: int, world: int,
+                balance: str = "cost", pixsize_x: Optional[float] = None) -> StripLayout:
+    """Balanced strips: grid-row bounds splitting a per-row histogram (all
+    visibilities, so every rank computes the same bounds without
+    communication) into `world` near-equal parts, each at least W rows high
+    (the halo then only reaches the next strip); image rows split into
+    near-equal multiples of COL_BLOCK. balance="cost": the measured per-rank
+    cost model (`row_costs`: visibilities, row slices, pass-A rows; needs
+    pixsize_x, default pixsize_y); "vis": visibility count only. uvw (nrow,
+    3), freq (nchan) tensors."""
     nv, W = int(params.nv), int(params.support)
     if world < 1:
         raise ValueError("world must be >= 1")
@@ -105,13 +140,19 @@ def plan_strips(uvw, freq, params, pixsize_y: float, npix_x: int, npix_y: int, w
                          f"{COL_BLOCK} image rows per rank")
     if nv < W * world:
         raise ValueError("grid too small for this many strips")
-    fx = freq / SPEED_OF_LIGHT
-    scale_v = float(params.nv) * pixsize_y
-    hist = torch.zeros(nv, dtype=torch.int64, device=uvw.device)
-    for a, b in _row_chunks(uvw.shape[0]):
-        hist += torch.bincount(origin_rows(uvw[a:b, 1], fx, scale_v, nv, W).reshape(-1), minlength=nv)
-    cum = np.cumsum(hist.cpu().numpy())
-    total = int(cum[-1]) if cum.size else 0
+    if balance == "cost":
+        hist = row_costs(uvw, freq, params, pixsize_y if pixsize_x is None else pixsize_x, pixsize_y)
+    elif balance == "vis":
+        fx = freq / SPEED_OF_LIGHT
+        scale_v = float(params.nv) * pixsize_y
+        h = torch.zeros(nv, dtype=torch.int64, device=uvw.device)
+        for a, b in _row_chunks(uvw.shape[0]):
+            h += torch.bincount(origin_rows(uvw[a:b, 1], fx, scale_v, nv, W).reshape(-1), minlength=nv)
+        hist = h.cpu().numpy()
+    else:
+        raise ValueError("balance must be 'cost' or 'vis'")
+    cum = np.cumsum(hist)
+    total = float(cum[-1]) if cum.size else 0.0
     bounds = [0]
     for r in range(1, world):
         target = total * r / world

@@ -64,7 +64,8 @@ def _strip_datas(uvw, f, vis, w, px, prm, layout):
 def test_strip_plan_partitions_visibilities(world):
     uvw, f, vis, w, px = _case()
     prm = _prm(px, 8)
-    layout = strips.plan_strips(torch.from_numpy(uvw), torch.from_numpy(f), _P(prm), px, NPIX, NPIX, world)
+    layout = strips.plan_strips(torch.from_numpy(uvw), torch.from_numpy(f), _P(prm), px, NPIX, NPIX, world,
+                                balance="vis")
     yb = layout.y_bounds
     assert yb[0] == 0 and yb[-1] == prm["nv"]
     assert all(b - a >= prm["support"] for a, b in zip(yb, yb[1:]))
@@ -187,3 +188,21 @@ def test_strips_with_empty_strips_and_no_data():
     assert layout0.y_bounds[0] == 0 and layout0.y_bounds[-1] == prm["nv"]
     rows, c0, c1 = strips.strip_slices(e, torch.from_numpy(f), _P(prm), px, *layout0.rows(1))
     assert rows.numel() == 0
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_strip_plan_balances_the_cost_model(world):
+    # the default balance: modelled per-rank cost (visibilities, row slices,
+    # pass-A rows; strips.row_costs) near-equal across strips
+    uvw, f, vis, w, px = _case(nrow=1500, nchan=32)
+    prm = _prm(px, 8)
+    tu, tf = torch.from_numpy(uvw), torch.from_numpy(f)
+    cost = strips.row_costs(tu, tf, _P(prm), px, px)
+    assert cost.shape == (prm["nv"],) and (cost > 0).all()
+    layout = strips.plan_strips(tu, tf, _P(prm), px, NPIX, NPIX, world)
+    share = [cost[a:b].sum() for a, b in zip(layout.y_bounds, layout.y_bounds[1:])]
+    window = np.convolve(cost, np.ones(2 * prm["support"])).max()
+    assert max(share) <= cost.sum() / world + window
+    # the strips still partition the visibilities
+    datas = _strip_datas(uvw, f, vis, w, px, prm, layout)
+    assert sum(d.nvis for d in datas) == vis.size
