@@ -787,20 +787,28 @@ static bool wgt_dtype_ok(int d) { return d == CIP_NONE || d == CIP_F32 || d == C
 // w planes per scatter work unit in w-stacking mode: G = 3 (a visibility
 // placed and its u, v, w kernels evaluated once for three planes; the unit
 // holds G sub-grids in 512-thread blocks), fewer where two such blocks would
-// not fit a CU's LDS (W >= 10: 2); CIP_WSTACK_GROUP=1/2 caps it (A/B); the
-// large supports always 1. Refcall C3: G = 1 / 2 / 3 -> 13.4 / 12.2 / 11.8 ms
+// not fit a CU's LDS (W >= 10: 2); the packed class's 8-byte cells allow up to
+// 5 (round 4); CIP_WSTACK_GROUP=1..5 caps it (A/B); the large supports always
+// 1. Refcall C3 (round 3, fp64 taps): G = 1 / 2 / 3 -> 13.4 / 12.2 / 11.8 ms
 // of scatter (profiles/r03_ab_wstack_group*.txt).
-static int wstack_group(const GridGeometry& g) {
+static int wstack_group(const GridGeometry& g, bool packed) {
   static const int env = [] {
     const char* e = getenv("CIP_WSTACK_GROUP");
-    const int v = e ? atoi(e) : 3;
-    return v < 1 ? 1 : (v > 3 ? 3 : v);
+    const int v = e ? atoi(e) : 0;
+    return v < 0 ? 0 : (v > 5 ? 5 : v);
   }();
   if (!g.do_wstacking || g.support > 16 || g.nplanes < 2) return 1;
-  // two 512-thread blocks per CU must fit their G sub-grids in 160 KB of LDS
   const int64_t P = kTile + g.support - 1;
+  if (packed) {
+    // 8-byte cells: up to 5 sub-grids in one 512-thread block (<= 64 KB of
+    // static LDS, cip_scatter.h kFitG5 / kFitG4), two blocks per CU
+    int G = env ? env : 5;
+    while (G > 3 && G * P * P * 8 + 4200 > 65536) --G;
+    return G;
+  }
+  // two 512-thread blocks per CU must fit their G sub-grids in 160 KB of LDS
   const int64_t per_plane = P * P * 16;
-  int G = env;
+  int G = env ? (env > 3 ? 3 : env) : 3;
   while (G > 1 && 2 * G * per_plane > 160 * 1024) --G;
   return G;
 }
@@ -961,7 +969,7 @@ static int prepare(Workspace* ws, const double* uvw, int64_t nrow, const double*
   out->red = red;
   if (grid_out) {
     // the grid is known now: zero its first plane group beside the planner
-    const int64_t gplanes = want_group ? wstack_group(out->g) : 1;
+    const int64_t gplanes = want_group ? wstack_group(out->g, packed) : 1;
     const size_t gbytes = sizeof(double) * 2 * out->g.nu * out->g.nv * gplanes;
     double* grid = buf<double>(ws, "grid", 2 * out->g.nu * out->g.nv * gplanes);
     if (!grid) return CIP_ENOMEM;
@@ -1007,7 +1015,7 @@ static int prepare(Workspace* ws, const double* uvw, int64_t nrow, const double*
   } else {
     ws->saved_valid = false;
     rc = make_plan(ws, uvw, fx, m, vis, vis_dtype, wgt, wgt_dtype, red, out->g, chunk_vis(packed, out->g.nu), s,
-                   &out->plan, &maxabs, want_group ? wstack_group(out->g) : 1);
+                   &out->plan, &maxabs, want_group ? wstack_group(out->g, packed) : 1);
     if (rc == CIP_OK && !ragged) {
       ws->saved_key = key;
       ws->saved_p = out->p;

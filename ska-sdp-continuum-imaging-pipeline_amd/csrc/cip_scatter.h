@@ -144,25 +144,21 @@ __device__ __forceinline__ VisFetch from_raw(const RawFetch<VisT, WK>& r, bool u
   return f;
 }
 
-// One packed single-precision tap (CIP_ACC_SINGLE): the contribution
-// ku * k(r|i) rounded to an integer in fp32 by one fma against 1.5 * 2^23
-// (exact for |x| < 2^22, which packed_chunk_gain guarantees), re and im
-// packed as re * 2^32 + im (two's complement: the high word takes im's sign
-// borrow) for ONE 64-bit LDS add. Two fp32 fmas + three integer ops per tap
-// instead of two fp64 fmas (4x the issue cycles on CDNA4) - the arithmetic
-// class of ducc0's float32 gridding that the reference's complex64 call uses.
-__device__ __forceinline__ unsigned long long packed_tap(float ku, float kr, float ki) {
-  const float qr = fmaf(ku, kr, kMagicF);
-  const float qi = fmaf(ku, ki, kMagicF);
-  const unsigned bi = __float_as_uint(qi);
-  const unsigned im = bi - kMagicFBits;
-  // the borrow is im < 0: qi's mantissa is 2^22 + im, so bit 22 of its bits
-  // is set exactly when im >= 0 (hi = re + bit22 - 1; no wait on im)
-  unsigned hi;
-  asm("v_add3_u32 %0, %1, %2, %3"
-      : "=v"(hi)
-      : "v"(__float_as_uint(qr)), "v"(__builtin_amdgcn_ubfe(bi, 22u, 1u)), "s"(0u - kMagicFBits - 1u));
-  return __builtin_bit_cast(unsigned long long, make_uint2(im, hi));
+// One packed single-precision tap (CIP_ACC_SINGLE): the contributions
+// ku * kr and ku * ki rounded to integers in fp32 by one packed fma against
+// 1.5 * 2^23 (exact for |x| < 2^22, which packed_chunk_gain guarantees): the
+// two results' bits, (M + im) in the low and (M + re) in the high word, are
+// one 64-bit integer, and subtracting M * (2^32 + 1) leaves re * 2^32 + im in
+// two's complement (the borrow of a negative im comes with the 64-bit
+// subtraction) for ONE 64-bit LDS add. Two VALU instructions per tap
+// (v_pk_fma_f32 + v_lshl_add_u64), against two fp64 fmas + a combine - the
+// arithmetic class of ducc0's float32 gridding that the reference's
+// complex64 call uses.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+constexpr unsigned long long kMagicPair = ((unsigned long long)kMagicFBits << 32) | kMagicFBits;
+__device__ __forceinline__ unsigned long long packed_tap(float ku, f32x2 k_ir) {
+  const f32x2 q = __builtin_elementwise_fma(f32x2{ku, ku}, k_ir, f32x2{kMagicF, kMagicF});
+  return __builtin_bit_cast(unsigned long long, q) - kMagicPair;
 }
 
 // The packed class's visibility: fp32 kernel values and tap products (the
@@ -188,16 +184,14 @@ __device__ __forceinline__ void grid_fetched_packed(const VisFetch& f, const Gri
   eval_kernel_f32<W>((float)yv, kv);
   unsigned long long* base = sub + (lx * P + ly);
   auto taps = [&](unsigned long long* bk, float vr, float vi) {
-    float kr[W], ki[W];
+    f32x2 k_ir[W];  // (kv vi, kv vr): the low / high word of each tap
+    const f32x2 v_ir{vi, vr};
 #pragma unroll
-    for (int j = 0; j < W; ++j) {
-      kr[j] = kv[j] * vr;
-      ki[j] = kv[j] * vi;
-    }
+    for (int j = 0; j < W; ++j) k_ir[j] = f32x2{kv[j], kv[j]} * v_ir;
 #pragma unroll
     for (int i = 0; i < W; ++i)
 #pragma unroll
-      for (int j = 0; j < W; ++j) atomicAdd(bk + (i * P + j), packed_tap(ku[i], kr[j], ki[j]));
+      for (int j = 0; j < W; ++j) atomicAdd(bk + (i * P + j), packed_tap(ku[i], k_ir[j]));
   };
   if constexpr (!WSTACK) {
     taps(base, vr0, vi0);
@@ -529,18 +523,40 @@ inline hipError_t scatter_dispatch_ws(bool ws, int group, bool pack, unsigned ld
       LAUNCH(false, PRM, PK, 1);      \
     }                                 \
   }
+  // the packed class's 8-byte cells fit larger plane groups (4, 5) in LDS
+#define LAUNCH_WS_PACKED(PRM)                                \
+  {                                                          \
+    bool hit = false;                                        \
+    if constexpr (kFitG5) {                                  \
+      if (ws && group == 5) {                                \
+        LAUNCH(true, PRM, true, 5);                          \
+        hit = true;                                          \
+      }                                                      \
+    }                                                        \
+    if constexpr (kFitG4) {                                  \
+      if (!hit && ws && group == 4) {                        \
+        LAUNCH(true, PRM, true, 4);                          \
+        hit = true;                                          \
+      }                                                      \
+    }                                                        \
+    if (!hit) LAUNCH_WS(PRM, true)                           \
+  }
   // the packed single-precision class exists for complex64 input only (the
   // reference's configuration; raw linear-feed columns are complex64 too)
+  // plane groups of 4 / 5 packed sub-grids while they fit 64 KB of static LDS
+  constexpr int P2 = (kTile + W - 1) * (kTile + W - 1);
+  constexpr bool kFitG5 = 5 * P2 * 8 + 4200 <= 65536;
+  constexpr bool kFitG4 = 4 * P2 * 8 + 4200 <= 65536;
   bool done = false;
   const bool wide = m.delta != nullptr;  // ragged row slices: u64 entries
   if constexpr (std::is_same<VisT, float2>::value || std::is_same<VisT, Pol4>::value) {
     if (pack) {
       if (perm && wide) {
-        LAUNCH_WS(2, true)
+        LAUNCH_WS_PACKED(2)
       } else if (perm) {
-        LAUNCH_WS(1, true)
+        LAUNCH_WS_PACKED(1)
       } else {
-        LAUNCH_WS(0, true)
+        LAUNCH_WS_PACKED(0)
       }
       done = true;
     }
@@ -554,6 +570,7 @@ inline hipError_t scatter_dispatch_ws(bool ws, int group, bool pack, unsigned ld
       LAUNCH_WS(0, false)
     }
   }
+#undef LAUNCH_WS_PACKED
 #undef LAUNCH_WS
 #undef LAUNCH
   return hipGetLastError();

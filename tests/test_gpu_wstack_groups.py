@@ -1,6 +1,7 @@
 """
-w-stacking plane groups (two planes per scatter work unit: each visibility
-placed and its u, v, w kernels evaluated once for both) against one plane per
+w-stacking plane groups (G = 2..3 planes per scatter work unit, up to 5 in the
+packed single class: each visibility placed and its u, v, w kernels evaluated
+once for all of them) against one plane per
 unit (CIP_WSTACK_GROUP=1, in a child process since the switch is read once):
 the same images up to the fp64 flush order of differently cut work units, for
 W = 4..16, odd plane counts, the packed single class, repeated calls (the
@@ -24,7 +25,10 @@ pytestmark = pytest.mark.gpu
 ROOT = Path(__file__).resolve().parents[1]
 
 CASES = [dict(support=6, npix=512), dict(support=8, npix=512), dict(support=4, npix=256),
-         dict(support=16, npix=512), dict(support=6, npix=512, single=True), dict(support=12, npix=384)]
+         dict(support=16, npix=512), dict(support=6, npix=512, single=True), dict(support=12, npix=384),
+         # the packed class's larger groups (round 4): 5 planes per unit up to W = 8, 4 at W = 10
+         dict(support=8, npix=512, single=True), dict(support=10, npix=384, single=True),
+         dict(support=4, npix=256, single=True), dict(support=16, npix=512, single=True)]
 
 CHILD = r"""
 import sys, numpy as np, torch
