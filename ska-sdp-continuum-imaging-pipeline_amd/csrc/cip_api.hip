@@ -566,14 +566,21 @@ static bool overlap_zero() {
   return on;
 }
 
-// CIP_ORDER_CLASS=compute: the order pass recomputes each visibility's bank
-// class instead of gathering the place pass's class bytes (A/B experiments)
-static bool order_gather() {
-  static const bool on = [] {
+// How the order pass gets each visibility's bank class (round 4 default
+// "runs": recomputed in fp32 from its run's row (u, v), carried through the
+// radix sort beside the run record, and f / c - no per-visibility class bytes
+// written by the place pass and gathered in tile order (~1 HBM line per row
+// slice, 1.24 GB at C3)); CIP_ORDER_CLASS=gather (round 3: the class bytes) or
+// =compute (recomputed from a uvw gather per slice) for A/B experiments.
+enum { ORDER_RUNS = 0, ORDER_GATHER = 1, ORDER_UVW = 2 };
+static int order_class_mode() {
+  static const int mode = [] {
     const char* e = getenv("CIP_ORDER_CLASS");
-    return !(e && std::strcmp(e, "compute") == 0);
+    if (e && std::strcmp(e, "gather") == 0) return (int)ORDER_GATHER;
+    if (e && std::strcmp(e, "compute") == 0) return (int)ORDER_UVW;
+    return (int)ORDER_RUNS;
   }();
-  return on;
+  return mode;
 }
 
 // CIP_GRID_MASK=0: no dirty-tile mask - the grid is zeroed in full before
@@ -643,13 +650,18 @@ static int make_plan(Workspace* ws, const double* uvw, const double* fx, const R
   const bool ragged = m.delta != nullptr;
   const bool order = scatter_order() && (ragged || nvis < ((int64_t)1 << 32));
   uint8_t* vis_class = nullptr;
-  if (order && order_gather()) {
+  uint64_t* park_uv = nullptr;
+  if (order && order_class_mode() == ORDER_GATHER) {
     vis_class = buf<uint8_t>(ws, "vis_class", nvis);
     if (!vis_class) return CIP_ENOMEM;
   }
   CIP_ALLOC(blk_cnt, int64_t, "blk_cnt", nblk)
   CIP_ALLOC(park_key, uint32_t, "park_key", (int64_t)nblk * 4096)
   CIP_ALLOC(park_run, uint64_t, "park_run", (int64_t)nblk * 4096)
+  if (order && order_class_mode() == ORDER_RUNS) {
+    park_uv = buf<uint64_t>(ws, "park_uv", (int64_t)nblk * 4096);
+    if (!park_uv) return CIP_ENOMEM;
+  }
   CIP_ALLOC(partial, double, "prep_partial", 2 * nblk)
   // the place pass also writes radix pass 0's histogram per place block; summed
   // per radix group of g0 blocks, its scan's last entry = runs
@@ -659,7 +671,7 @@ static int make_plan(Workspace* ws, const double* uvw, const double* fx, const R
   CIP_ALLOC(hist0g, int64_t, "radix_hist0g", 256 * ng0 + 1)
   CIP_ALLOC(scan_h0, int64_t, "scan_hist0", scan_tmp_elems(256 * ng0 + 1))
   CIP_HIP_CHECK(launch_plan_place(uvw, fx, m, vis, vis_dtype, wgt, wgt_dtype, g, err, vis_class, blk_cnt, park_key,
-                                  park_run, partial, hist0, s));
+                                  park_run, partial, hist0, s, park_uv));
   CIP_HIP_CHECK(launch_prep_final(partial, nblk, red, s));
   int key_bits = 1;
   while (key_bits < 32 && ((int64_t)1 << key_bits) < ntiles) ++key_bits;
@@ -685,19 +697,28 @@ static int make_plan(Workspace* ws, const double* uvw, const double* fx, const R
   CIP_ALLOC(key_b, uint32_t, "sort_key_b", nruns)
   CIP_ALLOC(run_a, uint64_t, "sort_run_a", nruns)
   CIP_ALLOC(run_b, uint64_t, "sort_run_b", nruns)
+  uint64_t *uv_a = nullptr, *uv_b = nullptr;
+  if (park_uv) {
+    uv_a = buf<uint64_t>(ws, "sort_uv_a", nruns);
+    uv_b = buf<uint64_t>(ws, "sort_uv_b", nruns);
+    if (!uv_a || !uv_b) return CIP_ENOMEM;
+  }
   const int64_t nbd = radix_blocks(nruns);
   const int64_t ng1 = (nbd + g1 - 1) / g1;
   CIP_ALLOC(hist, int64_t, "radix_hist", 256 * ng1 + 1)
   CIP_ALLOC(scan_h, int64_t, "scan_hist", scan_tmp_elems(256 * ng1 + 1))
-  CIP_HIP_CHECK(launch_radix_scatter(park_key, park_run, 0, blk_cnt, nblk, g0, 0, hist0g, key_a, run_a, s));
+  CIP_HIP_CHECK(launch_radix_scatter(park_key, park_run, 0, blk_cnt, nblk, g0, 0, hist0g, key_a, run_a, s, park_uv,
+                                     uv_a));
   uint32_t *kin = key_a, *kout = key_b;
   uint64_t *rin = run_a, *rout = run_b;
+  uint64_t *uin = uv_a, *uout = uv_b;
   for (int p = 1; p < npass; ++p) {
     CIP_HIP_CHECK(launch_radix_hist(kin, nruns, nullptr, nbd, g1, 8 * p, hist, s));
     CIP_HIP_CHECK(exclusive_scan_i64(hist, 256 * ng1 + 1, scan_h, s));
-    CIP_HIP_CHECK(launch_radix_scatter(kin, rin, nruns, nullptr, nbd, g1, 8 * p, hist, kout, rout, s));
+    CIP_HIP_CHECK(launch_radix_scatter(kin, rin, nruns, nullptr, nbd, g1, 8 * p, hist, kout, rout, s, uin, uout));
     std::swap(kin, kout);
     std::swap(rin, rout);
+    std::swap(uin, uout);
   }
   uint64_t* runs = rin;
   CIP_HIP_CHECK(launch_tile_offsets(kin, nruns, ntiles, tile_runs, s));
@@ -771,7 +792,7 @@ static int make_plan(Workspace* ws, const double* uvw, const double* fx, const R
     CIP_HIP_CHECK(launch_chunk_emit(tile_vis_off, tile_vis, win_off, run_goff, tile_runs, ntiles, kOrderWindow, 0, nwin,
                                     windows, s));
     CIP_ALLOC(perm, uint32_t, "perm", ragged ? 2 * nvis : nvis)
-    CIP_HIP_CHECK(launch_order(uvw, fx, vis_class, g, m, runs, run_goff, tile_runs, windows, nwin, perm, s));
+    CIP_HIP_CHECK(launch_order(uvw, fx, vis_class, g, m, runs, run_goff, tile_runs, windows, nwin, perm, s, uin));
     pr->perm = perm;
   }
   return CIP_OK;

@@ -132,7 +132,8 @@ __global__ __launch_bounds__(kOrderThreads, 8) void order_kernel(const double* _
                                                               const int64_t* __restrict__ run_goff,
                                                               const int64_t* __restrict__ tile_run_off,
                                                               const Chunk* __restrict__ windows, int64_t nwindows,
-                                                              void* __restrict__ perm) {
+                                                              void* __restrict__ perm,
+                                                              const uint64_t* __restrict__ run_uv) {
   __shared__ __attribute__((aligned(16))) unsigned s_cnt[32];
   // the staged slices are dead once every position has its class: the level
   // tables reuse their space
@@ -165,8 +166,12 @@ __global__ __launch_bounds__(kOrderThreads, 8) void order_kernel(const double* _
     s_rec[k] = rec;
     if constexpr (WIDE) sh.a.delta[k] = m.delta[(int64_t)(rec >> 32)];
     if constexpr (!GATHER) {
-      const int64_t row = (int64_t)(rec >> 32);
-      s_uv[k] = make_float2((float)(uvw[3 * row] * g.scale_u), (float)(uvw[3 * row + 1] * g.scale_v));
+      if (run_uv) {  // carried with the run through the sort: contiguous, no gather
+        s_uv[k] = __builtin_bit_cast(float2, run_uv[ch.first_run + k]);
+      } else {
+        const int64_t row = (int64_t)(rec >> 32);
+        s_uv[k] = make_float2((float)(uvw[3 * row] * g.scale_u), (float)(uvw[3 * row + 1] * g.scale_v));
+      }
     }
   }
   if (threadIdx.x < 32) s_cnt[threadIdx.x] = 0u;
@@ -237,11 +242,12 @@ __global__ __launch_bounds__(kOrderThreads, 8) void order_kernel(const double* _
 
 hipError_t launch_order(const double* uvw, const double* fx, const uint8_t* vis_class, const GridGeometry& g,
                         const RowMap& m, const uint64_t* runs, const int64_t* run_goff, const int64_t* tile_run_off,
-                        const Chunk* windows, int64_t nwindows, void* perm, hipStream_t s) {
+                        const Chunk* windows, int64_t nwindows, void* perm, hipStream_t s,
+                        const uint64_t* run_uv) {
   if (nwindows <= 0) return hipSuccess;
 #define ORDER(GA, WI)                                                              \
   order_kernel<GA, WI><<<dim3((unsigned)nwindows), dim3(kOrderThreads), 0, s>>>( \
-      uvw, fx, vis_class, g, m, runs, run_goff, tile_run_off, windows, nwindows, perm)
+      uvw, fx, vis_class, g, m, runs, run_goff, tile_run_off, windows, nwindows, perm, run_uv)
   const bool wide = m.delta != nullptr;  // ragged row slices: u64 entries
   if (vis_class) {
     if (wide) ORDER(true, true);

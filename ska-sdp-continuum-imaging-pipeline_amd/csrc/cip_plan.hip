@@ -190,10 +190,15 @@ hipError_t launch_w_range(const double* uvw, int64_t nrow, double fxmin, double 
 // at ~10-25 G/s on MI355X, which made an atomic counting sort of the 13 M
 // runs of C3 cost more than 1 ms).
 constexpr int kPlaceSegs = 64;  // 64-visibility segments per place block (4096 visibilities)
+
+// lane i <- lane i - 1 of the wave (lane 0 <- 0): one DPP move
+__device__ __forceinline__ uint32_t wave_shr1(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138 /* wave_shr:1 */, 0xf, 0xf, false);
+}
 constexpr uint32_t kNoKey = 0xffffffffu;  // visibility off the grid (tile keys are < 2^32 - 1)
 
 #ifndef CIP_PLACE_ABL
-#define CIP_PLACE_ABL 0  // experiment builds only: 1 no visibility load, 2 no run parking, 3 no class store
+#define CIP_PLACE_ABL 0  // experiment builds only: 1 no visibility load, 2 no run parking, 3 no class store, 4 no vis / weight load
 #endif
 #ifndef CIP_PLACE_WAVES
 #define CIP_PLACE_WAVES 1  // min waves per SIMD the place pass is compiled for
@@ -210,7 +215,8 @@ __global__ __launch_bounds__(256, CIP_PLACE_WAVES) void plan_place_kernel(const 
                                                          int64_t* __restrict__ blk_cnt,
                                                          uint32_t* __restrict__ park_key,
                                                          uint64_t* __restrict__ park_run, double* partial,
-                                                         int64_t* __restrict__ hist0) {
+                                                         int64_t* __restrict__ hist0,
+                                                         uint64_t* __restrict__ park_uv = nullptr) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   __shared__ unsigned s_nruns;
   __shared__ unsigned s_hist[256];
@@ -259,9 +265,13 @@ __global__ __launch_bounds__(256, CIP_PLACE_WAVES) void plan_place_kernel(const 
       w = uvw[3 * rl + 2];
       f = fx[cl];
     }
+#if CIP_PLACE_ABL == 4
+    const double wt = 1.0;  // ablation: neither weights nor visibilities read (uvw + fx only)
+#else
     const double wt = load_weight<WK>(wgt, m, il);
+#endif
     double vr, vi;
-#if CIP_PLACE_ABL == 1
+#if CIP_PLACE_ABL == 1 || CIP_PLACE_ABL == 4
     vr = 1.0; vi = 0.0;
 #else
     load_vis(vis, il, vr, vi);
@@ -292,8 +302,10 @@ __global__ __launch_bounds__(256, CIP_PLACE_WAVES) void plan_place_kernel(const 
         vis_class[i] = ok ? (uint8_t)((((unsigned)ix0 % kTile) * P + (unsigned)iy0 % kTile) & 31u) : (uint8_t)0;
 #endif
       if (__ballot(bad) != 0ull && lane == 0) atomicOr(err_flag, 1u);
-      const uint32_t prev = __shfl_up(key, 1, 64);
-      const uint32_t prev_r = __shfl_up((uint32_t)r, 1, 64);  // rows < 2^32
+      // the previous lane's key and row: DPP wave_shr:1 (a VALU move; __shfl_up
+      // is an LDS ds_bpermute with its own latency); lane 0 is a start anyway
+      const uint32_t prev = wave_shr1(key);
+      const uint32_t prev_r = wave_shr1((uint32_t)r);  // rows < 2^32
       const bool start = valid && (lane == 0 || (uint32_t)r != prev_r || key != prev);
       const unsigned long long starts = __ballot(start);
       const bool emit = start && key != kNoKey;
@@ -302,7 +314,7 @@ __global__ __launch_bounds__(256, CIP_PLACE_WAVES) void plan_place_kernel(const 
       // the block's runs are parked densely from slot 64 * kPlaceSegs * b on
       unsigned wbase = 0;
       if (lane == 0 && emits) wbase = atomicAdd(&s_nruns, (unsigned)__popcll(emits));
-      wbase = __shfl(wbase, 0, 64);
+      wbase = (unsigned)__builtin_amdgcn_readlane((int)wbase, 0);  // lane 0's slot base (scalar)
 #if CIP_PLACE_ABL == 2
       if (emit && key == 0x7fffffffu) {
 #else
@@ -314,6 +326,11 @@ __global__ __launch_bounds__(256, CIP_PLACE_WAVES) void plan_place_kernel(const 
         park_key[slot] = key;
         atomicAdd(&s_hist[key & 255u], 1u);
         park_run[slot] = ((uint64_t)r << 32) | ((uint64_t)c << 16) | (uint64_t)(c + (next - lane));
+        // the run's row pre-scaled (u nu dx, v nv dy) in fp32: the order pass
+        // recomputes each visibility's bank class from it and f / c, with no
+        // per-visibility class array and no uvw gather
+        if (park_uv)
+          park_uv[slot] = __builtin_bit_cast(uint64_t, make_float2((float)(u * g.scale_u), (float)(v * g.scale_v)));
       }
     }
   }
@@ -372,11 +389,13 @@ hipError_t launch_prep_reduce(const RowMap& m, const void* vis, int vis_dtype, c
 hipError_t launch_plan_place(const double* uvw, const double* fx, const RowMap& m,
                              const void* vis, int vis_dtype, const void* wgt, int wgt_dtype, const GridGeometry& g,
                              unsigned* err_flag, uint8_t* vis_class, int64_t* blk_cnt, uint32_t* park_key,
-                             uint64_t* park_run, double* partial, int64_t* hist0, hipStream_t s) {
+                             uint64_t* park_run, double* partial, int64_t* hist0, hipStream_t s,
+                             uint64_t* park_uv) {
   const dim3 gd(plan_blocks(m.nvis));
 #define PLACE(VT, WKV)                                                                                           \
   plan_place_kernel<VT, WKV><<<gd, dim3(256), 0, s>>>(uvw, fx, m, (const VT*)vis, wgt, g, err_flag,       \
-                                                      vis_class, blk_cnt, park_key, park_run, partial, hist0)
+                                                      vis_class, blk_cnt, park_key, park_run, partial, hist0, \
+                                                      park_uv)
   if (vis_dtype == CIP_POL4I) {
     PLACE(Pol4, WK_POL4I);
   } else if (vis_dtype == CIP_C64) {
@@ -505,10 +524,12 @@ __global__ void radix_group_hist_kernel(const int64_t* __restrict__ hist0, int64
   hg[t] = sum;
 }
 
+template <bool V2>
 __global__ __launch_bounds__(kRadixThreads) void radix_scatter_kernel(
     const uint32_t* __restrict__ keys, const uint64_t* __restrict__ vals, int64_t n,
     const int64_t* __restrict__ blk_cnt, int64_t nsub, int G, int shift, int64_t ngroups,
-    const int64_t* __restrict__ hist, uint32_t* __restrict__ keys_out, uint64_t* __restrict__ vals_out) {
+    const int64_t* __restrict__ hist, uint32_t* __restrict__ keys_out, uint64_t* __restrict__ vals_out,
+    const uint64_t* __restrict__ vals2 = nullptr, uint64_t* __restrict__ vals2_out = nullptr) {
   __shared__ unsigned wcnt[4][256];  // per-wave running digit counts
   __shared__ int64_t dnext[256];     // the group's next position per digit
   __shared__ int64_t woff[4][256];   // global position of each wave's first item per digit
@@ -531,12 +552,13 @@ __global__ __launch_bounds__(kRadixThreads) void radix_scatter_kernel(
 #pragma unroll
     for (int w = 0; w < 4; ++w) wcnt[w][threadIdx.x] = 0u;
     uint32_t key[kRadixPer];
-    uint64_t val[kRadixPer];
+    uint64_t val[kRadixPer], val2[kRadixPer];
 #pragma unroll
     for (int k = 0; k < kRadixPer; ++k) {
       const int64_t i = i0 + k * 64;
       key[k] = (k < steps && i < lim) ? keys[i] : 0u;
       val[k] = (k < steps && i < lim) ? vals[i] : 0ull;
+      if constexpr (V2) val2[k] = (k < steps && i < lim) ? vals2[i] : 0ull;
     }
     __syncthreads();
     unsigned rank[kRadixPer];
@@ -575,6 +597,7 @@ __global__ __launch_bounds__(kRadixThreads) void radix_scatter_kernel(
         const int64_t pos = woff[wave][(key[k] >> shift) & 255u] + rank[k];
         keys_out[pos] = key[k];
         vals_out[pos] = val[k];
+        if constexpr (V2) vals2_out[pos] = val2[k];
       }
     __syncthreads();  // wcnt / woff are reused by the next sub-block
   }
@@ -614,12 +637,16 @@ hipError_t launch_radix_group_hist(const int64_t* hist0, int64_t nsub, int G, in
 
 hipError_t launch_radix_scatter(const uint32_t* keys, const uint64_t* vals, int64_t n, const int64_t* blk_cnt,
                                 int64_t nsub, int G, int shift, const int64_t* hist, uint32_t* keys_out,
-                                uint64_t* vals_out, hipStream_t s) {
+                                uint64_t* vals_out, hipStream_t s, const uint64_t* vals2, uint64_t* vals2_out) {
   if (nsub == 0) return hipSuccess;
   const int64_t ngroups = (nsub + G - 1) / G;
-  radix_scatter_kernel<<<dim3((unsigned)ngroups), dim3(kRadixThreads), 0, s>>>(keys, vals, n, blk_cnt, nsub, G,
-                                                                              shift, ngroups, hist, keys_out,
-                                                                              vals_out);
+  // vals2 (optional): a second 8-byte value per item moved with it
+  if (vals2)
+    radix_scatter_kernel<true><<<dim3((unsigned)ngroups), dim3(kRadixThreads), 0, s>>>(
+        keys, vals, n, blk_cnt, nsub, G, shift, ngroups, hist, keys_out, vals_out, vals2, vals2_out);
+  else
+    radix_scatter_kernel<false><<<dim3((unsigned)ngroups), dim3(kRadixThreads), 0, s>>>(
+        keys, vals, n, blk_cnt, nsub, G, shift, ngroups, hist, keys_out, vals_out);
   return hipGetLastError();
 }
 

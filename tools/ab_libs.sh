@@ -4,7 +4,8 @@
 set -o pipefail
 mkdir -p gpurun_out; rm -f gpurun_out/ab_libs.txt
 for lib in "$@"; do
-  CIP_HIP_LIB=$lib timeout -k 10 200 python bench.py --no-cpu-baseline --steps ${STEPS:-10} --warmup ${WARMUP:-10} ${BENCH_ARGS} \
+  if [ "$lib" = default ]; then unset CIP_HIP_LIB; else export CIP_HIP_LIB=$lib; fi
+  timeout -k 10 200 python bench.py --no-cpu-baseline --steps ${STEPS:-10} --warmup ${WARMUP:-10} ${BENCH_ARGS} \
       > gpurun_out/ab_one.json 2> gpurun_out/ab_err.log || exit 1
   python -c "import json; d=json.load(open('gpurun_out/ab_one.json')); print('$lib', d['value'], d['phases_ms'])" \
       >> gpurun_out/ab_libs.txt
