@@ -206,17 +206,19 @@ constexpr uint32_t kNoKey = 0xffffffffu;  // visibility off the grid (tile keys 
 // PLACE = false: only the fused reduction (sum of weights, max |w V|,
 // non-finite check), in exactly the place pass's order - a call that reuses
 // its predecessor's plan (CIP_REUSE_PLAN) gets the same sums bit for bit.
-template <typename VisT, int WK, bool PLACE = true>
-__global__ __launch_bounds__(256, CIP_PLACE_WAVES) void plan_place_kernel(const double* __restrict__ uvw,
-                                                         const double* __restrict__ fx, RowMap m,
-                                                         const VisT* __restrict__ vis, const void* __restrict__ wgt,
-                                                         GridGeometry g, unsigned* err_flag,
-                                                         uint8_t* __restrict__ vis_class,
-                                                         int64_t* __restrict__ blk_cnt,
-                                                         uint32_t* __restrict__ park_key,
-                                                         uint64_t* __restrict__ park_run, double* partial,
-                                                         int64_t* __restrict__ hist0,
-                                                         uint64_t* __restrict__ park_uv = nullptr) {
+// LOADVIS = false (PLACE only): the placement without the reduction - no
+// visibility or weight loads, no partials (the split place pass: a separate
+// block of the same launch reduces the same visibilities, see
+// plan_place_split_kernel). blk / nblocks: this place block and their count.
+template <typename VisT, int WK, bool PLACE, bool LOADVIS>
+__device__ __forceinline__ void place_body(const double* __restrict__ uvw, const double* __restrict__ fx,
+                                           const RowMap& m, const VisT* __restrict__ vis,
+                                           const void* __restrict__ wgt, const GridGeometry& g, unsigned* err_flag,
+                                           uint8_t* __restrict__ vis_class, int64_t* __restrict__ blk_cnt,
+                                           uint32_t* __restrict__ park_key, uint64_t* __restrict__ park_run,
+                                           double* partial, int64_t* __restrict__ hist0,
+                                           uint64_t* __restrict__ park_uv, const int64_t blk, const int64_t nblocks) {
+  static_assert(PLACE || LOADVIS, "a place body places or reduces");
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   __shared__ unsigned s_nruns;
   __shared__ unsigned s_hist[256];
@@ -231,14 +233,14 @@ __global__ __launch_bounds__(256, CIP_PLACE_WAVES) void plan_place_kernel(const 
   const int64_t nseg = (nvis + 63) / 64;
   const int P = kTile + g.support - 1;
   // block b owns segments [64 b, 64 b + 64): wave w takes every 4th
-  const int64_t seg_end = ((int64_t)blockIdx.x + 1) * kPlaceSegs < nseg ? ((int64_t)blockIdx.x + 1) * kPlaceSegs : nseg;
+  const int64_t seg_end = (blk + 1) * kPlaceSegs < nseg ? (blk + 1) * kPlaceSegs : nseg;
   // (row, channel) of the lane's visibility, advanced by 256 visibilities per
   // step without a division
   // (ragged rows: looked up per visibility)
   int64_t r0 = 0, c0 = 0;
-  if (!ragged) split_index64(((int64_t)blockIdx.x * kPlaceSegs + wave) * 64 + lane, nchan, m.inv_nchan, &r0, &c0);
+  if (!ragged) split_index64((blk * kPlaceSegs + wave) * 64 + lane, nchan, m.inv_nchan, &r0, &c0);
   const int64_t step_r = 256 / nchan, step_c = 256 % nchan;
-  for (int64_t seg = (int64_t)blockIdx.x * kPlaceSegs + wave; seg < seg_end; seg += 4) {
+  for (int64_t seg = blk * kPlaceSegs + wave; seg < seg_end; seg += 4) {
     const int64_t i = seg * 64 + lane;
     const bool valid = i < nvis;
     int64_t r = r0, c = c0;
@@ -265,23 +267,25 @@ __global__ __launch_bounds__(256, CIP_PLACE_WAVES) void plan_place_kernel(const 
       w = uvw[3 * rl + 2];
       f = fx[cl];
     }
+    if constexpr (LOADVIS) {
 #if CIP_PLACE_ABL == 4
-    const double wt = 1.0;  // ablation: neither weights nor visibilities read (uvw + fx only)
+      const double wt = 1.0;  // ablation: neither weights nor visibilities read (uvw + fx only)
 #else
-    const double wt = load_weight<WK>(wgt, m, il);
+      const double wt = load_weight<WK>(wgt, m, il);
 #endif
-    double vr, vi;
+      double vr, vi;
 #if CIP_PLACE_ABL == 1 || CIP_PLACE_ABL == 4
-    vr = 1.0; vi = 0.0;
+      vr = 1.0; vi = 0.0;
 #else
-    load_vis(vis, il, vr, vi);
+      load_vis(vis, il, vr, vi);
 #endif
-    // zero-weight visibilities are skipped by the scatter, whatever they hold
-    const bool counted = valid & (wt != 0.0);
-    const double a = counted ? fabs(wt) * fmax(fabs(vr), fabs(vi)) : 0.0;
-    nonfinite = nonfinite | (counted && !(isfinite(wt) && isfinite(vr) && isfinite(vi)));
-    wsum = valid ? wsum + wt : wsum;
-    wvmax = fmax(wvmax, a);
+      // zero-weight visibilities are skipped by the scatter, whatever they hold
+      const bool counted = valid & (wt != 0.0);
+      const double a = counted ? fabs(wt) * fmax(fabs(vr), fabs(vi)) : 0.0;
+      nonfinite = nonfinite | (counted && !(isfinite(wt) && isfinite(vr) && isfinite(vi)));
+      wsum = valid ? wsum + wt : wsum;
+      wvmax = fmax(wvmax, a);
+    }
     if constexpr (PLACE) {
       int ix0, iy0;
       int64_t iw0;
@@ -322,7 +326,7 @@ __global__ __launch_bounds__(256, CIP_PLACE_WAVES) void plan_place_kernel(const 
 #endif
         const unsigned long long above = starts & ~((2ull << lane) - 1ull);  // lane 63: 2 << 63 == 0
         const int next = above ? (__ffsll((long long)above) - 1) : nvalid;
-        const int64_t slot = (int64_t)blockIdx.x * kPlaceSegs * 64 + wbase + __popcll(emits & ((1ull << lane) - 1ull));
+        const int64_t slot = blk * kPlaceSegs * 64 + wbase + __popcll(emits & ((1ull << lane) - 1ull));
         park_key[slot] = key;
         atomicAdd(&s_hist[key & 255u], 1u);
         park_run[slot] = ((uint64_t)r << 32) | ((uint64_t)c << 16) | (uint64_t)(c + (next - lane));
@@ -334,27 +338,69 @@ __global__ __launch_bounds__(256, CIP_PLACE_WAVES) void plan_place_kernel(const 
       }
     }
   }
-  if (nonfinite) atomicOr(err_flag, 2u);
-  for (int d = 32; d > 0; d >>= 1) {
-    wsum += __shfl_xor(wsum, d, 64);
-    wvmax = fmax(wvmax, __shfl_xor(wvmax, d, 64));
-  }
   __shared__ double ss[4], sm[4];
-  if (lane == 0) {
-    ss[threadIdx.x >> 6] = wsum;
-    sm[threadIdx.x >> 6] = wvmax;
+  if constexpr (LOADVIS) {
+    if (nonfinite) atomicOr(err_flag, 2u);
+    for (int d = 32; d > 0; d >>= 1) {
+      wsum += __shfl_xor(wsum, d, 64);
+      wvmax = fmax(wvmax, __shfl_xor(wvmax, d, 64));
+    }
+    if (lane == 0) {
+      ss[threadIdx.x >> 6] = wsum;
+      sm[threadIdx.x >> 6] = wvmax;
+    }
   }
   __syncthreads();
-  if constexpr (PLACE) hist0[(int64_t)threadIdx.x * gridDim.x + blockIdx.x] = s_hist[threadIdx.x];
+  if constexpr (PLACE) hist0[(int64_t)threadIdx.x * nblocks + blk] = s_hist[threadIdx.x];
   if (threadIdx.x == 0) {
-    partial[2 * blockIdx.x] = (ss[0] + ss[1]) + (ss[2] + ss[3]);
-    partial[2 * blockIdx.x + 1] = fmax(fmax(sm[0], sm[1]), fmax(sm[2], sm[3]));
+    if constexpr (LOADVIS) {
+      partial[2 * blk] = (ss[0] + ss[1]) + (ss[2] + ss[3]);
+      partial[2 * blk + 1] = fmax(fmax(sm[0], sm[1]), fmax(sm[2], sm[3]));
+    }
     if constexpr (PLACE) {
-      blk_cnt[blockIdx.x] = s_nruns;
-      if (blockIdx.x == 0) hist0[256 * (int64_t)gridDim.x] = 0;
+      blk_cnt[blk] = s_nruns;
+      if (blk == 0) hist0[256 * nblocks] = 0;
     }
   }
 }
+
+// The place pass (reduction fused, the place block = this workgroup); PLACE =
+// false: the reduction alone (CIP_REUSE_PLAN calls).
+template <typename VisT, int WK, bool PLACE = true>
+__global__ __launch_bounds__(256, CIP_PLACE_WAVES) void plan_place_kernel(const double* __restrict__ uvw,
+                                                         const double* __restrict__ fx, RowMap m,
+                                                         const VisT* __restrict__ vis, const void* __restrict__ wgt,
+                                                         GridGeometry g, unsigned* err_flag,
+                                                         uint8_t* __restrict__ vis_class,
+                                                         int64_t* __restrict__ blk_cnt,
+                                                         uint32_t* __restrict__ park_key,
+                                                         uint64_t* __restrict__ park_run, double* partial,
+                                                         int64_t* __restrict__ hist0,
+                                                         uint64_t* __restrict__ park_uv = nullptr) {
+  place_body<VisT, WK, PLACE, true>(uvw, fx, m, vis, wgt, g, err_flag, vis_class, blk_cnt, park_key, park_run,
+                                    partial, hist0, park_uv, blockIdx.x, gridDim.x);
+}
+
+// The split place pass (CIP_PLACE_SPLIT=1): workgroup 2 b places place block
+// b (uvw + f / c only), workgroup 2 b + 1 reduces its visibilities' weights
+// and values in the fused pass's order (the same partials bit for bit): the
+// streaming read and the VALU-heavy placement run in different waves side by
+// side on the CUs instead of one memory round trip per placed segment.
+template <typename VisT, int WK>
+__global__ __launch_bounds__(256, CIP_PLACE_WAVES) void plan_place_split_kernel(
+    const double* __restrict__ uvw, const double* __restrict__ fx, RowMap m, const VisT* __restrict__ vis,
+    const void* __restrict__ wgt, GridGeometry g, unsigned* err_flag, uint8_t* __restrict__ vis_class,
+    int64_t* __restrict__ blk_cnt, uint32_t* __restrict__ park_key, uint64_t* __restrict__ park_run,
+    double* partial, int64_t* __restrict__ hist0, uint64_t* __restrict__ park_uv) {
+  const int64_t nb = gridDim.x / 2;
+  if (blockIdx.x & 1)
+    place_body<VisT, WK, false, true>(uvw, fx, m, vis, wgt, g, err_flag, vis_class, blk_cnt, park_key, park_run,
+                                      partial, hist0, park_uv, blockIdx.x >> 1, nb);
+  else
+    place_body<VisT, WK, true, false>(uvw, fx, m, vis, wgt, g, err_flag, vis_class, blk_cnt, park_key, park_run,
+                                      partial, hist0, park_uv, blockIdx.x >> 1, nb);
+}
+
 
 static unsigned plan_blocks(int64_t nvis) {
   const int64_t segs = (nvis + 63) / 64;
@@ -363,6 +409,17 @@ static unsigned plan_blocks(int64_t nvis) {
 }
 
 int plan_place_blocks(int64_t nvis) { return (int)plan_blocks(nvis); }
+
+// CIP_PLACE_SPLIT=1: the placement and the weight / visibility reduction in
+// separate workgroups of one launch (plan_place_split_kernel); 0 (default):
+// one fused pass
+static bool place_split() {
+  static const bool on = [] {
+    const char* e = getenv("CIP_PLACE_SPLIT");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
 
 hipError_t launch_prep_reduce(const RowMap& m, const void* vis, int vis_dtype, const void* wgt, int wgt_dtype,
                               const GridGeometry& g, unsigned* err_flag, double* partial, hipStream_t s) {
@@ -392,10 +449,16 @@ hipError_t launch_plan_place(const double* uvw, const double* fx, const RowMap& 
                              uint64_t* park_run, double* partial, int64_t* hist0, hipStream_t s,
                              uint64_t* park_uv) {
   const dim3 gd(plan_blocks(m.nvis));
+  const dim3 gd2(2 * plan_blocks(m.nvis));
 #define PLACE(VT, WKV)                                                                                           \
-  plan_place_kernel<VT, WKV><<<gd, dim3(256), 0, s>>>(uvw, fx, m, (const VT*)vis, wgt, g, err_flag,       \
-                                                      vis_class, blk_cnt, park_key, park_run, partial, hist0, \
-                                                      park_uv)
+  if (place_split())                                                                                             \
+    plan_place_split_kernel<VT, WKV><<<gd2, dim3(256), 0, s>>>(uvw, fx, m, (const VT*)vis, wgt, g, err_flag,   \
+                                                               vis_class, blk_cnt, park_key, park_run, partial, \
+                                                               hist0, park_uv);                                  \
+  else                                                                                                           \
+    plan_place_kernel<VT, WKV><<<gd, dim3(256), 0, s>>>(uvw, fx, m, (const VT*)vis, wgt, g, err_flag,       \
+                                                        vis_class, blk_cnt, park_key, park_run, partial, hist0, \
+                                                        park_uv)
   if (vis_dtype == CIP_POL4I) {
     PLACE(Pol4, WK_POL4I);
   } else if (vis_dtype == CIP_C64) {
