@@ -266,6 +266,7 @@ static GridGeometry geometry(const cip_gridder_params& p, double px, double py) 
   g.oob = nullptr;
   g.plane_lo = 0;
   g.plane_hi = p.nplanes;
+  g.grid_f32 = 0;
   return g;
 }
 
@@ -566,19 +567,20 @@ static bool overlap_zero() {
   return on;
 }
 
-// How the order pass gets each visibility's bank class (round 4 default
-// "runs": recomputed in fp32 from its run's row (u, v), carried through the
-// radix sort beside the run record, and f / c - no per-visibility class bytes
-// written by the place pass and gathered in tile order (~1 HBM line per row
-// slice, 1.24 GB at C3)); CIP_ORDER_CLASS=gather (round 3: the class bytes) or
-// =compute (recomputed from a uvw gather per slice) for A/B experiments.
+// How the order pass gets each visibility's bank class: default "gather" -
+// the place pass's per-visibility class bytes, gathered in tile order (~1 HBM
+// line per row slice, 1.24 GB at C3); CIP_ORDER_CLASS=runs recomputes them in
+// fp32 from the run's row (u, v), carried through the radix sort beside the
+// run record, and f / c (no class bytes, no gather - but 8 more bytes per run
+// in both radix passes: planner 1.82 vs 1.47 ms at C3, interleaved A/B,
+// profiles/r04_ab_order_place.txt); =compute recomputes from a uvw gather.
 enum { ORDER_RUNS = 0, ORDER_GATHER = 1, ORDER_UVW = 2 };
 static int order_class_mode() {
   static const int mode = [] {
     const char* e = getenv("CIP_ORDER_CLASS");
-    if (e && std::strcmp(e, "gather") == 0) return (int)ORDER_GATHER;
+    if (e && std::strcmp(e, "runs") == 0) return (int)ORDER_RUNS;
     if (e && std::strcmp(e, "compute") == 0) return (int)ORDER_UVW;
-    return (int)ORDER_RUNS;
+    return (int)ORDER_GATHER;
   }();
   return mode;
 }
@@ -1086,7 +1088,8 @@ static int scatter_plane(const Prepared& pp, int64_t q, const double* uvw, const
   const int G = pp.plan.group;
   const int64_t p0 = g.do_wstacking ? q * G : 0;
   const int64_t np = g.do_wstacking ? std::min<int64_t>(G, g.nplanes - p0) : 1;
-  if (!zeroed) CIP_HIP_CHECK(hipMemsetAsync(grid, 0, sizeof(double) * 2 * g.nu * g.nv * np, s));
+  if (!zeroed)
+    CIP_HIP_CHECK(hipMemsetAsync(grid, 0, (g.grid_f32 ? sizeof(float) : sizeof(double)) * 2 * g.nu * g.nv * np, s));
   if (pp.plan.nchunks == 0) return CIP_OK;
   const int64_t k = g.do_wstacking ? q : 0;
   const int64_t cb = pp.plan.plane_chunk_off[k], ce = pp.plan.plane_chunk_off[k + 1];
@@ -1145,6 +1148,15 @@ static int correction_vectors(Workspace* ws, const GridGeometry& g, int64_t npix
   return CIP_OK;
 }
 
+// CIP_GRID_F32=0: the packed class keeps complex128 grid planes (A/B)
+static bool grid_f32_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("CIP_GRID_F32");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 // CIP_SCATTER_SHARE=0: pipelined calls' scatters take every CU slot (A/B)
 static bool share_cus_enabled() {
   static const bool on = [] {
@@ -1201,7 +1213,8 @@ static int plane_to_dirty(const DirtyStage& st, const GridGeometry& g, int64_t p
   hipEvent_t f0 = g_prof.mark(s);
   if (st.fast) {
     if (!fft_rowskip()) rowbits = nullptr;
-    CIP_HIP_CHECK(launch_fft_rows(grid, g.nu, g.nv, st.npix_x, st.tw_u, st.fft_h, dmask, g.ntx, rowbits != nullptr, s));
+    CIP_HIP_CHECK(launch_fft_rows(grid, g.nu, g.nv, st.npix_x, st.tw_u, st.fft_h, dmask, g.ntx, rowbits != nullptr, s,
+                                  g.grid_f32 != 0));
   } else if (hipfftExecZ2Z(st.plan, (hipfftDoubleComplex*)grid, (hipfftDoubleComplex*)grid, HIPFFT_BACKWARD) !=
              HIPFFT_SUCCESS) {
     return set_error(CIP_EHIP, "hipfftExecZ2Z failed");
@@ -1424,19 +1437,23 @@ static int ms2dirty_impl(const double* uvw, int64_t nrow, const double* freq, in
   }
   if (rc != CIP_OK) return rc;
   if (params_out) *params_out = pp.p;
+  DirtyStage st;
+  rc = dirty_stage(ws, pp.g, npix_x, npix_y, pixsize_x, pixsize_y, s, &st);
+  if (rc != CIP_OK) return rc;
+  // the packed class grids into complex64 planes on the pruned-FFT path (half
+  // the flush and pass-A bytes); CIP_GRID_F32=0 keeps complex128 (A/B)
+  pp.g.grid_f32 = (packed && st.fast && grid_f32_enabled()) ? 1 : 0;
   const GridGeometry& g = pp.g;
   // zeroed beside the planner, or left all-zero by the previous call
   bool clean = grid != nullptr;
   const int G = pp.plan.group;
   const int64_t plane_elems = 2 * g.nu * g.nv;
+  const size_t cell_bytes = g.grid_f32 ? sizeof(float) : sizeof(double);  // per real component
   if (!grid) grid = buf<double>(ws, "grid", plane_elems * G);
   if (!grid) return CIP_ENOMEM;
-  const size_t group_bytes = sizeof(double) * (size_t)plane_elems * (size_t)G;
+  const size_t group_bytes = cell_bytes * (size_t)plane_elems * (size_t)G;
   const size_t prev_clean = ws->grid_clean == grid ? ws->grid_clean_bytes : 0;
   clean = clean || prev_clean >= group_bytes;
-  DirtyStage st;
-  rc = dirty_stage(ws, g, npix_x, npix_y, pixsize_x, pixsize_y, s, &st);
-  if (rc != CIP_OK) return rc;
   ws->grid_clean = nullptr;  // dirty until a masked pass A has consumed every written tile
   const uint32_t* dmask = st.fast ? pp.plan.dmask : nullptr;
   // the plane groups holding planes [plane_lo, plane_hi) (the whole stack
@@ -1449,7 +1466,8 @@ static int ms2dirty_impl(const double* uvw, int64_t nrow, const double* freq, in
                        pipelined && share_cus_enabled());
     if (rc != CIP_OK) return rc;
     for (int64_t p = std::max(q * G, p_lo); p < std::min<int64_t>(q * G + G, p_hi); ++p) {
-      rc = plane_to_dirty(st, g, p, grid + (p - q * G) * plane_elems, dirty_out, s,
+      double* plane_p = (double*)((char*)grid + (size_t)(p - q * G) * (size_t)plane_elems * cell_bytes);
+      rc = plane_to_dirty(st, g, p, plane_p, dirty_out, s,
                           dmask ? dmask + p * (g.ntx * g.nty / 32) : nullptr, normalise ? pp.red : nullptr,
                           dmask ? dmask + g.nplanes * (g.ntx * g.nty / 32) + p * ((g.nty + 31) / 32) : nullptr,
                           p == p_lo);

@@ -185,6 +185,10 @@ struct GridGeometry {
   // cip_ms2dirty_wplanes): [plane_lo, plane_hi); the whole stack by default.
   // The planner drops visibilities feeding no plane of the range.
   int64_t plane_lo, plane_hi;
+  // HBM grid planes of complex64 (float re, im) instead of complex128: the
+  // packed single class's own planes on the pruned-FFT path (cip_ms2dirty),
+  // half the flush and pass-A bytes (ducc0's float class grids in float32)
+  int grid_f32;
 };
 
 // Buffer offset (complex cells) of grid cell (gx, gy) in wrapped coordinates,

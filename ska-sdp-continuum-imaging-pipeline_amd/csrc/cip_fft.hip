@@ -193,8 +193,13 @@ __device__ __forceinline__ void fft_core(double2* v, int t, double* lds, const d
 // y0 + blockIdx.x (a strip of the grid) go to H rows y - hy0 of
 // an H with hrows rows per block (the whole grid: y0 = hy0 = 0, hrows = nv);
 // ZERO (unmasked strips) zeroes every cell read.
-template <int N, bool MASKED, bool ZERO = false>
-__global__ __launch_bounds__(N / 16) void fft_rows_kernel(double2* __restrict__ gT, int64_t hrows, int64_t nx,
+// grid cells as stored (GT = double2, or float2 for the packed class's
+// complex64 planes), widened to fp64 for the transform
+__device__ __forceinline__ double2 widen(double2 v) { return v; }
+__device__ __forceinline__ double2 widen(float2 v) { return make_double2((double)v.x, (double)v.y); }
+
+template <int N, bool MASKED, bool ZERO = false, typename GT = double2>
+__global__ __launch_bounds__(N / 16) void fft_rows_kernel(GT* __restrict__ gT, int64_t hrows, int64_t nx,
                                                           const double2* __restrict__ tw, double2* __restrict__ H,
                                                           const uint32_t* __restrict__ dmask, int64_t ntx,
                                                           int64_t y0 = 0, int64_t hy0 = 0, bool skip_clean = false) {
@@ -202,7 +207,7 @@ __global__ __launch_bounds__(N / 16) void fft_rows_kernel(double2* __restrict__ 
   __shared__ double lds[N + N / 16];
   const int t = threadIdx.x;
   const int64_t y = y0 + blockIdx.x;
-  double2* row = gT + y * N;
+  GT* row = gT + y * N;
   double2 v[16];
   if constexpr (MASKED) {
     // the 32-tile word of element r is uniform over the block (T = N / 16
@@ -226,16 +231,16 @@ __global__ __launch_bounds__(N / 16) void fft_rows_kernel(double2* __restrict__ 
       const uint32_t word = words[r];
       v[r] = make_double2(0.0, 0.0);
       if ((word >> ((x >> 5) & 31)) & 1u) {
-        v[r] = row[x];
-        row[x] = make_double2(0.0, 0.0);
+        v[r] = widen(row[x]);
+        row[x] = GT{0, 0};
       }
     }
   } else {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) v[r] = row[t + r * S::T];
+    for (int r = 0; r < 16; ++r) v[r] = widen(row[t + r * S::T]);
     if constexpr (ZERO) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) row[t + r * S::T] = make_double2(0.0, 0.0);
+      for (int r = 0; r < 16; ++r) row[t + r * S::T] = GT{0, 0};
     }
   }
   fft_core<N>(v, t, lds, tw);
@@ -340,19 +345,26 @@ bool fast_fft_supported(int64_t nu, int64_t nv, int64_t nx, int64_t ny) {
 }
 
 hipError_t launch_fft_rows(double* gT, int64_t nu, int64_t nv, int64_t nx, const double* tw_u, double* H,
-                           const uint32_t* dmask, int64_t ntx, bool skip_clean, hipStream_t s) {
+                           const uint32_t* dmask, int64_t ntx, bool skip_clean, hipStream_t s, bool grid_f32) {
   if (!fft_len_ok(nu) || !fft_len_ok(nv) || nx > nu) return hipErrorInvalidValue;
   if (dmask && (nu % kTile != 0 || nv % kTile != 0 || ntx * kTile != nu || ntx % 32 != 0))
     return hipErrorInvalidValue;
   const dim3 gd((unsigned)nv);
   double2* g = (double2*)gT;
+  float2* gf = (float2*)gT;
   const double2* tw = (const double2*)tw_u;
   double2* h = (double2*)H;
-#define ROWS(NN)                                                                                         \
-  case NN:                                                                                               \
-    if (dmask) fft_rows_kernel<NN, true><<<gd, dim3(NN / 16), 0, s>>>(g, nv, nx, tw, h, dmask, ntx, 0, 0,  \
-                                                                      skip_clean);                      \
-    else fft_rows_kernel<NN, false><<<gd, dim3(NN / 16), 0, s>>>(g, nv, nx, tw, h, nullptr, 0);         \
+#define ROWS(NN)                                                                                              \
+  case NN:                                                                                                    \
+    if (grid_f32 && dmask)                                                                                    \
+      fft_rows_kernel<NN, true, false, float2><<<gd, dim3(NN / 16), 0, s>>>(gf, nv, nx, tw, h, dmask, ntx, 0, \
+                                                                            0, skip_clean);                   \
+    else if (grid_f32)                                                                                        \
+      fft_rows_kernel<NN, false, false, float2><<<gd, dim3(NN / 16), 0, s>>>(gf, nv, nx, tw, h, nullptr, 0);  \
+    else if (dmask)                                                                                           \
+      fft_rows_kernel<NN, true><<<gd, dim3(NN / 16), 0, s>>>(g, nv, nx, tw, h, dmask, ntx, 0, 0, skip_clean); \
+    else                                                                                                      \
+      fft_rows_kernel<NN, false><<<gd, dim3(NN / 16), 0, s>>>(g, nv, nx, tw, h, nullptr, 0);                  \
     break;
   switch (nu) {
     ROWS(1024)

@@ -461,6 +461,9 @@ __global__ __launch_bounds__(scatter_threads<G>(), CIP_SCATTER_WAVES) void scatt
     if (G > 1 && (plane + k < g.plane_lo || plane + k >= g.plane_hi)) continue;
     const unsigned long long* sk = sub + k * S;
     double* gk = grid + (int64_t)k * 2 * g.nu * g.nv;
+    // packed class on complex64 planes (GridGeometry::grid_f32)
+    float* gkf = (float*)grid + (int64_t)k * 2 * g.nu * g.nv;
+    const bool f32 = PACK && g.grid_f32 != 0;
     for (int cell = threadIdx.x; cell < P * P; cell += NT) {
       const int lcell = g.transposed ? (cell % P) * P + cell / P : cell;  // lx * P + ly
       long long re, im;
@@ -486,9 +489,21 @@ __global__ __launch_bounds__(scatter_threads<G>(), CIP_SCATTER_WAVES) void scatt
           if (g.oob) atomicOr(g.oob, 1u);
           continue;
         }
-        double* dst = gk + 2 * off;
         const int lx = lcell / P, ly = lcell % P;
-        if (own && lx >= W - 1 && lx < T && ly >= W - 1 && ly < T) {
+        const bool priv = own && lx >= W - 1 && lx < T && ly >= W - 1 && ly < T;
+        if (f32) {
+          float* dstf = gkf + 2 * off;
+          if (priv) {
+            *reinterpret_cast<float2*>(dstf) = make_float2((float)((double)re * inv_scale),
+                                                           (float)((double)im * inv_scale));
+          } else {
+            unsafeAtomicAdd(dstf, (float)((double)re * inv_scale));
+            unsafeAtomicAdd(dstf + 1, (float)((double)im * inv_scale));
+          }
+          continue;
+        }
+        double* dst = gk + 2 * off;
+        if (priv) {
           *reinterpret_cast<double2*>(dst) = make_double2((double)re * inv_scale, (double)im * inv_scale);
         } else {
           unsafeAtomicAdd(dst, (double)re * inv_scale);

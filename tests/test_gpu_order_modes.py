@@ -1,9 +1,8 @@
 """
-The bank-class order's three class sources give the same images: the round-4
-default recomputes each visibility's class in fp32 from its run's (u, v)
-carried through the radix sort (CIP_ORDER_CLASS unset), round 3 gathered the
-place pass's per-visibility class bytes (=gather), and =compute recomputes
-from a uvw gather per slice. The class only decides the order of a window's
+The bank-class order's three class sources give the same images: the default
+gathers the place pass's per-visibility class bytes, CIP_ORDER_CLASS=runs
+recomputes each class in fp32 from its run's (u, v) carried through the radix
+sort, and =compute recomputes from a uvw gather per slice. The class only decides the order of a window's
 visibilities (which LDS banks a wave's atomics hit); the fixed-point sums are
 exact and order-independent, so the images agree to the fp64 flush order
 (~1e-16 relative). The split place pass (CIP_PLACE_SPLIT=1: placement and the
@@ -64,7 +63,7 @@ def _run(tmp_path, **switches):
 
 def test_class_sources_give_the_same_images(gpu_device, tmp_path):
     base = _run(tmp_path)
-    for sw in (dict(CIP_ORDER_CLASS="gather"), dict(CIP_ORDER_CLASS="compute"), dict(CIP_PLACE_SPLIT="1")):
+    for sw in (dict(CIP_ORDER_CLASS="runs"), dict(CIP_ORDER_CLASS="compute"), dict(CIP_PLACE_SPLIT="1")):
         other = _run(tmp_path, **sw)
         for k in base.files:
             peak = float(np.abs(base[k]).max())
