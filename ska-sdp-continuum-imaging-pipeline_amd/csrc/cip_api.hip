@@ -836,6 +836,9 @@ static int wstack_group(const GridGeometry& g, bool packed) {
   return G;
 }
 
+static bool grid_is_transposed(const GridGeometry& g, int64_t npix_x, int64_t npix_y);
+static bool grid_f32_enabled();
+
 struct Prepared {
   cip_gridder_params p;
   GridGeometry g;
@@ -992,8 +995,11 @@ static int prepare(Workspace* ws, const double* uvw, int64_t nrow, const double*
   out->red = red;
   if (grid_out) {
     // the grid is known now: zero its first plane group beside the planner
+    // (complex64 cells for the packed class on the pruned-FFT path, as
+    // ms2dirty_impl lays them out)
     const int64_t gplanes = want_group ? wstack_group(out->g, packed) : 1;
-    const size_t gbytes = sizeof(double) * 2 * out->g.nu * out->g.nv * gplanes;
+    const bool f32 = packed && grid_is_transposed(out->g, npix_x, npix_y) && grid_f32_enabled();
+    const size_t gbytes = (f32 ? sizeof(float) : sizeof(double)) * 2 * out->g.nu * out->g.nv * gplanes;
     double* grid = buf<double>(ws, "grid", 2 * out->g.nu * out->g.nv * gplanes);
     if (!grid) return CIP_ENOMEM;
     if (ws->grid_clean != grid || ws->grid_clean_bytes < gbytes) {

@@ -225,15 +225,26 @@ __global__ __launch_bounds__(N / 16) void fft_rows_kernel(GT* __restrict__ gT, i
     // a clean tile row (every word of it is read above): nothing to transform
     // or zero, and pass B reads its H rows as zero (row_bits_kernel)
     if (skip_clean && any == 0u) return;
+    // cells as stored first, widened after every load is issued: a widen
+    // inside the branch makes each branch wait for its own load (16
+    // serialised loads for float2 cells, measured 381 vs 336 us a plane)
+    GT raw[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int x = t + r * S::T;
       const uint32_t word = words[r];
-      v[r] = make_double2(0.0, 0.0);
+      raw[r] = GT{0, 0};
       if ((word >> ((x >> 5) & 31)) & 1u) {
-        v[r] = widen(row[x]);
+        raw[r] = row[x];
         row[x] = GT{0, 0};
       }
+    }
+    // (the empty asm pins the raw values past the branches: without it the
+    // compiler sinks each widen back into its branch)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      if constexpr (sizeof(GT) == 8) asm volatile("" : "+v"(raw[r].x), "+v"(raw[r].y));
+      v[r] = widen(raw[r]);
     }
   } else {
 #pragma unroll

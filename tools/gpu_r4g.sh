@@ -1,0 +1,5 @@
+export TMPDIR=/tmp; mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu tests/test_gpu_wstack_groups.py > gpurun_out/t7.log 2>&1; echo "tests rc $?" >> gpurun_out/t7.log
+STEPS=3 BENCH_ARGS="--sync --wstacking --single --support 6" bash tools/ab_env_kstats.sh CIP_GRID_F32 - 0; echo "ks rc $?"
+OUT=ab_f32c REPS=2 BENCH_ARGS="--sync" bash tools/ab_variants.sh default env:CIP_GRID_F32=0; echo "ab rc $?"
+OUT=ab_f32c_single REPS=2 BENCH_ARGS="--single --no-secondary" bash tools/ab_variants.sh default env:CIP_GRID_F32=0; echo "ab2 rc $?"
