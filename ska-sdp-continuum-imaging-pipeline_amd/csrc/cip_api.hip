@@ -1230,7 +1230,7 @@ static int plane_to_dirty(const DirtyStage& st, const GridGeometry& g, int64_t p
   if (st.fast)
     CIP_HIP_CHECK(launch_fft_cols(st.fft_h, g.nv, st.npix_x, st.npix_y, st.tw_v, g.do_wstacking ? 1 : 0, dirty_out,
                                   st.cx, st.cy, st.px, st.py, w_plane, first, g.do_wstacking ? nullptr : norm,
-                                  dmask ? rowbits : nullptr, s));
+                                  dmask ? rowbits : nullptr, s, g.grid_f32 != 0));
   hipEvent_t f1 = g_prof.mark(s);
   g_prof.span(3, f0, f1);
   if (st.fast) {

@@ -197,10 +197,17 @@ __device__ __forceinline__ void fft_core(double2* v, int t, double* lds, const d
 // complex64 planes), widened to fp64 for the transform
 __device__ __forceinline__ double2 widen(double2 v) { return v; }
 __device__ __forceinline__ double2 widen(float2 v) { return make_double2((double)v.x, (double)v.y); }
+// pass A's output as stored (HT = double2, or float2 beside complex64 planes:
+// the packed class's precision, half the pass-A write and pass-B read bytes)
+template <typename HT>
+__device__ __forceinline__ HT narrow(double2 v) {
+  if constexpr (sizeof(HT) == 8) return HT{(float)v.x, (float)v.y};
+  else return v;
+}
 
-template <int N, bool MASKED, bool ZERO = false, typename GT = double2>
+template <int N, bool MASKED, bool ZERO = false, typename GT = double2, typename HT = double2>
 __global__ __launch_bounds__(N / 16) void fft_rows_kernel(GT* __restrict__ gT, int64_t hrows, int64_t nx,
-                                                          const double2* __restrict__ tw, double2* __restrict__ H,
+                                                          const double2* __restrict__ tw, HT* __restrict__ H,
                                                           const uint32_t* __restrict__ dmask, int64_t ntx,
                                                           int64_t y0 = 0, int64_t hy0 = 0, bool skip_clean = false) {
   using S = FftShape<N>;
@@ -261,7 +268,7 @@ __global__ __launch_bounds__(N / 16) void fft_rows_kernel(GT* __restrict__ gT, i
     for (int r = 0; r < S::RF; ++r) {
       const int k = out_pos<N, S::RF>(t, m, r, N / S::RF);
       const int64_t i = (int64_t)((k + (int)(nx / 2)) & (N - 1));
-      if (i < nx) H[((i / kColBlock) * hrows + (y - hy0)) * kColBlock + (i % kColBlock)] = v[m * S::RF + r];
+      if (i < nx) H[((i / kColBlock) * hrows + (y - hy0)) * kColBlock + (i % kColBlock)] = narrow<HT>(v[m * S::RF + r]);
     }
 }
 
@@ -287,8 +294,8 @@ struct ColEpilogue {
 // rowbits (may be NULL: every H row is read): bit ty of the plane's tile-row
 // words - H rows y of clean tile rows (y / kTile) were not written by pass A
 // and are zero.
-template <int N, int MODE>
-__global__ __launch_bounds__(N / 16) void fft_cols_kernel(const double2* __restrict__ H, int64_t nx, int64_t ny,
+template <int N, int MODE, typename HT = double2>
+__global__ __launch_bounds__(N / 16) void fft_cols_kernel(const HT* __restrict__ H, int64_t nx, int64_t ny,
                                                           const double2* __restrict__ tw, ColEpilogue ep,
                                                           int64_t i0 = 0, const uint32_t* __restrict__ rowbits = nullptr) {
   using S = FftShape<N>;
@@ -301,8 +308,9 @@ __global__ __launch_bounds__(N / 16) void fft_cols_kernel(const double2* __restr
   if (nrows % (8 * kColBlock) == 0)
     il = (b / (8 * kColBlock)) * (8 * kColBlock) + (b % 8) * kColBlock + (b / 8) % kColBlock;
   const int64_t i = i0 + il;
-  const double2* col = H + ((il / kColBlock) * N) * kColBlock + (il % kColBlock);
+  const HT* col = H + ((il / kColBlock) * N) * kColBlock + (il % kColBlock);
   double2 v[16];
+  HT raw[16];
   if (rowbits) {
     // the row-bit word of element r (rows t + r T, tile rows (t + r T) / 32)
     // is uniform over the block, as in pass A: scalar loads, one bit per lane
@@ -311,12 +319,18 @@ __global__ __launch_bounds__(N / 16) void fft_cols_kernel(const double2* __restr
     for (int r = 0; r < 16; ++r) {
       const int y = t + r * S::T;
       const uint32_t word = rowbits[(r * S::T) >> 10];
-      v[r] = make_double2(0.0, 0.0);
-      if ((word >> ((y >> 5) & 31)) & 1u) v[r] = col[(int64_t)y * kColBlock];
+      raw[r] = HT{0, 0};
+      if ((word >> ((y >> 5) & 31)) & 1u) raw[r] = col[(int64_t)y * kColBlock];
     }
   } else {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) v[r] = col[(int64_t)(t + r * S::T) * kColBlock];
+    for (int r = 0; r < 16; ++r) raw[r] = col[(int64_t)(t + r * S::T) * kColBlock];
+  }
+  // widened after every load is issued (as in pass A)
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    if constexpr (sizeof(HT) == 8) asm volatile("" : "+v"(raw[r].x), "+v"(raw[r].y));
+    v[r] = widen(raw[r]);
   }
   fft_core<N>(v, t, lds, tw);
   const int64_t p = i - nx / 2;
@@ -365,13 +379,15 @@ hipError_t launch_fft_rows(double* gT, int64_t nu, int64_t nv, int64_t nx, const
   float2* gf = (float2*)gT;
   const double2* tw = (const double2*)tw_u;
   double2* h = (double2*)H;
+  float2* hf = (float2*)H;  // complex64 planes: complex64 pass-A output
 #define ROWS(NN)                                                                                              \
   case NN:                                                                                                    \
     if (grid_f32 && dmask)                                                                                    \
-      fft_rows_kernel<NN, true, false, float2><<<gd, dim3(NN / 16), 0, s>>>(gf, nv, nx, tw, h, dmask, ntx, 0, \
-                                                                            0, skip_clean);                   \
+      fft_rows_kernel<NN, true, false, float2, float2><<<gd, dim3(NN / 16), 0, s>>>(gf, nv, nx, tw, hf, dmask, \
+                                                                                    ntx, 0, 0, skip_clean);   \
     else if (grid_f32)                                                                                        \
-      fft_rows_kernel<NN, false, false, float2><<<gd, dim3(NN / 16), 0, s>>>(gf, nv, nx, tw, h, nullptr, 0);  \
+      fft_rows_kernel<NN, false, false, float2, float2><<<gd, dim3(NN / 16), 0, s>>>(gf, nv, nx, tw, hf,      \
+                                                                                     nullptr, 0);             \
     else if (dmask)                                                                                           \
       fft_rows_kernel<NN, true><<<gd, dim3(NN / 16), 0, s>>>(g, nv, nx, tw, h, dmask, ntx, 0, 0, skip_clean); \
     else                                                                                                      \
@@ -440,15 +456,18 @@ hipError_t launch_fft_cols_strip(const double* H, int64_t nv, int64_t nx, int64_
 
 hipError_t launch_fft_cols(const double* H, int64_t nv, int64_t nx, int64_t ny, const double* tw_v, int mode,
                            double* out, const double* cx, const double* cy, double px, double py, double w_plane,
-                           int first, const double* norm, const uint32_t* rowbits, hipStream_t s) {
+                           int first, const double* norm, const uint32_t* rowbits, hipStream_t s, bool h_f32) {
   const dim3 gd((unsigned)nx);
   const double2* h = (const double2*)H;
+  const float2* hf = (const float2*)H;
   const double2* tw = (const double2*)tw_v;
   const ColEpilogue ep{out, cx, cy, px, py, w_plane, first, norm};
-#define COLS(NN)                                                                    \
-  case NN:                                                                          \
-    if (mode == 0) fft_cols_kernel<NN, 0><<<gd, dim3(NN / 16), 0, s>>>(h, nx, ny, tw, ep, 0, rowbits); \
-    else fft_cols_kernel<NN, 1><<<gd, dim3(NN / 16), 0, s>>>(h, nx, ny, tw, ep, 0, rowbits);          \
+#define COLS(NN)                                                                                           \
+  case NN:                                                                                                 \
+    if (h_f32 && mode == 0) fft_cols_kernel<NN, 0, float2><<<gd, dim3(NN / 16), 0, s>>>(hf, nx, ny, tw, ep, 0, rowbits); \
+    else if (h_f32) fft_cols_kernel<NN, 1, float2><<<gd, dim3(NN / 16), 0, s>>>(hf, nx, ny, tw, ep, 0, rowbits);         \
+    else if (mode == 0) fft_cols_kernel<NN, 0><<<gd, dim3(NN / 16), 0, s>>>(h, nx, ny, tw, ep, 0, rowbits); \
+    else fft_cols_kernel<NN, 1><<<gd, dim3(NN / 16), 0, s>>>(h, nx, ny, tw, ep, 0, rowbits);              \
     break;
   switch (nv) {
     COLS(1024)

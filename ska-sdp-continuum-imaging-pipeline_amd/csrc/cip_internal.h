@@ -169,12 +169,14 @@ bool fast_fft_supported(int64_t nu, int64_t nv, int64_t nx, int64_t ny);
 // cells of marked tiles are read and then ZEROED (the grid is left all-zero
 // for the next scatter)
 // grid_f32: the planes hold complex64 cells (the packed class, GridGeometry::grid_f32)
+// and H complex64 values (pass A's output; launch_fft_cols with h_f32)
 hipError_t launch_fft_rows(double* gT, int64_t nu, int64_t nv, int64_t nx, const double* tw_u, double* H,
                            const uint32_t* dmask, int64_t ntx, bool skip_clean, hipStream_t s,
                            bool grid_f32 = false);
 hipError_t launch_fft_cols(const double* H, int64_t nv, int64_t nx, int64_t ny, const double* tw_v, int mode,
                            double* out, const double* cx, const double* cy, double px, double py, double w_plane,
-                           int first, const double* norm, const uint32_t* rowbits, hipStream_t s);
+                           int first, const double* norm, const uint32_t* rowbits, hipStream_t s,
+                           bool h_f32 = false);
 // strips (multi-GPU strong scaling): pass A over rows [y0, y1)
 // of gT (zeroed after reading) into H with y1 - y0 rows per block; pass B for
 // image rows [i0, i1) (multiples of the column block) from an H holding those
