@@ -255,6 +255,7 @@ static GridGeometry geometry(const cip_gridder_params& p, double px, double py) 
   g.do_wstacking = p.do_wstacking;
   g.w0 = p.w0;
   g.dw = p.dw;
+  g.inv_dw = 1.0 / p.dw;
   g.nplanes = p.nplanes;
   g.tile = p.tile;
   g.ntx = (p.nu + p.tile - 1) / p.tile;

@@ -141,6 +141,37 @@ __device__ __forceinline__ void eval_kernel_f32(float y, float* out) {
   }
 }
 
+// The u and v kernels of one visibility at once (the packed class): both axes
+// share the polynomial pieces, so each Horner step is one v_pk_fma_f32 on
+// (u, v) against the broadcast coefficient - half the VALU issue of two
+// eval_kernel_f32 calls, the same fp32 values.
+typedef float cip_f32x2 __attribute__((ext_vector_type(2)));
+template <int W>
+__device__ __forceinline__ void eval_kernel_f32x2(cip_f32x2 y, cip_f32x2* out) {
+  using K = EsKernel<W>;
+  const cip_f32x2 z = y * y;
+#pragma unroll
+  for (int k = 0; k < W / 2; ++k) {
+    constexpr int D = K::D;
+    float c = sgpr_constf((float)K::coef(k, (D & 1) ? D - 1 : D));
+    cip_f32x2 e{c, c};
+#pragma unroll
+    for (int d = ((D & 1) ? D - 1 : D) - 2; d >= 0; d -= 2) {
+      c = sgpr_constf((float)K::coef(k, d));
+      e = __builtin_elementwise_fma(e, z, cip_f32x2{c, c});
+    }
+    c = sgpr_constf((float)K::coef(k, (D & 1) ? D : D - 1));
+    cip_f32x2 o{c, c};
+#pragma unroll
+    for (int d = ((D & 1) ? D : D - 1) - 2; d >= 1; d -= 2) {
+      c = sgpr_constf((float)K::coef(k, d));
+      o = __builtin_elementwise_fma(o, z, cip_f32x2{c, c});
+    }
+    out[k] = __builtin_elementwise_fma(y, o, e);
+    out[W - 1 - k] = __builtin_elementwise_fma(-y, o, e);
+  }
+}
+
 // Scale of a packed chunk of n visibilities relative to the launch's base
 // scale (which assumes n = kChunkVisPacked): 2^min(12 - ceil(lg n), 3), exact
 // (the cap keeps every contribution below 2^22, the fp32 rounding's range;
@@ -171,6 +202,7 @@ struct GridGeometry {
   double scale_u, scale_v;  // nu * pixsize_x, nv * pixsize_y
   int do_wstacking;
   double w0, dw;
+  double inv_dw;  // 1 / dw: the w coordinate (w f / c - w0) / dw as one multiply (planner, scatter, oracle alike)
   int64_t nplanes;
   int tile;                 // T
   int64_t ntx, nty, ntw;    // tiles per axis (ntw = nplanes - W + 1, or 1 in 2-D)
@@ -275,7 +307,7 @@ __device__ __forceinline__ bool place_vis(double u_m, double v_m, double w_m, do
   uv_origin(x, y, hw, g, ix0, yu, iy0, yv);
   bool ok = true;
   if (g.do_wstacking) {
-    const double xw = ((w_m * fx) - g.w0) / g.dw;
+    const double xw = ((w_m * fx) - g.w0) * g.inv_dw;
     footprint(xw, hw, iw0, yw);
     ok = ok && (*iw0 >= 0) && (*iw0 + g.support <= g.nplanes);
   } else {
@@ -319,7 +351,7 @@ __device__ __forceinline__ bool place_origin(double u_m, double v_m, double w_m,
   *ix0 = ix;
   *iy0 = iy;
   if (g.do_wstacking) {
-    const double xw = ((w_m * fx) - g.w0) / g.dw;
+    const double xw = ((w_m * fx) - g.w0) * g.inv_dw;
     double yw;
     footprint(xw, hw, iw0, &yw);
     // |x|, |y| < 2^30 + W here: finite and inside place_vis's bound

@@ -180,8 +180,15 @@ __device__ __forceinline__ void grid_fetched_packed(const VisFetch& f, const Gri
   const double sc0 = f.wt * fixed_scale;
   const float vr0 = (float)(f.vr * sc0), vi0 = (float)(f.vi * sc0);
   float ku[W], kv[W];
-  eval_kernel_f32<W>((float)yu, ku);
-  eval_kernel_f32<W>((float)yv, kv);
+  {
+    f32x2 kuv[W];
+    eval_kernel_f32x2<W>(f32x2{(float)yu, (float)yv}, kuv);
+#pragma unroll
+    for (int i = 0; i < W; ++i) {
+      ku[i] = kuv[i].x;
+      kv[i] = kuv[i].y;
+    }
+  }
   unsigned long long* base = sub + (lx * P + ly);
   auto taps = [&](unsigned long long* bk, float vr, float vi) {
     f32x2 k_ir[W];  // (kv vi, kv vr): the low / high word of each tap
