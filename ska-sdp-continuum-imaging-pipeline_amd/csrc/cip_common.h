@@ -57,7 +57,10 @@ constexpr int kTile = CIP_TILE;
 // merged range, not at a window boundary: there a chunk boundary may fall
 // inside a window, which is harmless because perm maps every position to a
 // visibility of the same uv tile, but the invariant does not hold).
-constexpr int kOrderWindow = 1024;
+#ifndef CIP_ORDER_WINDOW
+#define CIP_ORDER_WINDOW 1024  // experiment builds: 2048 (tools/build_variant_all.sh)
+#endif
+constexpr int kOrderWindow = CIP_ORDER_WINDOW;
 
 __host__ __device__ inline int64_t floor_div(int64_t a, int64_t b) {
   int64_t q = a / b;

@@ -92,7 +92,7 @@ hipError_t launch_add_scalar(const double* src, double* dst, hipStream_t s) {
 // slices). Atomic ranks make
 // the order within a class run-to-run variable; the integer sums are not.
 constexpr int kOrderThreads = 256;
-constexpr int kOrderPer = 4;
+constexpr int kOrderPer = kOrderWindow / kOrderThreads;
 constexpr int kOrderBatch = kOrderThreads * kOrderPer;
 static_assert(kOrderBatch == kOrderWindow, "one order block per window");
 
