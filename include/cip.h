@@ -233,9 +233,10 @@ int cip_grid_tiles(const double* slice_uvw, const int32_t* chan_start,
 
 /* cip_grid_tiles onto ONE uv strip's buffer instead of the whole grid (the
  * strong-scaling ranks of DESIGN.md 7 hold only their strip + halo rows): the
- * grid must be 2-D in the pruned-FFT layout (cip_grid_layout == 1, stored
- * gT[y][x]); `strip` holds nrows rows of nu complex128 cells, buffer row k =
- * grid row (row0 + k) mod nv. Every visibility's footprint must fall inside
+ * grid must be in the pruned-FFT layout (cip_grid_layout == 1, stored
+ * gT[y][x]); `strip` holds, per w plane (nplanes of them, 1 in 2-D), nrows
+ * rows of nu complex128 cells, buffer row k = grid row (row0 + k) mod nv
+ * (plane p at strip + 2 nu nrows p). Every visibility's footprint must fall inside
  * those rows (a strip's slices from its footprint-origin rows [y0, y1) need
  * nrows = y1 - y0 + W - 1): a cell outside is dropped and the call returns
  * CIP_ERANGE. Flags as cip_grid_tiles (CIP_GRID_ZEROED: buffer all zero).
@@ -276,6 +277,23 @@ int cip_strip_rows(double* grid, const cip_gridder_params* params,
 int cip_strip_cols(const double* H, const cip_gridder_params* params,
                    int64_t npix_x, int64_t npix_y, int64_t i0, int64_t i1,
                    const double* norm, void* hip_stream, double* dirty_rows);
+/* w-stacking strips (the reference's own gridding mode split by uv strips):
+ * cip_strip_rows runs per w plane (grid = the plane's rows of the strip
+ * buffer); cip_strip_cols_wplane is pass B for plane `plane` of image rows
+ * [i0, i1) with the w screen, adding into acc_rows ((i1 - i0) x npix_y f64;
+ * first != 0 overwrites: the rank's first plane); after the last plane
+ * cip_strip_wfinal applies the final w correction and grid correction to
+ * those rows, divided by *norm (device f64) when norm != NULL. Synchronous
+ * on hip_stream. */
+int cip_strip_cols_wplane(const double* H, const cip_gridder_params* params,
+                          int64_t npix_x, int64_t npix_y, double pixsize_x,
+                          double pixsize_y, int64_t i0, int64_t i1,
+                          int64_t plane, int first, void* hip_stream,
+                          double* acc_rows);
+int cip_strip_wfinal(double* acc_rows, const cip_gridder_params* params,
+                     int64_t npix_x, int64_t npix_y, double pixsize_x,
+                     double pixsize_y, int64_t i0, int64_t i1,
+                     const double* norm, void* hip_stream);
 
 /* Reference-exact UVW tile keys and constant-key channel runs (one run per
  * maximal range of channels with equal (iu, iv, iw) in a row), rows in

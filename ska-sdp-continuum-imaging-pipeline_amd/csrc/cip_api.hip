@@ -1246,9 +1246,9 @@ static int plane_to_dirty(const DirtyStage& st, const GridGeometry& g, int64_t p
 }
 
 // after the last plane: the w-stacking correction (2-D: nothing)
-static int finish_dirty(Workspace* ws, const DirtyStage& st, const cip_gridder_params& prm, const GridGeometry& g,
-                        double* dirty_out, hipStream_t s) {
-  if (!g.do_wstacking) return CIP_OK;
+// the w-stacking final correction's table of F (cached per workspace)
+static int w_correction_table(Workspace* ws, const cip_gridder_params& prm, const GridGeometry& g, hipStream_t s,
+                              double** table, int64_t* n, double* dnu_out) {
   HostKernel hk;
   host_kernel(g.support, &hk);
   KernelFT F(hk);
@@ -1265,6 +1265,19 @@ static int finish_dirty(Workspace* ws, const DirtyStage& st, const cip_gridder_p
     CIP_HIP_CHECK(hipStreamSynchronize(s));
     ws->fw_key = fw_key;
   }
+  *table = fwd;
+  *n = fw_n;
+  *dnu_out = dnu;
+  return CIP_OK;
+}
+
+static int finish_dirty(Workspace* ws, const DirtyStage& st, const cip_gridder_params& prm, const GridGeometry& g,
+                        double* dirty_out, hipStream_t s) {
+  if (!g.do_wstacking) return CIP_OK;
+  double* fwd = nullptr;
+  int64_t fw_n = 0;
+  double dnu = 0.0;
+  if (const int rc = w_correction_table(ws, prm, g, s, &fwd, &fw_n, &dnu); rc != CIP_OK) return rc;
   CIP_HIP_CHECK(launch_wfinal_correct(dirty_out, st.npix_x, st.npix_y, st.px, st.py, st.cx, st.cy, fwd, fw_n, dnu,
                                       g.dw, s));
   return CIP_OK;
@@ -1304,8 +1317,7 @@ static int grid_accumulate(const double* uvw, int64_t nrow, const double* freq, 
   unsigned* oob = nullptr;
   if (nrows > 0) {
     // a strip's row window (cip_grid_tiles_strip): rows [row0, row0 + nrows) mod nv
-    if (!transposed || pp.g.nplanes != 1)
-      return set_error(CIP_EINVAL, "strip buffers need a 2-D grid in the pruned-FFT layout");
+    if (!transposed) return set_error(CIP_EINVAL, "strip buffers need the pruned-FFT grid layout");
     if (row0 < 0 || row0 >= pp.g.nv || nrows > pp.g.nv) return set_error(CIP_EINVAL, "strip rows outside the grid");
     oob = buf<unsigned>(ws, "strip_oob", 1);
     if (!oob) return CIP_ENOMEM;
@@ -1661,7 +1673,6 @@ int cip_grid_plane(const double* uvw, int64_t nrow, const double* freq, int64_t 
 // strips of the pruned FFT (multi-GPU strong scaling)
 static int strip_check(const cip_gridder_params* params, int64_t npix_x, int64_t npix_y, GridGeometry* g) {
   if (!params) return set_error(CIP_EINVAL, "params is NULL");
-  if (params->do_wstacking) return set_error(CIP_EINVAL, "strips: 2-D grids only");
   *g = geometry(*params, 1.0, 1.0);
   if (!grid_is_transposed(*g, npix_x, npix_y))
     return set_error(CIP_EINVAL, "strips need the pruned-FFT grid layout (power-of-two grids, cip_grid_layout == 1)");
@@ -1702,6 +1713,53 @@ int cip_strip_cols(const double* H, const cip_gridder_params* params, int64_t np
   if (const int rc = fft_twiddles(ws, g.nv, s, &tw_v); rc != CIP_OK) return rc;
   if (const int rc = correction_vectors(ws, g, npix_x, npix_y, s, &cx, &cy); rc != CIP_OK) return rc;
   CIP_HIP_CHECK(launch_fft_cols_strip(H, g.nv, npix_x, npix_y, tw_v, i0, i1, dirty_rows, cx, cy, norm, s));
+  CIP_HIP_CHECK(hipStreamSynchronize(s));
+  return CIP_OK;
+}
+
+int cip_strip_cols_wplane(const double* H, const cip_gridder_params* params, int64_t npix_x, int64_t npix_y,
+                          double pixsize_x, double pixsize_y, int64_t i0, int64_t i1, int64_t plane, int first,
+                          void* hip_stream, double* acc_rows) {
+  g_last_error.clear();
+  GridGeometry g;
+  if (const int rc = strip_check(params, npix_x, npix_y, &g); rc != CIP_OK) return rc;
+  if (!params->do_wstacking) return set_error(CIP_EINVAL, "cip_strip_cols_wplane: w-stacking parameters only");
+  if (!H || !acc_rows) return set_error(CIP_EINVAL, "NULL H or acc_rows");
+  if (plane < 0 || plane >= params->nplanes) return set_error(CIP_EINVAL, "plane out of range");
+  if (i0 < 0 || i1 > npix_x || i1 <= i0 || i0 % 4 || i1 % 4)
+    return set_error(CIP_EINVAL, "image row range must be multiples of 4 inside [0, npix_x]");
+  hipStream_t s = (hipStream_t)hip_stream;
+  Workspace* ws = workspace();
+  if (!ws) return set_error(CIP_EHIP, "no HIP device");
+  if (const int sr = settle_async(ws, s); sr != CIP_OK) return sr;
+  double* tw_v = nullptr;
+  if (const int rc = fft_twiddles(ws, g.nv, s, &tw_v); rc != CIP_OK) return rc;
+  CIP_HIP_CHECK(launch_fft_cols_strip_wplane(H, g.nv, npix_x, npix_y, tw_v, i0, i1, acc_rows, pixsize_x, pixsize_y,
+                                             params->w0 + (double)plane * params->dw, first != 0, s));
+  CIP_HIP_CHECK(hipStreamSynchronize(s));
+  return CIP_OK;
+}
+
+int cip_strip_wfinal(double* acc_rows, const cip_gridder_params* params, int64_t npix_x, int64_t npix_y,
+                     double pixsize_x, double pixsize_y, int64_t i0, int64_t i1, const double* norm,
+                     void* hip_stream) {
+  g_last_error.clear();
+  GridGeometry g;
+  if (const int rc = strip_check(params, npix_x, npix_y, &g); rc != CIP_OK) return rc;
+  if (!params->do_wstacking) return set_error(CIP_EINVAL, "cip_strip_wfinal: w-stacking parameters only");
+  if (!acc_rows) return set_error(CIP_EINVAL, "NULL acc_rows");
+  if (i0 < 0 || i1 > npix_x || i1 <= i0) return set_error(CIP_EINVAL, "image rows outside [0, npix_x)");
+  hipStream_t s = (hipStream_t)hip_stream;
+  Workspace* ws = workspace();
+  if (!ws) return set_error(CIP_EHIP, "no HIP device");
+  if (const int sr = settle_async(ws, s); sr != CIP_OK) return sr;
+  double *cx = nullptr, *cy = nullptr, *fwd = nullptr;
+  int64_t fw_n = 0;
+  double dnu = 0.0;
+  if (const int rc = correction_vectors(ws, g, npix_x, npix_y, s, &cx, &cy); rc != CIP_OK) return rc;
+  if (const int rc = w_correction_table(ws, *params, g, s, &fwd, &fw_n, &dnu); rc != CIP_OK) return rc;
+  CIP_HIP_CHECK(launch_wfinal_correct(acc_rows, npix_x, npix_y, pixsize_x, pixsize_y, cx, cy, fwd, fw_n, dnu, g.dw, s,
+                                      i0, i1 - i0, norm));
   CIP_HIP_CHECK(hipStreamSynchronize(s));
   return CIP_OK;
 }

@@ -454,6 +454,32 @@ hipError_t launch_fft_cols_strip(const double* H, int64_t nv, int64_t nx, int64_
   return hipGetLastError();
 }
 
+hipError_t launch_fft_cols_strip_wplane(const double* H, int64_t nv, int64_t nx, int64_t ny, const double* tw_v,
+                                        int64_t i0, int64_t i1, double* acc, double px, double py, double w_plane,
+                                        bool first, hipStream_t s) {
+  if (i0 < 0 || i1 > nx || i1 <= i0 || i0 % kColBlock != 0 || (i1 - i0) % kColBlock != 0)
+    return hipErrorInvalidValue;
+  const dim3 gd((unsigned)(i1 - i0));
+  const double2* h = (const double2*)H;
+  const double2* tw = (const double2*)tw_v;
+  const ColEpilogue ep{acc, nullptr, nullptr, px, py, w_plane, first ? 1 : 0, nullptr};
+#define COLS(NN)                                                                \
+  case NN:                                                                      \
+    fft_cols_kernel<NN, 1><<<gd, dim3(NN / 16), 0, s>>>(h, nx, ny, tw, ep, i0); \
+    break;
+  switch (nv) {
+    COLS(1024)
+    COLS(2048)
+    COLS(4096)
+    COLS(8192)
+    COLS(16384)
+    default:
+      return hipErrorInvalidValue;
+  }
+#undef COLS
+  return hipGetLastError();
+}
+
 hipError_t launch_fft_cols(const double* H, int64_t nv, int64_t nx, int64_t ny, const double* tw_v, int mode,
                            double* out, const double* cx, const double* cy, double px, double py, double w_plane,
                            int first, const double* norm, const uint32_t* rowbits, hipStream_t s, bool h_f32) {

@@ -365,11 +365,15 @@ hipError_t launch_wplane_accumulate(const double* grid, const GridGeometry& g, i
 }
 
 // acc *= cx[i] cy[j] / (F(dw |n-1|) n): F from a uniform table (cubic Lagrange).
+// Image rows i0 + blockIdx.y (acc row blockIdx.y: a uv strip's image rows,
+// DESIGN.md 7); norm (may be NULL): also / *norm (the weight sum).
 __global__ void wfinal_correct_kernel(double* __restrict__ acc, int64_t nx, int64_t ny, double px, double py,
                                       const double* __restrict__ cx, const double* __restrict__ cy,
-                                      const double* __restrict__ fw, int64_t fw_n, double fw_dnu, double dw) {
+                                      const double* __restrict__ fw, int64_t fw_n, double fw_dnu, double dw,
+                                      int64_t i0, const double* __restrict__ norm) {
   const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t i = blockIdx.y;
+  const int64_t i = i0 + blockIdx.y;
+  double* row = acc + (int64_t)blockIdx.y * ny;
   if (j >= ny) return;
   const double nm1 = nm1_of(i, j, nx, ny, px, py);
   const double t = fabs(dw * nm1) / fw_dnu;
@@ -380,14 +384,18 @@ __global__ void wfinal_correct_kernel(double* __restrict__ acc, int64_t nx, int6
   const double f0 = fw[k - 1], f1 = fw[k], f2 = fw[k + 1], f3 = fw[k + 2];
   const double F = -x * (x - 1.0) * (x - 2.0) / 6.0 * f0 + (x + 1.0) * (x - 1.0) * (x - 2.0) / 2.0 * f1 -
                    (x + 1.0) * x * (x - 2.0) / 2.0 * f2 + (x + 1.0) * x * (x - 1.0) / 6.0 * f3;
-  acc[i * ny + j] *= cx[i] * cy[j] / (F * (nm1 + 1.0));
+  const double c = cx[i] * cy[j] / (F * (nm1 + 1.0));
+  row[j] *= norm ? c / *norm : c;
 }
 
 hipError_t launch_wfinal_correct(double* acc, int64_t npix_x, int64_t npix_y, double pixsize_x, double pixsize_y,
                                  const double* cx, const double* cy, const double* fw_table, int64_t fw_n,
-                                 double fw_dnu, double dw, hipStream_t s) {
-  wfinal_correct_kernel<<<dim3((unsigned)((npix_y + 255) / 256), (unsigned)npix_x), dim3(256), 0, s>>>(
-      acc, npix_x, npix_y, pixsize_x, pixsize_y, cx, cy, fw_table, fw_n, fw_dnu, dw);
+                                 double fw_dnu, double dw, hipStream_t s, int64_t i0, int64_t nrows,
+                                 const double* norm) {
+  if (nrows < 0) nrows = npix_x - i0;
+  if (nrows <= 0) return hipSuccess;
+  wfinal_correct_kernel<<<dim3((unsigned)((npix_y + 255) / 256), (unsigned)nrows), dim3(256), 0, s>>>(
+      acc, npix_x, npix_y, pixsize_x, pixsize_y, cx, cy, fw_table, fw_n, fw_dnu, dw, i0, norm);
   return hipGetLastError();
 }
 

@@ -155,9 +155,12 @@ hipError_t launch_crop_correct_2d(const double* grid, const GridGeometry& g, int
 hipError_t launch_wplane_accumulate(const double* grid, const GridGeometry& g, int64_t npix_x, int64_t npix_y,
                                     double pixsize_x, double pixsize_y, double w_plane, int first,
                                     double* acc, hipStream_t s);
+// image rows [i0, i0 + nrows) held as acc rows 0.. (nrows < 0: to npix_x);
+// norm (may be NULL): also / *norm
 hipError_t launch_wfinal_correct(double* acc, int64_t npix_x, int64_t npix_y, double pixsize_x, double pixsize_y,
                                  const double* cx, const double* cy, const double* fw_table, int64_t fw_n,
-                                 double fw_dnu, double dw, hipStream_t s);
+                                 double fw_dnu, double dw, hipStream_t s, int64_t i0 = 0, int64_t nrows = -1,
+                                 const double* norm = nullptr);
 
 // ---- pruned 2-D FFT (cip_fft.hip) -----------------------------------------
 // gT: the grid transposed (nv rows of nu cells); H: (nx / 8) x nv x 8 complex;
@@ -186,6 +189,11 @@ hipError_t launch_fft_rows_strip(double* gT, int64_t nu, int64_t nv, int64_t nx,
 hipError_t launch_fft_cols_strip(const double* H, int64_t nv, int64_t nx, int64_t ny, const double* tw_v, int64_t i0,
                                  int64_t i1, double* out, const double* cx, const double* cy, const double* norm,
                                  hipStream_t s);
+// the same for one w plane of a w-stacking strip: acc rows (+)= the plane's
+// screened contribution (mode 1 epilogue; first: overwrite)
+hipError_t launch_fft_cols_strip_wplane(const double* H, int64_t nv, int64_t nx, int64_t ny, const double* tw_v,
+                                        int64_t i0, int64_t i1, double* acc, double px, double py, double w_plane,
+                                        bool first, hipStream_t s);
 // out[0..n) /= *sumw (device scalar)
 hipError_t launch_scale_inverse(double* out, int64_t n, const double* sumw, hipStream_t s);
 

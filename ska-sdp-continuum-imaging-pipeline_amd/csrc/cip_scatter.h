@@ -467,9 +467,10 @@ __global__ __launch_bounds__(scatter_threads<G>(), CIP_SCATTER_WAVES) void scatt
     if (G > 1 && plane + k >= g.nplanes) break;
     if (G > 1 && (plane + k < g.plane_lo || plane + k >= g.plane_hi)) continue;
     const unsigned long long* sk = sub + k * S;
-    double* gk = grid + (int64_t)k * 2 * g.nu * g.nv;
+    // planes of g.rows rows (a uv strip's buffer holds its rows of every plane)
+    double* gk = grid + (int64_t)k * 2 * g.nu * g.rows;
     // packed class on complex64 planes (GridGeometry::grid_f32)
-    float* gkf = (float*)grid + (int64_t)k * 2 * g.nu * g.nv;
+    float* gkf = (float*)grid + (int64_t)k * 2 * g.nu * g.rows;
     const bool f32 = PACK && g.grid_f32 != 0;
     for (int cell = threadIdx.x; cell < P * P; cell += NT) {
       const int lcell = g.transposed ? (cell % P) * P + cell / P : cell;  // lx * P + ly

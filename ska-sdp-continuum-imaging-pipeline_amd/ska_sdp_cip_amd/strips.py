@@ -240,10 +240,16 @@ class HipStripBackend:
     clean (pass A zeroes the rows it reads; the halo rows are zeroed after
     they are sent); an invert that fails in between leaves it marked dirty and
     the next `grid_strip` zeroes it first instead of trusting CIP_GRID_ZEROED.
-    Unbound (rows=None) the buffer is the whole transposed grid."""
+    Unbound (rows=None) the buffer is the whole transposed grid.
+    w-stacking parameters (nplanes > 1): the buffer holds the strip's rows of
+    every w plane, (nplanes, nrows, nu, 2); pass A runs per plane, pass B per
+    plane with the w screen into the rank's image rows (`pass_cols_wplane`),
+    then `finish_rows` applies the final w and grid corrections.
+    `single_precision_accumulation`: the packed class (complex64 visibilities;
+    the reference call's float class), gridded into the same fp64 planes."""
 
     def __init__(self, params, pixsize_x: float, pixsize_y: float, npix_x: int, npix_y: int, device=None,
-                 rows: Optional[tuple] = None):
+                 rows: Optional[tuple] = None, single_precision_accumulation: bool = False):
         from . import _lib  # pylint: disable=import-outside-toplevel
         from .gridder import _require_gpu  # pylint: disable=import-outside-toplevel
 
@@ -253,9 +259,10 @@ class HipStripBackend:
         self.px, self.py = float(pixsize_x), float(pixsize_y)
         self.npix_x, self.npix_y = int(npix_x), int(npix_y)
         self.device = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
-        if int(params.nplanes) != 1 or not _lib.lib().cip_grid_layout(params, self.npix_x, self.npix_y):
-            raise ValueError("strips need a 2-D (no w-stacking) grid in the pruned-FFT layout "
-                             "(power-of-two grids)")
+        if not _lib.lib().cip_grid_layout(params, self.npix_x, self.npix_y):
+            raise ValueError("strips need a grid in the pruned-FFT layout (power-of-two grids)")
+        self.nplanes = int(params.nplanes) if int(params.do_wstacking) else 1
+        self.single = bool(single_precision_accumulation)
         self.rows = None
         self.grid = None
         self.dirty = False
@@ -267,7 +274,9 @@ class HipStripBackend:
             raise ValueError("strip rows outside the grid")
         if self.rows != (row0, nrows):
             self.grid = None  # free the old buffer first
-            self.grid = torch.zeros((nrows, int(self.params.nu), 2), dtype=torch.float64, device=self.device)
+            shape = (nrows, int(self.params.nu), 2) if self.nplanes == 1 else (self.nplanes, nrows,
+                                                                                 int(self.params.nu), 2)
+            self.grid = torch.zeros(shape, dtype=torch.float64, device=self.device)
             self.rows = (row0, nrows)
             self.dirty = False
 
@@ -275,7 +284,7 @@ class HipStripBackend:
         """A backend of the same configuration (another rank's, for the
         single-process emulation)."""
         return HipStripBackend(self.params, self.px, self.py, self.npix_x, self.npix_y, device=self.device,
-                               rows=self.rows)
+                               rows=self.rows, single_precision_accumulation=self.single)
 
     def bind(self, layout: StripLayout, rank: int) -> "HipStripBackend":
         """Hold rank `rank`'s strip + halo rows of `layout` (reallocates when they change)."""
@@ -286,7 +295,8 @@ class HipStripBackend:
         return torch.cuda.current_stream(self.device).cuda_stream
 
     def grid_strip(self, data: StripData, freq):
-        """Grid the strip's visibilities; returns (strip buffer (nrows, nu, 2) f64, weight sum (1,) f64)."""
+        """Grid the strip's visibilities; returns (strip buffer (nrows, nu, 2) f64 - (nplanes, nrows, nu, 2)
+        with w-stacking -, weight sum (1,) f64)."""
         from .gridder import _codes  # pylint: disable=import-outside-toplevel
 
         if self.dirty:  # a previous invert did not finish: the buffer may hold partial sums
@@ -302,7 +312,8 @@ class HipStripBackend:
                 data.wgt.data_ptr() if data.wgt is not None else None,
                 wgt_codes[data.wgt.dtype] if data.wgt is not None else self._lib.CIP_NONE,
                 self.params, self.px, self.py, self.npix_x, self.npix_y, self.rows[0], self.rows[1],
-                self._lib.CIP_GRID_ZEROED, self._stream(), self.grid.data_ptr(), sumw.data_ptr()))
+                self._lib.CIP_GRID_ZEROED | (self._lib.CIP_ACC_SINGLE if self.single else 0), self._stream(),
+                self.grid.data_ptr(), sumw.data_ptr()))
         return self.grid, sumw
 
     def mark_clean(self) -> None:
@@ -323,6 +334,21 @@ class HipStripBackend:
                                                        int(i0), int(i1), None if norm is None else norm.data_ptr(),
                                                        self._stream(), out.data_ptr()))
         return out
+
+    def pass_cols_wplane(self, H, i0: int, i1: int, plane: int, first: bool, acc):
+        """Pass B of w plane `plane` for image rows [i0, i1) with its w screen, into acc ((i1 - i0), npix_y)
+        f64 (overwritten when `first`)."""
+        self._lib.check(self._lib.lib().cip_strip_cols_wplane(
+            H.data_ptr(), self.params, self.npix_x, self.npix_y, self.px, self.py, int(i0), int(i1), int(plane),
+            int(bool(first)), self._stream(), acc.data_ptr()))
+        return acc
+
+    def finish_rows(self, acc, i0: int, i1: int, norm=None):
+        """The final w and grid corrections of image rows [i0, i1) (acc, in place), / norm."""
+        self._lib.check(self._lib.lib().cip_strip_wfinal(
+            acc.data_ptr(), self.params, self.npix_x, self.npix_y, self.px, self.py, int(i0), int(i1),
+            None if norm is None else norm.data_ptr(), self._stream()))
+        return acc
 
 
 def _assemble_H(pieces: Sequence, nb: int, layout: StripLayout, device, dtype):
@@ -369,39 +395,70 @@ def invert_strips(data: StripData, freq, layout: StripLayout, backend, *, dst: i
             t_last[0] = t
 
     mark("grid")
+    # w-stacking buffers hold every plane's rows: rows are the second axis
+    nplanes = int(getattr(backend, "nplanes", 1))
+    rowsel = (lambda a, b: buf[a:b]) if nplanes == 1 else (lambda a, b: buf[:, a:b])
     if world > 1:
         # halo: buffer rows [h, h + W - 1) = the grid rows past the strip ->
-        # the next rank, added to its first rows
-        send = buf[h:h + layout.halo].contiguous()
+        # the next rank, added to its first rows (every plane's at once)
+        send = rowsel(h, h + layout.halo).contiguous()
         recv = torch.empty_like(send)
         ops = [dist.P2POp(dist.isend, send, (rank + 1) % world, group),
                dist.P2POp(dist.irecv, recv, (rank - 1) % world, group)]
         for w in dist.batch_isend_irecv(ops):
             w.wait()
-        buf[h:h + layout.halo].zero_()
-        buf[:layout.halo] += recv
+        rowsel(h, h + layout.halo).zero_()
+        rowsel(0, layout.halo).add_(recv)
         dist.all_reduce(sumw, group=group)
     mark("halo")
+    if nplanes > 1:
+        # per w plane: pass A on this rank's rows, the all-to-all, pass B with
+        # the plane's w screen added into this rank's image rows
+        i0, i1 = layout.image_rows(rank)
+        acc = torch.empty((i1 - i0, backend.npix_y), dtype=torch.float64, device=buf.device)
+        for p in range(nplanes):
+            H = backend.pass_rows(buf[p], 0, h)
+            mark("rows")
+            Hm = _alltoall_H(H, layout, rank, world, group) if world > 1 else H
+            mark("alltoall")
+            backend.pass_cols_wplane(Hm, i0, i1, p, p == 0, acc)
+            mark("cols")
+        backend.mark_clean()
+        rows_img = backend.finish_rows(acc, i0, i1, norm=sumw)
+        mark("final")
+        return _gather_rows(rows_img, layout, rank, world, dst, group, mark)
     H = backend.pass_rows(buf, 0, h)
     backend.mark_clean()
     mark("rows")
-    if world > 1:
-        # all-to-all: rank s receives blocks [i0_s / 4, i1_s / 4) of every rank's rows
-        splits_in = [(layout.image_rows(s)[1] - layout.image_rows(s)[0]) // COL_BLOCK * h * COL_BLOCK * 2
-                     for s in range(world)]
-        i0, i1 = layout.image_rows(rank)
-        nb = (i1 - i0) // COL_BLOCK
-        splits_out = [nb * (layout.rows(r)[1] - layout.rows(r)[0]) * COL_BLOCK * 2 for r in range(world)]
-        recv = torch.empty(sum(splits_out), dtype=H.dtype, device=H.device)
-        dist.all_to_all_single(recv, H.reshape(-1), splits_out, splits_in, group=group)
-        pieces = list(torch.split(recv, splits_out))
-        Hm = _assemble_H(pieces, nb, layout, H.device, H.dtype)
-    else:
-        i0, i1 = layout.image_rows(0)
-        Hm = H
+    i0, i1 = layout.image_rows(rank)
+    Hm = _alltoall_H(H, layout, rank, world, group) if world > 1 else H
     mark("alltoall")
     rows_img = backend.pass_cols(Hm, i0, i1, norm=sumw)
     mark("cols")
+    return _gather_rows(rows_img, layout, rank, world, dst, group, mark)
+
+
+def _alltoall_H(H, layout: StripLayout, rank: int, world: int, group):
+    """The all-to-all of pass-A blocks: rank s receives blocks [i0_s / 4,
+    i1_s / 4) of every rank's rows -> its pass-B input (nb, nv, 4, 2)."""
+    import torch.distributed as dist  # pylint: disable=import-outside-toplevel
+
+    h = layout.rows(rank)[1] - layout.rows(rank)[0]
+    splits_in = [(layout.image_rows(s)[1] - layout.image_rows(s)[0]) // COL_BLOCK * h * COL_BLOCK * 2
+                 for s in range(world)]
+    i0, i1 = layout.image_rows(rank)
+    nb = (i1 - i0) // COL_BLOCK
+    splits_out = [nb * (layout.rows(r)[1] - layout.rows(r)[0]) * COL_BLOCK * 2 for r in range(world)]
+    recv = torch.empty(sum(splits_out), dtype=H.dtype, device=H.device)
+    dist.all_to_all_single(recv, H.reshape(-1), splits_out, splits_in, group=group)
+    pieces = list(torch.split(recv, splits_out))
+    return _assemble_H(pieces, nb, layout, H.device, H.dtype)
+
+
+def _gather_rows(rows_img, layout: StripLayout, rank: int, world: int, dst: int, group, mark):
+    """This rank's image rows -> the whole image on `dst` (None elsewhere)."""
+    import torch.distributed as dist  # pylint: disable=import-outside-toplevel
+
     if world == 1:
         return rows_img
     # gather the image rows (strips padded to the largest: gather needs equal sizes)
@@ -463,13 +520,40 @@ def invert_strips_local(datas: Sequence[StripData], freq, layout: StripLayout, b
     for sw in sums[1:]:
         sumw = sumw + sw
     hs = [layout.rows(r)[1] - layout.rows(r)[0] for r in range(world)]
+    nplanes = int(getattr(backend, "nplanes", 1))
+    rowsel = (lambda b, lo, hi: b[lo:hi]) if nplanes == 1 else (lambda b, lo, hi: b[:, lo:hi])
     if world > 1:
         halos = []
         for r in range(world):
-            halos.append(bufs[r][hs[r]:hs[r] + layout.halo].clone())
-            bufs[r][hs[r]:hs[r] + layout.halo].zero_()
+            halos.append(rowsel(bufs[r], hs[r], hs[r] + layout.halo).clone())
+            rowsel(bufs[r], hs[r], hs[r] + layout.halo).zero_()
         for r in range(world):
-            timed(r, "halo", lambda r=r: bufs[r][:layout.halo].add_(halos[(r - 1) % world]))
+            timed(r, "halo", lambda r=r: rowsel(bufs[r], 0, layout.halo).add_(halos[(r - 1) % world]))
+    if nplanes > 1:
+        # per w plane: every rank's pass A, the regrouping, every rank's pass B
+        # with the plane's w screen into its image rows; then the corrections
+        accs = []
+        for s in range(world):
+            i0, i1 = layout.image_rows(s)
+            accs.append(torch.empty((i1 - i0, backend.npix_y), dtype=torch.float64, device=bufs[0].device))
+        for p in range(nplanes):
+            Hs = [timed(r, "rows", lambda r=r: ranks[r].pass_rows(bufs[r][p], 0, hs[r])) for r in range(world)]
+            for s in range(world):
+                i0, i1 = layout.image_rows(s)
+                b0, b1 = i0 // COL_BLOCK, i1 // COL_BLOCK
+                if world == 1:
+                    Hm = Hs[0]
+                else:
+                    Hm = timed(s, "assemble", lambda b0=b0, b1=b1: _assemble_H([H[b0:b1] for H in Hs], b1 - b0,
+                                                                                layout, Hs[0].device, Hs[0].dtype))
+                timed(s, "cols", lambda s=s, Hm=Hm, i0=i0, i1=i1: ranks[s].pass_cols_wplane(
+                    Hm.contiguous(), i0, i1, p, p == 0, accs[s]))
+        out = []
+        for s in range(world):
+            ranks[s].mark_clean()
+            i0, i1 = layout.image_rows(s)
+            out.append(timed(s, "final", lambda s=s, i0=i0, i1=i1: ranks[s].finish_rows(accs[s], i0, i1, norm=sumw)))
+        return torch.cat(out, dim=0)
     Hs = []
     for r in range(world):
         Hs.append(timed(r, "rows", lambda r=r: ranks[r].pass_rows(bufs[r], 0, hs[r])))

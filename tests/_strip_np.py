@@ -6,7 +6,10 @@ ska_sdp_cip_amd.strips plugs in. grid_strip grids with the oracle
 backward FFT along u with the kept frequencies k = i - npix_x/2 (mod nu) laid
 out in blocks of 4 (cip.h cip_strip_rows); pass_cols the backward FFT along v,
 the crop sign (-1)^(p+q) and the grid correction (oracle.ms2dirty's
-definition).
+definition). w-stacking parameters: one buffer plane per w plane (grid_plane
+per plane), pass_cols_wplane adds the plane's w-screened rows and
+finish_rows applies the final w correction (oracle.ms2dirty's w-stacking
+branch, restricted to the rank's image rows).
 """
 import numpy as np
 import torch
@@ -21,6 +24,7 @@ class NumpyStripBackend:
         self.prm, self.px, self.py = prm, float(px), float(py)
         self.npix_x, self.npix_y = int(npix_x), int(npix_y)
         self.nu, self.nv = prm["nu"], prm["nv"]
+        self.nplanes = int(prm["nplanes"]) if prm.get("do_wstacking") else 1
         self.rows = None
         self.dirty = False
         self._alloc((0, self.nv) if rows is None else rows)
@@ -31,7 +35,8 @@ class NumpyStripBackend:
     def _alloc(self, rows):
         if self.rows != tuple(rows):
             self.rows = tuple(int(x) for x in rows)
-            self.grid = torch.zeros((self.rows[1], self.nu, 2), dtype=torch.float64)
+            shape = (self.rows[1], self.nu, 2) if self.nplanes == 1 else (self.nplanes, self.rows[1], self.nu, 2)
+            self.grid = torch.zeros(shape, dtype=torch.float64)
 
     def spawn(self):
         return NumpyStripBackend(self.prm, self.px, self.py, self.npix_x, self.npix_y, rows=self.rows)
@@ -64,14 +69,20 @@ class NumpyStripBackend:
             vis[s, c0[s]:c1[s]] = v[k:k + n]
             wgt[s, c0[s]:c1[s]] = 1.0 if w is None else w[k:k + n]
             k += n
-        g = oracle.grid_plane(data.slice_uvw.numpy(), freq.numpy(), vis, wgt, self.prm, self.px, self.py).T
         # the strip buffer's rows (row0 + k) mod nv; every other grid row must be empty
         row0, nrows = self.rows
         sel = (row0 + np.arange(nrows)) % self.nv
         rest = np.ones(self.nv, bool)
         rest[sel] = False
-        assert not np.any(g[rest]), "footprint outside the strip's rows"
-        self.grid += torch.view_as_real(torch.from_numpy(np.ascontiguousarray(g[sel])))
+        for p in range(self.nplanes):
+            g = oracle.grid_plane(data.slice_uvw.numpy(), freq.numpy(), vis, wgt, self.prm, self.px, self.py,
+                                  p).T
+            assert not np.any(g[rest]), "footprint outside the strip's rows"
+            part = torch.view_as_real(torch.from_numpy(np.ascontiguousarray(g[sel])))
+            if self.nplanes == 1:
+                self.grid += part
+            else:
+                self.grid[p] += part
         sumw += float(wgt.sum())
         return self.grid, sumw
 
@@ -97,3 +108,34 @@ class NumpyStripBackend:
         if norm is not None:
             out = out / float(norm.reshape(-1)[0])
         return torch.from_numpy(np.ascontiguousarray(out))
+
+    def _nm1_rows(self, i0, i1):
+        l = (np.arange(i0, i1) - self.npix_x // 2) * self.px  # noqa: E741
+        m = (np.arange(self.npix_y) - self.npix_y // 2) * self.py
+        e = l[:, None] ** 2 + m[None, :] ** 2
+        return -e / (np.sqrt(1.0 - e) + 1.0)
+
+    def pass_cols_wplane(self, H, i0, i1, plane, first, acc):
+        Hc = torch.view_as_complex(H.contiguous()).numpy()  # (nb, nv, 4)
+        cols = Hc.transpose(0, 2, 1).reshape(i1 - i0, self.nv)
+        F = np.fft.ifft(cols, axis=1) * self.nv
+        q = np.arange(self.npix_y) - self.npix_y // 2
+        p = np.arange(i0, i1) - self.npix_x // 2
+        sgn = np.where((p[:, None] + q[None, :]) % 2 == 0, 1.0, -1.0)
+        wp = self.prm["w0"] + plane * self.prm["dw"]
+        val = (sgn * F[:, q % self.nv] * np.exp(-2j * np.pi * wp * self._nm1_rows(i0, i1))).real
+        a = acc.numpy()
+        if first:
+            a[...] = val
+        else:
+            a += val
+        return acc
+
+    def finish_rows(self, acc, i0, i1, norm=None):
+        nm1 = self._nm1_rows(i0, i1)
+        fw = oracle.kernel_ft(self.prm["support"], np.abs(self.prm["dw"] * nm1).ravel()).reshape(nm1.shape)
+        a = acc.numpy()
+        a *= self.cx[i0:i1, None] * self.cy[None, :] / (fw * (nm1 + 1.0))
+        if norm is not None:
+            a /= float(norm.reshape(-1)[0])
+        return acc

@@ -89,6 +89,42 @@ def test_strip_decomposition_equals_one_shot(gpu_device, world, W, npix):
     assert torch.equal(img, img2)
 
 
+@pytest.mark.parametrize("world,W,single", [(1, 6, False), (2, 6, False), (3, 8, False), (8, 6, False),
+                                             (4, 6, True)])
+def test_wstacking_strip_decomposition_equals_one_shot(gpu_device, world, W, single):
+    # the reference's gridding mode split by uv strips: each rank grids every
+    # w plane's strip rows, the halos of all planes move at once, then per
+    # plane pass A / regrouping / pass B with the w screen into the rank's
+    # image rows, and the final w correction per rank
+    npix = 512
+    uvw, f, vis, w, px = _case(12000, 16, npix)
+    uvw = uvw * np.array([1.0, 1.0, 20.0])  # a deep w range: many planes
+    tu, tf, tv, tw = _to(gpu_device, uvw, f, vis.astype(np.complex64), w.astype(np.float32))
+    ref, prm = device_ms2dirty(tu, tf, tv, tw, npix, npix, px, px, support=W, do_wstacking=True, normalise=True,
+                               single_precision_accumulation=single)
+    assert prm.nplanes > W
+    layout = strips.plan_strips(tu, tf, prm, px, npix, npix, world)
+    datas = []
+    for r in range(world):
+        rows, c0, c1 = strips.strip_slices(tu, tf, prm, px, *layout.rows(r))
+        datas.append(strips.gather_strip(tu, tv, tw, rows, c0, c1))
+    be = strips.HipStripBackend(prm, px, px, npix, npix, device=gpu_device, single_precision_accumulation=single)
+    stages = []
+    img = strips.invert_strips_local(datas, tf, layout, be, stages=stages)
+    torch.cuda.synchronize()
+    peak = float(ref.abs().max())
+    # fp64 class: only the fixed-point quantum per gridding call differs; the
+    # packed class: the one-shot call's complex64 planes and pass-A output
+    # against the strips' complex128 planes (the class's own rounding)
+    assert float((img - ref).abs().max()) < (1e-5 if single else 1e-12) * peak
+    for r, b in enumerate(be.ranks):
+        assert tuple(b.grid.shape) == (prm.nplanes, b.rows[1], prm.nu, 2)
+        assert float(b.grid.abs().max()) == 0.0 and not b.dirty
+    assert all("final" in st for st in stages)
+    img2 = strips.invert_strips_local(datas, tf, layout, be)
+    assert torch.equal(img, img2)
+
+
 def test_strip_buffer_rejects_footprints_outside_its_rows(gpu_device):
     # cip_grid_tiles_strip: a visibility whose footprint leaves the buffer's
     # row window is an error (CIP_ERANGE), not an out-of-bounds write

@@ -39,8 +39,12 @@ def _case(nrow=801, nchan=16, seed=4):
     return uvw, f, vis, w, px
 
 
-def _prm(px, W):
-    return oracle.choose_params(NPIX, NPIX, px, px, support=W)
+def _prm(px, W, wstack=None):
+    """2-D parameters, or with wstack = (uvw, freq) the w-stacking stack of that data."""
+    if wstack is None:
+        return oracle.choose_params(NPIX, NPIX, px, px, support=W)
+    wmin, wmax = oracle.w_range(*wstack)
+    return oracle.choose_params(NPIX, NPIX, px, px, support=W, do_wstacking=True, wmin=wmin, wmax=wmax)
 
 
 class _P:  # the fields plan_strips / strip_slices read from cip_gridder_params
@@ -124,7 +128,29 @@ def test_strip_emulation_equals_one_shot(world, W):
         assert sum(b.rows[1] for b in be.ranks) == prm["nv"] + world * (W - 1)
 
 
-def _worker(rank, world, port, q, W):
+@pytest.mark.parametrize("world,W", [(1, 6), (2, 6), (3, 4), (5, 8)])
+def test_wstacking_strip_emulation_equals_one_shot(world, W):
+    # the reference's own gridding mode split by uv strips: every plane's
+    # strip rows, the halos of all planes, per-plane pass A / regrouping /
+    # pass B with the w screen, then the final w correction per rank
+    from _strip_np import NumpyStripBackend
+
+    uvw, f, vis, w, px = _case(nrow=601, nchan=8)
+    uvw = uvw * np.array([1.0, 1.0, 40.0])  # a deep w range: several planes
+    prm = _prm(px, W, wstack=(uvw, f))
+    assert prm["nplanes"] > W
+    layout = strips.plan_strips(torch.from_numpy(uvw), torch.from_numpy(f), _P(prm), px, NPIX, NPIX, world)
+    datas = _strip_datas(uvw, f, vis, w, px, prm, layout)
+    be = NumpyStripBackend(prm, px, px, NPIX, NPIX)
+    img = strips.invert_strips_local(datas, torch.from_numpy(f), layout, be).numpy()
+    full = oracle.ms2dirty(uvw, f, vis, w, NPIX, NPIX, px, px, support=W, do_wstacking=True,
+                           nthreads=1) / w.astype(np.float64).sum()
+    assert np.abs(img - full).max() < 1e-13 * max(1.0, np.abs(full).max())
+    for b in be.ranks:
+        assert float(b.grid.abs().max()) == 0.0 and not b.dirty
+
+
+def _worker(rank, world, port, q, W, wstack=False):
     import sys
     from pathlib import Path
 
@@ -134,14 +160,20 @@ def _worker(rank, world, port, q, W):
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    uvw, f, vis, w, px = _case()
-    prm = _prm(px, W)
+    if wstack:
+        uvw, f, vis, w, px = _case(nrow=601, nchan=8)
+        uvw = uvw * np.array([1.0, 1.0, 40.0])
+        prm = _prm(px, W, wstack=(uvw, f))
+    else:
+        uvw, f, vis, w, px = _case()
+        prm = _prm(px, W)
     layout = strips.plan_strips(torch.from_numpy(uvw), torch.from_numpy(f), _P(prm), px, NPIX, NPIX, world)
     data = _strip_datas(uvw, f, vis, w, px, prm, layout)[rank]  # each rank holds only its strip
     be = NumpyStripBackend(prm, px, px, NPIX, NPIX)
     img = strips.invert_strips(data, torch.from_numpy(f), layout, be, dst=0)
     if rank == 0:
-        full = oracle.ms2dirty(uvw, f, vis, w, NPIX, NPIX, px, px, support=W, nthreads=1) / w.astype(np.float64).sum()
+        full = oracle.ms2dirty(uvw, f, vis, w, NPIX, NPIX, px, px, support=W, do_wstacking=wstack,
+                               nthreads=1) / w.astype(np.float64).sum()
         q.put((float(np.abs(img.numpy() - full).max()), float(np.abs(full).max()), float(be.grid.abs().max())))
     else:
         assert img is None
@@ -149,12 +181,12 @@ def _worker(rank, world, port, q, W):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,W", [(2, 8), (3, 6)])
-def test_strip_halo_exchange_gloo(world, W):
+@pytest.mark.parametrize("world,W,wstack", [(2, 8, False), (3, 6, False), (2, 6, True)])
+def test_strip_halo_exchange_gloo(world, W, wstack):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q, W)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, W, wstack)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:

@@ -11,6 +11,9 @@ rank's stages (the 8-GPU node is the driver's, not ours):
 * `--mode wplanes`: the reference's w-stacking call on C3 (100M visibilities,
   8192^2 grid, epsilon 1e-4 -> W = 6) split by w-plane groups
   (`wplanes.invert_wplanes_local`): per-rank share times.
+* `--mode wstrips`: the same call split by uv strips (every rank grids all w
+  planes of its strip rows; per plane pass A, all-to-all, pass B with the w
+  screen; `strips.invert_strips_local` with w-stacking parameters).
 
 The exchanges are modelled at a per-link xGMI rate (MI355X: 7 links per GPU,
 ~153 GB/s each per direction, the prompt's figure; RCCL reaches a fraction of
@@ -170,16 +173,93 @@ def wplanes_model(args):
             "ranks": N, "one_rank_ms": round(t1, 3), "worst_rank_ms": round(worst, 3), "model": models, "runs": out}
 
 
+def wstrips_model(args):
+    import torch
+
+    sys.path.insert(0, str(ROOT))
+    import bench
+    from ska_sdp_cip_amd import strips, wplanes
+    from ska_sdp_cip_amd.gridder import device_ms2dirty
+
+    dev = torch.device("cuda", 0)
+    cfg = bench.CONFIGS["c3"]
+    uvw, freq, vis, wgt, px, _, _ = bench.make_inputs(cfg, 0, 1, dev)
+    npix = cfg["npix"]
+    params = wplanes.HipWPlaneBackend(uvw, freq, vis, wgt, npix, npix, px, px, epsilon=1e-4,
+                                      single_precision_accumulation=args.single).params()
+    # the one-shot reference call on one GPU (synchronous calls)
+    one = []
+    for k in range(args.steps + 1):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        device_ms2dirty(uvw, freq, vis, wgt, npix, npix, px, px, epsilon=1e-4, do_wstacking=True, normalise=True,
+                        single_precision_accumulation=args.single)
+        torch.cuda.synchronize()
+        if k:
+            one.append(time.perf_counter() - t0)
+    one_ms = 1e3 * sum(one) / len(one)
+    log(f"[wstrips] one-shot reference call {one_ms:.2f} ms")
+    out = {}
+    for world in sorted({1, args.ranks}):
+        layout = strips.plan_strips(uvw, freq, params, px, npix, npix, world)
+        datas = []
+        for r in range(world):
+            rw, c0, c1 = strips.strip_slices(uvw, freq, params, px, *layout.rows(r))
+            datas.append(strips.gather_strip(uvw, vis, wgt, rw, c0, c1))
+        be = strips.HipStripBackend(params, px, px, npix, npix, device=dev,
+                                    rows=strips.strip_buffer_rows(layout, 0),
+                                    single_precision_accumulation=args.single)
+        strips.invert_strips_local(datas, freq, layout, be)
+        torch.cuda.synchronize()
+        runs = []
+        for _ in range(args.steps):
+            st = []
+            strips.invert_strips_local(datas, freq, layout, be, stages=st)
+            runs.append(st)
+        out[world] = {"per_rank_ms": [{k: round(v, 3) for k, v in pr.items()} for pr in _avg(runs)],
+                      "strip_rows": [layout.rows(r) for r in range(world)],
+                      "strip_vis": [d.nvis for d in datas]}
+        log(f"[wstrips] world {world}: {out[world]['per_rank_ms']}")
+        del datas, be
+        torch.cuda.empty_cache()
+    N = args.ranks
+    pr = out[N]["per_rank_ms"]
+    stage_max = {k: max(p.get(k, 0.0) for p in pr) for k in ("grid", "rows", "cols", "final")}
+    t1 = sum(out[1]["per_rank_ms"][0].get(k, 0.0) for k in ("grid", "rows", "cols", "final"))
+    nplanes, W, nu = int(params.nplanes), int(params.support), int(params.nu)
+    H_bytes = [(npix // 4) * (b - a) * 4 * 16 for a, b in out[N]["strip_rows"]]  # one plane's pass-A output
+    models = {}
+    for link in args.link_gbs:
+        bw = link * 1e9
+        halo_ms = nplanes * (W - 1) * nu * 16 / bw * 1e3
+        a2a_ms = nplanes * max(H_bytes) / N / bw * 1e3 if N > 1 else 0.0
+        gather_ms = (npix // N) * npix * 8 / bw * 1e3 if N > 1 else 0.0
+        # grid (+ halo) then the plane loop: each plane's pass A, all-to-all and
+        # pass B in turn (the slowest rank's summed pass-A and pass-B times),
+        # the final correction, the gather
+        step = (stage_max["grid"] + halo_ms + stage_max["rows"] + a2a_ms + stage_max["cols"] + stage_max["final"] +
+                gather_ms)
+        models[f"{link:g}GB/s"] = {"halo_ms": round(halo_ms, 3), "alltoall_ms": round(a2a_ms, 3),
+                                   "gather_ms": round(gather_ms, 3), "step_ms": round(step, 3),
+                                   "speedup_vs_one_shot": round(one_ms / step, 2),
+                                   "speedup_vs_1_strip": round(t1 / step, 2),
+                                   "gvis_per_s": round(cfg["rows"] * cfg["nchan"] / step / 1e6, 1)}
+    return {"mode": "wstrips", "workload": f"C3 reference call by uv strips (epsilon 1e-4 -> W = {W}, {nplanes} "
+                                           f"w planes, {'packed single' if args.single else 'fp64'} class)",
+            "ranks": N, "one_shot_ms": round(one_ms, 3), "one_strip_ms": round(t1, 3),
+            "stage_max_ms": {k: round(v, 3) for k, v in stage_max.items()}, "model": models, "runs": out}
+
+
 def main():
     ap = argparse.ArgumentParser(description=__doc__.splitlines()[1])
-    ap.add_argument("--mode", choices=("strips", "wplanes"), default="strips")
+    ap.add_argument("--mode", choices=("strips", "wplanes", "wstrips"), default="strips")
     ap.add_argument("--ranks", type=int, default=8)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--rows", type=int, default=3_906_250)
     ap.add_argument("--single", action="store_true")
     ap.add_argument("--link-gbs", type=float, nargs="+", default=[153.0, 64.0])
     args = ap.parse_args()
-    res = strips_model(args) if args.mode == "strips" else wplanes_model(args)
+    res = {"strips": strips_model, "wplanes": wplanes_model, "wstrips": wstrips_model}[args.mode](args)
     print(json.dumps(res), flush=True)
 
 
