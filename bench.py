@@ -456,6 +456,93 @@ def run_strong_wplanes(args, world, rank, device):
     }
 
 
+def run_strong_wstrips(args, world, rank, device):
+    """
+    `--strong --wstacking --split strips`: the same w-stacking image (the
+    reference call on C3) split by uv strips (SURVEY.md 8(e) option 1, DESIGN.md
+    7): rank r grids every w plane's rows of its balanced strip (buffers of
+    strip + W - 1 halo rows per plane), the halos of all planes go to rank
+    r + 1, then per plane: pass A on its rows, one all-to-all, pass B with the
+    plane's w screen into its image rows; the final w correction per rank and
+    one gather. value = 100M vis x steps / time.
+    """
+    import torch
+    import torch.distributed as dist
+
+    from ska_sdp_cip_amd import strips, wplanes
+
+    cfg = CONFIGS["c3"]
+    uvw_d, freq_d, vis_d, wgt_d, px, _, _ = make_inputs(cfg, 0, 1, device)  # the same data on every rank
+    npix = cfg["npix"]
+    support = None if args.epsilon_call else args.support
+    params = wplanes.HipWPlaneBackend(uvw_d, freq_d, vis_d, wgt_d, npix, npix, px, px, epsilon=1e-4,
+                                      support=support, single_precision_accumulation=args.single).params()
+    layout = strips.plan_strips(uvw_d, freq_d, params, px, npix, npix, world)
+    rws, c0, c1 = strips.strip_slices(uvw_d, freq_d, params, px, *layout.rows(rank))
+    data = strips.gather_strip(uvw_d, vis_d, wgt_d, rws, c0, c1)
+    backend = strips.HipStripBackend(params, px, px, npix, npix, device=device,
+                                     rows=strips.strip_buffer_rows(layout, rank),
+                                     single_precision_accumulation=args.single)
+    y0, y1 = layout.rows(rank)
+    log(f"[bench --strong --wstacking] rank {rank}/{world}: strip rows [{y0}, {y1}) of {params.nv}, "
+        f"{data.nvis:,} vis, {params.nplanes} planes, support {params.support}")
+
+    def step(stages=None):
+        return strips.invert_strips(data, freq_d, layout, backend, dst=0, stages=stages)
+
+    for _ in range(args.warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    stages = {}
+    nprof = max(2, min(args.steps, 5))
+    for _ in range(nprof):
+        img = step(stages)
+    parity = None
+    if world == 1:
+        ref, _ = gridder_ms2dirty_ref(uvw_d, freq_d, vis_d, wgt_d, npix, px, params.support, args.single)
+        parity = {"max_abs_diff_vs_one_shot": float((img - ref).abs().max()), "peak": float(ref.abs().max()),
+                  "what": "normalised images: w-stacking invert_strips (1 strip) vs cip_ms2dirty"}
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    nvis = cfg["rows"] * cfg["nchan"]
+    return {
+        "metric": f"Mvis/s gridded (invert) on {params.nu // 1024}k^2 grid, support={params.support}, w-stacking",
+        "value": round(nvis * args.steps / elapsed / 1e6, 2),
+        "unit": "Mvis/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f32-class (packed 2x32-bit)" if args.single else "f64",
+        "data": "synthetic (seeded MeerKAT-like uvw tracks, random complex64 vis, float32 weights, 5% flagged)",
+        "config": {
+            "workload": (f"C3 reference call: {nvis:,} vis -> {params.nu}^2 grid ({npix}^2 image), support "
+                         f"{params.support}, w-stacking {params.nplanes} planes, "
+                         f"{'packed single-precision' if args.single else 'fp64'} accumulate"),
+            "parallelism": f"uv strips x{world} + per-plane all-to-all (SURVEY 8(e) option 1)",
+            "strip_rows": [layout.rows(r) for r in range(world)],
+        },
+        "stages_ms_rank0": {k: round(v / nprof * 1e3, 3) for k, v in stages.items()},
+        "parity": parity,
+        "roofline": None,
+        "cpu_baseline": None,
+    }
+
+
 def gridder_ms2dirty_ref(uvw, freq, vis, wgt, npix, px, support, single):
     from ska_sdp_cip_amd import gridder
 
@@ -536,6 +623,9 @@ def main():
     ap.add_argument("--epsilon-call", action="store_true",
                     help="with --strong --wstacking: epsilon = 1e-4 picks the support (the reference's call, W = 6) "
                          "instead of --support")
+    ap.add_argument("--split", choices=("strips", "wplanes"), default="strips",
+                    help="with --strong --wstacking: split the w-stacking image by uv strips (default) or by "
+                         "w-plane groups")
     ap.add_argument("--no-strong-secondary", action="store_true",
                     help="skip the strong-scaling C4 secondary (secondary.strong_c4) of the default run")
     args = ap.parse_args()
@@ -580,7 +670,8 @@ def main():
     device = torch.device("cuda", local_rank)
     torch.cuda.set_device(device)
     if args.strong:
-        result = (run_strong_wplanes(args, world, rank, device) if args.wstacking
+        result = ((run_strong_wstrips if args.split == "strips" else run_strong_wplanes)(args, world, rank, device)
+                  if args.wstacking
                   else run_strong(args, world, rank, device))
         result["communicator"] = comm
         if rank == 0:
