@@ -277,6 +277,16 @@ int cip_strip_rows(double* grid, const cip_gridder_params* params,
 int cip_strip_cols(const double* H, const cip_gridder_params* params,
                    int64_t npix_x, int64_t npix_y, int64_t i0, int64_t i1,
                    const double* norm, void* hip_stream, double* dirty_rows);
+/* cip_strip_rows that reads and zeroes only the dirty tiles' cells: tile_bits
+ * (device) holds the dirty-tile bits of the whole grid's plane, (nv / 32)
+ * rows of (nu / 1024) uint32 words, bit tx % 32 of word [ty][tx / 32] for
+ * tile (tx, ty) of 32 x 32 cells; buffer row y is grid row (row0 + y) mod nv.
+ * Every non-zero cell of rows [y0, y1) must lie in a marked tile (the rest is
+ * neither read nor zeroed). */
+int cip_strip_rows_masked(double* grid, const cip_gridder_params* params,
+                          int64_t npix_x, int64_t npix_y, int64_t y0,
+                          int64_t y1, int64_t row0, const uint32_t* tile_bits,
+                          void* hip_stream, double* H);
 /* w-stacking strips (the reference's own gridding mode split by uv strips):
  * cip_strip_rows runs per w plane (grid = the plane's rows of the strip
  * buffer); cip_strip_cols_wplane is pass B for plane `plane` of image rows

@@ -1697,6 +1697,27 @@ int cip_strip_rows(double* grid, const cip_gridder_params* params, int64_t npix_
   return CIP_OK;
 }
 
+int cip_strip_rows_masked(double* grid, const cip_gridder_params* params, int64_t npix_x, int64_t npix_y,
+                          int64_t y0, int64_t y1, int64_t row0, const uint32_t* tile_bits, void* hip_stream,
+                          double* H) {
+  g_last_error.clear();
+  GridGeometry g;
+  if (const int rc = strip_check(params, npix_x, npix_y, &g); rc != CIP_OK) return rc;
+  if (!grid || !H || !tile_bits) return set_error(CIP_EINVAL, "NULL grid, H or tile_bits");
+  if (y0 < 0 || y1 > g.nv || y1 <= y0) return set_error(CIP_EINVAL, "row range outside the grid");
+  if (row0 < 0 || row0 >= g.nv) return set_error(CIP_EINVAL, "row0 outside the grid");
+  if (g.ntx % 32 != 0) return set_error(CIP_EINVAL, "tile masks need nu / 32 to be a multiple of 32 tiles");
+  hipStream_t s = (hipStream_t)hip_stream;
+  Workspace* ws = workspace();
+  if (!ws) return set_error(CIP_EHIP, "no HIP device");
+  if (const int sr = settle_async(ws, s); sr != CIP_OK) return sr;
+  double* tw_u = nullptr;
+  if (const int rc = fft_twiddles(ws, g.nu, s, &tw_u); rc != CIP_OK) return rc;
+  CIP_HIP_CHECK(launch_fft_rows_strip(grid, g.nu, g.nv, npix_x, tw_u, y0, y1, H, s, tile_bits, row0));
+  CIP_HIP_CHECK(hipStreamSynchronize(s));
+  return CIP_OK;
+}
+
 int cip_strip_cols(const double* H, const cip_gridder_params* params, int64_t npix_x, int64_t npix_y, int64_t i0,
                    int64_t i1, const double* norm, void* hip_stream, double* dirty_rows) {
   g_last_error.clear();

@@ -209,7 +209,8 @@ template <int N, bool MASKED, bool ZERO = false, typename GT = double2, typename
 __global__ __launch_bounds__(N / 16) void fft_rows_kernel(GT* __restrict__ gT, int64_t hrows, int64_t nx,
                                                           const double2* __restrict__ tw, HT* __restrict__ H,
                                                           const uint32_t* __restrict__ dmask, int64_t ntx,
-                                                          int64_t y0 = 0, int64_t hy0 = 0, bool skip_clean = false) {
+                                                          int64_t y0 = 0, int64_t hy0 = 0, bool skip_clean = false,
+                                                          int64_t mrow0 = 0, int64_t mnv = 0) {
   using S = FftShape<N>;
   __shared__ double lds[N + N / 16];
   const int t = threadIdx.x;
@@ -221,7 +222,10 @@ __global__ __launch_bounds__(N / 16) void fft_rows_kernel(GT* __restrict__ gT, i
     // threads, t < T: (t + r T) / (32 kTile) = r T / 1024 for every t), so the
     // mask words are scalar loads and each lane tests one bit
     static_assert(kTile == 32 && 1024 % S::T == 0, "mask word per element uniform");
-    const uint32_t* mrow = dmask + (y / kTile) * (ntx / 32);
+    // the mask's grid row: y itself, or (a uv strip's buffer row y) grid row
+    // (mrow0 + y) mod mnv
+    const int64_t my = mnv ? (mrow0 + y) % mnv : y;
+    const uint32_t* mrow = dmask + (my / kTile) * (ntx / 32);
     uint32_t words[16];
     uint32_t any = 0u;
 #pragma unroll
@@ -406,15 +410,21 @@ hipError_t launch_fft_rows(double* gT, int64_t nu, int64_t nv, int64_t nx, const
 }
 
 hipError_t launch_fft_rows_strip(double* gT, int64_t nu, int64_t nv, int64_t nx, const double* tw_u, int64_t y0,
-                                 int64_t y1, double* H, hipStream_t s) {
+                                 int64_t y1, double* H, hipStream_t s, const uint32_t* dmask, int64_t row0) {
   if (!fft_len_ok(nu) || !fft_len_ok(nv) || nx > nu || y0 < 0 || y1 > nv || y1 <= y0) return hipErrorInvalidValue;
+  if (dmask && (nu % kTile != 0 || nv % kTile != 0 || (nu / kTile) % 32 != 0)) return hipErrorInvalidValue;
   const dim3 gd((unsigned)(y1 - y0));
   double2* g = (double2*)gT;
   const double2* tw = (const double2*)tw_u;
   double2* h = (double2*)H;
-#define ROWS(NN)                                                                                          \
-  case NN:                                                                                                \
-    fft_rows_kernel<NN, false, true><<<gd, dim3(NN / 16), 0, s>>>(g, y1 - y0, nx, tw, h, nullptr, 0, y0, y0); \
+  const int64_t ntx = nu / kTile;
+#define ROWS(NN)                                                                                               \
+  case NN:                                                                                                     \
+    if (dmask)                                                                                                 \
+      fft_rows_kernel<NN, true, false><<<gd, dim3(NN / 16), 0, s>>>(g, y1 - y0, nx, tw, h, dmask, ntx, y0, y0,  \
+                                                                     false, row0, nv);                         \
+    else                                                                                                       \
+      fft_rows_kernel<NN, false, true><<<gd, dim3(NN / 16), 0, s>>>(g, y1 - y0, nx, tw, h, nullptr, 0, y0, y0); \
     break;
   switch (nu) {
     ROWS(1024)

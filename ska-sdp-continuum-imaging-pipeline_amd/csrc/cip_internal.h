@@ -184,8 +184,12 @@ hipError_t launch_fft_cols(const double* H, int64_t nv, int64_t nx, int64_t ny, 
 // of gT (zeroed after reading) into H with y1 - y0 rows per block; pass B for
 // image rows [i0, i1) (multiples of the column block) from an H holding those
 // blocks (nv rows each), out = the strip's rows (2-D epilogue, / *norm if set)
+// dmask (may be NULL): dirty-tile bits of the whole grid (as launch_fft_rows),
+// buffer row y = grid row (row0 + y) mod nv; only the dirty tiles' cells are
+// read and zeroed (the rest of the buffer is zero)
 hipError_t launch_fft_rows_strip(double* gT, int64_t nu, int64_t nv, int64_t nx, const double* tw_u, int64_t y0,
-                                 int64_t y1, double* H, hipStream_t s);
+                                 int64_t y1, double* H, hipStream_t s, const uint32_t* dmask = nullptr,
+                                 int64_t row0 = 0);
 hipError_t launch_fft_cols_strip(const double* H, int64_t nv, int64_t nx, int64_t ny, const double* tw_v, int64_t i0,
                                  int64_t i1, double* out, const double* cx, const double* cy, const double* norm,
                                  hipStream_t s);

@@ -51,6 +51,7 @@ EXPORTED_SYMBOLS = (
     "cip_ms2dirty_wplanes",
     "cip_grid_to_dirty",
     "cip_strip_rows",
+    "cip_strip_rows_masked",
     "cip_strip_cols",
     "cip_strip_cols_wplane",
     "cip_strip_wfinal",
@@ -138,6 +139,8 @@ def lib() -> ctypes.CDLL:
     so.cip_grid_to_dirty.argtypes = [_vp, ctypes.POINTER(GridderParams), _i64, _i64, _f64, _f64, _vp, _vp]
     so.cip_strip_rows.argtypes = [_vp, ctypes.POINTER(GridderParams), _i64, _i64, _i64, _i64, _vp, _vp]
     so.cip_strip_cols.argtypes = [_vp, ctypes.POINTER(GridderParams), _i64, _i64, _i64, _i64, _vp, _vp, _vp]
+    so.cip_strip_rows_masked.argtypes = [_vp, ctypes.POINTER(GridderParams), _i64, _i64, _i64, _i64, _i64, _vp,
+                                         _vp, _vp]
     so.cip_strip_cols_wplane.argtypes = [_vp, ctypes.POINTER(GridderParams), _i64, _i64, _f64, _f64, _i64, _i64,
                                          _i64, _i32, _vp, _vp]
     so.cip_strip_wfinal.argtypes = [_vp, ctypes.POINTER(GridderParams), _i64, _i64, _f64, _f64, _i64, _i64, _vp,
@@ -153,7 +156,7 @@ def lib() -> ctypes.CDLL:
     so.cip_last_error.restype = ctypes.c_char_p
     so.cip_build_info.restype = ctypes.c_char_p
     for name in ("cip_choose_params", "cip_ms2dirty", "cip_ms2dirty_stokes_i", "cip_grid_plane", "cip_grid_layout", "cip_grid_ms", "cip_grid_ms_stokes_i",
-                 "cip_grid_tiles", "cip_grid_tiles_strip", "cip_ms2dirty_wplanes", "cip_grid_to_dirty", "cip_strip_rows", "cip_strip_cols", "cip_strip_cols_wplane", "cip_strip_wfinal", "cip_tile_runs",
+                 "cip_grid_tiles", "cip_grid_tiles_strip", "cip_ms2dirty_wplanes", "cip_grid_to_dirty", "cip_strip_rows", "cip_strip_rows_masked", "cip_strip_cols", "cip_strip_cols_wplane", "cip_strip_wfinal", "cip_tile_runs",
                  "cip_stokes_i", "cip_stokes", "cip_facet_rephase", "cip_allreduce_grid", "cip_release_collectives",
                  "cip_release_workspace", "cip_profile_enable", "cip_profile_last"):
         getattr(so, name).restype = ctypes.c_int

@@ -29,6 +29,7 @@ exchanging in memory - the single-GPU check of the decomposition.
 
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 from typing import Optional, Sequence
 
@@ -83,6 +84,68 @@ def origin_rows(v_m, fx, scale_v: float, nv: int, support: int):
     y = (v_m[:, None] * fx[None, :]) * scale_v + float(nv // 2)
     iy0 = torch.floor(y - float(support // 2)).to(torch.int64) + 1
     return torch.remainder(iy0, nv)
+
+
+TILE = 32  # the scatter's tile edge (cip_common.h kTile): the dirty-tile mask's unit
+
+
+def strip_tile_bits(data: "StripData", freq, params, pixsize_x: float, pixsize_y: float, y0: int,
+                    halo: int, chunk: int = 1 << 22):
+    """Dirty-tile bits of one rank's strip buffer after its gridding and the
+    halo add: (nplanes, nv / 32, nu / 1024) int32 words, bit tx % 32 of word
+    [p, ty, tx / 32] set when tile (tx, ty) of w plane p may hold a non-zero
+    cell (cip_strip_rows_masked then reads and zeroes only those tiles). The
+    footprint origins come from the gridder's own fp64 placement (place_vis:
+    the same operations in the same order, bit for bit), a footprint marks the
+    (up to) 2 x 2 tiles its W x W cells reach, a w layer iw0 marks planes
+    iw0 .. iw0 + W - 1; every tile of the tile rows holding the strip's first
+    W - 1 grid rows [y0, y0 + halo) is marked too (the previous rank's halo is
+    added there)."""
+    nu, nv, W = int(params.nu), int(params.nv), int(params.support)
+    ntx, nty = nu // TILE, nv // TILE
+    wstack = bool(int(params.do_wstacking))
+    nplanes = int(params.nplanes) if wstack else 1
+    nlayers = nplanes - W + 1 if wstack else 1
+    dev = data.slice_uvw.device
+    fx = freq.to(torch.float64) / SPEED_OF_LIGHT
+    su, sv = float(nu) * pixsize_x, float(nv) * pixsize_y
+    hw = float(W // 2)
+    occ = torch.zeros((nlayers, nty, ntx), dtype=torch.bool, device=dev)
+    c0 = data.chan_start.to(torch.int64)
+    lengths = data.chan_stop.to(torch.int64) - c0
+    ends = torch.cumsum(lengths, 0)
+    total = int(ends[-1]) if ends.numel() else 0
+    for a in range(0, total, chunk):
+        b = min(total, a + chunk)
+        k = torch.arange(a, b, device=dev)
+        sl = torch.searchsorted(ends, k, right=True)  # the slice of visibility k
+        ch = c0[sl] + (k - (ends[sl] - lengths[sl]))
+        f = fx[ch]
+        uvw = data.slice_uvw[sl]
+        ix0 = torch.remainder(torch.floor(((uvw[:, 0] * f) * su + float(nu // 2)) - hw).to(torch.int64) + 1, nu)
+        iy0 = torch.remainder(torch.floor(((uvw[:, 1] * f) * sv + float(nv // 2)) - hw).to(torch.int64) + 1, nv)
+        if wstack:
+            xw = ((uvw[:, 2] * f) - float(params.w0)) * (1.0 / float(params.dw))
+            iw0 = (torch.floor(xw - hw).to(torch.int64) + 1).clamp(0, nlayers - 1)
+        else:
+            iw0 = torch.zeros_like(ix0)
+        for tx in (ix0 // TILE, torch.remainder(ix0 + W - 1, nu) // TILE):
+            for ty in (iy0 // TILE, torch.remainder(iy0 + W - 1, nv) // TILE):
+                occ[iw0, ty, tx] = True
+    if wstack:
+        # plane p is fed by layers max(0, p - W + 1) .. min(p, nlayers - 1)
+        cs = torch.cumsum(torch.nn.functional.pad(occ.to(torch.int32), (0, 0, 0, 0, 1, 0)), 0)
+        pl = torch.arange(nplanes, device=dev)
+        hi = torch.clamp(pl, max=nlayers - 1) + 1
+        lo = torch.clamp(pl - W + 1, min=0)
+        mask = (cs[hi] - cs[lo]) > 0
+    else:
+        mask = occ
+    rows = torch.remainder(torch.arange(y0, y0 + max(halo, 1), device=dev), nv) // TILE
+    mask[:, rows, :] = True
+    bits = mask.view(nplanes, nty, ntx // 32, 32).to(torch.int64) << torch.arange(32, device=dev)
+    words = bits.sum(-1)
+    return torch.where(words >= (1 << 31), words - (1 << 32), words).to(torch.int32).contiguous()
 
 
 def _row_chunks(nrow: int, chunk: int = 65536):
@@ -263,6 +326,11 @@ class HipStripBackend:
             raise ValueError("strips need a grid in the pruned-FFT layout (power-of-two grids)")
         self.nplanes = int(params.nplanes) if int(params.do_wstacking) else 1
         self.single = bool(single_precision_accumulation)
+        # dirty-tile masks of the gridded strip (strip_tile_bits), cached per
+        # strip data object; CIP_STRIP_MASK=0 runs pass A over every cell
+        self.masked = os.environ.get("CIP_STRIP_MASK", "1") != "0"
+        self._bits = None
+        self._bits_key = None
         self.rows = None
         self.grid = None
         self.dirty = False
@@ -302,6 +370,12 @@ class HipStripBackend:
         if self.dirty:  # a previous invert did not finish: the buffer may hold partial sums
             self.grid.zero_()
         self.dirty = True
+        if self.masked:
+            key = (id(data), self.rows)
+            if self._bits_key is None or self._bits_key[0] != key or self._bits_key[1] is not data:
+                self._bits = strip_tile_bits(data, freq, self.params, self.px, self.py, self.rows[0],
+                                             int(self.params.support) - 1)
+                self._bits_key = (key, data)
         vis_codes, wgt_codes = _codes()
         sumw = torch.zeros(1, dtype=torch.float64, device=self.device)
         ns = int(data.slice_uvw.shape[0])
@@ -320,11 +394,17 @@ class HipStripBackend:
         """Pass A consumed the strip rows and the halo rows were zeroed."""
         self.dirty = False
 
-    def pass_rows(self, grid, y0: int, y1: int):
-        """Pass A over buffer rows [y0, y1) -> H (npix_x / 4, y1 - y0, 4, 2); zeroes the rows."""
+    def pass_rows(self, grid, y0: int, y1: int, plane: int = 0):
+        """Pass A over buffer rows [y0, y1) of w plane `plane` -> H (npix_x / 4, y1 - y0, 4, 2); zeroes the
+        rows (only the dirty tiles' cells are read when the gridded strip's mask is known)."""
         H = torch.empty((self.npix_x // COL_BLOCK, y1 - y0, COL_BLOCK, 2), dtype=torch.float64, device=self.device)
-        self._lib.check(self._lib.lib().cip_strip_rows(grid.data_ptr(), self.params, self.npix_x, self.npix_y,
-                                                       int(y0), int(y1), self._stream(), H.data_ptr()))
+        if self.masked and self._bits is not None and self.dirty:
+            self._lib.check(self._lib.lib().cip_strip_rows_masked(
+                grid.data_ptr(), self.params, self.npix_x, self.npix_y, int(y0), int(y1), int(self.rows[0]),
+                self._bits[plane].data_ptr(), self._stream(), H.data_ptr()))
+        else:
+            self._lib.check(self._lib.lib().cip_strip_rows(grid.data_ptr(), self.params, self.npix_x, self.npix_y,
+                                                           int(y0), int(y1), self._stream(), H.data_ptr()))
         return H
 
     def pass_cols(self, H, i0: int, i1: int, norm=None):
@@ -417,7 +497,7 @@ def invert_strips(data: StripData, freq, layout: StripLayout, backend, *, dst: i
         i0, i1 = layout.image_rows(rank)
         acc = torch.empty((i1 - i0, backend.npix_y), dtype=torch.float64, device=buf.device)
         for p in range(nplanes):
-            H = backend.pass_rows(buf[p], 0, h)
+            H = backend.pass_rows(buf[p], 0, h, plane=p)
             mark("rows")
             Hm = _alltoall_H(H, layout, rank, world, group) if world > 1 else H
             mark("alltoall")
@@ -537,7 +617,8 @@ def invert_strips_local(datas: Sequence[StripData], freq, layout: StripLayout, b
             i0, i1 = layout.image_rows(s)
             accs.append(torch.empty((i1 - i0, backend.npix_y), dtype=torch.float64, device=bufs[0].device))
         for p in range(nplanes):
-            Hs = [timed(r, "rows", lambda r=r: ranks[r].pass_rows(bufs[r][p], 0, hs[r])) for r in range(world)]
+            Hs = [timed(r, "rows", lambda r=r: ranks[r].pass_rows(bufs[r][p], 0, hs[r], plane=p))
+                  for r in range(world)]
             for s in range(world):
                 i0, i1 = layout.image_rows(s)
                 b0, b1 = i0 // COL_BLOCK, i1 // COL_BLOCK

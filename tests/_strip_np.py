@@ -86,7 +86,7 @@ class NumpyStripBackend:
         sumw += float(wgt.sum())
         return self.grid, sumw
 
-    def pass_rows(self, grid, y0, y1):
+    def pass_rows(self, grid, y0, y1, plane=0):
         rows = torch.view_as_complex(grid[y0:y1].contiguous()).numpy()
         F = np.fft.ifft(rows, axis=1) * self.nu
         k = (np.arange(self.npix_x) - self.npix_x // 2) % self.nu
