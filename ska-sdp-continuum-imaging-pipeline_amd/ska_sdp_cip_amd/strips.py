@@ -165,10 +165,16 @@ COST_PS_PER_CELL = 8.9
 
 def row_costs(uvw, freq, params, pixsize_x: float, pixsize_y: float):
     """Modelled cost (ps) of each grid row as a strip member: its visibilities
-    (by footprint-origin row), the row slices starting there (a slice starts
-    at each row's first channel and wherever the origin's 32-cell tile changes
-    along the channels) and its pass-A cells."""
+    (by footprint-origin row; per tap, W^2 taps per visibility, W^3 with
+    w-stacking - the C3 reference call's w-stacking strips measured 0.63 ps
+    per tap against 0.58 for C4's W = 8), the row slices starting there (a
+    slice starts at each row's first channel and wherever the origin's 32-cell
+    tile changes along the channels) and its pass-A cells (one pass per w
+    plane)."""
     nu, nv, W = int(params.nu), int(params.nv), int(params.support)
+    wstack = bool(int(getattr(params, "do_wstacking", 0)))
+    taps = W * W * (W if wstack else 1)
+    nplanes = int(params.nplanes) if wstack else 1
     fx = freq / SPEED_OF_LIGHT
     vis = torch.zeros(nv, dtype=torch.int64, device=uvw.device)
     runs = torch.zeros(nv, dtype=torch.int64, device=uvw.device)
@@ -180,7 +186,8 @@ def row_costs(uvw, freq, params, pixsize_x: float, pixsize_y: float):
         start[:, 1:] = key[:, 1:] != key[:, :-1]
         vis += torch.bincount(iy.reshape(-1), minlength=nv)
         runs += torch.bincount(iy[start], minlength=nv)
-    cost = (COST_PS_PER_VIS * vis.double() + COST_PS_PER_SLICE * runs.double() + COST_PS_PER_CELL * nu)
+    cost = (COST_PS_PER_VIS * (taps / 64.0) * vis.double() + COST_PS_PER_SLICE * runs.double() +
+            COST_PS_PER_CELL * nu * nplanes)
     return cost.cpu().numpy()
 
 
@@ -499,7 +506,7 @@ def invert_strips(data: StripData, freq, layout: StripLayout, backend, *, dst: i
         for p in range(nplanes):
             H = backend.pass_rows(buf[p], 0, h, plane=p)
             mark("rows")
-            Hm = _alltoall_H(H, layout, rank, world, group) if world > 1 else H
+            Hm = _alltoall_H(_wire(H, backend), layout, rank, world, group).to(torch.float64) if world > 1 else H
             mark("alltoall")
             backend.pass_cols_wplane(Hm, i0, i1, p, p == 0, acc)
             mark("cols")
@@ -511,11 +518,17 @@ def invert_strips(data: StripData, freq, layout: StripLayout, backend, *, dst: i
     backend.mark_clean()
     mark("rows")
     i0, i1 = layout.image_rows(rank)
-    Hm = _alltoall_H(H, layout, rank, world, group) if world > 1 else H
+    Hm = _alltoall_H(_wire(H, backend), layout, rank, world, group).to(torch.float64) if world > 1 else H
     mark("alltoall")
     rows_img = backend.pass_cols(Hm, i0, i1, norm=sumw)
     mark("cols")
     return _gather_rows(rows_img, layout, rank, world, dst, group, mark)
+
+
+def _wire(H, backend):
+    """The pass-A blocks as they cross the all-to-all: complex64 for the packed
+    class (its own precision; half the bytes), complex128 otherwise."""
+    return H.to(torch.float32) if getattr(backend, "single", False) else H
 
 
 def _alltoall_H(H, layout: StripLayout, rank: int, world: int, group):
@@ -625,8 +638,9 @@ def invert_strips_local(datas: Sequence[StripData], freq, layout: StripLayout, b
                 if world == 1:
                     Hm = Hs[0]
                 else:
-                    Hm = timed(s, "assemble", lambda b0=b0, b1=b1: _assemble_H([H[b0:b1] for H in Hs], b1 - b0,
-                                                                                layout, Hs[0].device, Hs[0].dtype))
+                    Hm = timed(s, "assemble", lambda b0=b0, b1=b1: _assemble_H(
+                        [_wire(H[b0:b1], backend) for H in Hs], b1 - b0, layout, Hs[0].device,
+                        _wire(Hs[0][:0], backend).dtype).to(torch.float64))
                 timed(s, "cols", lambda s=s, Hm=Hm, i0=i0, i1=i1: ranks[s].pass_cols_wplane(
                     Hm.contiguous(), i0, i1, p, p == 0, accs[s]))
         out = []
@@ -646,8 +660,9 @@ def invert_strips_local(datas: Sequence[StripData], freq, layout: StripLayout, b
         if world == 1:
             Hm = Hs[0]
         else:
-            Hm = timed(s, "assemble", lambda b0=b0, b1=b1: _assemble_H([H[b0:b1] for H in Hs], b1 - b0, layout,
-                                                                        Hs[0].device, Hs[0].dtype))
+            Hm = timed(s, "assemble", lambda b0=b0, b1=b1: _assemble_H(
+                [_wire(H[b0:b1], backend) for H in Hs], b1 - b0, layout, Hs[0].device,
+                _wire(Hs[0][:0], backend).dtype).to(torch.float64))
         out.append(timed(s, "cols", lambda s=s, Hm=Hm, i0=i0, i1=i1: ranks[s].pass_cols(Hm.contiguous(), i0, i1,
                                                                                          norm=sumw)))
     return torch.cat(out, dim=0)

@@ -227,7 +227,8 @@ def wstrips_model(args):
     stage_max = {k: max(p.get(k, 0.0) for p in pr) for k in ("grid", "rows", "cols", "final")}
     t1 = sum(out[1]["per_rank_ms"][0].get(k, 0.0) for k in ("grid", "rows", "cols", "final"))
     nplanes, W, nu = int(params.nplanes), int(params.support), int(params.nu)
-    H_bytes = [(npix // 4) * (b - a) * 4 * 16 for a, b in out[N]["strip_rows"]]  # one plane's pass-A output
+    # one plane's pass-A output as it crosses the all-to-all (complex64 for the packed class, strips._wire)
+    H_bytes = [(npix // 4) * (b - a) * 4 * (8 if args.single else 16) for a, b in out[N]["strip_rows"]]
     models = {}
     for link in args.link_gbs:
         bw = link * 1e9
