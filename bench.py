@@ -623,9 +623,10 @@ def main():
     ap.add_argument("--epsilon-call", action="store_true",
                     help="with --strong --wstacking: epsilon = 1e-4 picks the support (the reference's call, W = 6) "
                          "instead of --support")
-    ap.add_argument("--split", choices=("strips", "wplanes"), default="wplanes",
-                    help="with --strong --wstacking: split the w-stacking image by w-plane groups (default; "
-                         "modelled faster at 8 ranks on C3) or by uv strips")
+    ap.add_argument("--split", choices=("strips", "wplanes"), default="strips",
+                    help="with --strong --wstacking: split the w-stacking image by uv strips (default; modelled "
+                         "2.83x at 8 ranks on the C3 reference call against 2.49x for w-plane groups) or by "
+                         "w-plane groups")
     ap.add_argument("--no-strong-secondary", action="store_true",
                     help="skip the strong-scaling C4 secondary (secondary.strong_c4) of the default run")
     args = ap.parse_args()
