@@ -587,8 +587,11 @@ __global__ void radix_group_hist_kernel(const int64_t* __restrict__ hist0, int64
   hg[t] = sum;
 }
 
+#ifndef CIP_RADIX_WAVES
+#define CIP_RADIX_WAVES 1  // min waves per SIMD the radix scatter is compiled for (experiment builds)
+#endif
 template <bool V2>
-__global__ __launch_bounds__(kRadixThreads) void radix_scatter_kernel(
+__global__ __launch_bounds__(kRadixThreads, CIP_RADIX_WAVES) void radix_scatter_kernel(
     const uint32_t* __restrict__ keys, const uint64_t* __restrict__ vals, int64_t n,
     const int64_t* __restrict__ blk_cnt, int64_t nsub, int G, int shift, int64_t ngroups,
     const int64_t* __restrict__ hist, uint32_t* __restrict__ keys_out, uint64_t* __restrict__ vals_out,
