@@ -144,6 +144,10 @@ __device__ __forceinline__ VisFetch from_raw(const RawFetch<VisT, WK>& r, bool u
   return f;
 }
 
+#ifdef CIP_COUNT_KBLOCKS
+extern __device__ unsigned long long cip_kblock_count[192];
+#endif
+
 // One packed single-precision tap (CIP_ACC_SINGLE): the contributions
 // ku * kr and ku * ki rounded to integers in fp32 by one packed fma against
 // 1.5 * 2^23 (exact for |x| < 2^22, which packed_chunk_gain guarantees): the
@@ -205,9 +209,24 @@ __device__ __forceinline__ void grid_fetched_packed(const VisFetch& f, const Gri
   } else {
     float kwv[W];
     eval_kernel_f32<W>((float)yw, kwv);
+#ifdef CIP_COUNT_KBLOCKS
+    // experiment builds: per lane, slot lane counts the visits, slot 64 + lane
+    // the plane blocks it executes with work and slot 128 + lane those its
+    // wave executes (vector atomics on lane-indexed slots)
+    atomicAdd(&cip_kblock_count[threadIdx.x & 63u], 1ull);
+#endif
 #pragma unroll
     for (int k = 0; k < G; ++k) {
       const int64_t kw = plane + k - iw0;
+#ifdef CIP_COUNT_KBLOCKS
+      {
+        const unsigned ln = threadIdx.x & 63u;
+        const bool work = !(kw < 0 || kw >= W);
+        const unsigned long long any = __ballot(work);
+        if (any) atomicAdd(&cip_kblock_count[128 + ln], 1ull);
+        if (work) atomicAdd(&cip_kblock_count[64 + ln], 1ull);
+      }
+#endif
       if (kw < 0 || kw >= W) continue;  // the visibility does not feed plane + k
       if (plane + k < g.plane_lo || plane + k >= g.plane_hi) continue;  // outside the call's plane range
       float sel = 0.0f;
