@@ -33,6 +33,9 @@ namespace cip {
 #ifndef CIP_SCATTER_WAVES
 #define CIP_SCATTER_WAVES 4  // min waves per SIMD the scatter is compiled for (register budget)
 #endif
+#ifndef CIP_GROUP_THREADS
+#define CIP_GROUP_THREADS 512  // threads of a plane-group (G > 1) unit
+#endif
 constexpr int kScatterThreads = 256;
 constexpr int kRunBatch = 256;
 
@@ -381,7 +384,7 @@ __device__ __forceinline__ void grid_fetched(const VisFetch& f, const GridGeomet
 // (w-stacking plane groups; G > 1 runs 512-thread blocks holding G sub-grids).
 template <int G>
 constexpr int scatter_threads() {
-  return G == 1 ? kScatterThreads : 2 * kScatterThreads;
+  return G == 1 ? kScatterThreads : CIP_GROUP_THREADS;
 }
 template <int W, typename VisT, int WK, bool WSTACK, int PERM, bool PACK, int G = 1>
 __global__ __launch_bounds__(scatter_threads<G>(), CIP_SCATTER_WAVES) void scatter_kernel(
@@ -481,61 +484,72 @@ __global__ __launch_bounds__(scatter_threads<G>(), CIP_SCATTER_WAVES) void scatt
   // at the L2 (C4's 16384^2 grid: the flush is ~1.1 of the 4.9 ms scatter,
   // 0.28 ms less with the stores; profiles/r03_ab_flush_store.txt)
   const bool own = store_private != 0 && ch.sole != 0;
+  // packed class on complex64 planes (GridGeometry::grid_f32)
+  const bool f32 = PACK && g.grid_f32 != 0;
+  // one pass over the cells for all G planes: a cell's G sub-grid values are
+  // read together and its HBM offset (the wrap, the strip's row map, the
+  // transposed layout: ~45 VALU) is computed once, not once per plane - on the
+  // reference call's G = 5 plane groups the per-plane form was ~1/3 of the
+  // scatter's VALU instructions (7.25 -> 7.17 ms, profiles/r04_ab_flush_fused.txt)
+  for (int cell = threadIdx.x; cell < P * P; cell += NT) {
+    const int lcell = g.transposed ? (cell % P) * P + cell / P : cell;  // lx * P + ly
+    unsigned long long sv[G];  // PACK: re * 2^32 + im
+    unsigned long long si[G];  // !PACK: the im plane
+    bool any = false;
 #pragma unroll
-  for (int k = 0; k < G; ++k) {
-    if (G > 1 && plane + k >= g.nplanes) break;
-    if (G > 1 && (plane + k < g.plane_lo || plane + k >= g.plane_hi)) continue;
-    const unsigned long long* sk = sub + k * S;
-    // planes of g.rows rows (a uv strip's buffer holds its rows of every plane)
-    double* gk = grid + (int64_t)k * 2 * g.nu * g.rows;
-    // packed class on complex64 planes (GridGeometry::grid_f32)
-    float* gkf = (float*)grid + (int64_t)k * 2 * g.nu * g.rows;
-    const bool f32 = PACK && g.grid_f32 != 0;
-    for (int cell = threadIdx.x; cell < P * P; cell += NT) {
-      const int lcell = g.transposed ? (cell % P) * P + cell / P : cell;  // lx * P + ly
+    for (int k = 0; k < G; ++k) {
+      sv[k] = 0ull;
+      si[k] = 0ull;
+      if (G > 1 && (plane + k >= g.nplanes || plane + k < g.plane_lo || plane + k >= g.plane_hi)) continue;
+      sv[k] = sub[k * S + lcell];
+      if constexpr (!PACK) si[k] = sub[k * S + P * P + lcell];
+      any |= (sv[k] | si[k]) != 0ull;
+    }
+#if CIP_ABLATE == 4
+    any = any && sv[0] == 0x123456789ull;  // ablation: no flush (timing only)
+#endif
+    if (!any) continue;
+    // the sub-grid of an edge tile wraps around the periodic grid
+    int64_t gx = X0 + lcell / P, gy = Y0 + lcell % P;
+    gx -= (gx >= g.nu) ? g.nu : 0;
+    gy -= (gy >= g.nv) ? g.nv : 0;
+    const int64_t off = grid_cell_offset(g, gx, gy);
+    if (off < 0) {
+      if (g.oob) atomicOr(g.oob, 1u);
+      continue;
+    }
+    const int lx = lcell / P, ly = lcell % P;
+    const bool priv = own && lx >= W - 1 && lx < T && ly >= W - 1 && ly < T;
+#pragma unroll
+    for (int k = 0; k < G; ++k) {
+      if ((sv[k] | si[k]) == 0ull) continue;  // (also every plane outside the call's range)
       long long re, im;
       if constexpr (PACK) {
-        const unsigned long long sv = sk[lcell];
-        im = (long long)(int)(unsigned)sv;
-        re = (long long)(int)(unsigned)((sv - (unsigned long long)im) >> 32);
+        im = (long long)(int)(unsigned)sv[k];
+        re = (long long)(int)(unsigned)((sv[k] - (unsigned long long)im) >> 32);
       } else {
-        re = (long long)sk[lcell];
-        im = (long long)sk[P * P + lcell];
+        re = (long long)sv[k];
+        im = (long long)si[k];
       }
-#if CIP_ABLATE == 4
-      if (((re | im) != 0) && re == 0x123456789ll) {  // ablation: no flush (timing only)
-#else
-      if ((re | im) != 0) {
-#endif
-        // the sub-grid of an edge tile wraps around the periodic grid
-        int64_t gx = X0 + lcell / P, gy = Y0 + lcell % P;
-        gx -= (gx >= g.nu) ? g.nu : 0;
-        gy -= (gy >= g.nv) ? g.nv : 0;
-        const int64_t off = grid_cell_offset(g, gx, gy);
-        if (off < 0) {
-          if (g.oob) atomicOr(g.oob, 1u);
-          continue;
-        }
-        const int lx = lcell / P, ly = lcell % P;
-        const bool priv = own && lx >= W - 1 && lx < T && ly >= W - 1 && ly < T;
-        if (f32) {
-          float* dstf = gkf + 2 * off;
-          if (priv) {
-            *reinterpret_cast<float2*>(dstf) = make_float2((float)((double)re * inv_scale),
-                                                           (float)((double)im * inv_scale));
-          } else {
-            unsafeAtomicAdd(dstf, (float)((double)re * inv_scale));
-            unsafeAtomicAdd(dstf + 1, (float)((double)im * inv_scale));
-          }
-          continue;
-        }
-        double* dst = gk + 2 * off;
+      // planes of g.rows rows (a uv strip's buffer holds its rows of every plane)
+      const int64_t pk = (int64_t)k * 2 * g.nu * g.rows + 2 * off;
+      if (f32) {
+        float* dstf = (float*)grid + pk;
         if (priv) {
-          *reinterpret_cast<double2*>(dst) = make_double2((double)re * inv_scale, (double)im * inv_scale);
+          *reinterpret_cast<float2*>(dstf) = make_float2((float)((double)re * inv_scale),
+                                                         (float)((double)im * inv_scale));
         } else {
-          unsafeAtomicAdd(dst, (double)re * inv_scale);
-          unsafeAtomicAdd(dst + 1, (double)im * inv_scale);
+          unsafeAtomicAdd(dstf, (float)((double)re * inv_scale));
+          unsafeAtomicAdd(dstf + 1, (float)((double)im * inv_scale));
         }
+        continue;
+      }
+      double* dst = grid + pk;
+      if (priv) {
+        *reinterpret_cast<double2*>(dst) = make_double2((double)re * inv_scale, (double)im * inv_scale);
+      } else {
+        unsafeAtomicAdd(dst, (double)re * inv_scale);
+        unsafeAtomicAdd(dst + 1, (double)im * inv_scale);
       }
     }
   }
