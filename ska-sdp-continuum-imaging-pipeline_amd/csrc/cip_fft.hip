@@ -35,38 +35,64 @@ __device__ __constant__ const double kW16c[16] = {1.0,
                                                   0.70710678118654757,
                                                   0.92387953251128674};
 
+// The transform's complex type CT: double2, or float2 for the packed class
+// (complex64 planes, CIP_FFT_F32): the same passes on fp32 values and a
+// float LDS exchange array - half the LDS, so four N = 8192 workgroups share a
+// CU instead of two.
+template <typename CT>
+struct Cx;
+template <>
+struct Cx<double2> {
+  using R = double;
+  __device__ static __forceinline__ double2 make(double x, double y) { return make_double2(x, y); }
+};
+template <>
+struct Cx<float2> {
+  using R = float;
+  __device__ static __forceinline__ float2 make(float x, float y) { return make_float2(x, y); }
+};
+template <typename D, typename S>
+__device__ __forceinline__ D ccast(S v) {
+  using R = typename Cx<D>::R;
+  return Cx<D>::make((R)v.x, (R)v.y);
+}
+
 __device__ __forceinline__ double2 cmul(double2 a, double2 b) {
   return make_double2(fma(a.x, b.x, -a.y * b.y), fma(a.x, b.y, a.y * b.x));
+}
+__device__ __forceinline__ float2 cmul(float2 a, float2 b) {
+  return make_float2(fmaf(a.x, b.x, -a.y * b.y), fmaf(a.x, b.y, a.y * b.x));
 }
 
 // In-register DFT of size R (R | 16), natural order in and out, sign +.
 // Radix-2 decimation in frequency, then the bit-reversed result re-indexed
 // at compile time.
-template <int R>
-__device__ __forceinline__ void dft(double2* v) {
+template <int R, typename CT>
+__device__ __forceinline__ void dft(CT* v) {
+  using RT = typename Cx<CT>::R;
 #pragma unroll
   for (int span = R / 2; span >= 1; span >>= 1) {
 #pragma unroll
     for (int b = 0; b < R; b += 2 * span) {
 #pragma unroll
       for (int i = 0; i < span; ++i) {
-        const double2 a = v[b + i], c = v[b + i + span];
-        v[b + i] = make_double2(a.x + c.x, a.y + c.y);
-        const double2 d = make_double2(a.x - c.x, a.y - c.y);
+        const CT a = v[b + i], c = v[b + i + span];
+        v[b + i] = Cx<CT>::make(a.x + c.x, a.y + c.y);
+        const CT d = Cx<CT>::make(a.x - c.x, a.y - c.y);
         // twiddle exp(+2 pi i i / (2 span)) = W16^(i * 16 / (2 span))
         switch (2 * span) {
           case 2: v[b + i + span] = d; break;
-          case 4: v[b + i + span] = (i == 0) ? d : make_double2(-d.y, d.x); break;
+          case 4: v[b + i + span] = (i == 0) ? d : Cx<CT>::make(-d.y, d.x); break;
           default: {
             const int idx = (i * 16 / (2 * span)) & 15;
-            const double cc = kW16c[idx], ss = kW16c[(idx + 12) & 15];
-            v[b + i + span] = (i == 0) ? d : make_double2(fma(d.x, cc, -d.y * ss), fma(d.x, ss, d.y * cc));
+            const RT cc = (RT)kW16c[idx], ss = (RT)kW16c[(idx + 12) & 15];
+            v[b + i + span] = (i == 0) ? d : Cx<CT>::make(fma(d.x, cc, -d.y * ss), fma(d.x, ss, d.y * cc));
           }
         }
       }
     }
   }
-  double2 t[R];
+  CT t[R];
 #pragma unroll
   for (int i = 0; i < R; ++i) t[i] = v[i];
 #pragma unroll
@@ -81,8 +107,8 @@ __device__ __forceinline__ void dft(double2* v) {
 
 // One Stockham pass of radix R over the thread's 16 values (16 / R
 // butterflies j_m = t + m T), twiddles from the table tw[m] = exp(+2 pi i m / N).
-template <int N, int R>
-__device__ __forceinline__ void stockham_pass(double2* v, int t, int ns, const double2* __restrict__ tw) {
+template <int N, int R, typename CT>
+__device__ __forceinline__ void stockham_pass(CT* v, int t, int ns, const double2* __restrict__ tw) {
   constexpr int T = N / 16;
 #pragma unroll
   for (int m = 0; m < 16 / R; ++m) {
@@ -92,8 +118,8 @@ __device__ __forceinline__ void stockham_pass(double2* v, int t, int ns, const d
       // exp(+2 pi i r k / (ns R)) = w^r, w = tw[k N / (ns R)]: one table load
       // per butterfly (the loads were latency on the critical path), powers by
       // repeated products (error grows by ~1 ulp per power, R <= 16)
-      const double2 w = tw[(k * (N / (ns * R))) & (N - 1)];
-      double2 wr = w;
+      const CT w = ccast<CT>(tw[(k * (N / (ns * R))) & (N - 1)]);
+      CT wr = w;
 #pragma unroll
       for (int r = 1; r < R; ++r) {
         v[m * R + r] = cmul(v[m * R + r], wr);
@@ -123,8 +149,8 @@ __device__ __forceinline__ int in_pos(int t, int m, int r) {
 // exchange) then start 17 doubles apart, so 32 lanes cover all 64 banks
 __device__ __forceinline__ int pad(int p) { return p + (p >> 4); }
 
-template <int N, int R, int R2>
-__device__ __forceinline__ void exchange(double2* v, int t, int ns, double* lds) {
+template <int N, int R, int R2, typename CT>
+__device__ __forceinline__ void exchange(CT* v, int t, int ns, typename Cx<CT>::R* lds) {
   // real parts, then imaginary parts, through one N-double array
 #pragma unroll
   for (int half = 0; half < 2; ++half) {
@@ -137,7 +163,7 @@ __device__ __forceinline__ void exchange(double2* v, int t, int ns, double* lds)
     for (int m = 0; m < 16 / R2; ++m)
 #pragma unroll
       for (int r = 0; r < R2; ++r) {
-        const double x = lds[pad(in_pos<N, R2>(t, m, r))];
+        const auto x = lds[pad(in_pos<N, R2>(t, m, r))];
         if (half) v[m * R2 + r].y = x;
         else v[m * R2 + r].x = x;
       }
@@ -153,10 +179,25 @@ __device__ __forceinline__ void exchange(double2* v, int t, int ns, double* lds)
 #define CIP_FFT_COLBLOCK 4
 #endif
 constexpr int kColBlock = CIP_FFT_COLBLOCK;
+#ifndef CIP_FFT_ROWS_XCD
+#define CIP_FFT_ROWS_XCD 1  // 0: pass A's workgroup b transforms row b (A/B builds)
+#endif
 
 // All passes of an N-point transform (log2 N = 4 P + B: P radix-16 passes,
 // then one radix-2^B pass). On return v[m * RF + r] holds frequency
 // out_pos<N, RF>(t, m, r, N / RF).
+// min waves per SIMD the fp32 transforms are compiled for (A/B knob): 6 fits
+// three N = 8192 workgroups per CU in 80 VGPRs but spills, and measured slower
+// than the unconstrained 90-VGPR form (refcall FFT 5.32 vs 5.21 ms,
+// profiles/r04_ab_fft_f32.txt)
+#ifndef CIP_FFT_F32_WAVES
+#define CIP_FFT_F32_WAVES 1
+#endif
+template <typename CT>
+constexpr int fft_waves() {
+  return sizeof(CT) == 8 ? CIP_FFT_F32_WAVES : 1;
+}
+
 template <int N>
 struct FftShape {
   static constexpr int T = N / 16;
@@ -165,8 +206,8 @@ struct FftShape {
   static constexpr int RF = B ? (1 << B) : 16;  // radix of the final pass
 };
 
-template <int N>
-__device__ __forceinline__ void fft_core(double2* v, int t, double* lds, const double2* __restrict__ tw) {
+template <int N, typename CT>
+__device__ __forceinline__ void fft_core(CT* v, int t, typename Cx<CT>::R* lds, const double2* __restrict__ tw) {
   using S = FftShape<N>;
   int ns = 1;
   stockham_pass<N, 16>(v, t, ns, tw);
@@ -195,28 +236,34 @@ __device__ __forceinline__ void fft_core(double2* v, int t, double* lds, const d
 // ZERO (unmasked strips) zeroes every cell read.
 // grid cells as stored (GT = double2, or float2 for the packed class's
 // complex64 planes), widened to fp64 for the transform
-__device__ __forceinline__ double2 widen(double2 v) { return v; }
-__device__ __forceinline__ double2 widen(float2 v) { return make_double2((double)v.x, (double)v.y); }
+// (ccast: widened to the transform's type CT, or kept)
 // pass A's output as stored (HT = double2, or float2 beside complex64 planes:
 // the packed class's precision, half the pass-A write and pass-B read bytes)
-template <typename HT>
-__device__ __forceinline__ HT narrow(double2 v) {
-  if constexpr (sizeof(HT) == 8) return HT{(float)v.x, (float)v.y};
-  else return v;
-}
 
-template <int N, bool MASKED, bool ZERO = false, typename GT = double2, typename HT = double2>
-__global__ __launch_bounds__(N / 16) void fft_rows_kernel(GT* __restrict__ gT, int64_t hrows, int64_t nx,
+template <int N, bool MASKED, bool ZERO = false, typename GT = double2, typename HT = double2,
+          typename CT = double2>
+__global__ __launch_bounds__(N / 16, fft_waves<CT>()) void fft_rows_kernel(GT* __restrict__ gT, int64_t hrows, int64_t nx,
                                                           const double2* __restrict__ tw, HT* __restrict__ H,
                                                           const uint32_t* __restrict__ dmask, int64_t ntx,
                                                           int64_t y0 = 0, int64_t hy0 = 0, bool skip_clean = false,
                                                           int64_t mrow0 = 0, int64_t mnv = 0) {
   using S = FftShape<N>;
-  __shared__ double lds[N + N / 16];
+  __shared__ typename Cx<CT>::R lds[N + N / 16];
   const int t = threadIdx.x;
-  const int64_t y = y0 + blockIdx.x;
+  // rows y .. y + kColBlock - 1 share their H lines (kColBlock-column rows of
+  // 8 or 16 bytes): a group of 8 kColBlock consecutive workgroups (dispatched
+  // round-robin over the 8 XCDs) is remapped so that each XCD transforms
+  // kColBlock adjacent rows and their partial H lines meet in one L2
+  int64_t yl = blockIdx.x;
+#if CIP_FFT_ROWS_XCD
+  if (gridDim.x % (8 * kColBlock) == 0) {
+    const int64_t b = blockIdx.x;
+    yl = (b / (8 * kColBlock)) * (8 * kColBlock) + (b % 8) * kColBlock + (b / 8) % kColBlock;
+  }
+#endif
+  const int64_t y = y0 + yl;
   GT* row = gT + y * N;
-  double2 v[16];
+  CT v[16];
   if constexpr (MASKED) {
     // the 32-tile word of element r is uniform over the block (T = N / 16
     // threads, t < T: (t + r T) / (32 kTile) = r T / 1024 for every t), so the
@@ -255,11 +302,11 @@ __global__ __launch_bounds__(N / 16) void fft_rows_kernel(GT* __restrict__ gT, i
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       if constexpr (sizeof(GT) == 8) asm volatile("" : "+v"(raw[r].x), "+v"(raw[r].y));
-      v[r] = widen(raw[r]);
+      v[r] = ccast<CT>(raw[r]);
     }
   } else {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) v[r] = widen(row[t + r * S::T]);
+    for (int r = 0; r < 16; ++r) v[r] = ccast<CT>(row[t + r * S::T]);
     if constexpr (ZERO) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) row[t + r * S::T] = GT{0, 0};
@@ -272,7 +319,7 @@ __global__ __launch_bounds__(N / 16) void fft_rows_kernel(GT* __restrict__ gT, i
     for (int r = 0; r < S::RF; ++r) {
       const int k = out_pos<N, S::RF>(t, m, r, N / S::RF);
       const int64_t i = (int64_t)((k + (int)(nx / 2)) & (N - 1));
-      if (i < nx) H[((i / kColBlock) * hrows + (y - hy0)) * kColBlock + (i % kColBlock)] = narrow<HT>(v[m * S::RF + r]);
+      if (i < nx) H[((i / kColBlock) * hrows + (y - hy0)) * kColBlock + (i % kColBlock)] = ccast<HT>(v[m * S::RF + r]);
     }
 }
 
@@ -298,12 +345,12 @@ struct ColEpilogue {
 // rowbits (may be NULL: every H row is read): bit ty of the plane's tile-row
 // words - H rows y of clean tile rows (y / kTile) were not written by pass A
 // and are zero.
-template <int N, int MODE, typename HT = double2>
-__global__ __launch_bounds__(N / 16) void fft_cols_kernel(const HT* __restrict__ H, int64_t nx, int64_t ny,
+template <int N, int MODE, typename HT = double2, typename CT = double2>
+__global__ __launch_bounds__(N / 16, fft_waves<CT>()) void fft_cols_kernel(const HT* __restrict__ H, int64_t nx, int64_t ny,
                                                           const double2* __restrict__ tw, ColEpilogue ep,
                                                           int64_t i0 = 0, const uint32_t* __restrict__ rowbits = nullptr) {
   using S = FftShape<N>;
-  __shared__ double lds[N + N / 16];
+  __shared__ typename Cx<CT>::R lds[N + N / 16];
   const int t = threadIdx.x;
   const int64_t b = blockIdx.x;
   const int64_t nrows = gridDim.x;
@@ -313,7 +360,7 @@ __global__ __launch_bounds__(N / 16) void fft_cols_kernel(const HT* __restrict__
     il = (b / (8 * kColBlock)) * (8 * kColBlock) + (b % 8) * kColBlock + (b / 8) % kColBlock;
   const int64_t i = i0 + il;
   const HT* col = H + ((il / kColBlock) * N) * kColBlock + (il % kColBlock);
-  double2 v[16];
+  CT v[16];
   HT raw[16];
   if (rowbits) {
     // the row-bit word of element r (rows t + r T, tile rows (t + r T) / 32)
@@ -334,7 +381,7 @@ __global__ __launch_bounds__(N / 16) void fft_cols_kernel(const HT* __restrict__
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     if constexpr (sizeof(HT) == 8) asm volatile("" : "+v"(raw[r].x), "+v"(raw[r].y));
-    v[r] = widen(raw[r]);
+    v[r] = ccast<CT>(raw[r]);
   }
   fft_core<N>(v, t, lds, tw);
   const int64_t p = i - nx / 2;
@@ -349,7 +396,7 @@ __global__ __launch_bounds__(N / 16) void fft_cols_kernel(const HT* __restrict__
       if (j < ny) {
         const int64_t q = j - ny / 2;
         const double sgn = ((p + q) & 1) ? -1.0 : 1.0;
-        const double2 g = v[m * S::RF + r];
+        const double2 g = ccast<double2>(v[m * S::RF + r]);
         if constexpr (MODE == 0) {
           orow[j] = sgn * g.x * cxi * ep.cy[j];
         } else {
@@ -364,6 +411,16 @@ __global__ __launch_bounds__(N / 16) void fft_cols_kernel(const HT* __restrict__
         }
       }
     }
+}
+
+// CIP_FFT_F32=0: the packed class's complex64 planes transformed in fp64
+// (the round-4 form); default: in fp32, the class's own precision
+static bool fft_f32_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("CIP_FFT_F32");
+    return !(e && e[0] == '0');
+  }();
+  return on;
 }
 
 static bool fft_len_ok(int64_t n) { return n == 1024 || n == 2048 || n == 4096 || n == 8192 || n == 16384; }
@@ -384,9 +441,16 @@ hipError_t launch_fft_rows(double* gT, int64_t nu, int64_t nv, int64_t nx, const
   const double2* tw = (const double2*)tw_u;
   double2* h = (double2*)H;
   float2* hf = (float2*)H;  // complex64 planes: complex64 pass-A output
+  const bool fft_f32 = fft_f32_enabled();
 #define ROWS(NN)                                                                                              \
   case NN:                                                                                                    \
-    if (grid_f32 && dmask)                                                                                    \
+    if (grid_f32 && dmask && fft_f32)                                                                         \
+      fft_rows_kernel<NN, true, false, float2, float2, float2><<<gd, dim3(NN / 16), 0, s>>>(                  \
+          gf, nv, nx, tw, hf, dmask, ntx, 0, 0, skip_clean);                                                  \
+    else if (grid_f32 && fft_f32)                                                                             \
+      fft_rows_kernel<NN, false, false, float2, float2, float2><<<gd, dim3(NN / 16), 0, s>>>(gf, nv, nx, tw,  \
+                                                                                             hf, nullptr, 0); \
+    else if (grid_f32 && dmask)                                                                               \
       fft_rows_kernel<NN, true, false, float2, float2><<<gd, dim3(NN / 16), 0, s>>>(gf, nv, nx, tw, hf, dmask, \
                                                                                     ntx, 0, 0, skip_clean);   \
     else if (grid_f32)                                                                                        \
@@ -498,9 +562,14 @@ hipError_t launch_fft_cols(const double* H, int64_t nv, int64_t nx, int64_t ny, 
   const float2* hf = (const float2*)H;
   const double2* tw = (const double2*)tw_v;
   const ColEpilogue ep{out, cx, cy, px, py, w_plane, first, norm};
+  const bool fft_f32 = fft_f32_enabled();
 #define COLS(NN)                                                                                           \
   case NN:                                                                                                 \
-    if (h_f32 && mode == 0) fft_cols_kernel<NN, 0, float2><<<gd, dim3(NN / 16), 0, s>>>(hf, nx, ny, tw, ep, 0, rowbits); \
+    if (h_f32 && fft_f32 && mode == 0)                                                                     \
+      fft_cols_kernel<NN, 0, float2, float2><<<gd, dim3(NN / 16), 0, s>>>(hf, nx, ny, tw, ep, 0, rowbits);  \
+    else if (h_f32 && fft_f32)                                                                             \
+      fft_cols_kernel<NN, 1, float2, float2><<<gd, dim3(NN / 16), 0, s>>>(hf, nx, ny, tw, ep, 0, rowbits);  \
+    else if (h_f32 && mode == 0) fft_cols_kernel<NN, 0, float2><<<gd, dim3(NN / 16), 0, s>>>(hf, nx, ny, tw, ep, 0, rowbits); \
     else if (h_f32) fft_cols_kernel<NN, 1, float2><<<gd, dim3(NN / 16), 0, s>>>(hf, nx, ny, tw, ep, 0, rowbits);         \
     else if (mode == 0) fft_cols_kernel<NN, 0><<<gd, dim3(NN / 16), 0, s>>>(h, nx, ny, tw, ep, 0, rowbits); \
     else fft_cols_kernel<NN, 1><<<gd, dim3(NN / 16), 0, s>>>(h, nx, ny, tw, ep, 0, rowbits);              \

@@ -14,7 +14,7 @@ for rep in $(seq ${REPS:-2}); do
       esac
       timeout -k 10 200 python bench.py --no-cpu-baseline --no-strong-secondary --no-max-err --steps 10 --warmup 5 \
           > gpurun_out/ab_one.json 2> gpurun_out/ab_err.log || exit 1
-      python -c "import json; d=json.load(open('gpurun_out/ab_one.json')); r=d['secondary']['reference_call']; print('$v', d['value'], r['value'], r['phases_ms_sync'])" \
+      python -c "import json; d=json.load(open('gpurun_out/ab_one.json')); r=d['secondary']['reference_call']; print('$v', d['value'], d['phases_ms'], r['value'], r['phases_ms_sync'])" \
           >> gpurun_out/ab_refcall.txt
     ) || exit 1
   done
