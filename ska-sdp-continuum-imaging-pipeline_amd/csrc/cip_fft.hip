@@ -179,6 +179,9 @@ __device__ __forceinline__ void exchange(CT* v, int t, int ns, typename Cx<CT>::
 #define CIP_FFT_COLBLOCK 4
 #endif
 constexpr int kColBlock = CIP_FFT_COLBLOCK;
+#ifndef CIP_SCREEN_F32
+#define CIP_SCREEN_F32 1  // 0: fp64 w-screen sine / cosine on fp32 transforms too (A/B builds)
+#endif
 #ifndef CIP_FFT_ROWS_XCD
 #define CIP_FFT_ROWS_XCD 1  // 0: pass A's workgroup b transforms row b (A/B builds)
 #endif
@@ -404,7 +407,22 @@ __global__ __launch_bounds__(N / 16, fft_waves<CT>()) void fft_cols_kernel(const
           const double e = l * l + mm * mm;
           const double nm1 = -e / (sqrt(1.0 - e) + 1.0);
           double sn, cs;
-          sincospi(-2.0 * ep.w_plane * nm1, &sn, &cs);
+          const double ph = -2.0 * ep.w_plane * nm1;  // the screen's phase / pi
+          if constexpr (sizeof(CT) == 8 && CIP_SCREEN_F32 == 1) {
+            // fp32 transforms (the packed class): the phase is reduced exactly
+            // in fp64 to [-1, 1] (period 2) and only its sine and cosine are
+            // fp32 - ~1e-7, the class's own rounding of the plane values
+            const float r = (float)(ph - 2.0 * rint(0.5 * ph));
+            float sf, cf;
+            sincospif(r, &sf, &cf);
+            sn = sf;
+            cs = cf;
+          } else if constexpr (sizeof(CT) == 8 && CIP_SCREEN_F32 == 2) {
+            sn = 0.0 * ph;  // ablation (timing only, wrong images)
+            cs = 1.0;
+          } else {
+            sincospi(ph, &sn, &cs);
+          }
           const double val = sgn * (g.x * cs - g.y * sn);
           if (ep.first) orow[j] = val;
           else orow[j] += val;
