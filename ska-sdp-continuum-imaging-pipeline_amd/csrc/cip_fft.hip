@@ -412,9 +412,9 @@ __global__ __launch_bounds__(N / 16, fft_waves<CT>()) void fft_cols_kernel(const
             // fp32 transforms (the packed class): the phase is reduced exactly
             // in fp64 to [-1, 1] (period 2) and only its sine and cosine are
             // fp32 - ~1e-7, the class's own rounding of the plane values
-            const float r = (float)(ph - 2.0 * rint(0.5 * ph));
+            const float red = (float)(ph - 2.0 * rint(0.5 * ph));
             float sf, cf;
-            sincospif(r, &sf, &cf);
+            sincospif(red, &sf, &cf);
             sn = sf;
             cs = cf;
           } else if constexpr (sizeof(CT) == 8 && CIP_SCREEN_F32 == 2) {
