@@ -196,9 +196,16 @@ constexpr int kColBlock = CIP_FFT_COLBLOCK;
 #ifndef CIP_FFT_F32_WAVES
 #define CIP_FFT_F32_WAVES 1
 #endif
+#ifndef CIP_FFT_F32_WAVES_ROWS
+#define CIP_FFT_F32_WAVES_ROWS CIP_FFT_F32_WAVES  // pass A's own (A/B builds)
+#endif
 template <typename CT>
 constexpr int fft_waves() {
   return sizeof(CT) == 8 ? CIP_FFT_F32_WAVES : 1;
+}
+template <typename CT>
+constexpr int fft_waves_rows() {
+  return sizeof(CT) == 8 ? CIP_FFT_F32_WAVES_ROWS : 1;
 }
 
 template <int N>
@@ -245,7 +252,7 @@ __device__ __forceinline__ void fft_core(CT* v, int t, typename Cx<CT>::R* lds, 
 
 template <int N, bool MASKED, bool ZERO = false, typename GT = double2, typename HT = double2,
           typename CT = double2>
-__global__ __launch_bounds__(N / 16, fft_waves<CT>()) void fft_rows_kernel(GT* __restrict__ gT, int64_t hrows, int64_t nx,
+__global__ __launch_bounds__(N / 16, fft_waves_rows<CT>()) void fft_rows_kernel(GT* __restrict__ gT, int64_t hrows, int64_t nx,
                                                           const double2* __restrict__ tw, HT* __restrict__ H,
                                                           const uint32_t* __restrict__ dmask, int64_t ntx,
                                                           int64_t y0 = 0, int64_t hy0 = 0, bool skip_clean = false,
