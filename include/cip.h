@@ -200,6 +200,13 @@ int cip_grid_plane(const double* uvw, int64_t nrow, const double* freq,
 int cip_grid_layout(const cip_gridder_params* params, int64_t npix_x,
                     int64_t npix_y);
 
+/* w planes one w-stacking scatter pass grids together (the plane group: a
+ * visibility is placed once per group; 1 in 2-D mode and for supports > 16).
+ * packed != 0: the packed single class (CIP_ACC_SINGLE). Host-only. A w-plane
+ * split (cip_ms2dirty_wplanes ranges) cut on multiples of it runs no group
+ * pass twice. Replaces no reference call (ducc0 internal). */
+int cip_plane_group(const cip_gridder_params* params, int packed);
+
 /* Dense chunk: MS rows, as cip_ms2dirty (uvw (nrow,3), vis/wgt (nrow,nchan)). */
 int cip_grid_ms(const double* uvw, int64_t nrow, const double* freq,
                 int64_t nchan, const void* vis, int vis_dtype,

@@ -1566,6 +1566,12 @@ int cip_grid_layout(const cip_gridder_params* params, int64_t npix_x, int64_t np
   return fft_pruned() && fast_fft_supported(params->nu, params->nv, npix_x, npix_y) ? 1 : 0;
 }
 
+int cip_plane_group(const cip_gridder_params* params, int packed) {
+  g_last_error.clear();
+  if (!params) return set_error(CIP_EINVAL, "params is NULL");
+  return wstack_group(geometry(*params, 1.0, 1.0), packed != 0);
+}
+
 int cip_grid_ms(const double* uvw, int64_t nrow, const double* freq, int64_t nchan, const void* vis, int vis_dtype,
                 const void* wgt, int wgt_dtype, const cip_gridder_params* params, double pixsize_x, double pixsize_y,
                 int64_t npix_x, int64_t npix_y, int flags, void* hip_stream, double* grids, double* sum_wgt) {
@@ -1723,6 +1729,9 @@ int cip_strip_cols(const double* H, const cip_gridder_params* params, int64_t np
   g_last_error.clear();
   GridGeometry g;
   if (const int rc = strip_check(params, npix_x, npix_y, &g); rc != CIP_OK) return rc;
+  if (params->do_wstacking)
+    return set_error(CIP_EINVAL, "cip_strip_cols: 2-D grids only (w-stacking strips use cip_strip_cols_wplane + "
+                                 "cip_strip_wfinal)");
   if (!H || !dirty_rows) return set_error(CIP_EINVAL, "NULL H or dirty_rows");
   if (i0 < 0 || i1 > npix_x || i1 <= i0 || i0 % 4 || i1 % 4)
     return set_error(CIP_EINVAL, "image row range must be multiples of 4 inside [0, npix_x]");

@@ -44,6 +44,7 @@ EXPORTED_SYMBOLS = (
     "cip_ms2dirty_stokes_i",
     "cip_grid_plane",
     "cip_grid_layout",
+    "cip_plane_group",
     "cip_grid_ms",
     "cip_grid_ms_stokes_i",
     "cip_grid_tiles",
@@ -127,6 +128,7 @@ def lib() -> ctypes.CDLL:
     so.cip_grid_plane.argtypes = [_vp, _i64, _vp, _i64, _vp, _i32, _vp, _i32,
                                   ctypes.POINTER(GridderParams), _f64, _f64, _i64, _i32, _vp, _vp]
     so.cip_grid_layout.argtypes = [ctypes.POINTER(GridderParams), _i64, _i64]
+    so.cip_plane_group.argtypes = [ctypes.POINTER(GridderParams), _i32]
     so.cip_grid_ms.argtypes = [_vp, _i64, _vp, _i64, _vp, _i32, _vp, _i32, ctypes.POINTER(GridderParams),
                                _f64, _f64, _i64, _i64, _i32, _vp, _vp, _vp]
     so.cip_grid_ms_stokes_i.argtypes = [_vp, _i64, _vp, _i64, _vp, _vp, _vp, ctypes.POINTER(GridderParams),
@@ -155,7 +157,7 @@ def lib() -> ctypes.CDLL:
     so.cip_profile_last.argtypes = [_vp, _vp]
     so.cip_last_error.restype = ctypes.c_char_p
     so.cip_build_info.restype = ctypes.c_char_p
-    for name in ("cip_choose_params", "cip_ms2dirty", "cip_ms2dirty_stokes_i", "cip_grid_plane", "cip_grid_layout", "cip_grid_ms", "cip_grid_ms_stokes_i",
+    for name in ("cip_choose_params", "cip_ms2dirty", "cip_ms2dirty_stokes_i", "cip_grid_plane", "cip_grid_layout", "cip_plane_group", "cip_grid_ms", "cip_grid_ms_stokes_i",
                  "cip_grid_tiles", "cip_grid_tiles_strip", "cip_ms2dirty_wplanes", "cip_grid_to_dirty", "cip_strip_rows", "cip_strip_rows_masked", "cip_strip_cols", "cip_strip_cols_wplane", "cip_strip_wfinal", "cip_tile_runs",
                  "cip_stokes_i", "cip_stokes", "cip_facet_rephase", "cip_allreduce_grid", "cip_release_collectives",
                  "cip_release_workspace", "cip_profile_enable", "cip_profile_last"):
@@ -185,6 +187,14 @@ def choose_params(npix_x: int, npix_y: int, pixsize_x: float, pixsize_y: float,
                                   float(epsilon), int(support or 0), int(bool(do_wstacking)),
                                   float(wmin), float(wmax), ctypes.byref(out)))
     return out
+
+
+def plane_group(params: GridderParams, packed: bool = False) -> int:
+    """w planes one w-stacking scatter pass grids together (host-only)."""
+    g = int(lib().cip_plane_group(ctypes.byref(params), int(bool(packed))))
+    if g < 0:
+        check(g)
+    return g
 
 
 def profile_enable(on: bool = True) -> None:

@@ -228,8 +228,10 @@ class RowStreamer:
     it returned. The slots persist across calls (pinned allocation is slow).
     """
 
-    _cache = {}  # (thread id, device) -> ((rows, nchan), RowStreamer)
-    _lock = threading.Lock()
+    # per-thread slots: {device: ((rows, nchan), RowStreamer)} in a
+    # threading.local, so a worker thread's pinned slots are released with the
+    # thread and a new thread never inherits another's (ids are reused)
+    _local = threading.local()
     COLUMNS = (("uvw", np.float64, (3,)), ("vis4", np.complex64, ("c", 4)), ("flags4", np.uint8, ("c", 4)),
                ("wgt4", np.float32, ("c", 4)))
 
@@ -258,17 +260,27 @@ class RowStreamer:
         (thread, device): concurrent streamed inverts on several GPUs - e.g.
         LocalGPUClient's per-device worker threads - never evict or share each
         other's slots). A new shape replaces only this thread's slots."""
-        owner = (threading.get_ident(), str(torch.device(device)))
+        cache = getattr(cls._local, "slots", None)
+        if cache is None:
+            cache = cls._local.slots = {}
+        owner = str(torch.device(device))
         shape = (int(rows), int(nchan))
-        with cls._lock:
-            ent = cls._cache.get(owner)
-            if ent is not None and ent[0] == shape:
-                return ent[1]
-            cls._cache.pop(owner, None)
+        ent = cache.get(owner)
+        if ent is not None and ent[0] == shape:
+            return ent[1]
+        cache.pop(owner, None)  # drop the old slots before pinning new ones
         st = cls(device, rows, nchan)
-        with cls._lock:
-            cls._cache[owner] = (shape, st)
+        cache[owner] = (shape, st)
         return st
+
+    @classmethod
+    def release(cls) -> None:
+        """Free the calling thread's streamers (pinned and device slots)."""
+        cache = getattr(cls._local, "slots", None)
+        if cache:
+            for _, st in cache.values():
+                st.pool.shutdown(wait=True)
+            cache.clear()
 
     def fill(self, slot: int, reader, row0: int, row1: int) -> int:
         """Fill pinned slot `slot` with reader rows [row0, row1) (blocking;

@@ -129,8 +129,13 @@ def strip_tile_bits(data: "StripData", freq, params, pixsize_x: float, pixsize_y
             iw0 = (torch.floor(xw - hw).to(torch.int64) + 1).clamp(0, nlayers - 1)
         else:
             iw0 = torch.zeros_like(ix0)
-        for tx in (ix0 // TILE, torch.remainder(ix0 + W - 1, nu) // TILE):
-            for ty in (iy0 // TILE, torch.remainder(iy0 + W - 1, nv) // TILE):
+        # every tile the W cells from the origin reach: offsets 0, 32, 64, ...
+        # below W, and W - 1 (a footprint of W >= 34 cells crosses 3+ tiles)
+        offs = sorted(set(range(0, W, TILE)) | {W - 1})
+        txs = [torch.remainder(ix0 + d, nu) // TILE for d in offs]
+        tys = [torch.remainder(iy0 + d, nv) // TILE for d in offs]
+        for tx in txs:
+            for ty in tys:
                 occ[iw0, ty, tx] = True
     if wstack:
         # plane p is fed by layers max(0, p - W + 1) .. min(p, nlayers - 1)
@@ -378,11 +383,16 @@ class HipStripBackend:
             self.grid.zero_()
         self.dirty = True
         if self.masked:
+            # the mask depends on the data object, the strip rows AND the
+            # frequencies: a kept copy of freq is compared by value (nchan values)
             key = (id(data), self.rows)
-            if self._bits_key is None or self._bits_key[0] != key or self._bits_key[1] is not data:
+            fresh = (self._bits_key is None or self._bits_key[0] != key or self._bits_key[1] is not data
+                     or self._bits_key[2].shape != freq.shape or self._bits_key[2].dtype != freq.dtype
+                     or not torch.equal(self._bits_key[2], freq.detach().to(self._bits_key[2].device)))
+            if fresh:
                 self._bits = strip_tile_bits(data, freq, self.params, self.px, self.py, self.rows[0],
                                              int(self.params.support) - 1)
-                self._bits_key = (key, data)
+                self._bits_key = (key, data, freq.detach().clone())
         vis_codes, wgt_codes = _codes()
         sumw = torch.zeros(1, dtype=torch.float64, device=self.device)
         ns = int(data.slice_uvw.shape[0])

@@ -203,3 +203,72 @@ def pixel_size_for_grid(
 def pixel_size_asec(pixsize_lm: float) -> float:
     """Inverse of the reference's asec -> lm conversion (`invert.py:163`)."""
     return float(np.degrees(np.arcsin(pixsize_lm)) * 3600.0)
+
+
+# --- counter-based columns (strong-scaling runs: the same data at every N) ---
+
+_M32 = 0xFFFFFFFF
+
+
+def _hash32(x):
+    """A 32-bit integer finaliser on int64 tensors holding values in
+    [0, 2^32): two xorshift-multiply rounds (every product < 2^59, so the
+    int64 arithmetic never wraps; shifts act on non-negative values only)."""
+    x = (((x >> 16) ^ x) * 0x45D9F3B) & _M32
+    x = (((x >> 16) ^ x) * 0x45D9F3B) & _M32
+    return (x >> 16) ^ x
+
+
+def _uniform(idx, stream: int, seed: int):
+    """U(0, 1) float64 from the global visibility index `idx` (int64 tensor,
+    < 2^32), a stream number and a seed: a pure function of (idx, stream,
+    seed), so any rank - or any split of the rows - draws the same value."""
+    import torch  # pylint: disable=import-outside-toplevel
+
+    key = int(_hash32(torch.tensor(((seed * 0x9E3779B1) ^ (stream * 0x85EBCA6B)) & _M32, dtype=torch.int64)))
+    h = _hash32((idx ^ key) & _M32)
+    h = _hash32((h + stream * 0x27D4EB2F + 1) & _M32)
+    return (h.to(torch.float64) + 0.5) * (1.0 / 4294967296.0)
+
+
+def counter_columns(idx, seed: int = DEFAULT_SEED, flag_fraction: float = 0.05):
+    """Visibilities and weights of global visibility indices `idx` = row *
+    nchan + channel (int64 tensor, any shape, values < 2^32): complex64
+    visibilities with standard-normal real and imaginary parts (Box-Muller),
+    float32 weights U(0.5, 1.5) with `flag_fraction` of them zero (flagged).
+    The strong-scaling benchmark draws every rank's strip this way, so the
+    1G-visibility C4 image is the same image at every rank count."""
+    import torch  # pylint: disable=import-outside-toplevel
+
+    if idx.numel() and int(idx.max()) >= (1 << 32):
+        raise ValueError("counter_columns: global indices must be < 2^32")
+    u1 = _uniform(idx, 1, seed)
+    u2 = _uniform(idx, 2, seed)
+    r = torch.sqrt(-2.0 * torch.log(u1))
+    ph = (2.0 * np.pi) * u2
+    vis = torch.complex((r * torch.cos(ph)).to(torch.float32), (r * torch.sin(ph)).to(torch.float32))
+    wgt = (_uniform(idx, 3, seed) + 0.5).to(torch.float32)
+    wgt = torch.where(_uniform(idx, 4, seed) < flag_fraction, torch.zeros_like(wgt), wgt)
+    return vis.contiguous(), wgt.contiguous()
+
+
+def counter_columns_slices(rows, c0, c1, nchan: int, seed: int = DEFAULT_SEED, chunk: int = 1 << 25):
+    """`counter_columns` of Tile-layout row slices (slice s: channels
+    [c0[s], c1[s]) of MS row rows[s], visibilities concatenated in slice
+    order), drawn in chunks of `chunk` visibilities -> (vis (nvis,) complex64,
+    wgt (nvis,) float32) on the slices' device."""
+    import torch  # pylint: disable=import-outside-toplevel
+
+    rows, c0, c1 = rows.to(torch.int64), c0.to(torch.int64), c1.to(torch.int64)
+    lengths = c1 - c0
+    ends = torch.cumsum(lengths, 0)
+    total = int(ends[-1]) if ends.numel() else 0
+    vis = torch.empty(total, dtype=torch.complex64, device=rows.device)
+    wgt = torch.empty(total, dtype=torch.float32, device=rows.device)
+    for a in range(0, total, chunk):
+        b = min(total, a + chunk)
+        k = torch.arange(a, b, device=rows.device)
+        sl = torch.searchsorted(ends, k, right=True)
+        idx = rows[sl] * nchan + c0[sl] + (k - (ends[sl] - lengths[sl]))
+        vis[a:b], wgt[a:b] = counter_columns(idx, seed)
+    return vis, wgt

@@ -114,6 +114,14 @@ class HipWPlaneBackend:
         wmin, wmax = w_range_rows(uvw.cpu().numpy(), freq.cpu().numpy())
         return _lib.choose_params(nx, ny, px, py, self.kw["epsilon"], self.kw["support"] or 0, True, wmin, wmax)
 
+    def plane_group(self, params=None) -> int:
+        """The library's w-plane group for these parameters (cip_plane_group):
+        pass it to `split_planes` so no rank boundary falls inside a group."""
+        from . import _lib  # pylint: disable=import-outside-toplevel
+
+        return _lib.plane_group(self.params() if params is None else params,
+                                bool(self.kw["single_precision_accumulation"]))
+
     def __call__(self, planes, out=None, sum_weights=None):
         from .gridder import device_ms2dirty  # pylint: disable=import-outside-toplevel
 

@@ -89,3 +89,63 @@ def test_c4_shard_sampled_pixels_equal_dft(c4):
     scale = float(raw.abs().max().item()) / sumw
     assert float((out - raw / sw).abs().max().item()) <= 1e-12 * max(scale, 1e-300)
     torch.cuda.synchronize()
+
+
+def test_c4_full_eight_strips_equal_one_shot(gpu_device):
+    """The north star's strong split at C4's full size (BASELINE configs[3]:
+    1G visibilities, ONE 16384^2 grid, 8192^2 image, W = 8), 8 ranks emulated
+    on one GPU (strips.invert_strips_local: each rank grids its cost-balanced
+    uv strip into a strip + W - 1 halo buffer, halos move to the next rank,
+    pass A per strip, the pass-A blocks regroup per image-row strip (the
+    all-to-all), pass B per image-row strip), against the one-shot
+    cip_ms2dirty of the same visibilities (1e-12 of the peak: only the
+    fixed-point quantum of each gridding call differs) and against the fp64
+    DFT at sampled pixels. The visibilities are bench.py --strong's
+    counter-based columns, the same at every rank count."""
+    import torch
+
+    import dft_torch
+    from ska_sdp_cip_amd import strips
+
+    dev = torch.device("cuda", 0)
+    rows, world = 3_906_250, 8
+    uvw_h = syn.uvw_tracks(rows, N_ANT, array_radius_m=RADIUS, seed=SEED)
+    freq_h = syn.channel_frequencies(NCHAN)
+    px = syn.pixel_size_for_grid(uvw_h, freq_h, NPIX, support=8)
+    uvw, f = torch.from_numpy(uvw_h).to(dev), torch.from_numpy(freq_h).to(dev)
+    r = torch.arange(rows, device=dev)
+    vis, wgt = syn.counter_columns_slices(r, torch.zeros_like(r), torch.full_like(r, NCHAN), NCHAN, SEED)
+    vis, wgt = vis.view(rows, NCHAN), wgt.view(rows, NCHAN)
+    ref, prm = gridder.device_ms2dirty(uvw, f, vis, wgt, NPIX, NPIX, px, px, support=8, normalise=True)
+    assert (prm.nu, prm.nv) == (2 * NPIX, 2 * NPIX)
+    layout = strips.plan_strips(uvw, f, prm, px, NPIX, NPIX, world)
+    datas = []
+    for k in range(world):
+        rws, c0, c1 = strips.strip_slices(uvw, f, prm, px, *layout.rows(k))
+        datas.append(strips.gather_strip(uvw, vis, wgt, rws, c0, c1))
+    assert sum(d.nvis for d in datas) == rows * NCHAN
+    del vis, wgt
+    torch.cuda.empty_cache()
+    be = strips.HipStripBackend(prm, px, px, NPIX, NPIX, device=dev)
+    img = strips.invert_strips_local(datas, f, layout, be)
+    torch.cuda.synchronize()
+    peak = float(ref.abs().max())
+    diff = float((img - ref).abs().max())
+    print(f"C4 8 strips vs one-shot: max |diff| = {diff:.3e} (peak {peak:.3e}); strips {layout.y_bounds}")
+    assert diff < 1e-12 * peak
+    for k, b in enumerate(be.ranks):
+        assert b.rows == strips.strip_buffer_rows(layout, k)
+        assert float(b.grid.abs().max()) == 0.0 and not b.dirty
+    # the definition at sampled pixels, summed over the ranks' visibilities
+    pix = dft_torch.check_pixels(NPIX, NPIX)[:4]
+    sums, sw = np.zeros(len(pix)), 0.0
+    for d in datas:
+        s, w = dft_torch.dft_pixels_slices(d.slice_uvw, d.chan_start, d.chan_stop, f, d.vis, d.wgt, pix, NPIX, NPIX,
+                                           px, px)
+        sums, sw = sums + s, sw + w
+    got = np.array([float(img[i, j].item()) for i, j in pix])
+    err = float(np.abs(got - sums / sw).max())
+    print(f"C4 8 strips vs DFT pixels: {err:.3e} of sum w")
+    assert err < 1e-6
+    del be, datas, img, ref
+    torch.cuda.empty_cache()

@@ -186,8 +186,8 @@ def test_allreduce_grids_multi_gpu():
     assert torch.equal(ts[0].cpu(), want * torch.arange(n, dtype=torch.float64))
 
 
-@pytest.mark.parametrize("wstack", [False, True])
-def test_masked_strip_pass_a_equals_dense(gpu_device, monkeypatch, wstack):
+@pytest.mark.parametrize("wstack,support", [(False, 6), (True, 6), (False, 48), (False, 64)])
+def test_masked_strip_pass_a_equals_dense(gpu_device, monkeypatch, wstack, support):
     # cip_strip_rows_masked reads only the strip's dirty tiles; every other
     # cell is zero, so the images equal the dense pass A's bit for bit and
     # both leave the buffers clean
@@ -196,7 +196,8 @@ def test_masked_strip_pass_a_equals_dense(gpu_device, monkeypatch, wstack):
     if wstack:
         uvw = uvw * np.array([1.0, 1.0, 20.0])
     tu, tf, tv, tw = _to(gpu_device, uvw, f, vis.astype(np.complex64), w.astype(np.float32))
-    _, prm = device_ms2dirty(tu, tf, tv, tw, npix, npix, px, px, support=6, do_wstacking=wstack, normalise=True)
+    _, prm = device_ms2dirty(tu, tf, tv, tw, npix, npix, px, px, support=support, do_wstacking=wstack,
+                             normalise=True)
     world = 4
     layout = strips.plan_strips(tu, tf, prm, px, npix, npix, world)
     datas = []

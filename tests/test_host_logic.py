@@ -176,6 +176,26 @@ def test_params_match_oracle():
         _lib.choose_params(64, 64, 0.1, 0.1, 1e-4, do_wstacking=True)  # beyond the horizon
 
 
+def test_plane_group_and_wplane_split_on_its_lattice(monkeypatch):
+    # cip_plane_group is the scatter's w-plane group (cip_api.hip wstack_group):
+    # 1 in 2-D and above W = 16, 5 packed at small W, 3 / 2 in the fp64 class;
+    # split_planes with that group cuts only on group boundaries
+    from ska_sdp_cip_amd import wplanes
+
+    monkeypatch.delenv("CIP_WSTACK_GROUP", raising=False)
+    p2d = _lib.choose_params(4096, 4096, 1e-5, 1e-5, 1e-4, 8, False, 0, 0)
+    assert _lib.plane_group(p2d) == 1 and _lib.plane_group(p2d, packed=True) == 1
+    pw = _lib.choose_params(4096, 4096, 3e-6, 3e-6, 1e-4, 0, True, -60000.0, 60000.0)
+    assert pw.support == 6 and pw.nplanes > 10
+    assert _lib.plane_group(pw, packed=True) == 5 and _lib.plane_group(pw) == 3
+    pw12 = _lib.choose_params(4096, 4096, 3e-6, 3e-6, 1e-4, 12, True, -60000.0, 60000.0)
+    assert _lib.plane_group(pw12) == 2
+    g = _lib.plane_group(pw, packed=True)
+    split = wplanes.split_planes(np.ones(pw.nplanes), 3, group=g)
+    assert split[0][0] == 0 and split[-1][1] == pw.nplanes
+    assert all(a % g == 0 or a == pw.nplanes for a, _ in split[1:])
+
+
 def test_library_exports_every_declared_symbol():
     header = (ROOT / "include" / "cip.h").read_text()
     declared = set(re.findall(r"^(?:int|const char\*)\s+(cip_\w+)\(", header, flags=re.M))

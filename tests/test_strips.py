@@ -247,11 +247,12 @@ class _PW(_P):  # + the w-stacking fields strip_tile_bits reads
         self.nplanes, self.w0, self.dw = prm["nplanes"], prm["w0"], prm["dw"]
 
 
-@pytest.mark.parametrize("wstack", [False, True])
-def test_strip_tile_mask_covers_every_gridded_cell(wstack):
+@pytest.mark.parametrize("wstack,support", [(False, 8), (True, 6), (False, 48), (False, 64)])
+def test_strip_tile_mask_covers_every_gridded_cell(wstack, support):
     # cip_strip_rows_masked reads only the marked tiles: every non-zero cell of
     # a rank's gridded strip buffer (and the halo rows it receives) must lie in
-    # a marked tile of its plane, and the mask must be sparse
+    # a marked tile of its plane, and the mask must be sparse. W = 48 / 64
+    # footprints cross three 32-cell tiles per axis (the middle one included).
     from _strip_np import NumpyStripBackend
 
     npix = 512
@@ -260,9 +261,9 @@ def test_strip_tile_mask_covers_every_gridded_cell(wstack):
     if wstack:
         uvw = uvw * np.array([1.0, 1.0, 40.0])
         wmin, wmax = oracle.w_range(uvw, f)
-        prm = oracle.choose_params(npix, npix, px, px, support=6, do_wstacking=True, wmin=wmin, wmax=wmax)
+        prm = oracle.choose_params(npix, npix, px, px, support=support, do_wstacking=True, wmin=wmin, wmax=wmax)
     else:
-        prm = oracle.choose_params(npix, npix, px, px, support=8)
+        prm = oracle.choose_params(npix, npix, px, px, support=support)
     world = 3
     tu, tf = torch.from_numpy(uvw), torch.from_numpy(f)
     layout = strips.plan_strips(tu, tf, _P(prm), px, npix, npix, world)
@@ -285,4 +286,4 @@ def test_strip_tile_mask_covers_every_gridded_cell(wstack):
             words = bits[p][gy // 32, x // 1024].astype(np.int64) & 0xFFFFFFFF
             assert np.all((words >> ((x // 32) % 32)) & 1), (r, p)
             marked += int(np.unpackbits(bits[p].view(np.uint8)).sum())
-        assert marked < 0.5 * planes.shape[0] * (nu // 32) * (nv // 32)
+        assert marked < (0.5 if support <= 16 else 0.8) * planes.shape[0] * (nu // 32) * (nv // 32)

@@ -145,7 +145,7 @@ def wplanes_model(args):
     cost = wplanes.plane_cost(wplanes.plane_feeds(uvw, freq, params), params)
     out = {}
     for world in sorted({1, args.ranks}):
-        split = wplanes.split_planes(cost, world)
+        split = wplanes.split_planes(cost, world, group=be.plane_group(params))
         wplanes.invert_wplanes_local(be, split)
         torch.cuda.synchronize()
         runs = []
