@@ -382,10 +382,11 @@ int cip_release_workspace(void);
  * task_metrics.py:88-135). When enabled, hipEvents are recorded on the call's
  * stream around each phase; cip_profile_last fills
  *   ms[0..5]     = prep, plan, scatter, fft, correct, total  (milliseconds)
- *   counts[0..4] = visibilities, runs (row slices), chunks, planes, scatter launches
+ *   counts[0..5] = visibilities, runs (row slices), chunks, planes, scatter launches,
+ *                  time-pair row stride (0: the call gridded no time pairs)
  * of the most recent call. */
 #define CIP_PROFILE_PHASES 6
-#define CIP_PROFILE_COUNTS 5
+#define CIP_PROFILE_COUNTS 6
 int cip_profile_enable(int on);
 int cip_profile_last(double* ms, int64_t* counts);
 

@@ -292,6 +292,8 @@ struct PlanResult {
   Chunk* chunks = nullptr;
   void* perm = nullptr;  // bank-class ordered visibility stream (perm_encode entries), or NULL
   uint32_t* dmask = nullptr;  // grid tiles the scatter writes, per plane (bit-packed, ntx / 32 words per tile row)
+  const int64_t* pair_d = nullptr;  // time pairs: the dump stride the plan's pair flags were made with, or NULL
+  int64_t pair_stride = 0;          // its value (read back with the run count)
 };
 
 struct Workspace {
@@ -606,6 +608,15 @@ static bool chunks_full_first() {
   return on;
 }
 
+// CIP_PAIRS=0 disables the time pairs of the 2-D fp64 class (A/B experiments)
+static bool pairs_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("CIP_PAIRS");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 // CIP_SCATTER_ORDER=0 skips the bank-class order (A/B experiments)
 static bool scatter_order() {
   static const bool on = [] {
@@ -686,8 +697,11 @@ static int make_plan(Workspace* ws, const double* uvw, const double* fx, const R
   CIP_HIP_CHECK(hipMemcpyAsync(&h[0], hist0g + 256 * ng0, sizeof(int64_t), hipMemcpyDeviceToHost, s));
   CIP_HIP_CHECK(hipMemcpyAsync(&h[1], err, sizeof(unsigned), hipMemcpyDeviceToHost, s));
   CIP_HIP_CHECK(hipMemcpyAsync(&h[2], red + 1, sizeof(double), hipMemcpyDeviceToHost, s));
+  h[3] = 0;
+  if (m.pair_d) CIP_HIP_CHECK(hipMemcpyAsync(&h[3], m.pair_d, sizeof(int64_t), hipMemcpyDeviceToHost, s));
   CIP_HIP_CHECK(hipStreamSynchronize(s));
   const int64_t nruns = h[0];
+  pr->pair_stride = h[3];
   const unsigned errbits = (unsigned)h[1];
   std::memcpy(maxabs, &h[2], sizeof(double));
   if (errbits & 4u) return set_error(CIP_EINVAL, "channel frequencies must be positive");
@@ -786,6 +800,7 @@ static int make_plan(Workspace* ws, const double* uvw, const double* fx, const R
   else
     CIP_HIP_CHECK(launch_chunk_emit(tile_vis_off, tile_vis, chunk_off, run_goff, tile_runs, ntiles, cv, full_first,
                                     pr->nchunks, chunks, s));
+  pr->pair_d = m.pair_d;
   pr->runs = runs;
   pr->run_goff = run_goff;
   pr->tile_run_off = tile_runs;
@@ -1024,6 +1039,23 @@ static int prepare(Workspace* ws, const double* uvw, int64_t nrow, const double*
     out->plan.plane_chunk_off.assign((out->g.do_wstacking ? out->g.nplanes : 1) + 1, 0);  // group 1
     return CIP_OK;
   }
+  // time pairs: 2-D fp64 class on dense complex rows through
+  // the gathered bank-class order; the dump stride is detected on the device
+  // (no host round trip), and a plan reused later keeps the stride it was
+  // made with
+  m.pair_d = nullptr;
+  const bool pairable = pairs_enabled() && !ragged && !packed && !out->g.do_wstacking && out->g.support <= 16 &&
+                        (vis_dtype == CIP_C64 || vis_dtype == CIP_C128) && nrow >= 2 &&
+                        m.nvis < ((int64_t)1 << 31) && scatter_order() && order_class_mode() == ORDER_GATHER &&
+                        (want_group ? wstack_group(out->g, packed) : 1) == 1;
+  if (reusing) {
+    m.pair_d = ws->saved_plan.pair_d;
+  } else if (pairable) {
+    int64_t* pd = buf<int64_t>(ws, "pair_d", 1);
+    if (!pd) return CIP_ENOMEM;
+    CIP_HIP_CHECK(launch_pair_stride(uvw, nrow, pd, s));
+    m.pair_d = pd;
+  }
   int rc;
   if (reusing) {
     // the plan's buffers are read-only here; only the weight reduction runs
@@ -1065,6 +1097,7 @@ static int prepare(Workspace* ws, const double* uvw, int64_t nrow, const double*
   g_prof.counts[1] = out->plan.nruns;
   g_prof.counts[2] = out->plan.nchunks;
   g_prof.counts[3] = out->g.nplanes;
+  g_prof.counts[5] = out->plan.pair_d ? out->plan.pair_stride : 0;
   return rc;
 }
 

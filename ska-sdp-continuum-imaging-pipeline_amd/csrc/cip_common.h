@@ -120,6 +120,22 @@ __device__ __forceinline__ void eval_kernel(double y, double* out) {
   }
 }
 
+// The mirrored pieces k and W - 1 - k at y (z = y^2): out[0] = phi_k(y),
+// out[1] = phi_{W-1-k}(y) - eval_kernel's values, one pair at a time.
+template <int W>
+__device__ __forceinline__ void eval_piece_pair(int k, double y, double z, double* out) {
+  using K = EsKernel<W>;
+  constexpr int D = K::D;
+  double e = sgpr_const(K::coef(k, (D & 1) ? D - 1 : D));
+#pragma unroll
+  for (int d = ((D & 1) ? D - 1 : D) - 2; d >= 0; d -= 2) e = fma(e, z, sgpr_const(K::coef(k, d)));
+  double o = sgpr_const(K::coef(k, (D & 1) ? D : D - 1));
+#pragma unroll
+  for (int d = ((D & 1) ? D : D - 1) - 2; d >= 1; d -= 2) o = fma(o, z, sgpr_const(K::coef(k, d)));
+  out[0] = fma(y, o, e);
+  out[1] = fma(-y, o, e);
+}
+
 // All W kernel values at y in [-1, 1) in fp32 (the packed class): the same
 // polynomial pieces, coefficients rounded to float.
 __device__ __forceinline__ float sgpr_constf(float c) {
@@ -416,7 +432,23 @@ struct RowMap {
   // bit widths fit 64 bits (cbits = channel bits, rbits = row bits; 0 = the
   // (row << 16) | channel form, index = delta[row] + channel)
   int pk_cbits, pk_rbits;
+  // time pairs (2-D fp64 class, dense rows): device pointer to
+  // the detected row stride D of one dump (pair_stride_kernel), or NULL. Rows
+  // of even dump blocks (row / D even) pair with row + D at the same channel
+  // when both footprints start on the same cell: the planner marks the leader
+  // and the absorbed partner in the class byte, the order pass drops the
+  // absorbed entries, and the scatter grids a pair with ONE 64-bit atomic per
+  // tap and component for both visibilities.
+  const int64_t* pair_d = nullptr;
 };
+
+// Class-byte flags of a time pair (planner -> order pass): the class is bits
+// 0-4; the ordered stream marks a pair leader in bit 31 of its dense entry and
+// fills the positions of absorbed partners with kPermNull at the window's end.
+constexpr uint8_t kClassLeader = 0x80u;
+constexpr uint8_t kClassAbsorbed = 0x40u;
+constexpr uint32_t kPermLeader = 0x80000000u;
+constexpr uint32_t kPermNull = 0xffffffffu;
 
 __device__ __forceinline__ int64_t vis_index(const RowMap& m, int64_t r, int64_t c) {
   return m.delta ? m.delta[r] + c : r * m.nchan + c;

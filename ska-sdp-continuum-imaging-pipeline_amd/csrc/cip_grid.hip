@@ -124,7 +124,13 @@ __device__ __forceinline__ unsigned origin_class_f32(float us, float vs, float f
 // class array: a gathered byte per visibility cost more HBM lines than the
 // whole perm stream) and the window is counting-sorted into level-major
 // order: perm[g] = perm_encode(row, channel).
-template <bool GATHER, bool WIDE>
+// PAIRS (dense rows, gathered classes with time-pair flags, RowMap::pair_d):
+// the window's pair leaders first (their own level-major class order, entry |
+// kPermLeader), then the single visibilities (level-major), then one kPermNull
+// entry per absorbed partner - so the scatter's waves are uniformly pairs or
+// singles (one mixed wave at the boundary) and the nulls fill whole waves at
+// the window's end.
+template <bool GATHER, bool WIDE, bool PAIRS = false>
 __global__ __launch_bounds__(kOrderThreads, 8) void order_kernel(const double* __restrict__ uvw,
                                                               const double* __restrict__ fx,
                                                               const uint8_t* __restrict__ vis_class, GridGeometry g,
@@ -134,7 +140,9 @@ __global__ __launch_bounds__(kOrderThreads, 8) void order_kernel(const double* _
                                                               const Chunk* __restrict__ windows, int64_t nwindows,
                                                               void* __restrict__ perm,
                                                               const uint64_t* __restrict__ run_uv) {
-  __shared__ __attribute__((aligned(16))) unsigned s_cnt[32];
+  static_assert(!PAIRS || (GATHER && !WIDE), "time pairs: dense rows with gathered classes");
+  constexpr int NCLS = PAIRS ? 64 : 32;  // PAIRS: leaders' classes 0..31, singles' 32..63
+  __shared__ __attribute__((aligned(16))) unsigned s_cnt[NCLS];
   // the staged slices are dead once every position has its class: the level
   // tables reuse their space
   __shared__ union {
@@ -146,7 +154,7 @@ __global__ __launch_bounds__(kOrderThreads, 8) void order_kernel(const double* _
       uint16_t idx[kOrderBatch];  // slice of each position
     } a;
     struct {
-      unsigned S[kOrderBatch], M[kOrderBatch];
+      unsigned S[PAIRS ? 2 * kOrderBatch : kOrderBatch], M[PAIRS ? 2 * kOrderBatch : kOrderBatch];
     } b;
   } sh;
   float2* const s_uv = sh.a.uv;
@@ -174,7 +182,7 @@ __global__ __launch_bounds__(kOrderThreads, 8) void order_kernel(const double* _
       }
     }
   }
-  if (threadIdx.x < 32) s_cnt[threadIdx.x] = 0u;
+  if (threadIdx.x < NCLS) s_cnt[threadIdx.x] = 0u;
   __syncthreads();
   // expand: every position learns its slice (slices are <= 64 positions long)
   for (int k = threadIdx.x; k < nst; k += kOrderThreads) {
@@ -206,9 +214,14 @@ __global__ __launch_bounds__(kOrderThreads, 8) void order_kernel(const double* _
   }
 #pragma unroll
   for (int k = 0; k < kOrderPer; ++k) {
-    cls[k] = 32u;
+    cls[k] = (unsigned)NCLS;  // none (past the window)
     if (threadIdx.x + k * kOrderThreads < nsb) {
-      if constexpr (GATHER) {
+      if constexpr (PAIRS) {
+        // leaders -> 0..31, singles -> 32..63, absorbed partners -> none (64)
+        const unsigned b = vis_class[(int64_t)packed[k]];
+        cls[k] = (b & kClassAbsorbed) ? 64u : ((b & kClassLeader) ? (b & 31u) : 32u + (b & 31u));
+        if (b & kClassLeader) packed[k] |= (Entry)kPermLeader;
+      } else if constexpr (GATHER) {
         cls[k] = vis_class[WIDE ? sh.a.delta[slice[k]] + chan[k] : (int64_t)packed[k]];
       } else {
         const float2 uv = s_uv[slice[k]];
@@ -218,8 +231,43 @@ __global__ __launch_bounds__(kOrderThreads, 8) void order_kernel(const double* _
   }
 #pragma unroll
   for (int k = 0; k < kOrderPer; ++k)
-    if (cls[k] < 32u) rk[k] = atomicAdd(&s_cnt[cls[k]], 1u);
+    if (cls[k] < (unsigned)NCLS) rk[k] = atomicAdd(&s_cnt[cls[k]], 1u);
   __syncthreads();
+  if constexpr (PAIRS) {
+    // two level-major groups (leaders, singles) and the nulls after them
+    unsigned maxl = 0, maxs = 0, nlead = 0, nsing = 0;
+#pragma unroll
+    for (int i = 0; i < 32; ++i) {
+      maxl = s_cnt[i] > maxl ? s_cnt[i] : maxl;
+      maxs = s_cnt[32 + i] > maxs ? s_cnt[32 + i] : maxs;
+      nlead += s_cnt[i];
+      nsing += s_cnt[32 + i];
+    }
+    for (unsigned t = threadIdx.x; t < 2u * (unsigned)kOrderBatch; t += kOrderThreads) {
+      const unsigned grp = t / (unsigned)kOrderBatch, r = t % (unsigned)kOrderBatch;
+      if (r >= (grp ? maxs : maxl)) continue;
+      unsigned S = 0, M = 0;
+#pragma unroll
+      for (int c2 = 0; c2 < 32; ++c2) {
+        const unsigned cnt = s_cnt[32 * grp + c2];
+        S += cnt < r ? cnt : r;
+        M |= (cnt > r ? 1u : 0u) << c2;
+      }
+      s_S[t] = S;
+      s_M[t] = M;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kOrderPer; ++k) {
+      if (cls[k] < 64u) {
+        const unsigned grp = cls[k] >> 5, c = cls[k] & 31u;
+        const unsigned t = grp * (unsigned)kOrderBatch + rk[k];
+        ((Entry*)perm)[sb + (grp ? nlead : 0u) + s_S[t] + __popc(s_M[t] & ((1u << c) - 1u))] = packed[k];
+      }
+    }
+    for (int t = (int)(nlead + nsing) + threadIdx.x; t < nsb; t += kOrderThreads) ((Entry*)perm)[sb + t] = (Entry)kPermNull;
+    return;
+  }
   unsigned maxcnt = 0;
 #pragma unroll
   for (int i = 0; i < 32; ++i) maxcnt = s_cnt[i] > maxcnt ? s_cnt[i] : maxcnt;  // LDS broadcast reads
@@ -249,7 +297,10 @@ hipError_t launch_order(const double* uvw, const double* fx, const uint8_t* vis_
   order_kernel<GA, WI><<<dim3((unsigned)nwindows), dim3(kOrderThreads), 0, s>>>( \
       uvw, fx, vis_class, g, m, runs, run_goff, tile_run_off, windows, nwindows, perm, run_uv)
   const bool wide = m.delta != nullptr;  // ragged row slices: u64 entries
-  if (vis_class) {
+  if (vis_class && m.pair_d != nullptr && !wide) {
+    order_kernel<true, false, true><<<dim3((unsigned)nwindows), dim3(kOrderThreads), 0, s>>>(
+        uvw, fx, vis_class, g, m, runs, run_goff, tile_run_off, windows, nwindows, perm, run_uv);
+  } else if (vis_class) {
     if (wide) ORDER(true, true);
     else ORDER(true, false);
   } else {

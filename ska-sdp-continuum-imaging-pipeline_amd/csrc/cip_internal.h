@@ -53,6 +53,9 @@ hipError_t launch_plan_place(const double* uvw, const double* fx, const RowMap& 
                              unsigned* err_flag, uint8_t* vis_class, int64_t* blk_cnt, uint32_t* park_key,
                              uint64_t* park_run, double* partial, int64_t* hist0, hipStream_t s,
                              uint64_t* park_uv = nullptr);
+// time pairs: the row stride D of one dump (the same baseline one dump later)
+// detected from uvw on the device -> *out (0: none found; nothing pairs)
+hipError_t launch_pair_stride(const double* uvw, int64_t nrow, int64_t* out, hipStream_t s);
 // ragged rows: out[r] = chan_stop[r] - chan_start[r] (out[nrow] = 0; err bit
 // set for a range outside [0, nchan)); after the exclusive scan (off[r] = row
 // r's first visibility), launch_ragged_expand writes delta[r] = off[r] -

@@ -176,6 +176,51 @@ hipError_t launch_w_range(const double* uvw, int64_t nrow, double fxmin, double 
   return hipGetLastError();
 }
 
+// ------------------------------------------------------- time pairs ----
+// The row stride D of one dump: rows of an MS are time-major, baseline-minor,
+// so row r + D is row r's baseline one dump later, whose uvw differs by the
+// earth's rotation over the dump (~6e-4 of |uvw| for 8 s). D = the smallest d
+// for which every sampled row k (0, 1, 2, 3, nrow / 3, nrow / 2, with k + d <
+// nrow and uvw_k != 0) has |uvw_{k+d} - uvw_k| <= 1 % of |uvw_k|, with at
+// least three such rows. A performance hint only: the place pass pairs two
+// visibilities when their footprints start on the same cell, whatever D is.
+// One workgroup; candidates in blocks of 256, smallest first, stopping at the
+// first block holding a match.
+__global__ __launch_bounds__(256) void pair_stride_kernel(const double* __restrict__ uvw, int64_t nrow,
+                                                          int64_t* __restrict__ out) {
+  __shared__ unsigned long long best;
+  if (threadIdx.x == 0) best = ~0ull;
+  __syncthreads();
+  const int64_t dmax = nrow / 2 < ((int64_t)1 << 20) ? nrow / 2 : ((int64_t)1 << 20);
+  const int64_t ks[6] = {0, 1, 2, 3, nrow / 3, nrow / 2};
+  for (int64_t d0 = 1; d0 <= dmax; d0 += 256) {
+    const int64_t d = d0 + threadIdx.x;
+    if (d <= dmax) {
+      int checked = 0;
+      bool ok = true;
+      for (int i = 0; i < 6 && ok; ++i) {
+        const int64_t k = ks[i];
+        if (k + d >= nrow) continue;
+        const double a0 = uvw[3 * k], a1 = uvw[3 * k + 1], a2 = uvw[3 * k + 2];
+        const double n2 = a0 * a0 + a1 * a1 + a2 * a2;
+        if (!(n2 > 0.0)) continue;
+        const double b0 = uvw[3 * (k + d)] - a0, b1 = uvw[3 * (k + d) + 1] - a1, b2 = uvw[3 * (k + d) + 2] - a2;
+        ok = b0 * b0 + b1 * b1 + b2 * b2 <= 1e-4 * n2;
+        ++checked;
+      }
+      if (ok && checked >= 3) atomicMin(&best, (unsigned long long)d);
+    }
+    __syncthreads();
+    if (best != ~0ull) break;  // block-uniform
+  }
+  if (threadIdx.x == 0) *out = best == ~0ull ? 0 : (int64_t)best;
+}
+
+hipError_t launch_pair_stride(const double* uvw, int64_t nrow, int64_t* out, hipStream_t s) {
+  pair_stride_kernel<<<dim3(1), dim3(256), 0, s>>>(uvw, nrow, out);
+  return hipGetLastError();
+}
+
 // ---------------------------------------------------------- planner ----
 // A run is a maximal range of consecutive channels of one row with constant
 // tile key (cf. the reference's row slices, tiling_plan.py:150-181). Each
@@ -240,6 +285,12 @@ __device__ __forceinline__ void place_body(const double* __restrict__ uvw, const
   int64_t r0 = 0, c0 = 0;
   if (!ragged) split_index64((blk * kPlaceSegs + wave) * 64 + lane, nchan, m.inv_nchan, &r0, &c0);
   const int64_t step_r = 256 / nchan, step_c = 256 % nchan;
+  // time pairs (dense rows, m.pair_d): the dump stride D (0 = none)
+  int64_t pair_d = 0;
+  if constexpr (PLACE)
+    if (!ragged && m.pair_d != nullptr) pair_d = __builtin_amdgcn_readfirstlane((int)*m.pair_d);
+  const int64_t nrow_dense = ragged ? 0 : nvis / nchan;
+  const double inv_d = pair_d > 0 ? 1.0 / (double)pair_d : 0.0;
   for (int64_t seg = blk * kPlaceSegs + wave; seg < seg_end; seg += 4) {
     const int64_t i = seg * 64 + lane;
     const bool valid = i < nvis;
@@ -261,11 +312,27 @@ __device__ __forceinline__ void place_body(const double* __restrict__ uvw, const
     // position loads first: the visibility load of a PSF call is a branch,
     // and the wait inside it then covers every load (one memory round trip)
     double u = 0.0, v = 0.0, w = 0.0, f = 0.0;
+    // time pair partner: row rl + D in an even dump block, rl - D in an odd one
+    int64_t prow = rl;
+    bool pair_even = false, pair_has = false;
+    double pu = 0.0, pv = 0.0, pw = 0.0;
     if constexpr (PLACE) {
       u = uvw[3 * rl];
       v = uvw[3 * rl + 1];
       w = uvw[3 * rl + 2];
       f = fx[cl];
+      if (pair_d > 0) {
+        int64_t b = (int64_t)((double)rl * inv_d);
+        b -= (b * pair_d > rl) ? 1 : 0;
+        b += ((b + 1) * pair_d <= rl) ? 1 : 0;
+        pair_even = (b & 1) == 0;
+        const int64_t pr = pair_even ? rl + pair_d : rl - pair_d;
+        pair_has = valid && pr >= 0 && pr < nrow_dense;
+        prow = pair_has ? pr : rl;
+        pu = uvw[3 * prow];
+        pv = uvw[3 * prow + 1];
+        pw = uvw[3 * prow + 2];
+      }
     }
     if constexpr (LOADVIS) {
 #if CIP_PLACE_ABL == 4
@@ -301,9 +368,22 @@ __device__ __forceinline__ void place_body(const double* __restrict__ uvw, const
                                            (uint32_t)iw0)
                                         : kNoKey;
       const bool bad = valid & !ok;
+      // a time pair: both footprints start on the same cell (the scatter's
+      // placement, bit for bit) and both feed the call's planes; the even
+      // block's visibility leads, the odd block's is absorbed into it
+      uint8_t pair_flag = 0;
+      if (pair_d > 0) {  // wave-uniform
+        int pix0, piy0;
+        int64_t piw0;
+        const bool pok = place_origin(pu, pv, pw, f, g, &pix0, &piy0, &piw0);
+        const bool pfeeds = (piw0 + g.support > g.plane_lo) & (piw0 < g.plane_hi);
+        const bool same = pair_has & ok & feeds & pok & pfeeds & (pix0 == ix0) & (piy0 == iy0) & (piw0 == iw0);
+        pair_flag = same ? (pair_even ? kClassLeader : kClassAbsorbed) : (uint8_t)0;
+      }
 #if CIP_PLACE_ABL != 3
       if (vis_class && valid)
-        vis_class[i] = ok ? (uint8_t)((((unsigned)ix0 % kTile) * P + (unsigned)iy0 % kTile) & 31u) : (uint8_t)0;
+        vis_class[i] = ok ? (uint8_t)(((((unsigned)ix0 % kTile) * P + (unsigned)iy0 % kTile) & 31u) | pair_flag)
+                          : (uint8_t)0;
 #endif
       if (__ballot(bad) != 0ull && lane == 0) atomicOr(err_flag, 1u);
       // the previous lane's key and row: DPP wave_shr:1 (a VALU move; __shfl_up

@@ -379,6 +379,97 @@ __device__ __forceinline__ void grid_fetched(const VisFetch& f, const GridGeomet
 #endif
 }
 
+// Flush the touched cells of a work unit's sub-grid(s) to the HBM grid(s)
+// (called after the unit's last LDS atomic and a barrier).
+template <int W, bool PACK, int G, int NT>
+__device__ __forceinline__ void flush_subgrid(const unsigned long long* sub, const GridGeometry& g, int64_t plane,
+                                              int64_t X0, int64_t Y0, const Chunk& ch, int store_private,
+                                              double inv_scale, double* __restrict__ grid) {
+  constexpr int T = kTile;
+  constexpr int P = T + W - 1;
+  constexpr int S = P * P * (PACK ? 1 : 2);
+  // flush the touched cells of the sub-grid(s) to the fp64 HBM grid(s)
+  // (lanes walk the HBM grid's contiguous axis: y, or x when it is stored
+  // transposed for the pruned FFT); plane group: plane + k -> grid + k planes.
+  // A tile's cells [W - 1, T)^2 are written by its own units only (the
+  // neighbours' sub-grids reach W - 1 cells into it): when this unit is the
+  // tile's only one and the grid is zero (store_private: a cip_ms2dirty plane,
+  // not an accumulating one; set on 16384^2+ planes), those cells are stored,
+  // not added - one 16-B store instead of two read-modify-write fp64 atomics
+  // at the L2 (C4's 16384^2 grid: the flush is ~1.1 of the 4.9 ms scatter,
+  // 0.28 ms less with the stores; profiles/r03_ab_flush_store.txt)
+  const bool own = store_private != 0 && ch.sole != 0;
+  // packed class on complex64 planes (GridGeometry::grid_f32)
+  const bool f32 = PACK && g.grid_f32 != 0;
+  // one pass over the cells for all G planes: a cell's G sub-grid values are
+  // read together and its HBM offset (the wrap, the strip's row map, the
+  // transposed layout: ~45 VALU) is computed once, not once per plane - on the
+  // reference call's G = 5 plane groups the per-plane form was ~1/3 of the
+  // scatter's VALU instructions (7.25 -> 7.17 ms, profiles/r04_ab_flush_fused.txt)
+  for (int cell = threadIdx.x; cell < P * P; cell += NT) {
+    const int lcell = g.transposed ? (cell % P) * P + cell / P : cell;  // lx * P + ly
+    unsigned long long sv[G];  // PACK: re * 2^32 + im
+    unsigned long long si[G];  // !PACK: the im plane
+    bool any = false;
+#pragma unroll
+    for (int k = 0; k < G; ++k) {
+      sv[k] = 0ull;
+      si[k] = 0ull;
+      if (G > 1 && (plane + k >= g.nplanes || plane + k < g.plane_lo || plane + k >= g.plane_hi)) continue;
+      sv[k] = sub[k * S + lcell];
+      if constexpr (!PACK) si[k] = sub[k * S + P * P + lcell];
+      any |= (sv[k] | si[k]) != 0ull;
+    }
+#if CIP_ABLATE == 4
+    any = any && sv[0] == 0x123456789ull;  // ablation: no flush (timing only)
+#endif
+    if (!any) continue;
+    // the sub-grid of an edge tile wraps around the periodic grid
+    int64_t gx = X0 + lcell / P, gy = Y0 + lcell % P;
+    gx -= (gx >= g.nu) ? g.nu : 0;
+    gy -= (gy >= g.nv) ? g.nv : 0;
+    const int64_t off = grid_cell_offset(g, gx, gy);
+    if (off < 0) {
+      if (g.oob) atomicOr(g.oob, 1u);
+      continue;
+    }
+    const int lx = lcell / P, ly = lcell % P;
+    const bool priv = own && lx >= W - 1 && lx < T && ly >= W - 1 && ly < T;
+#pragma unroll
+    for (int k = 0; k < G; ++k) {
+      if ((sv[k] | si[k]) == 0ull) continue;  // (also every plane outside the call's range)
+      long long re, im;
+      if constexpr (PACK) {
+        im = (long long)(int)(unsigned)sv[k];
+        re = (long long)(int)(unsigned)((sv[k] - (unsigned long long)im) >> 32);
+      } else {
+        re = (long long)sv[k];
+        im = (long long)si[k];
+      }
+      // planes of g.rows rows (a uv strip's buffer holds its rows of every plane)
+      const int64_t pk = (int64_t)k * 2 * g.nu * g.rows + 2 * off;
+      if (f32) {
+        float* dstf = (float*)grid + pk;
+        if (priv) {
+          *reinterpret_cast<float2*>(dstf) = make_float2((float)((double)re * inv_scale),
+                                                         (float)((double)im * inv_scale));
+        } else {
+          unsafeAtomicAdd(dstf, (float)((double)re * inv_scale));
+          unsafeAtomicAdd(dstf + 1, (float)((double)im * inv_scale));
+        }
+        continue;
+      }
+      double* dst = grid + pk;
+      if (priv) {
+        *reinterpret_cast<double2*>(dst) = make_double2((double)re * inv_scale, (double)im * inv_scale);
+      } else {
+        unsafeAtomicAdd(dst, (double)re * inv_scale);
+        unsafeAtomicAdd(dst + 1, (double)im * inv_scale);
+      }
+    }
+  }
+}
+
 // PERM: 0 = tile order through the row slices, 1 / 2 = the bank-class ordered
 // stream of dense (u32) / ragged (u64) entries. G: w planes per work unit
 // (w-stacking plane groups; G > 1 runs 512-thread blocks holding G sub-grids).
@@ -473,86 +564,187 @@ __global__ __launch_bounds__(scatter_threads<G>(), CIP_SCATTER_WAVES) void scatt
     }
   }
   __syncthreads();
-  // flush the touched cells of the sub-grid(s) to the fp64 HBM grid(s)
-  // (lanes walk the HBM grid's contiguous axis: y, or x when it is stored
-  // transposed for the pruned FFT); plane group: plane + k -> grid + k planes.
-  // A tile's cells [W - 1, T)^2 are written by its own units only (the
-  // neighbours' sub-grids reach W - 1 cells into it): when this unit is the
-  // tile's only one and the grid is zero (store_private: a cip_ms2dirty plane,
-  // not an accumulating one; set on 16384^2+ planes), those cells are stored,
-  // not added - one 16-B store instead of two read-modify-write fp64 atomics
-  // at the L2 (C4's 16384^2 grid: the flush is ~1.1 of the 4.9 ms scatter,
-  // 0.28 ms less with the stores; profiles/r03_ab_flush_store.txt)
-  const bool own = store_private != 0 && ch.sole != 0;
-  // packed class on complex64 planes (GridGeometry::grid_f32)
-  const bool f32 = PACK && g.grid_f32 != 0;
-  // one pass over the cells for all G planes: a cell's G sub-grid values are
-  // read together and its HBM offset (the wrap, the strip's row map, the
-  // transposed layout: ~45 VALU) is computed once, not once per plane - on the
-  // reference call's G = 5 plane groups the per-plane form was ~1/3 of the
-  // scatter's VALU instructions (7.25 -> 7.17 ms, profiles/r04_ab_flush_fused.txt)
-  for (int cell = threadIdx.x; cell < P * P; cell += NT) {
-    const int lcell = g.transposed ? (cell % P) * P + cell / P : cell;  // lx * P + ly
-    unsigned long long sv[G];  // PACK: re * 2^32 + im
-    unsigned long long si[G];  // !PACK: the im plane
-    bool any = false;
+  flush_subgrid<W, PACK, G, NT>(sub, g, plane, X0, Y0, ch, store_private, inv_scale, grid);
+}
+
+// ------------------------------------------------------- time pairs ----
+// The 2-D fp64-class scatter over the time-paired ordered stream (dense rows,
+// RowMap::pair_d). An entry is a single visibility, a pair
+// leader (kPermLeader: row r of an even dump block, whose row r + D at the
+// same channel starts its footprint on the same cell - the planner checked it
+// with this placement, bit for bit) or kPermNull (an absorbed partner's
+// position). A pair grids BOTH visibilities with one 64-bit fixed-point
+// atomic per tap and component: fma(ku_a, kr_a, fma(ku_b, kr_b, 1.5 2^52))
+// rounds each product to the integer grid in turn, so the item's integer is a
+// fixed function of its two visibilities (the sums stay exact and
+// order-independent; within one quantum of the two separately rounded
+// contributions). At C3 58 % of the visibilities pair: 0.71 LDS items per
+// visibility.
+template <typename VisT, int WK>
+struct PairFetch {
+  using WT = typename std::conditional<WK == WK_F64, double, float>::type;
+  double u, v, fx, u2, v2;  // 2-D only: no w
+  VisT vis, vis2;
+  WT wt, wt2;
+  int kind;  // 0 null, 1 single, 2 pair
+};
+
+template <typename VisT, int WK>
+__device__ __forceinline__ void fetch_pair(uint32_t e, int64_t pair_d, const double* __restrict__ uvw,
+                                           const double* __restrict__ fx, const VisT* __restrict__ vis_ld,
+                                           bool unit_vis, const void* __restrict__ wgt, const RowMap& m,
+                                           PairFetch<VisT, WK>& f) {
+  using WT = typename PairFetch<VisT, WK>::WT;
+  // branch-free: a null entry loads visibility 0, a single its own row twice
+  f.kind = e == kPermNull ? 0 : ((e & kPermLeader) ? 2 : 1);
+  const int64_t il = e == kPermNull ? 0 : (int64_t)(e & ~kPermLeader);
+  int64_t r, c;
+  split_index64(il, m.nchan, m.inv_nchan, &r, &c);
+  const int64_t r2 = f.kind == 2 ? r + pair_d : r;
+  const int64_t il2 = f.kind == 2 ? il + pair_d * m.nchan : il;
+  f.u = uvw[3 * r];
+  f.v = uvw[3 * r + 1];
+  f.u2 = uvw[3 * r2];
+  f.v2 = uvw[3 * r2 + 1];
+  f.fx = fx[c];
+  f.vis = vis_ld[unit_vis ? 0 : il];
+  f.vis2 = vis_ld[unit_vis ? 0 : il2];
+  if constexpr (WK != WK_NONE) {
+    f.wt = ((const WT*)wgt)[il];
+    f.wt2 = ((const WT*)wgt)[il2];
+  }
+}
+
+template <int W, typename VisT, int WK>
+__device__ __forceinline__ void grid_pair(const PairFetch<VisT, WK>& f, bool unit_vis, const GridGeometry& g,
+                                          int64_t X0, int64_t Y0, double fixed_scale, unsigned long long* sub) {
+  constexpr int T = kTile;
+  constexpr int P = T + W - 1;
+  const bool pr = f.kind == 2;
+  const double wa = WK == WK_NONE ? 1.0 : (double)f.wt, wb = WK == WK_NONE ? 1.0 : (double)f.wt2;
+  if (f.kind == 0 || (wa == 0.0 && !(pr && wb != 0.0))) return;
+  int64_t ix0, iy0, iw0;
+  double yu, yv, yw;
+  if (!place_vis(f.u, f.v, 0.0, f.fx, g, &ix0, &yu, &iy0, &yv, &iw0, &yw)) return;
+  const int64_t lx = ix0 - X0, ly = iy0 - Y0;
+  if (lx < 0 || lx >= T || ly < 0 || ly >= T) return;  // never for a consistent plan
+  // the visibilities' values scaled to the fixed point (zero-weight members
+  // contribute an exact zero, whatever their values hold)
+  const double vra = wa == 0.0 ? 0.0 : (unit_vis ? 1.0 : (double)f.vis.x) * (wa * fixed_scale);
+  const double via = wa == 0.0 ? 0.0 : (unit_vis ? 0.0 : (double)f.vis.y) * (wa * fixed_scale);
+  double vrb = 0.0, vib = 0.0, yub = yu, yvb = yv;
+  if (__ballot(pr) != 0ull) {
+    int64_t jx0, jy0, jw0;
+    double ywb;
+    const bool okb = place_vis(f.u2, f.v2, 0.0, f.fx, g, &jx0, &yub, &jy0, &yvb, &jw0, &ywb);
+    const bool same = pr && okb && jx0 == ix0 && jy0 == iy0;
+    if (pr && !same && g.oob) atomicOr(g.oob, 2u);  // a plan / scatter placement mismatch (never)
+    vrb = (same && wb != 0.0) ? (unit_vis ? 1.0 : (double)f.vis2.x) * (wb * fixed_scale) : 0.0;
+    vib = (same && wb != 0.0) ? (unit_vis ? 0.0 : (double)f.vis2.y) * (wb * fixed_scale) : 0.0;
+    yub = same ? yub : yu;
+    yvb = same ? yvb : yv;
+  } else {
+    // a wave of single visibilities: the plain lane kernel
+    VisFetch a;
+    a.u = f.u;
+    a.v = f.v;
+    a.w = 0.0;
+    a.fx = f.fx;
+    a.vr = unit_vis ? 1.0 : (double)f.vis.x;
+    a.vi = unit_vis ? 0.0 : (double)f.vis.y;
+    a.wt = wa;
+    grid_fetched<W, false, false, 1>(a, g, 0, X0, Y0, fixed_scale, sub);
+    return;
+  }
+  double kra[W], kia[W], krb[W], kib[W];
+  {
+    double kv[W];
+    eval_kernel<W>(yv, kv);
 #pragma unroll
-    for (int k = 0; k < G; ++k) {
-      sv[k] = 0ull;
-      si[k] = 0ull;
-      if (G > 1 && (plane + k >= g.nplanes || plane + k < g.plane_lo || plane + k >= g.plane_hi)) continue;
-      sv[k] = sub[k * S + lcell];
-      if constexpr (!PACK) si[k] = sub[k * S + P * P + lcell];
-      any |= (sv[k] | si[k]) != 0ull;
+    for (int j = 0; j < W; ++j) {
+      kra[j] = kv[j] * vra;
+      kia[j] = kv[j] * via;
     }
-#if CIP_ABLATE == 4
-    any = any && sv[0] == 0x123456789ull;  // ablation: no flush (timing only)
-#endif
-    if (!any) continue;
-    // the sub-grid of an edge tile wraps around the periodic grid
-    int64_t gx = X0 + lcell / P, gy = Y0 + lcell % P;
-    gx -= (gx >= g.nu) ? g.nu : 0;
-    gy -= (gy >= g.nv) ? g.nv : 0;
-    const int64_t off = grid_cell_offset(g, gx, gy);
-    if (off < 0) {
-      if (g.oob) atomicOr(g.oob, 1u);
-      continue;
-    }
-    const int lx = lcell / P, ly = lcell % P;
-    const bool priv = own && lx >= W - 1 && lx < T && ly >= W - 1 && ly < T;
+    eval_kernel<W>(yvb, kv);
 #pragma unroll
-    for (int k = 0; k < G; ++k) {
-      if ((sv[k] | si[k]) == 0ull) continue;  // (also every plane outside the call's range)
-      long long re, im;
-      if constexpr (PACK) {
-        im = (long long)(int)(unsigned)sv[k];
-        re = (long long)(int)(unsigned)((sv[k] - (unsigned long long)im) >> 32);
-      } else {
-        re = (long long)sv[k];
-        im = (long long)si[k];
-      }
-      // planes of g.rows rows (a uv strip's buffer holds its rows of every plane)
-      const int64_t pk = (int64_t)k * 2 * g.nu * g.rows + 2 * off;
-      if (f32) {
-        float* dstf = (float*)grid + pk;
-        if (priv) {
-          *reinterpret_cast<float2*>(dstf) = make_float2((float)((double)re * inv_scale),
-                                                         (float)((double)im * inv_scale));
-        } else {
-          unsafeAtomicAdd(dstf, (float)((double)re * inv_scale));
-          unsafeAtomicAdd(dstf + 1, (float)((double)im * inv_scale));
-        }
-        continue;
-      }
-      double* dst = grid + pk;
-      if (priv) {
-        *reinterpret_cast<double2*>(dst) = make_double2((double)re * inv_scale, (double)im * inv_scale);
-      } else {
-        unsafeAtomicAdd(dst, (double)re * inv_scale);
-        unsafeAtomicAdd(dst + 1, (double)im * inv_scale);
+    for (int j = 0; j < W; ++j) {
+      krb[j] = kv[j] * vrb;
+      kib[j] = kv[j] * vib;
+    }
+  }
+  // the u kernels row by row, mirrored pieces k and W - 1 - k together (the
+  // even / odd halves of eval_kernel): four u values live instead of 2 W
+  unsigned long long* base = sub + (lx * P + ly);
+  const double za = yu * yu, zb = yub * yub;
+#pragma unroll
+  for (int k = 0; k < W / 2; ++k) {
+    double ua[2], ub[2];
+    eval_piece_pair<W>(k, yu, za, ua);
+    eval_piece_pair<W>(k, yub, zb, ub);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int i = h ? W - 1 - k : k;
+#pragma unroll
+      for (int j = 0; j < W; ++j) {
+        const double qr = fma(ua[h], kra[j], fma(ub[h], krb[j], kMagic));
+        const double qi = fma(ua[h], kia[j], fma(ub[h], kib[j], kMagic));
+        atomicAdd(base + (i * P + j), (unsigned long long)__double_as_longlong(qr) - 0x4338000000000000ull);
+        atomicAdd(base + P * P + (i * P + j), (unsigned long long)__double_as_longlong(qi) - 0x4338000000000000ull);
       }
     }
   }
+}
+
+#ifndef CIP_PAIR_WAVES
+#define CIP_PAIR_WAVES 3  // pipelined calls cap the scatter at 3 blocks per CU anyway (share_cus)
+#endif
+template <int W, typename VisT, int WK>
+__global__ __launch_bounds__(kScatterThreads, CIP_PAIR_WAVES) void scatter_pair_kernel(
+    const double* __restrict__ uvw, const double* __restrict__ fx, const VisT* __restrict__ vis,
+    const void* __restrict__ wgt, RowMap m, const uint32_t* __restrict__ perm, const Chunk* __restrict__ chunks,
+    int64_t chunk_begin, GridGeometry g, double fixed_scale, double inv_scale, double* __restrict__ grid,
+    int store_private) {
+  constexpr int T = kTile;
+  constexpr int P = T + W - 1;
+  constexpr int S = P * P * 2;
+  constexpr int NT = kScatterThreads;
+  __shared__ unsigned long long sub[S];
+  const Chunk ch = chunks[chunk_begin + blockIdx.x];
+  int64_t X0, Y0;
+  tile_origin(ch.tile, g, &X0, &Y0);
+  for (int i = threadIdx.x; i < S; i += NT) sub[i] = 0ull;
+  const int64_t pair_d = (int64_t)__builtin_amdgcn_readfirstlane((int)*m.pair_d);
+  __syncthreads();
+  const bool unit_vis = vis == nullptr;
+  const VisT* vis_ld = unit_vis ? (const VisT*)uvw : vis;
+  // software pipeline as scatter_kernel's: the entry of q + 512 and the data
+  // of q + 256 in flight while q grids
+  int64_t q = ch.g0 + threadIdx.x;
+  bool have = q < ch.g1;
+  PairFetch<VisT, WK> cur;
+  int64_t qn = q + NT;
+  bool hn = qn < ch.g1;
+  uint32_t pn = kPermNull;
+  if (have) {
+    fetch_pair<VisT, WK>(perm[q], pair_d, uvw, fx, vis_ld, unit_vis, wgt, m, cur);
+    pn = perm[hn ? qn : q];
+  }
+  while (have) {
+    const int64_t qnn = qn + NT;
+    const bool hnn = qnn < ch.g1;
+    const uint32_t pnn = perm[hnn ? qnn : q];
+    PairFetch<VisT, WK> nxt;
+    fetch_pair<VisT, WK>(hn ? pn : kPermNull, pair_d, uvw, fx, vis_ld, unit_vis, wgt, m, nxt);
+    grid_pair<W, VisT, WK>(cur, unit_vis, g, X0, Y0, fixed_scale, sub);
+    cur = nxt;
+    q = qn;
+    have = hn;
+    qn = qnn;
+    hn = hnn;
+    pn = pnn;
+  }
+  __syncthreads();
+  flush_subgrid<W, false, 1, NT>(sub, g, 0, X0, Y0, ch, store_private, inv_scale, grid);
 }
 
 template <int W, typename VisT, int WK>
@@ -605,6 +797,15 @@ inline hipError_t scatter_dispatch_ws(bool ws, int group, bool pack, unsigned ld
   constexpr bool kFitG4 = 4 * P2 * 8 + 4200 <= 65536;
   bool done = false;
   const bool wide = m.delta != nullptr;  // ragged row slices: u64 entries
+  if constexpr (std::is_same<VisT, float2>::value || std::is_same<VisT, double2>::value) {
+    // time pairs: 2-D fp64 class over the paired dense ordered stream
+    if (m.pair_d != nullptr && perm && !wide && !ws && !pack && group == 1) {
+      scatter_pair_kernel<W, VisT, WK><<<grid_dim, dim3(kScatterThreads), lds_extra, s>>>(
+          uvw, fx, (const VisT*)vis, wgt, m, (const uint32_t*)perm, chunks, chunk_begin, g, fs, 1.0 / fs, grid,
+          store_private);
+      return hipGetLastError();
+    }
+  }
   if constexpr (std::is_same<VisT, float2>::value || std::is_same<VisT, Pol4>::value) {
     if (pack) {
       if (perm && wide) {

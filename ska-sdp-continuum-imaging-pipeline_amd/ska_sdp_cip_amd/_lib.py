@@ -70,7 +70,7 @@ EXPORTED_SYMBOLS = (
 )
 
 PROFILE_PHASES = ("prep", "plan", "scatter", "fft", "correct", "total")
-PROFILE_COUNTS = ("visibilities", "runs", "chunks", "planes", "scatter_launches")
+PROFILE_COUNTS = ("visibilities", "runs", "chunks", "planes", "scatter_launches", "pair_stride")
 
 
 class GridderParams(ctypes.Structure):

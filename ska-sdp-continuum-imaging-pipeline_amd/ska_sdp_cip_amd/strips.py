@@ -424,6 +424,17 @@ class HipStripBackend:
                                                            int(y0), int(y1), self._stream(), H.data_ptr()))
         return H
 
+    def live_rows(self, h: int, plane: int = 0):
+        """Buffer rows [0, h) of `plane` that may hold a non-zero cell (their
+        tile row has a dirty tile in the gridded strip's mask), or None when
+        no mask is known: pass A of every other row is exactly zero."""
+        if not (self.masked and self._bits is not None):
+            return None
+        words = self._bits[plane]  # (nty, ntx / 32) int32
+        tile_live = (words != 0).any(dim=1)
+        rows = torch.remainder(torch.arange(self.rows[0], self.rows[0] + h, device=words.device), int(self.params.nv))
+        return tile_live[rows // TILE]
+
     def pass_cols(self, H, i0: int, i1: int, norm=None):
         """Pass B for image rows [i0, i1) from H ((i1 - i0) / 4, nv, 4, 2)."""
         out = torch.empty((i1 - i0, self.npix_y), dtype=torch.float64, device=self.device)
@@ -448,26 +459,35 @@ class HipStripBackend:
         return acc
 
 
-def _assemble_H(pieces: Sequence, nb: int, layout: StripLayout, device, dtype):
+def _assemble_H(pieces: Sequence, nb: int, layout: StripLayout, device, dtype, idx=None):
     """Rank s's pass-B input from every rank's pass-A blocks [i0_s / 4, i1_s / 4)
-    (piece r: (nb, h_r, 4, 2)) -> (nb, nv, 4, 2)."""
-    H = torch.empty((nb, layout.nv, COL_BLOCK, 2), dtype=dtype, device=device)
+    (piece r: (nb, h_r, 4, 2), or with idx[r] (sparse) only rank r's rows
+    idx[r] of its strip: (nb, len(idx[r]), 4, 2), the other rows zero) ->
+    (nb, nv, 4, 2)."""
+    sparse = idx is not None and any(i is not None for i in idx)
+    H = (torch.zeros if sparse else torch.empty)((nb, layout.nv, COL_BLOCK, 2), dtype=dtype, device=device)
     for r, piece in enumerate(pieces):
         y0, y1 = layout.rows(r)
-        H[:, y0:y1] = piece.reshape(nb, y1 - y0, COL_BLOCK, 2)
+        if idx is None or idx[r] is None:
+            H[:, y0:y1] = piece.reshape(nb, y1 - y0, COL_BLOCK, 2)
+        elif idx[r].numel():
+            H[:, y0 + idx[r]] = piece.reshape(nb, idx[r].numel(), COL_BLOCK, 2)
     return H
 
 
 def invert_strips(data: StripData, freq, layout: StripLayout, backend, *, dst: int = 0, group=None,
-                  stages: Optional[dict] = None):
+                  stages: Optional[dict] = None, sparse: bool = True):
     """This rank's share of the strip-distributed invert (torch.distributed
     initialised, one rank per strip). Returns the normalised dirty image
     (npix_x, npix_y) on `dst`, None elsewhere. Collectives: one point-to-point
     halo exchange with the ring neighbours, one all-to-all of the pass-A
     blocks, a scalar all-reduce of the weight sum, a gather of image rows.
     The backend is bound to this rank's strip + halo rows (`strip_buffer_rows`).
+    `sparse` (default): the all-to-all carries only the rows of the pass-A
+    output that can be non-zero (after an all-gather of the live-row masks).
     `stages` (a dict, diagnostic): each stage is synchronised and its seconds
-    added under its name (grid, halo, rows, alltoall, cols, gather)."""
+    added under its name (grid, halo, rows, alltoall, cols, gather), and the
+    all-to-all's bytes sent by this rank under a2a_send_bytes."""
     import time  # pylint: disable=import-outside-toplevel
 
     import torch.distributed as dist  # pylint: disable=import-outside-toplevel
@@ -516,7 +536,9 @@ def invert_strips(data: StripData, freq, layout: StripLayout, backend, *, dst: i
         for p in range(nplanes):
             H = backend.pass_rows(buf[p], 0, h, plane=p)
             mark("rows")
-            Hm = _alltoall_H(_wire(H, backend), layout, rank, world, group).to(torch.float64) if world > 1 else H
+            Hm = (_alltoall_H(_wire(H, backend), layout, rank, world, group,
+                              live=_live_of(backend, H, h, p) if sparse else None, stats=stages).to(torch.float64)
+                  if world > 1 else H)
             mark("alltoall")
             backend.pass_cols_wplane(Hm, i0, i1, p, p == 0, acc)
             mark("cols")
@@ -525,10 +547,12 @@ def invert_strips(data: StripData, freq, layout: StripLayout, backend, *, dst: i
         mark("final")
         return _gather_rows(rows_img, layout, rank, world, dst, group, mark)
     H = backend.pass_rows(buf, 0, h)
+    live = _live_of(backend, H, h) if (sparse and world > 1) else None
     backend.mark_clean()
     mark("rows")
     i0, i1 = layout.image_rows(rank)
-    Hm = _alltoall_H(_wire(H, backend), layout, rank, world, group).to(torch.float64) if world > 1 else H
+    Hm = (_alltoall_H(_wire(H, backend), layout, rank, world, group, live=live, stats=stages).to(torch.float64)
+          if world > 1 else H)
     mark("alltoall")
     rows_img = backend.pass_cols(Hm, i0, i1, norm=sumw)
     mark("cols")
@@ -541,21 +565,51 @@ def _wire(H, backend):
     return H.to(torch.float32) if getattr(backend, "single", False) else H
 
 
-def _alltoall_H(H, layout: StripLayout, rank: int, world: int, group):
+def _live_of(backend, H, h: int, plane: int = 0):
+    """Rows of this rank's pass-A output H (nb, h, 4, 2) that can be non-zero:
+    the backend's dirty-tile rows when it knows them, else a scan of H (a
+    row whose grid row was empty transforms to exact zeros either way)."""
+    fn = getattr(backend, "live_rows", None)
+    live = fn(h, plane) if fn is not None else None
+    if live is None:
+        live = (H != 0).reshape(H.shape[0], h, -1).any(dim=2).any(dim=0)
+    return live.to(torch.bool)
+
+
+def _alltoall_H(H, layout: StripLayout, rank: int, world: int, group, live=None, stats: Optional[dict] = None):
     """The all-to-all of pass-A blocks: rank s receives blocks [i0_s / 4,
-    i1_s / 4) of every rank's rows -> its pass-B input (nb, nv, 4, 2)."""
+    i1_s / 4) of every rank's rows -> its pass-B input (nb, nv, 4, 2).
+    Sparse (`live`, this rank's rows that can be non-zero): the ranks first
+    all-gather their live-row masks, then send only live rows; a receiver
+    fills the others with zeros. The tall edge strips of C4's cost-balanced
+    layout are mostly empty long-baseline rows."""
     import torch.distributed as dist  # pylint: disable=import-outside-toplevel
 
     h = layout.rows(rank)[1] - layout.rows(rank)[0]
-    splits_in = [(layout.image_rows(s)[1] - layout.image_rows(s)[0]) // COL_BLOCK * h * COL_BLOCK * 2
-                 for s in range(world)]
     i0, i1 = layout.image_rows(rank)
     nb = (i1 - i0) // COL_BLOCK
-    splits_out = [nb * (layout.rows(r)[1] - layout.rows(r)[0]) * COL_BLOCK * 2 for r in range(world)]
+    hs = [layout.rows(r)[1] - layout.rows(r)[0] for r in range(world)]
+    if live is None:
+        idx = [None] * world
+        counts = hs
+    else:
+        hmax = max(hs)
+        mine = torch.zeros(hmax, dtype=torch.uint8, device=H.device)
+        mine[:h] = live.to(torch.uint8)
+        allm = [torch.empty_like(mine) for _ in range(world)]
+        dist.all_gather(allm, mine, group=group)
+        idx = [torch.nonzero(allm[r][:hs[r]]).reshape(-1) for r in range(world)]
+        counts = [int(i.numel()) for i in idx]
+        H = H.index_select(1, idx[rank])  # (nb_all, live rows, 4, 2)
+    splits_in = [(layout.image_rows(s)[1] - layout.image_rows(s)[0]) // COL_BLOCK * counts[rank] * COL_BLOCK * 2
+                 for s in range(world)]
+    splits_out = [nb * counts[r] * COL_BLOCK * 2 for r in range(world)]
+    if stats is not None:
+        stats["a2a_send_bytes"] = stats.get("a2a_send_bytes", 0) + sum(splits_in) * H.element_size()
     recv = torch.empty(sum(splits_out), dtype=H.dtype, device=H.device)
     dist.all_to_all_single(recv, H.reshape(-1), splits_out, splits_in, group=group)
     pieces = list(torch.split(recv, splits_out))
-    return _assemble_H(pieces, nb, layout, H.device, H.dtype)
+    return _assemble_H(pieces, nb, layout, H.device, H.dtype, idx)
 
 
 def _gather_rows(rows_img, layout: StripLayout, rank: int, world: int, dst: int, group, mark):
@@ -576,8 +630,32 @@ def _gather_rows(rows_img, layout: StripLayout, rank: int, world: int, dst: int,
     return torch.cat([g[:layout.image_rows(r)[1] - layout.image_rows(r)[0]] for r, g in enumerate(gathered)])
 
 
+def _count_a2a(stages, Hs, lives, layout: StripLayout, backend):
+    """Add each rank's all-to-all send bytes (to the other ranks) to its
+    stage dict: (N - 1) / N of its (live) pass-A rows on the wire."""
+    if stages is None or layout.world == 1:
+        return
+    esize = _wire(Hs[0][:0], backend).element_size()
+    for r, H in enumerate(Hs):
+        rows = int(lives[r].sum()) if lives is not None else H.shape[1]
+        i0, i1 = layout.image_rows(r)
+        own = (i1 - i0) // COL_BLOCK
+        stages[r]["a2a_send_bytes"] = stages[r].get("a2a_send_bytes", 0) + \
+            (H.shape[0] - own) * rows * COL_BLOCK * 2 * esize
+
+
+def _local_pieces(Hs, b0: int, b1: int, backend, lives):
+    """The emulated all-to-all for one receiver: blocks [b0, b1) of every
+    rank's H, only its live rows when `lives` (sparse) - as _alltoall_H
+    sends them."""
+    if lives is None:
+        return [_wire(H[b0:b1], backend) for H in Hs], None
+    idx = [torch.nonzero(lv).reshape(-1) for lv in lives]
+    return [_wire(H[b0:b1].index_select(1, i), backend) for H, i in zip(Hs, idx)], idx
+
+
 def invert_strips_local(datas: Sequence[StripData], freq, layout: StripLayout, backend,
-                        stages: Optional[list] = None):
+                        stages: Optional[list] = None, sparse: bool = True):
     """All ranks' stages in ONE process on one device, the exchanges done in
     memory (the single-GPU check of the decomposition and its kernels, and the
     per-rank cost breakdown of the N-GPU split). Rank r's stages run on its
@@ -585,9 +663,12 @@ def invert_strips_local(datas: Sequence[StripData], freq, layout: StripLayout, b
     `backend.ranks`), in the distributed order: every rank grids its strip,
     the halos move to the next rank, pass A runs per strip, the pass-A blocks
     are regrouped per image-row strip (the all-to-all) and pass B runs per
-    image-row strip. `stages` (a list, diagnostic): filled with one dict per
-    rank of synchronised seconds (grid, halo, rows, assemble, cols). Returns
-    the normalised dirty image (npix_x, npix_y)."""
+    image-row strip. `sparse`: the regrouping moves only each rank's live
+    rows (as the distributed sparse all-to-all). `stages` (a list,
+    diagnostic): filled with one dict per rank of synchronised seconds (grid,
+    halo, rows, assemble, cols) and the bytes the rank would send in the
+    all-to-all (a2a_send_bytes). Returns the normalised dirty image
+    (npix_x, npix_y)."""
     import time  # pylint: disable=import-outside-toplevel
 
     world = layout.world
@@ -642,15 +723,19 @@ def invert_strips_local(datas: Sequence[StripData], freq, layout: StripLayout, b
         for p in range(nplanes):
             Hs = [timed(r, "rows", lambda r=r: ranks[r].pass_rows(bufs[r][p], 0, hs[r], plane=p))
                   for r in range(world)]
+            lives = [_live_of(ranks[r], Hs[r], hs[r], p) for r in range(world)] if (sparse and world > 1) else None
+            _count_a2a(stages, Hs, lives, layout, backend)
             for s in range(world):
                 i0, i1 = layout.image_rows(s)
                 b0, b1 = i0 // COL_BLOCK, i1 // COL_BLOCK
                 if world == 1:
                     Hm = Hs[0]
                 else:
-                    Hm = timed(s, "assemble", lambda b0=b0, b1=b1: _assemble_H(
-                        [_wire(H[b0:b1], backend) for H in Hs], b1 - b0, layout, Hs[0].device,
-                        _wire(Hs[0][:0], backend).dtype).to(torch.float64))
+                    def regroup(b0=b0, b1=b1):
+                        pieces, idx = _local_pieces(Hs, b0, b1, backend, lives)
+                        return _assemble_H(pieces, b1 - b0, layout, Hs[0].device, _wire(Hs[0][:0], backend).dtype,
+                                           idx).to(torch.float64)
+                    Hm = timed(s, "assemble", regroup)
                 timed(s, "cols", lambda s=s, Hm=Hm, i0=i0, i1=i1: ranks[s].pass_cols_wplane(
                     Hm.contiguous(), i0, i1, p, p == 0, accs[s]))
         out = []
@@ -659,10 +744,13 @@ def invert_strips_local(datas: Sequence[StripData], freq, layout: StripLayout, b
             i0, i1 = layout.image_rows(s)
             out.append(timed(s, "final", lambda s=s, i0=i0, i1=i1: ranks[s].finish_rows(accs[s], i0, i1, norm=sumw)))
         return torch.cat(out, dim=0)
-    Hs = []
+    Hs, lives = [], []
     for r in range(world):
         Hs.append(timed(r, "rows", lambda r=r: ranks[r].pass_rows(bufs[r], 0, hs[r])))
+        lives.append(_live_of(ranks[r], Hs[r], hs[r]) if (sparse and world > 1) else None)
         ranks[r].mark_clean()
+    lives = lives if (sparse and world > 1) else None
+    _count_a2a(stages, Hs, lives, layout, backend)
     out = []
     for s in range(world):
         i0, i1 = layout.image_rows(s)
@@ -670,9 +758,11 @@ def invert_strips_local(datas: Sequence[StripData], freq, layout: StripLayout, b
         if world == 1:
             Hm = Hs[0]
         else:
-            Hm = timed(s, "assemble", lambda b0=b0, b1=b1: _assemble_H(
-                [_wire(H[b0:b1], backend) for H in Hs], b1 - b0, layout, Hs[0].device,
-                _wire(Hs[0][:0], backend).dtype).to(torch.float64))
+            def regroup(b0=b0, b1=b1):
+                pieces, idx = _local_pieces(Hs, b0, b1, backend, lives)
+                return _assemble_H(pieces, b1 - b0, layout, Hs[0].device, _wire(Hs[0][:0], backend).dtype,
+                                   idx).to(torch.float64)
+            Hm = timed(s, "assemble", regroup)
         out.append(timed(s, "cols", lambda s=s, Hm=Hm, i0=i0, i1=i1: ranks[s].pass_cols(Hm.contiguous(), i0, i1,
                                                                                          norm=sumw)))
     return torch.cat(out, dim=0)

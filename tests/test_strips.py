@@ -287,3 +287,34 @@ def test_strip_tile_mask_covers_every_gridded_cell(wstack, support):
             assert np.all((words >> ((x // 32) % 32)) & 1), (r, p)
             marked += int(np.unpackbits(bits[p].view(np.uint8)).sum())
         assert marked < (0.5 if support <= 16 else 0.8) * planes.shape[0] * (nu // 32) * (nv // 32)
+
+
+@pytest.mark.parametrize("wstack", [False, True])
+def test_sparse_alltoall_equals_dense_and_sends_less(wstack):
+    # the all-to-all carries only each rank's live pass-A rows (rows of an empty
+    # grid row transform to exact zeros): the same image bit for bit, fewer
+    # bytes. A concentrated uv coverage (short baselines) on a 256^2 image
+    # leaves most grid rows empty.
+    from _strip_np import NumpyStripBackend
+
+    npix, world, W = 256, 4, 6
+    uvw, f, vis, w, _ = _case(nrow=700, nchan=8)
+    px = syn.pixel_size_for_grid(uvw, f, npix) * 0.3  # the tracks fill ~30 % of the uv plane
+    if wstack:
+        wmin, wmax = oracle.w_range(uvw, f)
+        prm = oracle.choose_params(npix, npix, px, px, support=W, do_wstacking=True, wmin=wmin, wmax=wmax)
+    else:
+        prm = oracle.choose_params(npix, npix, px, px, support=W)
+    layout = strips.plan_strips(torch.from_numpy(uvw), torch.from_numpy(f), _P(prm), px, npix, npix, world,
+                                balance="vis")
+    datas = _strip_datas(uvw, f, vis, w, px, prm, layout)
+    imgs, sent = {}, {}
+    for sparse in (False, True):
+        be = NumpyStripBackend(prm, px, px, npix, npix)
+        st = []
+        imgs[sparse] = strips.invert_strips_local(datas, torch.from_numpy(f), layout, be, stages=st,
+                                                  sparse=sparse).numpy()
+        sent[sparse] = sum(s["a2a_send_bytes"] for s in st)
+    # (the oracle's OpenMP gridding sums in thread order: ~1e-16 run to run)
+    assert np.abs(imgs[True] - imgs[False]).max() <= 1e-14 * np.abs(imgs[False]).max()
+    assert sent[True] < 0.8 * sent[False], sent

@@ -100,12 +100,16 @@ def strips_model(args):
     stage_max = {k: max(p.get(k, 0.0) for p in pr) for k in ("grid", "halo", "rows", "cols")}
     t1 = sum(out[1]["per_rank_ms"][0].get(k, 0.0) for k in ("grid", "rows", "cols"))
     H_bytes = [(npix // 4) * (b - a) * 4 * 16 for a, b in out[N]["strip_rows"]]  # each rank's pass-A output
+    # what each rank sends in the (sparse) all-to-all: its live pass-A rows'
+    # blocks for the other N - 1 ranks (invert_strips_local's count)
+    send_bytes = [int(p.get("a2a_send_bytes", 0.0) * 1e-3) for p in out[N]["per_rank_ms"]]
     img_rows = npix // N
     models = {}
     for link in args.link_gbs:
         bw = link * 1e9
         halo_ms = 7 * params.nu * 16 / bw * 1e3
-        a2a_ms = max(h * (N - 1) / N / (N - 1) for h in H_bytes) / bw * 1e3 if N > 1 else 0.0
+        # one link per peer: a rank's send bytes / (N - 1) per link
+        a2a_ms = max(b / (N - 1) for b in send_bytes) / bw * 1e3 if N > 1 else 0.0
         gather_ms = img_rows * npix * 8 / bw * 1e3 if N > 1 else 0.0
         # the dependencies of the distributed run: rank r's pass A starts once
         # it and both neighbours have gridded (their halo rows) and the halo
@@ -125,7 +129,8 @@ def strips_model(args):
                                           f"{params.nu}^2 grid, W = 8, 2-D, fp64",
             "ranks": N, "one_rank_ms": round(t1, 3), "stage_max_ms": {k: round(v, 3) for k, v in stage_max.items()},
             "model": models, "runs": out,
-            "alltoall_bytes_per_rank": H_bytes, "gather_bytes_per_rank": img_rows * npix * 8}
+            "alltoall_bytes_per_rank_dense": H_bytes, "alltoall_send_bytes_per_rank": send_bytes,
+            "gather_bytes_per_rank": img_rows * npix * 8}
 
 
 def wplanes_model(args):
@@ -229,11 +234,13 @@ def wstrips_model(args):
     nplanes, W, nu = int(params.nplanes), int(params.support), int(params.nu)
     # one plane's pass-A output as it crosses the all-to-all (complex64 for the packed class, strips._wire)
     H_bytes = [(npix // 4) * (b - a) * 4 * (8 if args.single else 16) for a, b in out[N]["strip_rows"]]
+    # the sparse all-to-all's bytes per rank, summed over the planes (measured)
+    send_bytes = [int(p.get("a2a_send_bytes", 0.0) * 1e-3) for p in out[N]["per_rank_ms"]]
     models = {}
     for link in args.link_gbs:
         bw = link * 1e9
         halo_ms = nplanes * (W - 1) * nu * 16 / bw * 1e3
-        a2a_ms = nplanes * max(H_bytes) / N / bw * 1e3 if N > 1 else 0.0
+        a2a_ms = max(b / (N - 1) for b in send_bytes) / bw * 1e3 if N > 1 else 0.0
         gather_ms = (npix // N) * npix * 8 / bw * 1e3 if N > 1 else 0.0
         # grid (+ halo) then the plane loop: each plane's pass A, all-to-all and
         # pass B in turn (the slowest rank's summed pass-A and pass-B times),
@@ -248,7 +255,8 @@ def wstrips_model(args):
     return {"mode": "wstrips", "workload": f"C3 reference call by uv strips (epsilon 1e-4 -> W = {W}, {nplanes} "
                                            f"w planes, {'packed single' if args.single else 'fp64'} class)",
             "ranks": N, "one_shot_ms": round(one_ms, 3), "one_strip_ms": round(t1, 3),
-            "stage_max_ms": {k: round(v, 3) for k, v in stage_max.items()}, "model": models, "runs": out}
+            "stage_max_ms": {k: round(v, 3) for k, v in stage_max.items()}, "model": models, "runs": out,
+            "alltoall_bytes_per_rank_dense": [nplanes * h for h in H_bytes], "alltoall_send_bytes_per_rank": send_bytes}
 
 
 def main():
