@@ -290,19 +290,37 @@ def run_strong(args, world, rank, device, steps=None, warmup=None):
     log(f"[bench --strong] rank {rank}/{world}: strip rows [{y0}, {y1}) of {params.nv}, {nvis:,} vis "
         f"({data.slice_uvw.shape[0]:,} slices), plan {t_plan:.2f} s")
 
+    # step k's image-row gather runs on the communicator's stream while step
+    # k + 1 grids (its buffers are not touched by the next step); it is waited
+    # for before step k + 2 and after the last step, inside the timed region
+    pending = [None]
+
     def step(stages=None):
-        return strips.invert_strips(data, freq, layout, backend, dst=0, stages=stages)
+        if stages is not None:  # profiled steps: every stage synchronised
+            return strips.invert_strips(data, freq, layout, backend, dst=0, stages=stages)
+        prev = pending[0]
+        pending[0] = strips.invert_strips(data, freq, layout, backend, dst=0, gather_async=True)
+        if prev is not None:
+            prev.wait()
+        return None
+
+    def drain():
+        img_last = pending[0].wait() if pending[0] is not None else None
+        pending[0] = None
+        return img_last
 
     steps = args.steps if steps is None else steps
     warmup = args.warmup if warmup is None else warmup
     for _ in range(warmup):
         step()
+    drain()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(steps):
         step()
+    drain()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -357,8 +375,9 @@ def run_strong(args, world, rank, device, steps=None, warmup=None):
                          f"{params.nu}x{params.nv} grid ({npix}^2 image), support {params.support}, 2-D, fp64 "
                          "accumulate"),
             "parallelism": (f"uv strips x{world}: balanced grid-row strips + {params.support - 1}-row halo "
-                            "send/recv, strip pass A, all-to-all of pass-A blocks, pass B per image-row strip, "
-                            "gather of image rows" if world > 1 else "uv strips x1 (whole C4 on one GPU)"),
+                            "send/recv, strip pass A, sparse all-to-all of the live pass-A rows, pass B per "
+                            "image-row strip, gather of image rows (step k's gather in flight during step k + 1's "
+                            "gridding)" if world > 1 else "uv strips x1 (whole C4 on one GPU)"),
             "strip_rows": [layout.rows(r) for r in range(world)],
             "strip_vis": per_rank,
             "grid_rows_per_rank": [strips.strip_buffer_rows(layout, r)[1] for r in range(world)],

@@ -608,13 +608,14 @@ static bool chunks_full_first() {
   return on;
 }
 
-// CIP_PAIRS=0 disables the time pairs of the 2-D fp64 class (A/B experiments)
+// CIP_PAIRS=1 enables the time pairs of the 2-D fp64 class (opt-in, read per
+// call). Measured at C3 (profiles/r05_pairs.md): the scatter 2.90 -> 2.58 ms,
+// but the planner 1.59 -> 1.91 ms (the partner placement in the place pass,
+// the two-group order pass), so the pipelined step is 4.62 -> 4.79 ms - off by
+// default.
 static bool pairs_enabled() {
-  static const bool on = [] {
-    const char* e = getenv("CIP_PAIRS");
-    return !(e && e[0] == '0');
-  }();
-  return on;
+  const char* e = getenv("CIP_PAIRS");
+  return e && e[0] == '1';
 }
 
 // CIP_SCATTER_ORDER=0 skips the bank-class order (A/B experiments)

@@ -338,6 +338,19 @@ __device__ __forceinline__ bool place_vis(double u_m, double v_m, double w_m, do
   return ok;
 }
 
+// The unwrapped footprint-origin floors floor(x - W/2), floor(y - W/2) of a
+// visibility, in place_origin's operations and order (two visibilities with
+// equal floors have the same wrapped origin; the planner's time-pair test).
+__device__ __forceinline__ void origin_floors(double u_m, double v_m, double fx, const GridGeometry& g, double* flx,
+                                              double* fly) {
+#pragma clang fp contract(off)
+  const int hw = g.support / 2;
+  const double x = (u_m * fx) * g.scale_u + (double)(g.nu / 2);
+  const double y = (v_m * fx) * g.scale_v + (double)(g.nv / 2);
+  *flx = floor(x - (double)hw);
+  *fly = floor(y - (double)hw);
+}
+
 // The planner's placement: the footprint origins place_vis computes (the same
 // integers), without the kernel variables and without divergent branches in
 // the common case - |origin| < 2^30 and within one grid period of the grid,

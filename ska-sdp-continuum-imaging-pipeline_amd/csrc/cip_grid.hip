@@ -131,7 +131,7 @@ __device__ __forceinline__ unsigned origin_class_f32(float us, float vs, float f
 // singles (one mixed wave at the boundary) and the nulls fill whole waves at
 // the window's end.
 template <bool GATHER, bool WIDE, bool PAIRS = false>
-__global__ __launch_bounds__(kOrderThreads, 8) void order_kernel(const double* __restrict__ uvw,
+__global__ __launch_bounds__(kOrderThreads, PAIRS ? 6 : 8) void order_kernel(const double* __restrict__ uvw,
                                                               const double* __restrict__ fx,
                                                               const uint8_t* __restrict__ vis_class, GridGeometry g,
                                                               RowMap m, const uint64_t* __restrict__ runs,
@@ -243,19 +243,23 @@ __global__ __launch_bounds__(kOrderThreads, 8) void order_kernel(const double* _
       nlead += s_cnt[i];
       nsing += s_cnt[32 + i];
     }
-    for (unsigned t = threadIdx.x; t < 2u * (unsigned)kOrderBatch; t += kOrderThreads) {
-      const unsigned grp = t / (unsigned)kOrderBatch, r = t % (unsigned)kOrderBatch;
-      if (r >= (grp ? maxs : maxl)) continue;
-      unsigned S = 0, M = 0;
+    // one group at a time (a compile-time offset: the 32 counts of one group
+    // live in registers, not both groups' 64)
+    auto tables = [&](const unsigned* cnt_g, unsigned* S_g, unsigned* M_g, unsigned nlev) {
+      for (unsigned r = threadIdx.x; r < nlev; r += kOrderThreads) {
+        unsigned S = 0, M = 0;
 #pragma unroll
-      for (int c2 = 0; c2 < 32; ++c2) {
-        const unsigned cnt = s_cnt[32 * grp + c2];
-        S += cnt < r ? cnt : r;
-        M |= (cnt > r ? 1u : 0u) << c2;
+        for (int c2 = 0; c2 < 32; ++c2) {
+          const unsigned cnt = cnt_g[c2];
+          S += cnt < r ? cnt : r;
+          M |= (cnt > r ? 1u : 0u) << c2;
+        }
+        S_g[r] = S;
+        M_g[r] = M;
       }
-      s_S[t] = S;
-      s_M[t] = M;
-    }
+    };
+    tables(s_cnt, s_S, s_M, maxl);
+    tables(s_cnt + 32, s_S + kOrderBatch, s_M + kOrderBatch, maxs);
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < kOrderPer; ++k) {

@@ -315,7 +315,7 @@ __device__ __forceinline__ void place_body(const double* __restrict__ uvw, const
     // time pair partner: row rl + D in an even dump block, rl - D in an odd one
     int64_t prow = rl;
     bool pair_even = false, pair_has = false;
-    double pu = 0.0, pv = 0.0, pw = 0.0;
+    double pu = 0.0, pv = 0.0;
     if constexpr (PLACE) {
       u = uvw[3 * rl];
       v = uvw[3 * rl + 1];
@@ -331,7 +331,6 @@ __device__ __forceinline__ void place_body(const double* __restrict__ uvw, const
         prow = pair_has ? pr : rl;
         pu = uvw[3 * prow];
         pv = uvw[3 * prow + 1];
-        pw = uvw[3 * prow + 2];
       }
     }
     if constexpr (LOADVIS) {
@@ -372,12 +371,13 @@ __device__ __forceinline__ void place_body(const double* __restrict__ uvw, const
       // placement, bit for bit) and both feed the call's planes; the even
       // block's visibility leads, the odd block's is absorbed into it
       uint8_t pair_flag = 0;
-      if (pair_d > 0) {  // wave-uniform
-        int pix0, piy0;
-        int64_t piw0;
-        const bool pok = place_origin(pu, pv, pw, f, g, &pix0, &piy0, &piw0);
-        const bool pfeeds = (piw0 + g.support > g.plane_lo) & (piw0 < g.plane_hi);
-        const bool same = pair_has & ok & feeds & pok & pfeeds & (pix0 == ix0) & (piy0 == iy0) & (piw0 == iw0);
+      if (pair_d > 0) {  // wave-uniform; 2-D calls only (no w layer to compare)
+        // the unwrapped footprint-origin floors of both (place_origin's
+        // operations in its order: the own ones are common subexpressions)
+        double fxa, fya, fxb, fyb;
+        origin_floors(u, v, f, g, &fxa, &fya);
+        origin_floors(pu, pv, f, g, &fxb, &fyb);
+        const bool same = pair_has & ok & feeds & (fxa == fxb) & (fya == fyb);
         pair_flag = same ? (pair_even ? kClassLeader : kClassAbsorbed) : (uint8_t)0;
       }
 #if CIP_PLACE_ABL != 3

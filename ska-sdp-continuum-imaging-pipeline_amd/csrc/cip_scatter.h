@@ -27,6 +27,17 @@
 #define CIP_ABLATE 0
 #endif
 
+// CIP_TAP_BIAS=1 (fp64 class, one plane per unit): the taps add the raw bits
+// of fma(k, v, 1.5 2^52) - the integer plus the constant bias 0x4338 << 48 -
+// with no per-tap subtraction; each item counts itself at its footprint
+// origin (one ds_add_u32), and the flush removes n x bias from a cell, n =
+// the items whose W x W footprint covers it (a box sum of the origin counts).
+// One VALU instruction per tap and component fewer; the same integers.
+#ifndef CIP_TAP_BIAS
+#define CIP_TAP_BIAS 0
+#endif
+constexpr unsigned long long kTapBias = 0x4338000000000000ull;
+
 namespace cip {
 
 // ------------------------------------------------------------ scatter ----
@@ -243,9 +254,11 @@ __device__ __forceinline__ void grid_fetched_packed(const VisFetch& f, const Gri
 // One visibility onto the unit's sub-grid(s). G > 1 (w-stacking): the unit
 // grids planes plane .. plane + G - 1 at once (G sub-grids, S u64 apart), the
 // visibility placed and its u, v, w kernels evaluated once for all of them.
-template <int W, bool WSTACK, bool PACK, int G = 1>
+template <int W, bool WSTACK, bool PACK, int G = 1, bool BIAS = false>
 __device__ __forceinline__ void grid_fetched(const VisFetch& f, const GridGeometry& g, int64_t plane, int64_t X0,
-                                             int64_t Y0, double fixed_scale, unsigned long long* sub) {
+                                             int64_t Y0, double fixed_scale, unsigned long long* sub,
+                                             unsigned* cnt = nullptr) {
+  static_assert(!BIAS || (!PACK && G == 1), "tap bias: fp64 class, one plane per unit");
   constexpr int T = kTile;
   constexpr int P = T + W - 1;
 #if CIP_ABLATE == 0 || CIP_ABLATE == 4
@@ -319,6 +332,7 @@ __device__ __forceinline__ void grid_fetched(const VisFetch& f, const GridGeomet
     sc *= sel;
   }
   const double vr = f.vr * sc, vi = f.vi * sc;
+  if constexpr (BIAS) atomicAdd(cnt + (lx * P + ly), 1u);  // the item's origin (its bias count)
   double ku[W], kv[W];
 #if CIP_ABLATE == 3
 #pragma unroll
@@ -368,8 +382,8 @@ __device__ __forceinline__ void grid_fetched(const VisFetch& f, const GridGeomet
 #endif
         atomicAdd(base + (i * P + j), __builtin_bit_cast(unsigned long long, make_uint2((unsigned)bi, hi)));
       } else {
-        atomicAdd(base + (i * P + j), br - 0x4338000000000000ull);
-        atomicAdd(base + P * P + (i * P + j), bi - 0x4338000000000000ull);
+        atomicAdd(base + (i * P + j), BIAS ? br : br - kTapBias);
+        atomicAdd(base + P * P + (i * P + j), BIAS ? bi : bi - kTapBias);
       }
     }
   }
@@ -381,13 +395,26 @@ __device__ __forceinline__ void grid_fetched(const VisFetch& f, const GridGeomet
 
 // Flush the touched cells of a work unit's sub-grid(s) to the HBM grid(s)
 // (called after the unit's last LDS atomic and a barrier).
-template <int W, bool PACK, int G, int NT>
+template <int W, bool PACK, int G, int NT, bool BIAS = false>
 __device__ __forceinline__ void flush_subgrid(const unsigned long long* sub, const GridGeometry& g, int64_t plane,
                                               int64_t X0, int64_t Y0, const Chunk& ch, int store_private,
-                                              double inv_scale, double* __restrict__ grid) {
+                                              double inv_scale, double* __restrict__ grid, unsigned* cnt = nullptr) {
   constexpr int T = kTile;
   constexpr int P = T + W - 1;
   constexpr int S = P * P * (PACK ? 1 : 2);
+  if constexpr (BIAS) {
+    // n(x, y) = items with origin in [x - W + 1, x] x [y - W + 1, y]: the
+    // origin counts (cnt[0 .. P^2)) summed over x into cnt[P^2 ..), then over
+    // y per cell below
+    for (int cell = threadIdx.x; cell < P * P; cell += NT) {
+      const int lx = cell / P, ly = cell - lx * P;
+      unsigned a = 0u;
+#pragma unroll
+      for (int i = 0; i < W; ++i) a += (lx - i >= 0) ? cnt[(lx - i) * P + ly] : 0u;
+      cnt[P * P + cell] = a;
+    }
+    __syncthreads();
+  }
   // flush the touched cells of the sub-grid(s) to the fp64 HBM grid(s)
   // (lanes walk the HBM grid's contiguous axis: y, or x when it is stored
   // transposed for the pruned FFT); plane group: plane + k -> grid + k planes.
@@ -411,13 +438,22 @@ __device__ __forceinline__ void flush_subgrid(const unsigned long long* sub, con
     unsigned long long sv[G];  // PACK: re * 2^32 + im
     unsigned long long si[G];  // !PACK: the im plane
     bool any = false;
+    unsigned long long bias = 0ull;  // BIAS: n x kTapBias, removed from both planes
+    if constexpr (BIAS) {
+      const int lx = lcell / P, ly = lcell - (lcell / P) * P;
+      unsigned n = 0u;
+#pragma unroll
+      for (int j = 0; j < W; ++j) n += (ly - j >= 0) ? cnt[P * P + lx * P + ly - j] : 0u;
+      if (n == 0u) continue;  // no item's footprint covers the cell
+      bias = (unsigned long long)n * kTapBias;
+    }
 #pragma unroll
     for (int k = 0; k < G; ++k) {
       sv[k] = 0ull;
       si[k] = 0ull;
       if (G > 1 && (plane + k >= g.nplanes || plane + k < g.plane_lo || plane + k >= g.plane_hi)) continue;
-      sv[k] = sub[k * S + lcell];
-      if constexpr (!PACK) si[k] = sub[k * S + P * P + lcell];
+      sv[k] = sub[k * S + lcell] - bias;
+      if constexpr (!PACK) si[k] = sub[k * S + P * P + lcell] - bias;
       any |= (sv[k] | si[k]) != 0ull;
     }
 #if CIP_ABLATE == 4
@@ -489,6 +525,8 @@ __global__ __launch_bounds__(scatter_threads<G>(), CIP_SCATTER_WAVES) void scatt
   constexpr int S = P * P * (PACK ? 1 : 2);
   constexpr int NT = scatter_threads<G>();
   __shared__ unsigned long long sub[G * S];
+  constexpr bool kBias = CIP_TAP_BIAS != 0 && !PACK && G == 1;
+  __shared__ unsigned s_cnt[kBias ? 2 * P * P : 1];  // origin counts, then their x sums
   __shared__ int64_t s_voff[PERM ? 1 : kRunBatch + 1];
   __shared__ uint64_t s_run[PERM ? 1 : kRunBatch];
   constexpr bool kWide = PERM == 2;
@@ -497,6 +535,8 @@ __global__ __launch_bounds__(scatter_threads<G>(), CIP_SCATTER_WAVES) void scatt
   int64_t X0, Y0;
   tile_origin(ch.tile, g, &X0, &Y0);
   for (int i = threadIdx.x; i < G * S; i += NT) sub[i] = 0ull;
+  if constexpr (kBias)
+    for (int i = threadIdx.x; i < P * P; i += NT) s_cnt[i] = 0u;
   if constexpr (PACK) {
     fixed_scale *= packed_chunk_gain(ch.g1 - ch.g0);
     inv_scale = 1.0 / fixed_scale;
@@ -523,7 +563,8 @@ __global__ __launch_bounds__(scatter_threads<G>(), CIP_SCATTER_WAVES) void scatt
       const uint64_t pnn = perm_entry_t<kWide>(perm, hnn ? qnn : q);
       RawFetch<VisT, WK> nxt;
       fetch_raw<VisT, WK, kWide>(pn, uvw, fx, vis_ld, unit_vis, wgt, m, nxt);
-      grid_fetched<W, WSTACK, PACK, G>(from_raw<VisT, WK>(cur, unit_vis), g, plane, X0, Y0, fixed_scale, sub);
+      grid_fetched<W, WSTACK, PACK, G, kBias>(from_raw<VisT, WK>(cur, unit_vis), g, plane, X0, Y0, fixed_scale, sub,
+                                              s_cnt);
       cur = nxt;
       q = qn;
       have = hn;
@@ -554,7 +595,7 @@ __global__ __launch_bounds__(scatter_threads<G>(), CIP_SCATTER_WAVES) void scatt
         const bool hn = qn < bend;
         VisFetch nxt;
         if (hn) fetch_vis<VisT, WK>(qn, s_voff, s_run, nst, uvw, fx, vis, wgt, m, nxt);
-        grid_fetched<W, WSTACK, PACK, G>(cur, g, plane, X0, Y0, fixed_scale, sub);
+        grid_fetched<W, WSTACK, PACK, G, kBias>(cur, g, plane, X0, Y0, fixed_scale, sub, s_cnt);
         cur = nxt;
         q = qn;
         have = hn;
@@ -564,7 +605,7 @@ __global__ __launch_bounds__(scatter_threads<G>(), CIP_SCATTER_WAVES) void scatt
     }
   }
   __syncthreads();
-  flush_subgrid<W, PACK, G, NT>(sub, g, plane, X0, Y0, ch, store_private, inv_scale, grid);
+  flush_subgrid<W, PACK, G, NT, kBias>(sub, g, plane, X0, Y0, ch, store_private, inv_scale, grid, s_cnt);
 }
 
 // ------------------------------------------------------- time pairs ----
@@ -615,9 +656,10 @@ __device__ __forceinline__ void fetch_pair(uint32_t e, int64_t pair_d, const dou
   }
 }
 
-template <int W, typename VisT, int WK>
+template <int W, typename VisT, int WK, bool BIAS>
 __device__ __forceinline__ void grid_pair(const PairFetch<VisT, WK>& f, bool unit_vis, const GridGeometry& g,
-                                          int64_t X0, int64_t Y0, double fixed_scale, unsigned long long* sub) {
+                                          int64_t X0, int64_t Y0, double fixed_scale, unsigned long long* sub,
+                                          unsigned* cnt) {
   constexpr int T = kTile;
   constexpr int P = T + W - 1;
   const bool pr = f.kind == 2;
@@ -653,50 +695,40 @@ __device__ __forceinline__ void grid_pair(const PairFetch<VisT, WK>& f, bool uni
     a.vr = unit_vis ? 1.0 : (double)f.vis.x;
     a.vi = unit_vis ? 0.0 : (double)f.vis.y;
     a.wt = wa;
-    grid_fetched<W, false, false, 1>(a, g, 0, X0, Y0, fixed_scale, sub);
+    grid_fetched<W, false, false, 1, BIAS>(a, g, 0, X0, Y0, fixed_scale, sub, cnt);
     return;
   }
-  double kra[W], kia[W], krb[W], kib[W];
-  {
-    double kv[W];
-    eval_kernel<W>(yv, kv);
-#pragma unroll
-    for (int j = 0; j < W; ++j) {
-      kra[j] = kv[j] * vra;
-      kia[j] = kv[j] * via;
-    }
-    eval_kernel<W>(yvb, kv);
-#pragma unroll
-    for (int j = 0; j < W; ++j) {
-      krb[j] = kv[j] * vrb;
-      kib[j] = kv[j] * vib;
-    }
-  }
-  // the u kernels row by row, mirrored pieces k and W - 1 - k together (the
-  // even / odd halves of eval_kernel): four u values live instead of 2 W
+  if constexpr (BIAS) atomicAdd(cnt + (lx * P + ly), 1u);  // one bias per item (the pair's nested fma)
+  // the u kernels of both visibilities held (2 W values); the v kernels
+  // streamed in mirrored pairs of columns j = k, W - 1 - k (the even / odd
+  // halves of eval_kernel) - 48 live fp64 registers of taps instead of 72
+  double kua[W], kub[W];
+  eval_kernel<W>(yu, kua);
+  eval_kernel<W>(yub, kub);
   unsigned long long* base = sub + (lx * P + ly);
-  const double za = yu * yu, zb = yub * yub;
+  const double za = yv * yv, zb = yvb * yvb;
 #pragma unroll
   for (int k = 0; k < W / 2; ++k) {
-    double ua[2], ub[2];
-    eval_piece_pair<W>(k, yu, za, ua);
-    eval_piece_pair<W>(k, yub, zb, ub);
+    double va[2], vb[2];
+    eval_piece_pair<W>(k, yv, za, va);
+    eval_piece_pair<W>(k, yvb, zb, vb);
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      const int i = h ? W - 1 - k : k;
+      const int j = h ? W - 1 - k : k;
+      const double kra = va[h] * vra, kia = va[h] * via, krb = vb[h] * vrb, kib = vb[h] * vib;
 #pragma unroll
-      for (int j = 0; j < W; ++j) {
-        const double qr = fma(ua[h], kra[j], fma(ub[h], krb[j], kMagic));
-        const double qi = fma(ua[h], kia[j], fma(ub[h], kib[j], kMagic));
-        atomicAdd(base + (i * P + j), (unsigned long long)__double_as_longlong(qr) - 0x4338000000000000ull);
-        atomicAdd(base + P * P + (i * P + j), (unsigned long long)__double_as_longlong(qi) - 0x4338000000000000ull);
+      for (int i = 0; i < W; ++i) {
+        const double qr = fma(kua[i], kra, fma(kub[i], krb, kMagic));
+        const double qi = fma(kua[i], kia, fma(kub[i], kib, kMagic));
+        atomicAdd(base + (i * P + j), (unsigned long long)__double_as_longlong(qr) - (BIAS ? 0ull : kTapBias));
+        atomicAdd(base + P * P + (i * P + j), (unsigned long long)__double_as_longlong(qi) - (BIAS ? 0ull : kTapBias));
       }
     }
   }
 }
 
 #ifndef CIP_PAIR_WAVES
-#define CIP_PAIR_WAVES 3  // pipelined calls cap the scatter at 3 blocks per CU anyway (share_cus)
+#define CIP_PAIR_WAVES 4  // min waves per SIMD (the lane kernel's 4; share_cus caps pipelined calls at 3 blocks per CU)
 #endif
 template <int W, typename VisT, int WK>
 __global__ __launch_bounds__(kScatterThreads, CIP_PAIR_WAVES) void scatter_pair_kernel(
@@ -709,10 +741,14 @@ __global__ __launch_bounds__(kScatterThreads, CIP_PAIR_WAVES) void scatter_pair_
   constexpr int S = P * P * 2;
   constexpr int NT = kScatterThreads;
   __shared__ unsigned long long sub[S];
+  constexpr bool kBias = CIP_TAP_BIAS != 0;
+  __shared__ unsigned s_cnt[kBias ? 2 * P * P : 1];
   const Chunk ch = chunks[chunk_begin + blockIdx.x];
   int64_t X0, Y0;
   tile_origin(ch.tile, g, &X0, &Y0);
   for (int i = threadIdx.x; i < S; i += NT) sub[i] = 0ull;
+  if constexpr (kBias)
+    for (int i = threadIdx.x; i < P * P; i += NT) s_cnt[i] = 0u;
   const int64_t pair_d = (int64_t)__builtin_amdgcn_readfirstlane((int)*m.pair_d);
   __syncthreads();
   const bool unit_vis = vis == nullptr;
@@ -735,7 +771,7 @@ __global__ __launch_bounds__(kScatterThreads, CIP_PAIR_WAVES) void scatter_pair_
     const uint32_t pnn = perm[hnn ? qnn : q];
     PairFetch<VisT, WK> nxt;
     fetch_pair<VisT, WK>(hn ? pn : kPermNull, pair_d, uvw, fx, vis_ld, unit_vis, wgt, m, nxt);
-    grid_pair<W, VisT, WK>(cur, unit_vis, g, X0, Y0, fixed_scale, sub);
+    grid_pair<W, VisT, WK, kBias>(cur, unit_vis, g, X0, Y0, fixed_scale, sub, s_cnt);
     cur = nxt;
     q = qn;
     have = hn;
@@ -744,7 +780,7 @@ __global__ __launch_bounds__(kScatterThreads, CIP_PAIR_WAVES) void scatter_pair_
     pn = pnn;
   }
   __syncthreads();
-  flush_subgrid<W, false, 1, NT>(sub, g, 0, X0, Y0, ch, store_private, inv_scale, grid);
+  flush_subgrid<W, false, 1, NT, kBias>(sub, g, 0, X0, Y0, ch, store_private, inv_scale, grid, s_cnt);
 }
 
 template <int W, typename VisT, int WK>

@@ -168,14 +168,15 @@ COST_PS_PER_SLICE = 112.0
 COST_PS_PER_CELL = 8.9
 
 
-def row_costs(uvw, freq, params, pixsize_x: float, pixsize_y: float):
+def row_costs(uvw, freq, params, pixsize_x: float, pixsize_y: float, a2a_ps_per_row: float = 0.0):
     """Modelled cost (ps) of each grid row as a strip member: its visibilities
     (by footprint-origin row; per tap, W^2 taps per visibility, W^3 with
     w-stacking - the C3 reference call's w-stacking strips measured 0.63 ps
     per tap against 0.58 for C4's W = 8), the row slices starting there (a
     slice starts at each row's first channel and wherever the origin's 32-cell
     tile changes along the channels) and its pass-A cells (one pass per w
-    plane)."""
+    plane), plus `a2a_ps_per_row` per row and plane: the row's pass-A output
+    crossing the all-to-all (a rank's exchange time grows with its rows)."""
     nu, nv, W = int(params.nu), int(params.nv), int(params.support)
     wstack = bool(int(getattr(params, "do_wstacking", 0)))
     taps = W * W * (W if wstack else 1)
@@ -192,20 +193,27 @@ def row_costs(uvw, freq, params, pixsize_x: float, pixsize_y: float):
         vis += torch.bincount(iy.reshape(-1), minlength=nv)
         runs += torch.bincount(iy[start], minlength=nv)
     cost = (COST_PS_PER_VIS * (taps / 64.0) * vis.double() + COST_PS_PER_SLICE * runs.double() +
-            COST_PS_PER_CELL * nu * nplanes)
+            (COST_PS_PER_CELL * nu + a2a_ps_per_row) * nplanes)
     return cost.cpu().numpy()
 
 
 def plan_strips(uvw, freq, params, pixsize_y: float, npix_x: int, npix_y: int, world: int,
-                balance: str = "cost", pixsize_x: Optional[float] = None) -> StripLayout:
+                balance: str = "cost", pixsize_x: Optional[float] = None,
+                link_gbs: Optional[float] = None) -> StripLayout:
     """Balanced strips: grid-row bounds splitting a per-row histogram (all
     visibilities, so every rank computes the same bounds without
     communication) into `world` near-equal parts, each at least W rows high
     (the halo then only reaches the next strip); image rows split into
     near-equal multiples of COL_BLOCK. balance="cost": the measured per-rank
     cost model (`row_costs`: visibilities, row slices, pass-A rows; needs
-    pixsize_x, default pixsize_y); "vis": visibility count only. uvw (nrow,
-    3), freq (nchan) tensors."""
+    pixsize_x, default pixsize_y) plus, for world > 1 and `link_gbs` (off by
+    default), each row's share of the all-to-all: its pass-A output (npix_x
+    complex128) leaves on world - 1 links, 16 npix_x / world bytes per link
+    at link_gbs - the tall, sparse edge strips of long baselines get fewer
+    rows (C4 at 8 ranks: 5.86x modelled at 64 GB/s against 5.93x unpriced,
+    profiles/r05g_strong_model_c4_bal64.json - the grid imbalance costs more
+    than the exchange gains); "vis":
+    visibility count only. uvw (nrow, 3), freq (nchan) tensors."""
     nv, W = int(params.nv), int(params.support)
     if world < 1:
         raise ValueError("world must be >= 1")
@@ -216,7 +224,9 @@ def plan_strips(uvw, freq, params, pixsize_y: float, npix_x: int, npix_y: int, w
     if nv < W * world:
         raise ValueError("grid too small for this many strips")
     if balance == "cost":
-        hist = row_costs(uvw, freq, params, pixsize_y if pixsize_x is None else pixsize_x, pixsize_y)
+        a2a = 16.0 * npix_x / world / (link_gbs * 1e9) * 1e12 if (world > 1 and link_gbs) else 0.0
+        hist = row_costs(uvw, freq, params, pixsize_y if pixsize_x is None else pixsize_x, pixsize_y,
+                         a2a_ps_per_row=a2a)
     elif balance == "vis":
         fx = freq / SPEED_OF_LIGHT
         scale_v = float(params.nv) * pixsize_y
@@ -476,7 +486,7 @@ def _assemble_H(pieces: Sequence, nb: int, layout: StripLayout, device, dtype, i
 
 
 def invert_strips(data: StripData, freq, layout: StripLayout, backend, *, dst: int = 0, group=None,
-                  stages: Optional[dict] = None, sparse: bool = True):
+                  stages: Optional[dict] = None, sparse: bool = True, gather_async: bool = False):
     """This rank's share of the strip-distributed invert (torch.distributed
     initialised, one rank per strip). Returns the normalised dirty image
     (npix_x, npix_y) on `dst`, None elsewhere. Collectives: one point-to-point
@@ -485,6 +495,9 @@ def invert_strips(data: StripData, freq, layout: StripLayout, backend, *, dst: i
     The backend is bound to this rank's strip + halo rows (`strip_buffer_rows`).
     `sparse` (default): the all-to-all carries only the rows of the pass-A
     output that can be non-zero (after an all-gather of the live-row masks).
+    `gather_async`: return a `PendingGather` at once (the image-row gather in
+    flight on the communicator's stream, e.g. beside the next invert's
+    gridding); `.wait()` gives the image.
     `stages` (a dict, diagnostic): each stage is synchronised and its seconds
     added under its name (grid, halo, rows, alltoall, cols, gather), and the
     all-to-all's bytes sent by this rank under a2a_send_bytes."""
@@ -545,7 +558,7 @@ def invert_strips(data: StripData, freq, layout: StripLayout, backend, *, dst: i
         backend.mark_clean()
         rows_img = backend.finish_rows(acc, i0, i1, norm=sumw)
         mark("final")
-        return _gather_rows(rows_img, layout, rank, world, dst, group, mark)
+        return _gather_rows(rows_img, layout, rank, world, dst, group, mark, async_op=gather_async)
     H = backend.pass_rows(buf, 0, h)
     live = _live_of(backend, H, h) if (sparse and world > 1) else None
     backend.mark_clean()
@@ -556,7 +569,7 @@ def invert_strips(data: StripData, freq, layout: StripLayout, backend, *, dst: i
     mark("alltoall")
     rows_img = backend.pass_cols(Hm, i0, i1, norm=sumw)
     mark("cols")
-    return _gather_rows(rows_img, layout, rank, world, dst, group, mark)
+    return _gather_rows(rows_img, layout, rank, world, dst, group, mark, async_op=gather_async)
 
 
 def _wire(H, backend):
@@ -612,18 +625,46 @@ def _alltoall_H(H, layout: StripLayout, rank: int, world: int, group, live=None,
     return _assemble_H(pieces, nb, layout, H.device, H.dtype, idx)
 
 
-def _gather_rows(rows_img, layout: StripLayout, rank: int, world: int, dst: int, group, mark):
-    """This rank's image rows -> the whole image on `dst` (None elsewhere)."""
+class PendingGather:
+    """A strip invert whose image-row gather is in flight
+    (`invert_strips(..., gather_async=True)`): the collective runs on the
+    communicator's stream while the caller goes on - e.g. with the next
+    invert's gridding, which touches none of its buffers. `wait()` returns
+    the image on `dst` (None elsewhere)."""
+
+    def __init__(self, work, gathered, layout: StripLayout, rank: int, dst: int, image=None):
+        self._work, self._gathered, self._layout = work, gathered, layout
+        self._rank, self._dst, self._image = rank, dst, image
+        self._done = work is None
+
+    def wait(self):
+        if not self._done:
+            self._work.wait()
+            self._done = True
+            if self._rank == self._dst:
+                lay = self._layout
+                self._image = torch.cat([g[:lay.image_rows(r)[1] - lay.image_rows(r)[0]]
+                                         for r, g in enumerate(self._gathered)])
+            self._gathered = None
+        return self._image
+
+
+def _gather_rows(rows_img, layout: StripLayout, rank: int, world: int, dst: int, group, mark,
+                 async_op: bool = False):
+    """This rank's image rows -> the whole image on `dst` (None elsewhere);
+    async_op: a PendingGather instead."""
     import torch.distributed as dist  # pylint: disable=import-outside-toplevel
 
     if world == 1:
-        return rows_img
+        return PendingGather(None, None, layout, rank, dst, rows_img) if async_op else rows_img
     # gather the image rows (strips padded to the largest: gather needs equal sizes)
     hmax = max(layout.image_rows(r)[1] - layout.image_rows(r)[0] for r in range(world))
     if rows_img.shape[0] < hmax:
         rows_img = torch.cat([rows_img, rows_img.new_zeros((hmax - rows_img.shape[0], rows_img.shape[1]))])
     gathered = [torch.empty_like(rows_img) for _ in range(world)] if rank == dst else None
-    dist.gather(rows_img, gathered, dst=dst, group=group)
+    work = dist.gather(rows_img, gathered, dst=dst, group=group, async_op=async_op)
+    if async_op:
+        return PendingGather(work, gathered, layout, rank, dst)
     mark("gather")
     if rank != dst:
         return None

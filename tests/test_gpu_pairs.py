@@ -7,9 +7,10 @@ footprints start on the same cell, and one 64-bit atomic per tap grids both.
 
 * the stride is detected (profile counter `pair_stride` = the baselines per
   dump) and the image equals the CPU oracle at the fp64 gate;
-* the same call with CIP_PAIRS=0 (a child process: the switch is read once)
-  gives the same image to the fixed-point quantum (a pair's integer is within
-  one quantum of its two separately rounded contributions);
+* the same call with CIP_PAIRS=0 (time pairs are opt-in: CIP_PAIRS=1, read
+  per call; here in child processes) gives the same image to the fixed-point
+  quantum (a pair's integer is within one quantum of its two separately
+  rounded contributions);
 * NaN visibilities under zero weights - in leaders and in absorbed partners -
   stay out of the image; complex128 input, no weights, the PSF, W = 4 / 16;
 * rows that are not time-major (shuffled) find no stride and grid as before.
@@ -29,6 +30,14 @@ from ska_sdp_cip_amd import synthetic as syn
 from ska_sdp_cip_amd.gridder import device_ms2dirty
 
 pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(autouse=True)
+def _pairs_on(monkeypatch):
+    # time pairs are opt-in (CIP_PAIRS=1, read per call)
+    monkeypatch.setenv("CIP_PAIRS", "1")
+
+
 ROOT = Path(__file__).resolve().parents[1]
 N_ANT = 20
 NBL = N_ANT * (N_ANT - 1) // 2  # 190 baselines per dump
@@ -130,7 +139,7 @@ np.savez(out, img=img.cpu().numpy(), stride=stride)
 def _child(tmp_path, **env_over):
     out = tmp_path / ("pairs_" + "_".join(f"{k}{v}" for k, v in env_over.items()) + ".npz")
     env = dict(os.environ)
-    env.pop("CIP_PAIRS", None)
+    env["CIP_PAIRS"] = "1"
     env.update(env_over)
     subprocess.run([sys.executable, "-c", CHILD, str(ROOT), str(out)], env=env, check=True, timeout=180)
     return np.load(out)

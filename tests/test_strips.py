@@ -171,12 +171,17 @@ def _worker(rank, world, port, q, W, wstack=False):
     data = _strip_datas(uvw, f, vis, w, px, prm, layout)[rank]  # each rank holds only its strip
     be = NumpyStripBackend(prm, px, px, NPIX, NPIX)
     img = strips.invert_strips(data, torch.from_numpy(f), layout, be, dst=0)
+    # two more inverts with the gather in flight while the next one grids
+    p1 = strips.invert_strips(data, torch.from_numpy(f), layout, be, dst=0, gather_async=True)
+    p2 = strips.invert_strips(data, torch.from_numpy(f), layout, be, dst=0, gather_async=True)
+    img1, img2 = p1.wait(), p2.wait()
     if rank == 0:
         full = oracle.ms2dirty(uvw, f, vis, w, NPIX, NPIX, px, px, support=W, do_wstacking=wstack,
                                nthreads=1) / w.astype(np.float64).sum()
-        q.put((float(np.abs(img.numpy() - full).max()), float(np.abs(full).max()), float(be.grid.abs().max())))
+        err = max(float(np.abs(i.numpy() - full).max()) for i in (img, img1, img2))
+        q.put((err, float(np.abs(full).max()), float(be.grid.abs().max())))
     else:
-        assert img is None
+        assert img is None and img1 is None and img2 is None
     dist.barrier()
     dist.destroy_process_group()
 

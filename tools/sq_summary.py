@@ -11,7 +11,7 @@ for d in sys.argv[1:]:
             name = row["Kernel_Name"].split("(")[0][:70]
             vals[name][row["Counter_Name"]].append(float(row["Counter_Value"]))
 for k, cs in vals.items():
-    if not any(s in k for s in ("scatter_kernel", "order_kernel", "plan_place", "fft_", "radix")):
+    if not any(s in k for s in ("scatter_kernel", "scatter_pair", "lds_pattern", "order_kernel", "plan_place", "fft_", "radix")):
         continue
     print(k)
     for c, v in sorted(cs.items()):
