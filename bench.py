@@ -900,16 +900,22 @@ def main():
         "launch_ms": round(scatter_ms, 4),
     }
     # the bound that actually limits the scatter: LDS atomic bytes. Each tap is
-    # a 64-bit fixed-point add to the re and the im plane (16 B of LDS RMW),
-    # and gfx950 sustains one conflict-free 64-lane ds_add_u64 per 8.12
-    # CU-cycles (tools/microbench/lds_ops.hip, profiles/microbench_r01.txt).
+    # a 64-bit fixed-point add to the re and the im plane (16 B of LDS RMW).
+    # Round 5 (tools/microbench/lds_conflict.hip, profiles/r05_pairs.md): a
+    # conflict-free 64-lane ds_add_u64 keeps the LDS 4 cycles busy (128 B per
+    # CU-cycle, the LDS width); the round-1 basis of 8.12 CU-cycles was an 8 x 8
+    # tap pattern with half its cycles in bank conflicts, as the scatter has
+    # (36 % of its LDS-active cycles: the level-major class order's leftovers)
     lds_bytes = vis_per_launch * params.support ** 2 * (8 if args.single else 16)  # packed: one u64 per tap
-    lds_peak = 64 * 8 / 8.12 * 2.4e9 * 256 / 1e9  # GB/s: 256 CUs at 2.4 GHz
+    lds_peak = 128.0 * 2.4e9 * 256 / 1e9  # GB/s: 128 B / CU-cycle, 256 CUs at 2.4 GHz
+    lds_tap_peak = 64 * 8 / 8.12 * 2.4e9 * 256 / 1e9  # the tap pattern's rate (its conflicts included)
     lds_achieved = lds_bytes / (scatter_ms * 1e-3) / 1e9
     roofline["lds_atomic"] = {"achieved": round(lds_achieved, 1), "peak": round(lds_peak, 1), "unit": "GB/s",
                               "frac": round(lds_achieved / lds_peak, 4),
-                              "basis": f"{8 if args.single else 16} B of ds_add_u64 per tap; 8.12 CU-cycles per "
-                                       "conflict-free wave-instr"}
+                              "frac_of_tap_pattern_rate": round(lds_achieved / lds_tap_peak, 4),
+                              "basis": f"{8 if args.single else 16} B of ds_add_u64 per tap; peak = 4 LDS cycles per "
+                                       "conflict-free wave-instr (128 B/CU-cycle); the scatter's own bank conflicts "
+                                       "(~36 % of its LDS cycles, profiles/r05_sq_c3_pairs.md) are inside 'achieved'"}
     tr = traffic_from_profiles(args.config)
     # the committed PMC pass is of the default workload (support 8, 2-D, fp64 class)
     if tr and not args.wstacking and not args.single and not args.raw and args.support == tr.get("support", 8):

@@ -1279,6 +1279,27 @@ static int plane_to_dirty(const DirtyStage& st, const GridGeometry& g, int64_t p
   return CIP_OK;
 }
 
+// CIP_WSTACK_PAIRB=1: w-stacking pass B over plane pairs (the packed class's
+// complex64 pass-A outputs of two planes side by side in the pass-A buffer,
+// one image read-modify-write per pair; the same image bit for bit). Off by
+// default: measured on the C3 reference call FFT 5.33 vs 4.91 ms
+// (profiles/r05_ab_wstack_pairb.txt) - the pair kernel needs ~250 VGPRs, one
+// 512-thread block per CU instead of two, and the lost occupancy costs more
+// than the 134 MB image read-modify-write it saves per pair.
+static bool wstack_pair_b() {
+  const char* e = getenv("CIP_WSTACK_PAIRB");
+  return e && e[0] == '1';
+}
+
+// pass A of plane p into pass-A slot `slot` of the buffer (complex64 slots)
+static int plane_pass_a(const DirtyStage& st, const GridGeometry& g, double* grid, int slot, hipStream_t s,
+                        const uint32_t* dmask, const uint32_t* rowbits) {
+  if (!fft_rowskip()) rowbits = nullptr;
+  double* h = st.fft_h + (size_t)slot * (size_t)st.npix_x * (size_t)g.nv;  // npix_x nv complex64 = as many doubles
+  CIP_HIP_CHECK(launch_fft_rows(grid, g.nu, g.nv, st.npix_x, st.tw_u, h, dmask, g.ntx, rowbits != nullptr, s, true));
+  return CIP_OK;
+}
+
 // after the last plane: the w-stacking correction (2-D: nothing)
 // the w-stacking final correction's table of F (cached per workspace)
 static int w_correction_table(Workspace* ws, const cip_gridder_params& prm, const GridGeometry& g, hipStream_t s,
@@ -1513,6 +1534,12 @@ static int ms2dirty_impl(const double* uvw, int64_t nrow, const double* freq, in
   // unless cip_ms2dirty_wplanes); an empty range leaves a zero image
   const int64_t p_lo = g.plane_lo, p_hi = g.plane_hi;
   if (p_lo >= p_hi) CIP_HIP_CHECK(hipMemsetAsync(dirty_out, 0, sizeof(double) * npix_x * npix_y, s));
+  // plane pairs through pass B (CIP_WSTACK_PAIRB, packed class): the pass-A
+  // output of an odd plane waits in slot 0 for its partner
+  const bool pair_b = st.fast && g.do_wstacking && g.grid_f32 && wstack_pair_b() && g.nv <= 8192;
+  int64_t pending = -1;  // plane whose pass A sits in slot 0
+  const int64_t rb_stride = (g.nty + 31) / 32;
+  const uint32_t* rowbits0 = dmask ? dmask + g.nplanes * (g.ntx * g.nty / 32) : nullptr;
   for (int64_t q = p_lo / G; q * G < p_hi; ++q) {
     // pipelined calls: leave CU slots to the next call's planner (profiles/r03_ab_scatter_share.txt)
     rc = scatter_plane(pp, q, uvw, vis, vis_dtype, wgt, wgt_dtype, st.fast, grid, s, clean,
@@ -1520,10 +1547,25 @@ static int ms2dirty_impl(const double* uvw, int64_t nrow, const double* freq, in
     if (rc != CIP_OK) return rc;
     for (int64_t p = std::max(q * G, p_lo); p < std::min<int64_t>(q * G + G, p_hi); ++p) {
       double* plane_p = (double*)((char*)grid + (size_t)(p - q * G) * (size_t)plane_elems * cell_bytes);
-      rc = plane_to_dirty(st, g, p, plane_p, dirty_out, s,
-                          dmask ? dmask + p * (g.ntx * g.nty / 32) : nullptr, normalise ? pp.red : nullptr,
-                          dmask ? dmask + g.nplanes * (g.ntx * g.nty / 32) + p * ((g.nty + 31) / 32) : nullptr,
-                          p == p_lo);
+      const uint32_t* dm = dmask ? dmask + p * (g.ntx * g.nty / 32) : nullptr;
+      const uint32_t* rbp = rowbits0 ? rowbits0 + p * rb_stride : nullptr;
+      if (pair_b && (pending >= 0 || p + 1 < p_hi)) {
+        hipEvent_t f0 = g_prof.mark(s);
+        rc = plane_pass_a(st, g, plane_p, pending >= 0 ? 1 : 0, s, dm, rbp);
+        if (rc != CIP_OK) return rc;
+        if (pending >= 0) {
+          CIP_HIP_CHECK(launch_fft_cols_wstack(st.fft_h, (int64_t)st.npix_x * g.nv * 8, 2, pending, g.nv, st.npix_x,
+                                               st.npix_y, st.tw_v, dirty_out, st.px, st.py, g.w0, g.dw,
+                                               pending == p_lo ? 1 : 0, fft_rowskip() ? rowbits0 : nullptr,
+                                               rb_stride, s, true));
+          pending = -1;
+        } else {
+          pending = p;
+        }
+        g_prof.span(3, f0, g_prof.mark(s));
+        continue;
+      }
+      rc = plane_to_dirty(st, g, p, plane_p, dirty_out, s, dm, normalise ? pp.red : nullptr, rbp, p == p_lo);
       if (rc != CIP_OK) return rc;
     }
     // a group's planes outside the range were neither written (the scatter

@@ -448,6 +448,149 @@ static bool fft_f32_enabled() {
   return on;
 }
 
+// Pass B of a w-stacking batch (round 5): the screened contributions of nb
+// consecutive w planes (global planes pbase .. pbase + nb - 1, their pass-A
+// outputs H + q hstride) summed in registers per image row and written once:
+// one image write per batch instead of a read-modify-write per plane (the
+// C3 reference call: 14 planes -> one write of the 134 MB image instead of 13
+// read-modify-writes). The sum runs in plane order from the batch's first
+// plane (first: overwrite, else: the image row's current values first), the
+// per-plane kernel's additions in the same order - the same image bit for bit.
+// rowbits: plane p's tile-row words at rowbits + p rb_stride (NULL: dense).
+template <int N, typename HT, typename CT, int NB>
+__global__ __launch_bounds__(N / 16, fft_waves<CT>()) void fft_cols_wstack_kernel(
+    const HT* __restrict__ H, int64_t hstride, int64_t pbase, int64_t nx, int64_t ny,
+    const double2* __restrict__ tw, double* __restrict__ out, double px, double py, double w0, double dw, int first,
+    const uint32_t* __restrict__ rowbits, int64_t rb_stride) {
+  using S = FftShape<N>;
+  constexpr int NO = 16;  // outputs per thread (16 / RF blocks of RF)
+  __shared__ typename Cx<CT>::R lds[N + N / 16];
+  const int t = threadIdx.x;
+  const int64_t b = blockIdx.x;
+  const int64_t nrows = gridDim.x;
+  int64_t il = b;
+  if (nrows % (8 * kColBlock) == 0)
+    il = (b / (8 * kColBlock)) * (8 * kColBlock) + (b % 8) * kColBlock + (b / 8) % kColBlock;
+  const int64_t i = il;
+  const int64_t p = i - nx / 2;
+  double* orow = out + il * ny;
+  double acc[NO];
+  double nm1v[NO];
+  // the outputs this thread owns: j of element (m, r), kept when j < ny
+#pragma unroll
+  for (int m = 0; m < 16 / S::RF; ++m)
+#pragma unroll
+    for (int r = 0; r < S::RF; ++r) {
+      const int k = out_pos<N, S::RF>(t, m, r, N / S::RF);
+      const int64_t j = (int64_t)((k + (int)(ny / 2)) & (N - 1));
+      const int e_ = m * S::RF + r;
+      acc[e_] = 0.0;
+      nm1v[e_] = 0.0;
+      if (j < ny) {
+        const int64_t q = j - ny / 2;
+        const double l = (double)p * px, mm = (double)q * py;
+        const double e = l * l + mm * mm;
+        nm1v[e_] = -e / (sqrt(1.0 - e) + 1.0);
+        if (!first) acc[e_] = orow[j];
+      }
+    }
+  const HT* colb = H + ((il / kColBlock) * N) * kColBlock + (il % kColBlock);
+  // NB planes in straight-line code (a runtime plane loop around the
+  // transform made the compiler keep ~1300 VGPRs of loop state in scratch)
+#pragma unroll
+  for (int qp = 0; qp < NB; ++qp) {
+    const double2* twq = tw;
+    const int tq = t;
+    const HT* col = colb + (int64_t)qp * hstride;
+    const uint32_t* rb = rowbits ? rowbits + (pbase + qp) * rb_stride : nullptr;
+    CT v[16];
+    HT raw[16];
+    if (rb) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int y = tq + r * S::T;
+        const uint32_t word = rb[(r * S::T) >> 10];
+        raw[r] = HT{0, 0};
+        if ((word >> ((y >> 5) & 31)) & 1u) raw[r] = col[(int64_t)y * kColBlock];
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) raw[r] = col[(int64_t)(tq + r * S::T) * kColBlock];
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      if constexpr (sizeof(HT) == 8) asm volatile("" : "+v"(raw[r].x), "+v"(raw[r].y));
+      v[r] = ccast<CT>(raw[r]);
+    }
+    fft_core<N>(v, tq, lds, twq);
+    const double w_plane = w0 + (double)(pbase + qp) * dw;
+    // every element's contribution computed branch-free (the outputs past ny
+    // too, then dropped): a divergent branch per element made the carried
+    // accumulators spill (~1300 VGPRs); the kept values are bit-identical
+#pragma unroll
+    for (int m = 0; m < 16 / S::RF; ++m)
+#pragma unroll
+      for (int r = 0; r < S::RF; ++r) {
+        const int k = out_pos<N, S::RF>(tq, m, r, N / S::RF);
+        const int64_t j = (int64_t)((k + (int)(ny / 2)) & (N - 1));
+        const int e_ = m * S::RF + r;
+        const int64_t q = j - ny / 2;
+        const double sgn = ((p + q) & 1) ? -1.0 : 1.0;
+        const double2 g = ccast<double2>(v[e_]);
+        const double ph = -2.0 * w_plane * nm1v[e_];  // the screen's phase / pi
+        double sn, cs;
+        if constexpr (sizeof(CT) == 8 && CIP_SCREEN_F32 == 1) {
+          const float red = (float)(ph - 2.0 * rint(0.5 * ph));
+          float sf, cf;
+          sincospif(red, &sf, &cf);
+          sn = sf;
+          cs = cf;
+        } else {
+          sincospi(ph, &sn, &cs);
+        }
+        const double val = sgn * (g.x * cs - g.y * sn);
+        acc[e_] = (first && qp == 0) ? val : acc[e_] + val;
+      }
+  }
+#pragma unroll
+  for (int m = 0; m < 16 / S::RF; ++m)
+#pragma unroll
+    for (int r = 0; r < S::RF; ++r) {
+      const int k = out_pos<N, S::RF>(t, m, r, N / S::RF);
+      const int64_t j = (int64_t)((k + (int)(ny / 2)) & (N - 1));
+      if (j < ny) orow[j] = acc[m * S::RF + r];
+    }
+}
+
+hipError_t launch_fft_cols_wstack(const double* H, int64_t hstride_bytes, int nb, int64_t pbase, int64_t nv,
+                                  int64_t nx, int64_t ny, const double* tw_v, double* out, double px, double py,
+                                  double w0, double dw, int first, const uint32_t* rowbits, int64_t rb_stride,
+                                  hipStream_t s, bool h_f32) {
+  if (nb <= 0) return hipSuccess;
+  const dim3 gd((unsigned)nx);
+  const double2* tw = (const double2*)tw_v;
+  const bool fft_f32 = fft_f32_enabled();
+  const int64_t hs = hstride_bytes / (h_f32 ? (int64_t)sizeof(float2) : (int64_t)sizeof(double2));
+  // the packed class's plane pairs, grids up to 8192 (16384: one 1024-thread
+  // block per CU would spill the pair's state)
+  if (nb != 2 || !h_f32 || !fft_f32 || nv > 8192) return hipErrorInvalidValue;
+#define COLSW(NN)                                                                                              \
+  case NN:                                                                                                     \
+    fft_cols_wstack_kernel<NN, float2, float2, 2><<<gd, dim3(NN / 16), 0, s>>>(                                \
+        (const float2*)H, hs, pbase, nx, ny, tw, out, px, py, w0, dw, first, rowbits, rb_stride);              \
+    break;
+  switch (nv) {
+    COLSW(1024)
+    COLSW(2048)
+    COLSW(4096)
+    COLSW(8192)
+    default:
+      return hipErrorInvalidValue;
+  }
+#undef COLSW
+  return hipGetLastError();
+}
+
 static bool fft_len_ok(int64_t n) { return n == 1024 || n == 2048 || n == 4096 || n == 8192 || n == 16384; }
 
 bool fast_fft_supported(int64_t nu, int64_t nv, int64_t nx, int64_t ny) {

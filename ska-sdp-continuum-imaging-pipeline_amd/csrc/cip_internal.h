@@ -183,6 +183,14 @@ hipError_t launch_fft_cols(const double* H, int64_t nv, int64_t nx, int64_t ny, 
                            double* out, const double* cx, const double* cy, double px, double py, double w_plane,
                            int first, const double* norm, const uint32_t* rowbits, hipStream_t s,
                            bool h_f32 = false);
+// w-stacking pass B over nb consecutive planes (global pbase ..): their
+// pass-A outputs at H + q hstride_bytes, summed per image row in plane order
+// and written once (first: overwrite, else added to out's values); rowbits:
+// plane p's tile-row words at rowbits + p rb_stride (NULL: dense)
+hipError_t launch_fft_cols_wstack(const double* H, int64_t hstride_bytes, int nb, int64_t pbase, int64_t nv,
+                                  int64_t nx, int64_t ny, const double* tw_v, double* out, double px, double py,
+                                  double w0, double dw, int first, const uint32_t* rowbits, int64_t rb_stride,
+                                  hipStream_t s, bool h_f32);
 // strips (multi-GPU strong scaling): pass A over rows [y0, y1)
 // of gT (zeroed after reading) into H with y1 - y0 rows per block; pass B for
 // image rows [i0, i1) (multiples of the column block) from an H holding those

@@ -1,0 +1,59 @@
+"""
+w-stacking pass B over plane pairs (CIP_WSTACK_PAIRB=1, cip_fft.hip
+fft_cols_wstack_kernel): the packed class's two planes' screened
+contributions summed in registers and the image written once per pair, in the
+per-plane path's order of additions - the same image bit for bit, for odd and
+even plane counts and a w-plane range (cip_ms2dirty_wplanes). Each mode runs
+in a child process.
+"""
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = Path(__file__).resolve().parents[1]
+
+CHILD = r"""
+import sys, numpy as np, torch
+sys.path[:0] = [sys.argv[1] + "/ska-sdp-continuum-imaging-pipeline_amd"]
+from ska_sdp_cip_amd import synthetic as syn
+from ska_sdp_cip_amd.gridder import device_ms2dirty
+out = sys.argv[2]
+ms = syn.make_measurement_set(8000, 32, n_ant=24, array_radius_m=2500.0, seed=31)
+vis = np.ascontiguousarray(ms.visibilities()[..., 0], dtype=np.complex64)
+w = np.ascontiguousarray(ms.weights()[..., 0], dtype=np.float32)
+uvw, f = ms.uvw(), ms.channel_frequencies()
+t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()
+res = {}
+for npix, wscale in ((1024, 20.0), (2048, 35.0)):
+    px = syn.pixel_size_for_grid(uvw, f, npix)
+    u = uvw * np.array([1.0, 1.0, wscale])
+    img, prm = device_ms2dirty(t(u), t(f), t(vis), t(w), npix, npix, px, px, epsilon=1e-4, do_wstacking=True,
+                               single_precision_accumulation=True)
+    res["n%d" % npix] = img.cpu().numpy()
+    res["planes%d" % npix] = prm.nplanes
+    img2, _ = device_ms2dirty(t(u), t(f), t(vis), t(w), npix, npix, px, px, epsilon=1e-4, do_wstacking=True,
+                              single_precision_accumulation=True, planes=(1, prm.nplanes - 2))
+    res["r%d" % npix] = img2.cpu().numpy()
+np.savez(out, **res)
+"""
+
+
+def _run(tmp_path, on):
+    out = tmp_path / f"pairb{on}.npz"
+    env = dict(os.environ, CIP_WSTACK_PAIRB="1" if on else "0")
+    subprocess.run([sys.executable, "-c", CHILD, str(ROOT), str(out)], env=env, check=True, timeout=180)
+    return np.load(out)
+
+
+def test_plane_pair_pass_b_is_bit_identical(gpu_device, tmp_path):
+    off, on = _run(tmp_path, False), _run(tmp_path, True)
+    counts = {int(off["planes1024"]) % 2, int(off["planes2048"]) % 2}
+    print("plane counts", int(off["planes1024"]), int(off["planes2048"]))
+    for k in off.files:
+        assert np.array_equal(off[k], on[k]), k
+    assert counts  # (odd and even counts both exercised when the two differ in parity)
