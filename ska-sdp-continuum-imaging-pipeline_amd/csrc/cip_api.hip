@@ -627,6 +627,16 @@ static bool scatter_order() {
   return on;
 }
 
+// CIP_PACKED_RUNS=0: ragged runs keep the (row, channel start, channel stop)
+// record and the order pass gathers delta[row] per run (A/B experiments)
+static bool packed_runs() {
+  static const bool on = [] {
+    const char* e = getenv("CIP_PACKED_RUNS");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 // sub-blocks per radix workgroup: pass 0 (place blocks of ~500 runs) and the
 // dense passes (4096 runs); CIP_RADIX_G0 / CIP_RADIX_G1 override (A/B)
 static int radix_group(int pass) {
@@ -685,12 +695,16 @@ static int make_plan(Workspace* ws, const double* uvw, const double* fx, const R
   CIP_ALLOC(hist0, int64_t, "radix_hist0", 256 * (int64_t)nblk + 1)
   CIP_ALLOC(hist0g, int64_t, "radix_hist0g", 256 * ng0 + 1)
   CIP_ALLOC(scan_h0, int64_t, "scan_hist0", scan_tmp_elems(256 * ng0 + 1))
-  CIP_HIP_CHECK(launch_plan_place(uvw, fx, m, vis, vis_dtype, wgt, wgt_dtype, g, err, vis_class, blk_cnt, park_key,
-                                  park_run, partial, hist0, s, park_uv));
-  CIP_HIP_CHECK(launch_prep_final(partial, nblk, red, s));
   int key_bits = 1;
   while (key_bits < 32 && ((int64_t)1 << key_bits) < ntiles) ++key_bits;
   const int npass = (key_bits + 7) / 8;
+  // packed ragged runs (RowMap::pk_runs): the lane scatter's ordered plans
+  // whose radix digits stay below the length bits
+  RowMap mp = m;
+  mp.pk_runs = (ragged && m.pk_cbits && order && g.support <= 16 && 8 * npass <= kRunLenShift && packed_runs()) ? 1 : 0;
+  CIP_HIP_CHECK(launch_plan_place(uvw, fx, mp, vis, vis_dtype, wgt, wgt_dtype, g, err, vis_class, blk_cnt, park_key,
+                                  park_run, partial, hist0, s, park_uv));
+  CIP_HIP_CHECK(launch_prep_final(partial, nblk, red, s));
   CIP_HIP_CHECK(launch_radix_group_hist(hist0, nblk, g0, hist0g, s));
   CIP_HIP_CHECK(exclusive_scan_i64(hist0g, 256 * ng0 + 1, scan_h0, s));
   int64_t* h = (int64_t*)pinned(ws, 4 * sizeof(int64_t));
@@ -739,11 +753,11 @@ static int make_plan(Workspace* ws, const double* uvw, const double* fx, const R
     std::swap(uin, uout);
   }
   uint64_t* runs = rin;
-  CIP_HIP_CHECK(launch_tile_offsets(kin, nruns, ntiles, tile_runs, s));
+  CIP_HIP_CHECK(launch_tile_offsets(kin, nruns, ntiles, tile_runs, s, mp.pk_runs ? kRunKeyMask : 0xffffffffu));
   const int64_t* tile_run_off = tile_runs;
   CIP_ALLOC(run_goff, int64_t, "run_goff", nruns + 1)
   CIP_ALLOC(scan_tmp2, int64_t, "scan_tmp2", scan_tmp_elems(nruns + 1))
-  CIP_HIP_CHECK(scan_run_offsets(runs, nruns, run_goff, scan_tmp2, s));
+  CIP_HIP_CHECK(scan_run_offsets(runs, nruns, run_goff, scan_tmp2, s, mp.pk_runs ? kin : nullptr));
   CIP_HIP_CHECK(launch_tile_vis(run_goff, tile_run_off, ntiles, tile_vis_off, tile_vis, s));
   if (g.ntx % 32 == 0 && grid_mask()) {
     CIP_ALLOC(dmask, uint8_t, "dirty_mask", g.ntx * g.nty * g.nplanes)
@@ -811,7 +825,7 @@ static int make_plan(Workspace* ws, const double* uvw, const double* fx, const R
     CIP_HIP_CHECK(launch_chunk_emit(tile_vis_off, tile_vis, win_off, run_goff, tile_runs, ntiles, kOrderWindow, 0, nwin,
                                     windows, s));
     CIP_ALLOC(perm, uint32_t, "perm", ragged ? 2 * nvis : nvis)
-    CIP_HIP_CHECK(launch_order(uvw, fx, vis_class, g, m, runs, run_goff, tile_runs, windows, nwin, perm, s, uin));
+    CIP_HIP_CHECK(launch_order(uvw, fx, vis_class, g, mp, runs, run_goff, tile_runs, windows, nwin, perm, s, uin));
     pr->perm = perm;
   }
   return CIP_OK;
@@ -919,7 +933,9 @@ static int prepare(Workspace* ws, const double* uvw, int64_t nrow, const double*
   m.nchan = nchan;
   m.inv_nchan = 1.0 / (double)nchan;
   m.delta = nullptr;
-  m.vis_row = nullptr;
+  m.off = nullptr;
+  m.seg_row = nullptr;
+  m.nrow = 0;
   m.pk_cbits = m.pk_rbits = 0;
   m.flags4 = vis_dtype == CIP_POL4I ? flags4 : nullptr;
   m.nvis = nrow * nchan;
@@ -929,10 +945,10 @@ static int prepare(Workspace* ws, const double* uvw, int64_t nrow, const double*
     if (nrow > 0) {
       int64_t* off = buf<int64_t>(ws, "ragged_off", nrow + 1);
       int64_t* delta = buf<int64_t>(ws, "ragged_delta", nrow);
-      uint32_t* vis_row = buf<uint32_t>(ws, "ragged_vis_row", ragged->nvis);
+      uint32_t* seg_row = buf<uint32_t>(ws, "ragged_seg_row", (ragged->nvis + 63) / 64 + 1);
       int64_t* scan_tmp = buf<int64_t>(ws, "ragged_scan", scan_tmp_elems(nrow + 1));
       unsigned* rerr = buf<unsigned>(ws, "ragged_err", 1);
-      if (!off || !delta || !vis_row || !scan_tmp || !rerr) return CIP_ENOMEM;
+      if (!off || !delta || !seg_row || !scan_tmp || !rerr) return CIP_ENOMEM;
       CIP_HIP_CHECK(hipMemsetAsync(rerr, 0, sizeof(unsigned), s));
       CIP_HIP_CHECK(launch_ragged_lengths(ragged->chan_start, ragged->chan_stop, nrow, nchan, off, rerr, s));
       CIP_HIP_CHECK(exclusive_scan_i64(off, nrow + 1, scan_tmp, s));
@@ -943,9 +959,11 @@ static int prepare(Workspace* ws, const double* uvw, int64_t nrow, const double*
       CIP_HIP_CHECK(hipStreamSynchronize(s));
       if ((unsigned)hr[1] != 0u) return set_error(CIP_EINVAL, "row slice channel range outside [0, nchan)");
       if (hr[0] != ragged->nvis) return set_error(CIP_EINVAL, "visibility count differs from the row slices' total");
-      CIP_HIP_CHECK(launch_ragged_expand(off, ragged->chan_start, nrow, delta, vis_row, s));
+      CIP_HIP_CHECK(launch_ragged_expand(off, ragged->chan_start, nrow, delta, seg_row, s));
       m.delta = delta;
-      m.vis_row = vis_row;
+      m.off = off;
+      m.seg_row = seg_row;
+      m.nrow = nrow;
       // ordered-stream entries (index, row, channel) when they fit 64 bits
       auto bits = [](int64_t n) {
         int b = 1;

@@ -432,19 +432,28 @@ __device__ __forceinline__ void split_index(uint32_t i, int64_t nchan, double in
 // row-major (nrow, nchan), index row * nchan + c. Ragged: row slices (the
 // uvw_tiling Tile layout, reference uvw_tiling/tile.py:14-124): row r holds
 // channels [c0_r, c1_r) at vis[off_r, off_r + c1_r - c0_r), so the index is
-// delta[r] + c with delta[r] = off_r - c0_r, and vis_row[i] is the row of
-// visibility i.
+// delta[r] + c with delta[r] = off_r - c0_r; seg_row[k] is the row of
+// visibility 64 k (the place pass's wave segments find their lanes' rows from
+// it and the row starts off[], ragged_row_of below).
 struct RowMap {
   int64_t nchan;            // channels (f/c entries)
   int64_t nvis;             // visibilities
   double inv_nchan;         // 1 / nchan
   const int64_t* delta;     // ragged: per-row index offset; NULL = dense
-  const uint32_t* vis_row;  // ragged: row of each visibility
+  const int64_t* off;       // ragged: row starts (nrow + 1 entries)
+  const uint32_t* seg_row;  // ragged: row of each 64-visibility segment's first visibility
+  int64_t nrow;             // ragged: rows (slices)
   const uint8_t* flags4;    // raw linear-feed input (WK_POL4I): (nvis, 4) flags, or NULL = none flagged
   // ragged ordered-stream entries packed as (index, row, channel) when their
   // bit widths fit 64 bits (cbits = channel bits, rbits = row bits; 0 = the
   // (row << 16) | channel form, index = delta[row] + channel)
   int pk_cbits, pk_rbits;
+  // packed ragged runs (pk_cbits != 0, bank-class ordered plans of the lane
+  // scatter, keys of <= 24 bits; make_plan): a run record is the ordered-stream
+  // entry of its first visibility (position d of the run: entry + d (1 +
+  // 2^(cbits + rbits))) and its length - 1 rides in bits 26-31 of its sort key,
+  // above the radix digits - so the order pass needs no delta[row] gather
+  int pk_runs = 0;
   // time pairs (2-D fp64 class, dense rows): device pointer to
   // the detected row stride D of one dump (pair_stride_kernel), or NULL. Rows
   // of even dump blocks (row / D even) pair with row + D at the same channel
@@ -454,6 +463,9 @@ struct RowMap {
   // tap and component for both visibilities.
   const int64_t* pair_d = nullptr;
 };
+
+constexpr int kRunLenShift = 26;  // RowMap::pk_runs: run length - 1 in sort-key bits 26-31
+constexpr uint32_t kRunKeyMask = (1u << kRunLenShift) - 1u;
 
 // Class-byte flags of a time pair (planner -> order pass): the class is bits
 // 0-4; the ordered stream marks a pair leader in bit 31 of its dense entry and
@@ -467,14 +479,29 @@ __device__ __forceinline__ int64_t vis_index(const RowMap& m, int64_t r, int64_t
   return m.delta ? m.delta[r] + c : r * m.nchan + c;
 }
 
-__device__ __forceinline__ void vis_rowchan(const RowMap& m, int64_t i, int64_t* r, int64_t* c) {
-  if (m.delta) {
-    const int64_t rr = (int64_t)m.vis_row[i];
-    *r = rr;
-    *c = i - m.delta[rr];
-  } else {
-    split_index64(i, m.nchan, m.inv_nchan, r, c);
+// Ragged rows: the row of lane visibility i of a wave's 64-visibility segment
+// (wave-uniform s = seg_row[seg], nx = off[s + 1], ilast = the segment's last
+// visibility; lanes past the end pass any i of the segment). A segment that
+// stays inside row s (rows longer than a wave: every segment of whole
+// 256-channel rows) needs no more, else the row starts after s are loaded one
+// per lane and each lane counts those <= i (sorted; empty rows repeat a start).
+__device__ __forceinline__ int64_t ragged_row_of(const RowMap& m, int64_t s, int64_t nx, int64_t ilast, int64_t i) {
+  const int lane = threadIdx.x & 63;
+  if (nx > ilast) return s;  // uniform
+  int64_t r = s;
+  for (int64_t base = s + 1;; base += 64) {
+    const int64_t q = base + lane;
+    const int64_t o = q <= m.nrow ? m.off[q] : INT64_MAX;
+    const unsigned long long in = __ballot(o <= ilast);  // a prefix of the lanes (sorted)
+    const int nb = __popcll(in);
+    for (int j = 0; j < nb; ++j) {
+      const int64_t oj = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(o >> 32), j) << 32) |
+                                   (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)o, j));
+      r += i >= oj ? 1 : 0;
+    }
+    if (nb < 64) break;
   }
+  return r;
 }
 
 // Entries of the bank-class ordered stream (perm, cip_grid.hip order_kernel):

@@ -130,7 +130,7 @@ __device__ __forceinline__ unsigned origin_class_f32(float us, float vs, float f
 // entry per absorbed partner - so the scatter's waves are uniformly pairs or
 // singles (one mixed wave at the boundary) and the nulls fill whole waves at
 // the window's end.
-template <bool GATHER, bool WIDE, bool PAIRS = false>
+template <bool GATHER, int WIDE, bool PAIRS = false>
 __global__ __launch_bounds__(kOrderThreads, PAIRS ? 6 : 8) void order_kernel(const double* __restrict__ uvw,
                                                               const double* __restrict__ fx,
                                                               const uint8_t* __restrict__ vis_class, GridGeometry g,
@@ -140,7 +140,7 @@ __global__ __launch_bounds__(kOrderThreads, PAIRS ? 6 : 8) void order_kernel(con
                                                               const Chunk* __restrict__ windows, int64_t nwindows,
                                                               void* __restrict__ perm,
                                                               const uint64_t* __restrict__ run_uv) {
-  static_assert(!PAIRS || (GATHER && !WIDE), "time pairs: dense rows with gathered classes");
+  static_assert(!PAIRS || (GATHER && WIDE == 0), "time pairs: dense rows with gathered classes");
   constexpr int NCLS = PAIRS ? 64 : 32;  // PAIRS: leaders' classes 0..31, singles' 32..63
   __shared__ __attribute__((aligned(16))) unsigned s_cnt[NCLS];
   // the staged slices are dead once every position has its class: the level
@@ -149,7 +149,7 @@ __global__ __launch_bounds__(kOrderThreads, PAIRS ? 6 : 8) void order_kernel(con
     struct {
       float2 uv[GATHER ? 1 : kOrderBatch];  // (u scale_u, v scale_v) of each slice's row (recompute only)
       uint64_t rec[kOrderBatch];
-      int64_t delta[WIDE ? kOrderBatch : 1];  // ragged: delta[row] of each slice (index = delta + channel)
+      int64_t delta[WIDE == 1 ? kOrderBatch : 1];  // ragged: delta[row] of each slice (index = delta + channel)
       int off[kOrderBatch + 1];  // slice starts relative to the window start
       uint16_t idx[kOrderBatch];  // slice of each position
     } a;
@@ -171,13 +171,25 @@ __global__ __launch_bounds__(kOrderThreads, PAIRS ? 6 : 8) void order_kernel(con
   for (int k = threadIdx.x; k < nst; k += kOrderThreads) {
     s_off[k] = (int)(run_goff[ch.first_run + k] - sb);
     const uint64_t rec = runs[ch.first_run + k];
-    s_rec[k] = rec;
-    if constexpr (WIDE) sh.a.delta[k] = m.delta[(int64_t)(rec >> 32)];
+    if constexpr (WIDE == 2) {
+      // packed ragged entries: the slice's first entry; position d of the
+      // slice is that + d (index + d, channel + d); packed runs carry it
+      if (m.pk_runs) {
+        s_rec[k] = rec;
+      } else {
+        const int64_t row = (int64_t)(rec >> 32), c = (int64_t)((rec >> 16) & 0xffff);
+        s_rec[k] = perm_encode_wide(m, m.delta[row] + c, row, c);
+      }
+    } else {
+      s_rec[k] = rec;
+    }
+    if constexpr (WIDE == 1) sh.a.delta[k] = m.delta[(int64_t)(rec >> 32)];
     if constexpr (!GATHER) {
       if (run_uv) {  // carried with the run through the sort: contiguous, no gather
         s_uv[k] = __builtin_bit_cast(float2, run_uv[ch.first_run + k]);
       } else {
-        const int64_t row = (int64_t)(rec >> 32);
+        const int64_t row = m.pk_runs ? (int64_t)((rec >> m.pk_cbits) & ((1ull << m.pk_rbits) - 1ull))
+                                      : (int64_t)(rec >> 32);
         s_uv[k] = make_float2((float)(uvw[3 * row] * g.scale_u), (float)(uvw[3 * row + 1] * g.scale_v));
       }
     }
@@ -191,11 +203,13 @@ __global__ __launch_bounds__(kOrderThreads, PAIRS ? 6 : 8) void order_kernel(con
     for (int p = a; p < b; ++p) s_idx[p] = (uint16_t)k;
   }
   __syncthreads();
-  using Entry = typename std::conditional<WIDE, uint64_t, uint32_t>::type;
+  using Entry = typename std::conditional<WIDE != 0, uint64_t, uint32_t>::type;
+  const int pk_shift = m.pk_cbits + m.pk_rbits;  // WIDE == 2: entry = (index << pk_shift) | (row << cbits) | channel
+  const uint64_t pk_step = WIDE == 2 ? (1ull << pk_shift) + 1ull : 0ull;
   Entry packed[kOrderPer];
   unsigned cls[kOrderPer], rk[kOrderPer];
   int slice[kOrderPer];
-  int64_t chan[kOrderPer];
+  int chan[kOrderPer];
   // indices first, then the class loads back to back: one memory round trip
   // for the thread's positions instead of one each
 #pragma unroll
@@ -203,13 +217,19 @@ __global__ __launch_bounds__(kOrderThreads, PAIRS ? 6 : 8) void order_kernel(con
     const int qi = threadIdx.x + k * kOrderThreads;
     if (qi < nsb) {
       const int lo = s_idx[qi];
-      const uint64_t rec = s_rec[lo];
-      const int64_t row = (int64_t)(rec >> 32);
-      const int64_t c = (int64_t)((rec >> 16) & 0xffff) + (qi - s_off[lo]);
-      if constexpr (WIDE) packed[k] = (Entry)perm_encode_wide(m, sh.a.delta[lo] + c, row, c);
-      else packed[k] = (Entry)(row * m.nchan + c);
+      const int d = qi - s_off[lo];
+      if constexpr (WIDE == 2) {
+        packed[k] = (Entry)(s_rec[lo] + (uint64_t)d * pk_step);
+        chan[k] = (int)(packed[k] & ((1ull << m.pk_cbits) - 1ull));
+      } else {
+        const uint64_t rec = s_rec[lo];
+        const int64_t row = (int64_t)(rec >> 32);
+        const int64_t c = (int64_t)((rec >> 16) & 0xffff) + d;
+        if constexpr (WIDE == 1) packed[k] = (Entry)perm_encode_wide(m, sh.a.delta[lo] + c, row, c);
+        else packed[k] = (Entry)(row * m.nchan + c);
+        chan[k] = (int)c;
+      }
       slice[k] = lo;
-      chan[k] = c;
     }
   }
 #pragma unroll
@@ -222,7 +242,9 @@ __global__ __launch_bounds__(kOrderThreads, PAIRS ? 6 : 8) void order_kernel(con
         cls[k] = (b & kClassAbsorbed) ? 64u : ((b & kClassLeader) ? (b & 31u) : 32u + (b & 31u));
         if (b & kClassLeader) packed[k] |= (Entry)kPermLeader;
       } else if constexpr (GATHER) {
-        cls[k] = vis_class[WIDE ? sh.a.delta[slice[k]] + chan[k] : (int64_t)packed[k]];
+        cls[k] = vis_class[WIDE == 2   ? (int64_t)((uint64_t)packed[k] >> pk_shift)
+                           : WIDE == 1 ? sh.a.delta[slice[k]] + chan[k]
+                                       : (int64_t)packed[k]];
       } else {
         const float2 uv = s_uv[slice[k]];
         cls[k] = origin_class_f32(uv.x, uv.y, (float)fx[chan[k]], g);
@@ -300,16 +322,19 @@ hipError_t launch_order(const double* uvw, const double* fx, const uint8_t* vis_
 #define ORDER(GA, WI)                                                              \
   order_kernel<GA, WI><<<dim3((unsigned)nwindows), dim3(kOrderThreads), 0, s>>>( \
       uvw, fx, vis_class, g, m, runs, run_goff, tile_run_off, windows, nwindows, perm, run_uv)
-  const bool wide = m.delta != nullptr;  // ragged row slices: u64 entries
+  // ragged row slices: u64 entries (2: packed (index, row, channel))
+  const int wide = m.delta == nullptr ? 0 : (m.pk_cbits ? 2 : 1);
   if (vis_class && m.pair_d != nullptr && !wide) {
-    order_kernel<true, false, true><<<dim3((unsigned)nwindows), dim3(kOrderThreads), 0, s>>>(
+    order_kernel<true, 0, true><<<dim3((unsigned)nwindows), dim3(kOrderThreads), 0, s>>>(
         uvw, fx, vis_class, g, m, runs, run_goff, tile_run_off, windows, nwindows, perm, run_uv);
   } else if (vis_class) {
-    if (wide) ORDER(true, true);
-    else ORDER(true, false);
+    if (wide == 2) ORDER(true, 2);
+    else if (wide) ORDER(true, 1);
+    else ORDER(true, 0);
   } else {
-    if (wide) ORDER(false, true);
-    else ORDER(false, false);
+    if (wide == 2) ORDER(false, 2);
+    else if (wide) ORDER(false, 1);
+    else ORDER(false, 0);
   }
 #undef ORDER
   return hipGetLastError();

@@ -26,7 +26,10 @@ int set_error(int code, const std::string& msg);
 int64_t scan_tmp_elems(int64_t n);
 // run_goff[k] = sum of the lengths of runs [0, k), k in [0, nruns] (fused
 // run-length + exclusive scan)
-hipError_t scan_run_offsets(const uint64_t* runs, int64_t nruns, int64_t* run_goff, int64_t* tmp, hipStream_t s);
+// run lengths from the run records, or (run_keys, RowMap::pk_runs) from the
+// sorted keys' bits 26-31
+hipError_t scan_run_offsets(const uint64_t* runs, int64_t nruns, int64_t* run_goff, int64_t* tmp, hipStream_t s,
+                            const uint32_t* run_keys = nullptr);
 hipError_t exclusive_scan_i64(int64_t* data, int64_t n, int64_t* tmp, hipStream_t s);
 
 // ---- gridder planner (cip_plan.hip) ----------------------------------------
@@ -59,11 +62,11 @@ hipError_t launch_pair_stride(const double* uvw, int64_t nrow, int64_t* out, hip
 // ragged rows: out[r] = chan_stop[r] - chan_start[r] (out[nrow] = 0; err bit
 // set for a range outside [0, nchan)); after the exclusive scan (off[r] = row
 // r's first visibility), launch_ragged_expand writes delta[r] = off[r] -
-// chan_start[r] and vis_row for every visibility.
+// chan_start[r] and seg_row[k] = the row of visibility 64 k.
 hipError_t launch_ragged_lengths(const int32_t* c0, const int32_t* c1, int64_t nrow, int64_t nchan, int64_t* out,
                                  unsigned* err, hipStream_t s);
 hipError_t launch_ragged_expand(const int64_t* off, const int32_t* c0, int64_t nrow, int64_t* delta,
-                                uint32_t* vis_row, hipStream_t s);
+                                uint32_t* seg_row, hipStream_t s);
 // one stable LSD radix sort pass on digit (key >> shift) & 255 over nblocks
 // blocks of 4096 slots: dense (blk_cnt NULL, n items) or the place pass's
 // parked runs (blk_cnt). hist: 256 * nblocks + 1 entries, exclusive-scanned
@@ -79,7 +82,7 @@ hipError_t launch_radix_scatter(const uint32_t* keys, const uint64_t* vals, int6
                                 uint64_t* vals_out, hipStream_t s, const uint64_t* vals2 = nullptr,
                                 uint64_t* vals2_out = nullptr);
 hipError_t launch_tile_offsets(const uint32_t* keys, int64_t nruns, int64_t ntiles, int64_t* tile_run_off,
-                               hipStream_t s);
+                               hipStream_t s, uint32_t kmask = 0xffffffffu);
 // per grid plane (nplanes x ntx x nty bytes); bits (optional, ntx % 32 ==
 // 0): the masks bit-packed, ntx / 32 words per tile row, ntx nty / 32 per plane
 hipError_t launch_dirty_mask(const int64_t* tile_vis, int64_t ntx, int64_t nty, int64_t ntw, int support,

@@ -12,12 +12,22 @@ constexpr int kScanThreads = 1024;
 constexpr int kScanItems = 4;
 constexpr int64_t kScanBlock = (int64_t)kScanThreads * kScanItems;
 
-// RUNS: the input is the run records (n - 1 of them): item k is run k's
-// length (channel stop - start), item n - 1 is 0, and the scan goes to `data`
-// (the fused run-length pass of the slice offsets)
-template <bool RUNS>
+// RUNS: the input is the runs (n - 1 of them): item k is run k's length, item
+// n - 1 is 0, and the scan goes to `data` (the fused run-length pass of the
+// slice offsets); RUNS = 1: lengths from the run records (channel stop -
+// start), 2: from the sort keys (RowMap::pk_runs: length - 1 in bits 26-31)
+template <int RUNS>
+__device__ __forceinline__ int64_t run_length_at(const void* __restrict__ src, int64_t k) {
+  if constexpr (RUNS == 2) {
+    return (int64_t)(((const uint32_t*)src)[k] >> kRunLenShift) + 1;
+  } else {
+    const uint64_t rec = ((const uint64_t*)src)[k];
+    return (int64_t)(rec & 0xffff) - (int64_t)((rec >> 16) & 0xffff);
+  }
+}
+template <int RUNS>
 __global__ __launch_bounds__(kScanThreads) void scan_local_kernel(int64_t* data, int64_t n, int64_t* block_sums,
-                                                                  const uint64_t* __restrict__ runs) {
+                                                                  const void* __restrict__ runs) {
   __shared__ int64_t wave_tot[kScanThreads / 64];
   const int64_t base = (int64_t)blockIdx.x * kScanBlock + (int64_t)threadIdx.x * kScanItems;
   int64_t v[kScanItems];
@@ -28,8 +38,7 @@ __global__ __launch_bounds__(kScanThreads) void scan_local_kernel(int64_t* data,
 #pragma unroll
     for (int i = 0; i < kScanItems; ++i) {
       if constexpr (RUNS) {
-        const uint64_t rec = runs[base + i];
-        v[i] = (int64_t)(rec & 0xffff) - (int64_t)((rec >> 16) & 0xffff);
+        v[i] = run_length_at<RUNS>(runs, base + i);
       } else {
         v[i] = data[base + i];
       }
@@ -39,10 +48,7 @@ __global__ __launch_bounds__(kScanThreads) void scan_local_kernel(int64_t* data,
     for (int i = 0; i < kScanItems; ++i) {
       if constexpr (RUNS) {
         v[i] = 0;
-        if (base + i < n - 1) {
-          const uint64_t rec = runs[base + i];
-          v[i] = (int64_t)(rec & 0xffff) - (int64_t)((rec >> 16) & 0xffff);
-        }
+        if (base + i < n - 1) v[i] = run_length_at<RUNS>(runs, base + i);
       } else {
         v[i] = (base + i < n) ? data[base + i] : 0;
       }
@@ -107,13 +113,16 @@ int64_t scan_tmp_elems(int64_t n) {
   return total + 1;
 }
 
-static hipError_t scan_impl(int64_t* data, int64_t n, int64_t* tmp, const uint64_t* runs, hipStream_t s) {
+static hipError_t scan_impl(int64_t* data, int64_t n, int64_t* tmp, const uint64_t* runs, hipStream_t s,
+                            const uint32_t* run_keys = nullptr) {
   if (n <= 0) return hipSuccess;
   const int64_t nb = (n + kScanBlock - 1) / kScanBlock;
-  if (runs)
-    scan_local_kernel<true><<<dim3((unsigned)nb), dim3(kScanThreads), 0, s>>>(data, n, tmp, runs);
+  if (run_keys)
+    scan_local_kernel<2><<<dim3((unsigned)nb), dim3(kScanThreads), 0, s>>>(data, n, tmp, run_keys);
+  else if (runs)
+    scan_local_kernel<1><<<dim3((unsigned)nb), dim3(kScanThreads), 0, s>>>(data, n, tmp, runs);
   else
-    scan_local_kernel<false><<<dim3((unsigned)nb), dim3(kScanThreads), 0, s>>>(data, n, tmp, nullptr);
+    scan_local_kernel<0><<<dim3((unsigned)nb), dim3(kScanThreads), 0, s>>>(data, n, tmp, nullptr);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || nb == 1) return e;
   e = scan_impl(tmp, nb, tmp + nb, nullptr, s);
@@ -126,8 +135,9 @@ hipError_t exclusive_scan_i64(int64_t* data, int64_t n, int64_t* tmp, hipStream_
   return scan_impl(data, n, tmp, nullptr, s);
 }
 
-hipError_t scan_run_offsets(const uint64_t* runs, int64_t nruns, int64_t* run_goff, int64_t* tmp, hipStream_t s) {
-  return scan_impl(run_goff, nruns + 1, tmp, runs, s);
+hipError_t scan_run_offsets(const uint64_t* runs, int64_t nruns, int64_t* run_goff, int64_t* tmp, hipStream_t s,
+                            const uint32_t* run_keys) {
+  return scan_impl(run_goff, nruns + 1, tmp, runs, s, run_keys);
 }
 
 // ------------------------------------------------------------ helpers ----
@@ -281,7 +291,7 @@ __device__ __forceinline__ void place_body(const double* __restrict__ uvw, const
   const int64_t seg_end = (blk + 1) * kPlaceSegs < nseg ? (blk + 1) * kPlaceSegs : nseg;
   // (row, channel) of the lane's visibility, advanced by 256 visibilities per
   // step without a division
-  // (ragged rows: looked up per visibility)
+  // (ragged rows: from the segment's first row, ragged_row_of)
   int64_t r0 = 0, c0 = 0;
   if (!ragged) split_index64((blk * kPlaceSegs + wave) * 64 + lane, nchan, m.inv_nchan, &r0, &c0);
   const int64_t step_r = 256 / nchan, step_c = 256 % nchan;
@@ -291,7 +301,21 @@ __device__ __forceinline__ void place_body(const double* __restrict__ uvw, const
     if (!ragged && m.pair_d != nullptr) pair_d = __builtin_amdgcn_readfirstlane((int)*m.pair_d);
   const int64_t nrow_dense = ragged ? 0 : nvis / nchan;
   const double inv_d = pair_d > 0 ? 1.0 / (double)pair_d : 0.0;
-  for (int64_t seg = blk * kPlaceSegs + wave; seg < seg_end; seg += 4) {
+  // ragged rows: the first rows of the wave's kPlaceSegs / 4 segments and the
+  // starts of the rows after them, loaded once (lane j: segment j), so the
+  // loop's row lookup is a register read, not a chain of dependent loads
+  static_assert(kPlaceSegs / 4 <= 64, "one lane per segment of the wave");
+  int seg_s = 0;
+  int64_t seg_nx = 0;
+  if (ragged) {
+    const int64_t sj = blk * kPlaceSegs + wave + 4 * (int64_t)lane;
+    if (lane < kPlaceSegs / 4 && sj < seg_end) {
+      seg_s = (int)m.seg_row[sj];
+      seg_nx = m.off[seg_s + 1];
+    }
+  }
+  int it = 0;
+  for (int64_t seg = blk * kPlaceSegs + wave; seg < seg_end; seg += 4, ++it) {
     const int64_t i = seg * 64 + lane;
     const bool valid = i < nvis;
     int64_t r = r0, c = c0;
@@ -299,7 +323,11 @@ __device__ __forceinline__ void place_body(const double* __restrict__ uvw, const
     // loads); their results are masked by `valid`
     const int64_t il = valid ? i : 0;
     if (ragged) {
-      vis_rowchan(m, il, &r, &c);
+      const int64_t s = (int64_t)(uint32_t)__builtin_amdgcn_readlane(seg_s, it);
+      const int64_t nx = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(seg_nx >> 32), it) << 32) |
+                                   (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)seg_nx, it));
+      r = ragged_row_of(m, s, nx, seg * 64 + 63 < nvis ? seg * 64 + 63 : nvis - 1, i);
+      c = il - m.delta[r];
     } else {
       c0 += step_c;
       r0 += step_r;
@@ -407,9 +435,14 @@ __device__ __forceinline__ void place_body(const double* __restrict__ uvw, const
         const unsigned long long above = starts & ~((2ull << lane) - 1ull);  // lane 63: 2 << 63 == 0
         const int next = above ? (__ffsll((long long)above) - 1) : nvalid;
         const int64_t slot = blk * kPlaceSegs * 64 + wbase + __popcll(emits & ((1ull << lane) - 1ull));
-        park_key[slot] = key;
         atomicAdd(&s_hist[key & 255u], 1u);
-        park_run[slot] = ((uint64_t)r << 32) | ((uint64_t)c << 16) | (uint64_t)(c + (next - lane));
+        if (m.pk_runs) {  // wave-uniform (ragged rows only)
+          park_key[slot] = key | ((uint32_t)(next - lane - 1) << kRunLenShift);
+          park_run[slot] = perm_encode_wide(m, i, r, c);
+        } else {
+          park_key[slot] = key;
+          park_run[slot] = ((uint64_t)r << 32) | ((uint64_t)c << 16) | (uint64_t)(c + (next - lane));
+        }
         // the run's row pre-scaled (u nu dx, v nv dy) in fp32: the order pass
         // recomputes each visibility's bank class from it and f / c, with no
         // per-visibility class array and no uvw gather
@@ -574,25 +607,25 @@ hipError_t launch_ragged_lengths(const int32_t* c0, const int32_t* c1, int64_t n
   return hipGetLastError();
 }
 
-// one wave per row: delta[r] = off[r] - chan_start[r], and its lanes write the
-// row index over the row's visibility slots
+// one thread per row: delta[r] = off[r] - chan_start[r], and the row of every
+// 64-visibility segment that starts inside it (seg_row[k] = r for
+// 64 k in [off[r], off[r + 1]); one entry per 64 visibilities, where a
+// per-visibility row array cost 4 bytes per visibility written and read)
 __global__ __launch_bounds__(256) void ragged_expand_kernel(const int64_t* __restrict__ off,
                                                             const int32_t* __restrict__ c0, int64_t nrow,
                                                             int64_t* __restrict__ delta,
-                                                            uint32_t* __restrict__ vis_row) {
-  const int64_t r = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const int lane = threadIdx.x & 63;
+                                                            uint32_t* __restrict__ seg_row) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= nrow) return;
   const int64_t a = off[r], b = off[r + 1];
-  for (int64_t i = a + lane; i < b; i += 64) vis_row[i] = (uint32_t)r;
-  if (lane == 0) delta[r] = a - (int64_t)c0[r];
+  delta[r] = a - (int64_t)c0[r];
+  for (int64_t k = (a + 63) >> 6; k * 64 < b; ++k) seg_row[k] = (uint32_t)r;
 }
 
 hipError_t launch_ragged_expand(const int64_t* off, const int32_t* c0, int64_t nrow, int64_t* delta,
-                                uint32_t* vis_row, hipStream_t s) {
+                                uint32_t* seg_row, hipStream_t s) {
   if (nrow <= 0) return hipSuccess;
-  ragged_expand_kernel<<<dim3((unsigned)((nrow * 64 + 255) / 256)), dim3(256), 0, s>>>(off, c0, nrow, delta,
-                                                                                      vis_row);
+  ragged_expand_kernel<<<dim3((unsigned)((nrow + 255) / 256)), dim3(256), 0, s>>>(off, c0, nrow, delta, seg_row);
   return hipGetLastError();
 }
 
@@ -749,15 +782,16 @@ __global__ __launch_bounds__(kRadixThreads, CIP_RADIX_WAVES) void radix_scatter_
   }
 }
 
-// tile_run_off[t] = first sorted run with key >= t (t in [0, ntiles])
+// tile_run_off[t] = first sorted run with key >= t (t in [0, ntiles]; key
+// bits outside kmask carry run lengths, RowMap::pk_runs)
 __global__ void tile_offsets_kernel(const uint32_t* __restrict__ keys, int64_t nruns, int64_t ntiles,
-                                    int64_t* __restrict__ tile_run_off) {
+                                    int64_t* __restrict__ tile_run_off, uint32_t kmask) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t > ntiles) return;
   int64_t lo = 0, hi = nruns;
   while (lo < hi) {
     const int64_t mid = (lo + hi) >> 1;
-    if ((int64_t)keys[mid] < t) lo = mid + 1;
+    if ((int64_t)(keys[mid] & kmask) < t) lo = mid + 1;
     else hi = mid;
   }
   tile_run_off[t] = lo;
@@ -797,8 +831,9 @@ hipError_t launch_radix_scatter(const uint32_t* keys, const uint64_t* vals, int6
 }
 
 hipError_t launch_tile_offsets(const uint32_t* keys, int64_t nruns, int64_t ntiles, int64_t* tile_run_off,
-                               hipStream_t s) {
-  tile_offsets_kernel<<<dim3((unsigned)((ntiles + 256) / 256)), dim3(256), 0, s>>>(keys, nruns, ntiles, tile_run_off);
+                               hipStream_t s, uint32_t kmask) {
+  tile_offsets_kernel<<<dim3((unsigned)((ntiles + 256) / 256)), dim3(256), 0, s>>>(keys, nruns, ntiles, tile_run_off,
+                                                                                 kmask);
   return hipGetLastError();
 }
 
