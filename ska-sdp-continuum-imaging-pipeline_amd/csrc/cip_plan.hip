@@ -306,12 +306,13 @@ __device__ __forceinline__ void place_body(const double* __restrict__ uvw, const
   // loop's row lookup is a register read, not a chain of dependent loads
   static_assert(kPlaceSegs / 4 <= 64, "one lane per segment of the wave");
   int seg_s = 0;
-  int64_t seg_nx = 0;
+  int64_t seg_nx = 0, seg_dl = 0;
   if (ragged) {
     const int64_t sj = blk * kPlaceSegs + wave + 4 * (int64_t)lane;
     if (lane < kPlaceSegs / 4 && sj < seg_end) {
       seg_s = (int)m.seg_row[sj];
       seg_nx = m.off[seg_s + 1];
+      seg_dl = m.delta[seg_s];
     }
   }
   int it = 0;
@@ -326,8 +327,16 @@ __device__ __forceinline__ void place_body(const double* __restrict__ uvw, const
       const int64_t s = (int64_t)(uint32_t)__builtin_amdgcn_readlane(seg_s, it);
       const int64_t nx = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(seg_nx >> 32), it) << 32) |
                                    (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)seg_nx, it));
-      r = ragged_row_of(m, s, nx, seg * 64 + 63 < nvis ? seg * 64 + 63 : nvis - 1, i);
-      c = il - m.delta[r];
+      const int64_t ilast = seg * 64 + 63 < nvis ? seg * 64 + 63 : nvis - 1;
+      if (nx > ilast) {  // the segment inside row s (uniform): its delta is prefetched too
+        const int64_t dl = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(seg_dl >> 32), it) << 32) |
+                                     (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)seg_dl, it));
+        r = s;
+        c = il - dl;
+      } else {
+        r = ragged_row_of(m, s, nx, ilast, i);
+        c = il - m.delta[r];
+      }
     } else {
       c0 += step_c;
       r0 += step_r;
