@@ -323,8 +323,17 @@ struct Workspace {
   // call k - 1's work on the caller's stream (ev_done[parity]: its scatter
   // read the plan, its FFT the masks and weight sum); the caller's stream
   // waits for the plan (ev_planned).
-  hipStream_t plan_stream = nullptr;
+  // Two plan streams (one per parity): a 2-D pipelined call's scatter runs on
+  // its plan stream after its planner (scatter_on_plan_stream), so call k's
+  // pass B on s overlaps call k + 1's scatter while call k + 1's planner
+  // overlaps call k's scatter on the other plan stream.
+  hipStream_t plan_stream = nullptr, plan_stream1 = nullptr;
   hipEvent_t ev_done[2] = {nullptr, nullptr}, ev_planned = nullptr, ev_entry = nullptr;
+  // the grid consumed (its pass A done) by the last call, if that call was a
+  // plan-stream-scatter call (grid_seq == its call_seq): the next such call's
+  // scatter waits for ev_grid only, not for the pass B queued after it on s
+  hipEvent_t ev_grid = nullptr, ev_scattered = nullptr, ev_gate = nullptr;
+  uint64_t call_seq = 0, grid_seq = ~0ull;
   int parity = 0;
   bool parity_scope = false;
   // a planner ran on a caller's stream (parity-0 buffer names) since the last
@@ -397,6 +406,7 @@ static void destroy_workspace(Workspace* ws) {
   if (prev_dev != ws->device) (void)hipSetDevice(ws->device);
   if (ws->async_stream) (void)hipStreamSynchronize(ws->async_stream);
   if (ws->plan_stream) (void)hipStreamSynchronize(ws->plan_stream);
+  if (ws->plan_stream1) (void)hipStreamSynchronize(ws->plan_stream1);
   for (auto& kv : ws->bufs)
     if (kv.second.ptr) (void)hipFree(kv.second.ptr);
   for (auto& p : ws->plans) (void)hipfftDestroy(p.h);
@@ -407,11 +417,14 @@ static void destroy_workspace(Workspace* ws) {
   }
   if (ws->ev_fork) (void)hipEventDestroy(ws->ev_fork);
   if (ws->ev_join) (void)hipEventDestroy(ws->ev_join);
-  if (ws->plan_stream) {
-    (void)hipStreamSynchronize(ws->plan_stream);
-    (void)hipStreamDestroy(ws->plan_stream);
-  }
+  for (hipStream_t ps : {ws->plan_stream, ws->plan_stream1})
+    if (ps) {
+      (void)hipStreamSynchronize(ps);
+      (void)hipStreamDestroy(ps);
+    }
   for (hipEvent_t e : ws->ev_done)
+    if (e) (void)hipEventDestroy(e);
+  for (hipEvent_t e : {ws->ev_grid, ws->ev_scattered, ws->ev_gate})
     if (e) (void)hipEventDestroy(e);
   if (ws->ev_planned) (void)hipEventDestroy(ws->ev_planned);
   if (ws->ev_entry) (void)hipEventDestroy(ws->ev_entry);
@@ -449,7 +462,10 @@ static Workspace* workspace() {
   g_reaper.armed = true;
   std::lock_guard<std::mutex> lock(g_ws_mutex);
   auto it = g_ws.find(key);
-  if (it != g_ws.end()) return it->second;
+  if (it != g_ws.end()) {
+    ++it->second->call_seq;  // every entry point takes its workspace once per call
+    return it->second;
+  }
   Workspace* ws = new Workspace();
   ws->device = dev;
   g_ws[key] = ws;
@@ -1216,6 +1232,16 @@ static bool grid_f32_enabled() {
   return on;
 }
 
+// CIP_PIPE_SCATTER=1: a pipelined 2-D call's scatter runs on the plan stream
+// (after its planner and the previous call's pass A), so the previous call's
+// pass B overlaps it. Off by default: measured 21.11 vs 21.36 Gvis/s at C3
+// (profiles/r05t_ab_pipe_scatter.txt) - the co-running planner, starved of
+// wave slots beside the scatter, is the pipelined step's critical path either way.
+static bool scatter_on_plan_stream() {
+  const char* e = getenv("CIP_PIPE_SCATTER");  // read per call (tests switch it)
+  return e && e[0] == '1';
+}
+
 // CIP_SCATTER_SHARE=0: pipelined calls' scatters take every CU slot (A/B)
 static bool share_cus_enabled() {
   static const bool on = [] {
@@ -1265,9 +1291,10 @@ static bool fft_rowskip() {
 }
 
 // rowbits (with dmask): the plane's tile-row bits (row_bits_kernel)
+// after_rows (may be NULL): recorded on s once pass A has consumed the grid
 static int plane_to_dirty(const DirtyStage& st, const GridGeometry& g, int64_t p, double* grid, double* dirty_out,
                           hipStream_t s, const uint32_t* dmask = nullptr, const double* norm = nullptr,
-                          const uint32_t* rowbits = nullptr, int first = -1) {
+                          const uint32_t* rowbits = nullptr, int first = -1, hipEvent_t after_rows = nullptr) {
   if (first < 0) first = p == 0;  // the first plane overwrites the image, later ones add
   hipEvent_t f0 = g_prof.mark(s);
   if (st.fast) {
@@ -1278,6 +1305,7 @@ static int plane_to_dirty(const DirtyStage& st, const GridGeometry& g, int64_t p
              HIPFFT_SUCCESS) {
     return set_error(CIP_EHIP, "hipfftExecZ2Z failed");
   }
+  if (after_rows) CIP_HIP_CHECK(hipEventRecord(after_rows, s));
   const double w_plane = g.w0 + (double)p * g.dw;
   // pass B carries the crop epilogue: it is booked under "fft"
   if (st.fast)
@@ -1474,9 +1502,21 @@ static int ms2dirty_impl(const double* uvw, int64_t nrow, const double* freq, in
   hipStream_t ps = s;
   if (pipelined) {
     if (!ws->plan_stream) {
-      CIP_HIP_CHECK(hipStreamCreateWithFlags(&ws->plan_stream, hipStreamNonBlocking));
+      // the plan streams at the lowest priority: the scatter on s keeps first
+      // call on freed wave slots (C3 pipelined 21.58-21.62 vs 21.46-21.53
+      // Gvis/s at the default priority, 21.15-21.24 at the highest,
+      // profiles/r05v_ab_plan_priority.txt); CIP_PLAN_PRIORITY=default / high (A/B)
+      int prio_lo = 0, prio_hi = 0;
+      CIP_HIP_CHECK(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
+      const char* pe = getenv("CIP_PLAN_PRIORITY");
+      const int prio = (pe && std::strcmp(pe, "high") == 0) ? prio_hi : (pe && std::strcmp(pe, "default") == 0) ? 0 : prio_lo;
+      CIP_HIP_CHECK(hipStreamCreateWithPriority(&ws->plan_stream, hipStreamNonBlocking, prio));
+      CIP_HIP_CHECK(hipStreamCreateWithPriority(&ws->plan_stream1, hipStreamNonBlocking, prio));
       CIP_HIP_CHECK(hipEventCreateWithFlags(&ws->ev_planned, hipEventDisableTiming));
       CIP_HIP_CHECK(hipEventCreateWithFlags(&ws->ev_entry, hipEventDisableTiming));
+      CIP_HIP_CHECK(hipEventCreateWithFlags(&ws->ev_grid, hipEventDisableTiming));
+      CIP_HIP_CHECK(hipEventCreateWithFlags(&ws->ev_scattered, hipEventDisableTiming));
+      CIP_HIP_CHECK(hipEventCreateWithFlags(&ws->ev_gate, hipEventDisableTiming));
       for (hipEvent_t& e : ws->ev_done) {
         CIP_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         // the first pipelined calls: the planner starts after the work already on s
@@ -1485,14 +1525,15 @@ static int ms2dirty_impl(const double* uvw, int64_t nrow, const double* freq, in
     }
     if (ws->plan_unscoped) {
       // a planner ran on s since the last pipelined call: its buffers (parity
-      // 0) may still be read there
+      // 0) may still be read there - both plan streams wait for it
       CIP_HIP_CHECK(hipEventRecord(ws->ev_entry, s));
       CIP_HIP_CHECK(hipStreamWaitEvent(ws->plan_stream, ws->ev_entry, 0));
+      CIP_HIP_CHECK(hipStreamWaitEvent(ws->plan_stream1, ws->ev_entry, 0));
       ws->plan_unscoped = false;
     }
     ws->parity ^= 1;
-    CIP_HIP_CHECK(hipStreamWaitEvent(ws->plan_stream, ws->ev_done[ws->parity], 0));
-    ps = ws->plan_stream;
+    ps = ws->parity ? ws->plan_stream1 : ws->plan_stream;
+    CIP_HIP_CHECK(hipStreamWaitEvent(ps, ws->ev_done[ws->parity], 0));
   } else if (ws->parity) {
     // back to the parity-0 buffers: their last pipelined user may still be queued on s
     ws->parity = 0;
@@ -1516,11 +1557,23 @@ static int ms2dirty_impl(const double* uvw, int64_t nrow, const double* freq, in
                    (overlap_zero() && !pipelined) ? &grid : nullptr, nullptr, (flags & CIP_REUSE_PLAN) != 0, flags4,
                    true, plane_begin, plane_end);
   ws->parity_scope = false;
-  if (pipelined) {
-    // s continues once the plan exists (also after a failed one: nothing then runs on it)
-    CIP_HIP_CHECK(hipEventRecord(ws->ev_planned, ps));
-    CIP_HIP_CHECK(hipStreamWaitEvent(s, ws->ev_planned, 0));
-  }
+  // s continues once the plan exists (also after a failed one, or any early
+  // return: nothing then runs on it); a plan-stream scatter joins s after the
+  // scatter instead
+  struct PlanJoin {
+    Workspace* ws;
+    hipStream_t ps, s;
+    bool joined;
+    int join() {
+      if (joined) return CIP_OK;
+      joined = true;
+      CIP_HIP_CHECK(hipEventRecord(ws->ev_planned, ps));
+      CIP_HIP_CHECK(hipStreamWaitEvent(s, ws->ev_planned, 0));
+      return CIP_OK;
+    }
+    ~PlanJoin() { (void)join(); }
+  } plan_join{ws, ps, s, !pipelined};
+  if (rc != CIP_OK) (void)plan_join.join();
   if (grid) {
     // join the side stream whatever happened (the workspace grid must not be
     // written by a later call while its memset is still queued)
@@ -1558,7 +1611,33 @@ static int ms2dirty_impl(const double* uvw, int64_t nrow, const double* freq, in
   int64_t pending = -1;  // plane whose pass A sits in slot 0
   const int64_t rb_stride = (g.nty + 31) / 32;
   const uint32_t* rowbits0 = dmask ? dmask + g.nplanes * (g.ntx * g.nty / 32) : nullptr;
-  for (int64_t q = p_lo / G; q * G < p_hi; ++q) {
+  // pipelined 2-D calls: the scatter on the plan stream after the planner and
+  // after the grid is free (the previous call's pass A), s joins it before
+  // pass A, and this call's pass B then overlaps the next call's scatter
+  const bool scatter_ps = pipelined && st.fast && !g.do_wstacking && G == 1 && p_hi - p_lo == 1 && !pair_b &&
+                          scatter_on_plan_stream();
+  if (scatter_ps) {
+    if (ws->grid_seq + 1 == ws->call_seq) {
+      CIP_HIP_CHECK(hipStreamWaitEvent(ps, ws->ev_grid, 0));
+    } else {  // another call used the workspace since: everything queued on s
+      CIP_HIP_CHECK(hipEventRecord(ws->ev_gate, s));
+      CIP_HIP_CHECK(hipStreamWaitEvent(ps, ws->ev_gate, 0));
+    }
+    plan_join.joined = true;  // s joins after the scatter
+    rc = scatter_plane(pp, p_lo, uvw, vis, vis_dtype, wgt, wgt_dtype, st.fast, grid, ps, clean, share_cus_enabled());
+    CIP_HIP_CHECK(hipEventRecord(ws->ev_scattered, ps));
+    CIP_HIP_CHECK(hipStreamWaitEvent(s, ws->ev_scattered, 0));
+    if (rc != CIP_OK) return rc;
+    const uint32_t* dm = dmask ? dmask + p_lo * (g.ntx * g.nty / 32) : nullptr;
+    const uint32_t* rbp = rowbits0 ? rowbits0 + p_lo * rb_stride : nullptr;
+    rc = plane_to_dirty(st, g, p_lo, grid, dirty_out, s, dm, normalise ? pp.red : nullptr, rbp, 1, ws->ev_grid);
+    if (rc != CIP_OK) return rc;
+    ws->grid_seq = ws->call_seq;
+    clean = dmask != nullptr;
+  } else if (const int jr = plan_join.join(); jr != CIP_OK) {
+    return jr;
+  }
+  for (int64_t q = p_lo / G; !scatter_ps && q * G < p_hi; ++q) {
     // pipelined calls: leave CU slots to the next call's planner (profiles/r03_ab_scatter_share.txt)
     rc = scatter_plane(pp, q, uvw, vis, vis_dtype, wgt, wgt_dtype, st.fast, grid, s, clean,
                        pipelined && share_cus_enabled());

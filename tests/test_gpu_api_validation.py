@@ -141,6 +141,38 @@ def test_async_call_matches_synchronous(gpu_device, wstack, resident):
         assert float(sw.item()) == float(sets[k % 2][3].double().sum().item())
 
 
+@pytest.mark.parametrize("pipe_scatter", ["0", "1"])
+def test_pipelined_calls_interleaved_with_other_calls(gpu_device, monkeypatch, pipe_scatter):
+    """With CIP_PIPE_SCATTER=1 a pipelined 2-D call grids on its plan stream
+    once the previous call's pass A has consumed the workspace grid, so its
+    scatter overlaps that call's pass B (cip_api.hip scatter_on_plan_stream). Calls of another kind
+    in between - synchronous, asynchronous without resident inputs, pipelined
+    w-stacking - also use the grid: the next plan-stream scatter must wait
+    for all of their work. Every image equals its synchronous reference."""
+    import torch
+
+    monkeypatch.setenv("CIP_PIPE_SCATTER", pipe_scatter)  # read per call
+    a = _inputs(512)
+    b = (a[0], a[1], a[2] * (0.5 - 2.0j), a[3] * 0.25 + 1.0) + a[4:]
+    ref = {}
+    for name, args in (("a", a), ("b", b)):
+        for ws in (False, True):
+            img, _ = gridder.device_ms2dirty(*args, support=8, normalise=True, do_wstacking=ws)
+            ref[name, ws] = img.clone()
+    seq = [("a", "pipe", False), ("b", "pipe", False), ("a", "sync", False), ("b", "pipe", False),
+           ("a", "async", False), ("b", "pipe", False), ("a", "pipe", True), ("b", "pipe", False),
+           ("a", "pipe", False), ("b", "pipe", True), ("a", "pipe", False)]
+    outs = []
+    for name, mode, ws in seq:
+        out = torch.empty_like(ref["a", False])
+        gridder.device_ms2dirty(*(a if name == "a" else b), support=8, normalise=True, out=out,
+                                synchronize=mode == "sync", resident_inputs=mode == "pipe", do_wstacking=ws)
+        outs.append(out)
+    torch.cuda.synchronize()
+    for (name, mode, ws), out in zip(seq, outs):
+        assert torch.equal(out, ref[name, ws]), (name, mode, ws)
+
+
 def test_async_call_sees_inputs_written_on_the_stream(gpu_device):
     """Without resident_inputs, an asynchronous call starts in stream order: a
     kernel that rewrites the visibilities between two calls is seen by the
