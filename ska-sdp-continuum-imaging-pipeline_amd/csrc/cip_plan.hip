@@ -265,7 +265,9 @@ constexpr uint32_t kNoKey = 0xffffffffu;  // visibility off the grid (tile keys 
 // visibility or weight loads, no partials (the split place pass: a separate
 // block of the same launch reduces the same visibilities, see
 // plan_place_split_kernel). blk / nblocks: this place block and their count.
-template <typename VisT, int WK, bool PLACE, bool LOADVIS>
+// RM: the row map, at compile time (each mode's registers only): 0 dense MS
+// rows, 1 dense rows that may pair (RowMap::pair_d), 2 ragged row slices
+template <typename VisT, int WK, bool PLACE, bool LOADVIS, int RM>
 __device__ __forceinline__ void place_body(const double* __restrict__ uvw, const double* __restrict__ fx,
                                            const RowMap& m, const VisT* __restrict__ vis,
                                            const void* __restrict__ wgt, const GridGeometry& g, unsigned* err_flag,
@@ -284,7 +286,7 @@ __device__ __forceinline__ void place_body(const double* __restrict__ uvw, const
   double wsum = 0.0, wvmax = 0.0;
   bool nonfinite = false;
   const int64_t nvis = m.nvis, nchan = m.nchan;
-  const bool ragged = m.delta != nullptr;
+  constexpr bool ragged = RM == 2;
   const int64_t nseg = (nvis + 63) / 64;
   const int P = kTile + g.support - 1;
   // block b owns segments [64 b, 64 b + 64): wave w takes every 4th
@@ -298,7 +300,7 @@ __device__ __forceinline__ void place_body(const double* __restrict__ uvw, const
   // time pairs (dense rows, m.pair_d): the dump stride D (0 = none)
   int64_t pair_d = 0;
   if constexpr (PLACE)
-    if (!ragged && m.pair_d != nullptr) pair_d = __builtin_amdgcn_readfirstlane((int)*m.pair_d);
+    if (RM == 1 && m.pair_d != nullptr) pair_d = __builtin_amdgcn_readfirstlane((int)*m.pair_d);
   const int64_t nrow_dense = ragged ? 0 : nvis / nchan;
   const double inv_d = pair_d > 0 ? 1.0 / (double)pair_d : 0.0;
   // ragged rows: the first rows of the wave's kPlaceSegs / 4 segments and the
@@ -445,7 +447,7 @@ __device__ __forceinline__ void place_body(const double* __restrict__ uvw, const
         const int next = above ? (__ffsll((long long)above) - 1) : nvalid;
         const int64_t slot = blk * kPlaceSegs * 64 + wbase + __popcll(emits & ((1ull << lane) - 1ull));
         atomicAdd(&s_hist[key & 255u], 1u);
-        if (m.pk_runs) {  // wave-uniform (ragged rows only)
+        if (ragged && m.pk_runs) {  // wave-uniform
           park_key[slot] = key | ((uint32_t)(next - lane - 1) << kRunLenShift);
           park_run[slot] = perm_encode_wide(m, i, r, c);
         } else {
@@ -488,7 +490,7 @@ __device__ __forceinline__ void place_body(const double* __restrict__ uvw, const
 
 // The place pass (reduction fused, the place block = this workgroup); PLACE =
 // false: the reduction alone (CIP_REUSE_PLAN calls).
-template <typename VisT, int WK, bool PLACE = true>
+template <typename VisT, int WK, bool PLACE = true, int RM = 0>
 __global__ __launch_bounds__(256, CIP_PLACE_WAVES) void plan_place_kernel(const double* __restrict__ uvw,
                                                          const double* __restrict__ fx, RowMap m,
                                                          const VisT* __restrict__ vis, const void* __restrict__ wgt,
@@ -499,8 +501,8 @@ __global__ __launch_bounds__(256, CIP_PLACE_WAVES) void plan_place_kernel(const 
                                                          uint64_t* __restrict__ park_run, double* partial,
                                                          int64_t* __restrict__ hist0,
                                                          uint64_t* __restrict__ park_uv = nullptr) {
-  place_body<VisT, WK, PLACE, true>(uvw, fx, m, vis, wgt, g, err_flag, vis_class, blk_cnt, park_key, park_run,
-                                    partial, hist0, park_uv, blockIdx.x, gridDim.x);
+  place_body<VisT, WK, PLACE, true, RM>(uvw, fx, m, vis, wgt, g, err_flag, vis_class, blk_cnt, park_key, park_run,
+                                        partial, hist0, park_uv, blockIdx.x, gridDim.x);
 }
 
 // The split place pass (CIP_PLACE_SPLIT=1): workgroup 2 b places place block
@@ -508,7 +510,7 @@ __global__ __launch_bounds__(256, CIP_PLACE_WAVES) void plan_place_kernel(const 
 // and values in the fused pass's order (the same partials bit for bit): the
 // streaming read and the VALU-heavy placement run in different waves side by
 // side on the CUs instead of one memory round trip per placed segment.
-template <typename VisT, int WK>
+template <typename VisT, int WK, int RM>
 __global__ __launch_bounds__(256, CIP_PLACE_WAVES) void plan_place_split_kernel(
     const double* __restrict__ uvw, const double* __restrict__ fx, RowMap m, const VisT* __restrict__ vis,
     const void* __restrict__ wgt, GridGeometry g, unsigned* err_flag, uint8_t* __restrict__ vis_class,
@@ -516,11 +518,11 @@ __global__ __launch_bounds__(256, CIP_PLACE_WAVES) void plan_place_split_kernel(
     double* partial, int64_t* __restrict__ hist0, uint64_t* __restrict__ park_uv) {
   const int64_t nb = gridDim.x / 2;
   if (blockIdx.x & 1)
-    place_body<VisT, WK, false, true>(uvw, fx, m, vis, wgt, g, err_flag, vis_class, blk_cnt, park_key, park_run,
-                                      partial, hist0, park_uv, blockIdx.x >> 1, nb);
+    place_body<VisT, WK, false, true, RM>(uvw, fx, m, vis, wgt, g, err_flag, vis_class, blk_cnt, park_key, park_run,
+                                          partial, hist0, park_uv, blockIdx.x >> 1, nb);
   else
-    place_body<VisT, WK, true, false>(uvw, fx, m, vis, wgt, g, err_flag, vis_class, blk_cnt, park_key, park_run,
-                                      partial, hist0, park_uv, blockIdx.x >> 1, nb);
+    place_body<VisT, WK, true, false, RM>(uvw, fx, m, vis, wgt, g, err_flag, vis_class, blk_cnt, park_key, park_run,
+                                          partial, hist0, park_uv, blockIdx.x >> 1, nb);
 }
 
 
@@ -572,15 +574,26 @@ hipError_t launch_plan_place(const double* uvw, const double* fx, const RowMap& 
                              uint64_t* park_uv) {
   const dim3 gd(plan_blocks(m.nvis));
   const dim3 gd2(2 * plan_blocks(m.nvis));
-#define PLACE(VT, WKV)                                                                                           \
-  if (place_split())                                                                                             \
-    plan_place_split_kernel<VT, WKV><<<gd2, dim3(256), 0, s>>>(uvw, fx, m, (const VT*)vis, wgt, g, err_flag,   \
-                                                               vis_class, blk_cnt, park_key, park_run, partial, \
-                                                               hist0, park_uv);                                  \
-  else                                                                                                           \
-    plan_place_kernel<VT, WKV><<<gd, dim3(256), 0, s>>>(uvw, fx, m, (const VT*)vis, wgt, g, err_flag,       \
-                                                        vis_class, blk_cnt, park_key, park_run, partial, hist0, \
-                                                        park_uv)
+  const int rm = m.delta != nullptr ? 2 : (m.pair_d != nullptr ? 1 : 0);
+#define PLACE_RM(VT, WKV, RMV)                                                                                      \
+  if (place_split())                                                                                                \
+    plan_place_split_kernel<VT, WKV, RMV><<<gd2, dim3(256), 0, s>>>(uvw, fx, m, (const VT*)vis, wgt, g, err_flag,   \
+                                                                    vis_class, blk_cnt, park_key, park_run,         \
+                                                                    partial, hist0, park_uv);                       \
+  else                                                                                                              \
+    plan_place_kernel<VT, WKV, true, RMV><<<gd, dim3(256), 0, s>>>(uvw, fx, m, (const VT*)vis, wgt, g, err_flag,   \
+                                                                   vis_class, blk_cnt, park_key, park_run, partial, \
+                                                                   hist0, park_uv)
+#define PLACE(VT, WKV)            \
+  do {                            \
+    if (rm == 2) {                \
+      PLACE_RM(VT, WKV, 2);       \
+    } else if (rm == 1) {         \
+      PLACE_RM(VT, WKV, 1);       \
+    } else {                      \
+      PLACE_RM(VT, WKV, 0);       \
+    }                             \
+  } while (0)
   if (vis_dtype == CIP_POL4I) {
     PLACE(Pol4, WK_POL4I);
   } else if (vis_dtype == CIP_C64) {
@@ -593,6 +606,7 @@ hipError_t launch_plan_place(const double* uvw, const double* fx, const RowMap& 
     else PLACE(double2, WK_NONE);
   }
 #undef PLACE
+#undef PLACE_RM
   return hipGetLastError();
 }
 
