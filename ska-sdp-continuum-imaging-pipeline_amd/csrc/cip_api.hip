@@ -646,11 +646,16 @@ static bool scatter_order() {
 // CIP_PACKED_RUNS=0: ragged runs keep the (row, channel start, channel stop)
 // record and the order pass gathers delta[row] per run (A/B experiments)
 static bool packed_runs() {
-  static const bool on = [] {
-    const char* e = getenv("CIP_PACKED_RUNS");
-    return !(e && e[0] == '0');
-  }();
-  return on;
+  const char* e = getenv("CIP_PACKED_RUNS");  // read per call (tests switch it)
+  return !(e && e[0] == '0');
+}
+
+// CIP_RAGGED_PACK=0: ragged ordered-stream entries in the (row << 16) |
+// channel form with the delta[row] gather, as for inputs too large to pack
+// (tests: the fallback form on small inputs)
+static bool ragged_pack() {
+  const char* e = getenv("CIP_RAGGED_PACK");  // read per call
+  return !(e && e[0] == '0');
 }
 
 // sub-blocks per radix workgroup: pass 0 (place blocks of ~500 runs) and the
@@ -987,7 +992,7 @@ static int prepare(Workspace* ws, const double* uvw, int64_t nrow, const double*
         return b;
       };
       const int cb = bits(nchan), rb = bits(nrow), ib = bits(ragged->nvis);
-      if (cb + rb + ib <= 64) {
+      if (cb + rb + ib <= 64 && ragged_pack()) {
         m.pk_cbits = cb;
         m.pk_rbits = rb;
       }

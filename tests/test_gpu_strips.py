@@ -239,3 +239,37 @@ def test_strip_mask_follows_the_frequencies(gpu_device):
     assert float(be.grid.abs().max()) == 0.0
     ref, _ = device_ms2dirty(tu, tf2, tv, tw, npix, npix, px, px, support=W, normalise=True)
     assert float((img - ref).abs().max()) <= 1e-12 * float(ref.abs().max())
+
+
+@pytest.mark.parametrize("wstack,W", [(False, 8), (False, 16), (True, 6)])
+def test_ragged_stream_forms_are_bit_identical(gpu_device, monkeypatch, wstack, W):
+    """The strips' ragged row slices grid through three forms of the planner's
+    ordered stream: packed runs (the default: a run record is its first
+    stream entry, its length rides in the sort key), packed entries built from
+    (row, channel) run records with the delta[row] gather (CIP_PACKED_RUNS=0),
+    and the (row << 16) | channel entries of inputs too large to pack
+    (CIP_RAGGED_PACK=0; both switches are read per call). Fixed-point integer
+    sums: the same image bit for bit, at W = 8 / 16 and in w-stacking."""
+    npix = 512
+    uvw, f, vis, w, px = _case(20000, 24, npix)
+    if wstack:
+        uvw = uvw * np.array([1.0, 1.0, 20.0])
+    tu, tf, tv, tw = _to(gpu_device, uvw, f, vis.astype(np.complex64), w.astype(np.float32))
+    _, prm = device_ms2dirty(tu, tf, tv, tw, npix, npix, px, px, support=W, do_wstacking=wstack)
+    layout = strips.plan_strips(tu, tf, prm, px, npix, npix, 3)
+    datas = []
+    for r in range(3):
+        rows, c0, c1 = strips.strip_slices(tu, tf, prm, px, *layout.rows(r))
+        datas.append(strips.gather_strip(tu, tv, tw, rows, c0, c1))
+    imgs = []
+    for env in ({}, {"CIP_PACKED_RUNS": "0"}, {"CIP_RAGGED_PACK": "0"}):
+        for k in ("CIP_PACKED_RUNS", "CIP_RAGGED_PACK"):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        be = strips.HipStripBackend(prm, px, px, npix, npix, device=gpu_device)
+        imgs.append(strips.invert_strips_local(datas, tf, layout, be).clone())
+    torch.cuda.synchronize()
+    assert float(imgs[0].abs().max()) > 0.0
+    assert torch.equal(imgs[0], imgs[1])
+    assert torch.equal(imgs[0], imgs[2])
