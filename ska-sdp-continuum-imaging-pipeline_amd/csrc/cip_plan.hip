@@ -312,9 +312,10 @@ __device__ __forceinline__ void place_body(const double* __restrict__ uvw, const
   if (ragged) {
     const int64_t sj = blk * kPlaceSegs + wave + 4 * (int64_t)lane;
     if (lane < kPlaceSegs / 4 && sj < seg_end) {
-      seg_s = (int)m.seg_row[sj];
-      seg_nx = m.off[seg_s + 1];
-      seg_dl = m.delta[seg_s];
+      const uint32_t s0 = m.seg_row[sj];  // rows < 2^32
+      seg_s = (int)s0;
+      seg_nx = m.off[(int64_t)s0 + 1];
+      seg_dl = m.delta[s0];
     }
   }
   int it = 0;
