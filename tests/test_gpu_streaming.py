@@ -112,6 +112,37 @@ def test_grid_tiles_edge_cases(gpu_device):
     assert float(np.abs(dirty.cpu().numpy() - ref).max()) / sw < TIGHT
 
 
+@pytest.mark.parametrize("wstack", [False, True])
+def test_grid_tiles_ragged_slices_stress(gpu_device, wstack):
+    # the place pass finds each lane's slice from its 64-visibility segment's
+    # first slice (cip_common.h ragged_row_of): slices of 0 .. nchan channels
+    # cross segment starts, several start inside one segment, and a run of 200
+    # empty slices (more than one wave of repeated starts) sits between two
+    # segments; against the same visibilities as a dense masked-weight MS
+    nrow, nchan = 3000, 40
+    _, uvw, f, vis, w = _case(nrow, nchan, seed=6)
+    npix = 256
+    px = syn.pixel_size_for_grid(uvw, f, npix)
+    rng = np.random.default_rng(4)
+    c0 = rng.integers(0, nchan, nrow).astype(np.int32)
+    ln = np.where(rng.uniform(size=nrow) < 0.5, rng.integers(0, 4, nrow), rng.integers(0, nchan + 1, nrow))
+    c1 = np.minimum(c0 + ln, nchan).astype(np.int32)
+    c1[1000:1200] = c0[1000:1200]
+    rows = np.arange(nrow)
+    v = np.concatenate([vis[r, a:b] for r, a, b in zip(rows, c0, c1)])
+    ww = np.concatenate([w[r, a:b] for r, a, b in zip(rows, c0, c1)])
+    acc = GridAccumulator(npix, npix, px, px, support=8, do_wstacking=wstack, w_range=w_range_rows(uvw, f))
+    acc.add_tile(_t(uvw), _t(c0), _t(c1), _t(f), _t(v), _t(ww))
+    dirty, sumw = acc.dirty()
+    wd = np.zeros((nrow, nchan), np.float32)
+    for r, a, b in zip(rows, c0, c1):
+        wd[r, a:b] = w[r, a:b]
+    ref = oracle.ms2dirty(uvw, f, vis, wd, npix, npix, px, px, support=8, do_wstacking=wstack)
+    sw = float(wd.astype(np.float64).sum())
+    assert abs(float(sumw.item()) - sw) < 1e-9 * sw
+    assert float(np.abs(dirty.cpu().numpy() - ref).max()) / sw < TIGHT
+
+
 def _golden_like_ms(seed=11):
     ms = syn.make_measurement_set(1_500, 8, n_ant=20, array_radius_m=2000.0, fov_l=0.01, seed=seed)
     return InMemoryMeasurementSet(ms.uvw(), ms.visibilities(), ms.flags(), ms.weights(),
