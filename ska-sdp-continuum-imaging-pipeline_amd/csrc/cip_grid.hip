@@ -355,7 +355,13 @@ hipError_t launch_scatter(int support, int vis_dtype, int wgt_dtype, bool packed
   if (share_cus && group == 1 && support <= 16) {
     const unsigned P = (unsigned)(kTile + support - 1);
     const unsigned stat = P * P * (packed ? 8u : 16u) + 64u;
-    const unsigned need = 160u * 1024u / 4u + 256u;
+    // CIP_SHARE_BLOCKS=1..3: the scatter blocks per CU beside the planner (A/B)
+    static const unsigned nb = [] {
+      const char* e = getenv("CIP_SHARE_BLOCKS");
+      const int v = e ? atoi(e) : 3;
+      return (unsigned)(v >= 1 && v <= 3 ? v : 3);
+    }();
+    const unsigned need = 160u * 1024u / (nb + 1u) + 256u;
     pad = stat < need ? need - stat : 0u;
   }
 #define CASE(WW)                                                                                             \
