@@ -1622,7 +1622,7 @@ static int ms2dirty_impl(const double* uvw, int64_t nrow, const double* freq, in
   const bool scatter_ps = pipelined && st.fast && !g.do_wstacking && G == 1 && p_hi - p_lo == 1 && !pair_b &&
                           scatter_on_plan_stream();
   if (scatter_ps) {
-    if (ws->grid_seq + 1 == ws->call_seq) {
+    if (ws->grid_seq != ~0ull && ws->grid_seq + 1 == ws->call_seq) {
       CIP_HIP_CHECK(hipStreamWaitEvent(ps, ws->ev_grid, 0));
     } else {  // another call used the workspace since: everything queued on s
       CIP_HIP_CHECK(hipEventRecord(ws->ev_gate, s));
