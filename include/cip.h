@@ -294,6 +294,30 @@ int cip_strip_rows_masked(double* grid, const cip_gridder_params* params,
                           int64_t npix_x, int64_t npix_y, int64_t y0,
                           int64_t y1, int64_t row0, const uint32_t* tile_bits,
                           void* hip_stream, double* H);
+/* cip_strip_rows_masked's packed form (round 5, the sparse all-to-all's send
+ * buffer written by pass A itself): buffer row y goes to H row
+ * row_slot[y - y0] of an H with nlive rows per 4-column block ((npix_x / 4,
+ * nlive, 4) complex128); rows with row_slot < 0 must hold no dirty tile and
+ * are skipped (device int64, y1 - y0 entries). */
+int cip_strip_rows_packed(double* grid, const cip_gridder_params* params,
+                          int64_t npix_x, int64_t npix_y, int64_t y0,
+                          int64_t y1, int64_t row0, const uint32_t* tile_bits,
+                          const int64_t* row_slot, int64_t nlive,
+                          void* hip_stream, double* H);
+/* The strips' sparse all-to-all of pass-A rows (round 5). A record is row y
+ * of one 4-column block of H ((nb, rows, 4) complex elements of elem_bytes =
+ * 16 (complex128) or 8 (complex64)). cip_strip_pack_rows: out (nb, nlive, 4)
+ * <- the rows y of H (nb, h, 4) with slot[y] >= 0, at position slot[y]
+ * (device int64, h entries). cip_strip_unpack_rows: H (nb, nv, 4) <- row y
+ * from recv record rec[y] + b * stride[y] for block b, zeros where
+ * rec[y] < 0 (device int64, nv entries each). Stream-ordered on hip_stream
+ * (no host wait). Replace: strips.py's index_select / advanced-index copies. */
+int cip_strip_pack_rows(const void* H, int64_t nb, int64_t h, int elem_bytes,
+                        const int64_t* slot, int64_t nlive, void* hip_stream,
+                        void* out);
+int cip_strip_unpack_rows(const void* recv, int64_t nb, int64_t nv, int elem_bytes,
+                          const int64_t* rec, const int64_t* stride,
+                          void* hip_stream, void* H);
 /* w-stacking strips (the reference's own gridding mode split by uv strips):
  * cip_strip_rows runs per w plane (grid = the plane's rows of the strip
  * buffer); cip_strip_cols_wplane is pass B for plane `plane` of image rows

@@ -1902,6 +1902,30 @@ int cip_strip_rows_masked(double* grid, const cip_gridder_params* params, int64_
   return CIP_OK;
 }
 
+int cip_strip_rows_packed(double* grid, const cip_gridder_params* params, int64_t npix_x, int64_t npix_y,
+                          int64_t y0, int64_t y1, int64_t row0, const uint32_t* tile_bits, const int64_t* row_slot,
+                          int64_t nlive, void* hip_stream, double* H) {
+  g_last_error.clear();
+  GridGeometry g;
+  if (const int rc = strip_check(params, npix_x, npix_y, &g); rc != CIP_OK) return rc;
+  if (!grid || !tile_bits || !row_slot) return set_error(CIP_EINVAL, "NULL grid, tile_bits or row_slot");
+  if (y0 < 0 || y1 > g.nv || y1 <= y0) return set_error(CIP_EINVAL, "row range outside the grid");
+  if (row0 < 0 || row0 >= g.nv) return set_error(CIP_EINVAL, "row0 outside the grid");
+  if (nlive < 0 || nlive > y1 - y0) return set_error(CIP_EINVAL, "nlive outside [0, y1 - y0]");
+  if (nlive > 0 && !H) return set_error(CIP_EINVAL, "NULL H");
+  if (g.ntx % 32 != 0) return set_error(CIP_EINVAL, "tile masks need nu / 32 to be a multiple of 32 tiles");
+  hipStream_t s = (hipStream_t)hip_stream;
+  Workspace* ws = workspace();
+  if (!ws) return set_error(CIP_EHIP, "no HIP device");
+  if (const int sr = settle_async(ws, s); sr != CIP_OK) return sr;
+  double* tw_u = nullptr;
+  if (const int rc = fft_twiddles(ws, g.nu, s, &tw_u); rc != CIP_OK) return rc;
+  CIP_HIP_CHECK(launch_fft_rows_strip(grid, g.nu, g.nv, npix_x, tw_u, y0, y1, H, s, tile_bits, row0, row_slot,
+                                      nlive));
+  CIP_HIP_CHECK(hipStreamSynchronize(s));
+  return CIP_OK;
+}
+
 int cip_strip_cols(const double* H, const cip_gridder_params* params, int64_t npix_x, int64_t npix_y, int64_t i0,
                    int64_t i1, const double* norm, void* hip_stream, double* dirty_rows) {
   g_last_error.clear();
@@ -1922,6 +1946,28 @@ int cip_strip_cols(const double* H, const cip_gridder_params* params, int64_t np
   if (const int rc = correction_vectors(ws, g, npix_x, npix_y, s, &cx, &cy); rc != CIP_OK) return rc;
   CIP_HIP_CHECK(launch_fft_cols_strip(H, g.nv, npix_x, npix_y, tw_v, i0, i1, dirty_rows, cx, cy, norm, s));
   CIP_HIP_CHECK(hipStreamSynchronize(s));
+  return CIP_OK;
+}
+
+int cip_strip_pack_rows(const void* H, int64_t nb, int64_t h, int elem_bytes, const int64_t* slot, int64_t nlive,
+                        void* hip_stream, void* out) {
+  g_last_error.clear();
+  if (elem_bytes != 8 && elem_bytes != 16) return set_error(CIP_EINVAL, "elem_bytes must be 8 or 16");
+  if (nb < 0 || h < 0 || nlive < 0 || nlive > h) return set_error(CIP_EINVAL, "bad pack sizes");
+  if (nb > 65535) return set_error(CIP_EINVAL, "more than 65535 column blocks");
+  if (nb * h * nlive > 0 && (!H || !slot || !out)) return set_error(CIP_EINVAL, "NULL pointer");
+  CIP_HIP_CHECK(launch_strip_pack(H, nb, h, elem_bytes / 4, slot, nlive, out, (hipStream_t)hip_stream));
+  return CIP_OK;
+}
+
+int cip_strip_unpack_rows(const void* recv, int64_t nb, int64_t nv, int elem_bytes, const int64_t* rec,
+                          const int64_t* stride, void* hip_stream, void* H) {
+  g_last_error.clear();
+  if (elem_bytes != 8 && elem_bytes != 16) return set_error(CIP_EINVAL, "elem_bytes must be 8 or 16");
+  if (nb < 0 || nv < 0) return set_error(CIP_EINVAL, "bad unpack sizes");
+  if (nb > 65535) return set_error(CIP_EINVAL, "more than 65535 column blocks");
+  if (nb * nv > 0 && (!rec || !stride || !H)) return set_error(CIP_EINVAL, "NULL pointer");
+  CIP_HIP_CHECK(launch_strip_unpack(recv, nb, nv, elem_bytes / 4, rec, stride, H, (hipStream_t)hip_stream));
   return CIP_OK;
 }
 

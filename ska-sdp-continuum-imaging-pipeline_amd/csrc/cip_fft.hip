@@ -256,7 +256,8 @@ __global__ __launch_bounds__(N / 16, fft_waves_rows<CT>()) void fft_rows_kernel(
                                                           const double2* __restrict__ tw, HT* __restrict__ H,
                                                           const uint32_t* __restrict__ dmask, int64_t ntx,
                                                           int64_t y0 = 0, int64_t hy0 = 0, bool skip_clean = false,
-                                                          int64_t mrow0 = 0, int64_t mnv = 0) {
+                                                          int64_t mrow0 = 0, int64_t mnv = 0,
+                                                          const int64_t* __restrict__ row_slot = nullptr) {
   using S = FftShape<N>;
   __shared__ typename Cx<CT>::R lds[N + N / 16];
   const int t = threadIdx.x;
@@ -273,6 +274,14 @@ __global__ __launch_bounds__(N / 16, fft_waves_rows<CT>()) void fft_rows_kernel(
 #endif
   const int64_t y = y0 + yl;
   GT* row = gT + y * N;
+  // row_slot (uv strips' packed pass A): the row's place among the live
+  // rows - H holds those only, in order; a dead row (no dirty tile in its
+  // tile row: nothing to read or zero) is skipped
+  int64_t orow = y - hy0;
+  if (row_slot) {
+    orow = row_slot[y - hy0];
+    if (orow < 0) return;
+  }
   CT v[16];
   if constexpr (MASKED) {
     // the 32-tile word of element r is uniform over the block (T = N / 16
@@ -329,7 +338,7 @@ __global__ __launch_bounds__(N / 16, fft_waves_rows<CT>()) void fft_rows_kernel(
     for (int r = 0; r < S::RF; ++r) {
       const int k = out_pos<N, S::RF>(t, m, r, N / S::RF);
       const int64_t i = (int64_t)((k + (int)(nx / 2)) & (N - 1));
-      if (i < nx) H[((i / kColBlock) * hrows + (y - hy0)) * kColBlock + (i % kColBlock)] = ccast<HT>(v[m * S::RF + r]);
+      if (i < nx) H[((i / kColBlock) * hrows + orow) * kColBlock + (i % kColBlock)] = ccast<HT>(v[m * S::RF + r]);
     }
 }
 
@@ -642,7 +651,8 @@ hipError_t launch_fft_rows(double* gT, int64_t nu, int64_t nv, int64_t nx, const
 }
 
 hipError_t launch_fft_rows_strip(double* gT, int64_t nu, int64_t nv, int64_t nx, const double* tw_u, int64_t y0,
-                                 int64_t y1, double* H, hipStream_t s, const uint32_t* dmask, int64_t row0) {
+                                 int64_t y1, double* H, hipStream_t s, const uint32_t* dmask, int64_t row0,
+                                 const int64_t* row_slot, int64_t nlive) {
   if (!fft_len_ok(nu) || !fft_len_ok(nv) || nx > nu || y0 < 0 || y1 > nv || y1 <= y0) return hipErrorInvalidValue;
   if (dmask && (nu % kTile != 0 || nv % kTile != 0 || (nu / kTile) % 32 != 0)) return hipErrorInvalidValue;
   const dim3 gd((unsigned)(y1 - y0));
@@ -653,8 +663,9 @@ hipError_t launch_fft_rows_strip(double* gT, int64_t nu, int64_t nv, int64_t nx,
 #define ROWS(NN)                                                                                               \
   case NN:                                                                                                     \
     if (dmask)                                                                                                 \
-      fft_rows_kernel<NN, true, false><<<gd, dim3(NN / 16), 0, s>>>(g, y1 - y0, nx, tw, h, dmask, ntx, y0, y0,  \
-                                                                     false, row0, nv);                         \
+      fft_rows_kernel<NN, true, false><<<gd, dim3(NN / 16), 0, s>>>(g, row_slot ? nlive : y1 - y0, nx, tw, h,   \
+                                                                     dmask, ntx, y0, y0, false, row0, nv,      \
+                                                                     row_slot);                                \
     else                                                                                                       \
       fft_rows_kernel<NN, false, true><<<gd, dim3(NN / 16), 0, s>>>(g, y1 - y0, nx, tw, h, nullptr, 0, y0, y0); \
     break;

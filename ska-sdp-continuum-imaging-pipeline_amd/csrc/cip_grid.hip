@@ -485,4 +485,60 @@ hipError_t launch_wfinal_correct(double* acc, int64_t npix_x, int64_t npix_y, do
   return hipGetLastError();
 }
 
+// ------------------------------------------- strip all-to-all packing ----
+// The uv strips' sparse all-to-all moves pass-A rows in
+// records: row y of block b of H (b, y, 4 columns) = `units` 16-byte units
+// (4: complex128, 2: complex64). Pack: this rank's live rows, compacted
+// (slot[y] >= 0: the row's place among them) - the send buffer, block-major,
+// so each receiver's block range is contiguous. Unpack: a receiver's H from
+// the received pieces, rec[y] = the record of row y's block 0 in recv (-1:
+// no rank sent it, zeros), stride[y] = the records between its blocks (its
+// source's live row count). One pass each, coalesced along the rows.
+template <int UNITS>
+__global__ __launch_bounds__(256) void strip_pack_kernel(const uint4* __restrict__ H, int64_t h,
+                                                         const int64_t* __restrict__ slot, int64_t nlive,
+                                                         uint4* __restrict__ out) {
+  const int64_t b = blockIdx.y;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= h * UNITS) return;
+  const int64_t y = i / UNITS, u = i % UNITS;  // UNITS: 2 or 4 (shifts)
+  const int64_t k = slot[y];
+  if (k >= 0) out[(b * nlive + k) * UNITS + u] = H[(b * h + y) * UNITS + u];
+}
+
+template <int UNITS>
+__global__ __launch_bounds__(256) void strip_unpack_kernel(const uint4* __restrict__ recv, int64_t nv,
+                                                           const int64_t* __restrict__ rec,
+                                                           const int64_t* __restrict__ stride,
+                                                           uint4* __restrict__ H) {
+  const int64_t b = blockIdx.y;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= nv * UNITS) return;
+  const int64_t y = i / UNITS, u = i % UNITS;
+  const int64_t r = rec[y];
+  H[(b * nv + y) * UNITS + u] = r >= 0 ? recv[(r + b * stride[y]) * UNITS + u] : make_uint4(0u, 0u, 0u, 0u);
+}
+
+hipError_t launch_strip_pack(const void* H, int64_t nb, int64_t h, int units, const int64_t* slot, int64_t nlive,
+                             void* out, hipStream_t s) {
+  if (nb <= 0 || h <= 0 || nlive <= 0) return hipSuccess;
+  const dim3 gd((unsigned)((h * units + 255) / 256), (unsigned)nb);
+  if (units == 4)
+    strip_pack_kernel<4><<<gd, dim3(256), 0, s>>>((const uint4*)H, h, slot, nlive, (uint4*)out);
+  else
+    strip_pack_kernel<2><<<gd, dim3(256), 0, s>>>((const uint4*)H, h, slot, nlive, (uint4*)out);
+  return hipGetLastError();
+}
+
+hipError_t launch_strip_unpack(const void* recv, int64_t nb, int64_t nv, int units, const int64_t* rec,
+                               const int64_t* stride, void* H, hipStream_t s) {
+  if (nb <= 0 || nv <= 0) return hipSuccess;
+  const dim3 gd((unsigned)((nv * units + 255) / 256), (unsigned)nb);
+  if (units == 4)
+    strip_unpack_kernel<4><<<gd, dim3(256), 0, s>>>((const uint4*)recv, nv, rec, stride, (uint4*)H);
+  else
+    strip_unpack_kernel<2><<<gd, dim3(256), 0, s>>>((const uint4*)recv, nv, rec, stride, (uint4*)H);
+  return hipGetLastError();
+}
+
 }  // namespace cip

@@ -201,9 +201,12 @@ hipError_t launch_fft_cols_wstack(const double* H, int64_t hstride_bytes, int nb
 // dmask (may be NULL): dirty-tile bits of the whole grid (as launch_fft_rows),
 // buffer row y = grid row (row0 + y) mod nv; only the dirty tiles' cells are
 // read and zeroed (the rest of the buffer is zero)
+// row_slot (with dmask; may be NULL): the packed form - buffer row y goes to
+// H row row_slot[y - y0] of an H with nlive rows per block, rows with
+// row_slot < 0 (no dirty tile in their tile row) are skipped
 hipError_t launch_fft_rows_strip(double* gT, int64_t nu, int64_t nv, int64_t nx, const double* tw_u, int64_t y0,
                                  int64_t y1, double* H, hipStream_t s, const uint32_t* dmask = nullptr,
-                                 int64_t row0 = 0);
+                                 int64_t row0 = 0, const int64_t* row_slot = nullptr, int64_t nlive = 0);
 hipError_t launch_fft_cols_strip(const double* H, int64_t nv, int64_t nx, int64_t ny, const double* tw_v, int64_t i0,
                                  int64_t i1, double* out, const double* cx, const double* cy, const double* norm,
                                  hipStream_t s);
@@ -228,5 +231,12 @@ hipError_t launch_facet_rephase(const double* uvw, int64_t nrow, const double* f
                                 double* delay, void* vis_out, hipStream_t s);
 hipError_t launch_stokes(int stokes, const void* vis4, const uint8_t* flags4, const float* wgt4, int64_t n,
                          void* vis_i, uint8_t* flag_i, float* wgt_i, float* eff_w, hipStream_t s);
+
+// the strips' sparse all-to-all: pack this rank's live pass-A rows / unpack
+// a receiver's pass-B input (cip_grid.hip; units = 16-B units per record)
+hipError_t launch_strip_pack(const void* H, int64_t nb, int64_t h, int units, const int64_t* slot, int64_t nlive,
+                             void* out, hipStream_t s);
+hipError_t launch_strip_unpack(const void* recv, int64_t nb, int64_t nv, int units, const int64_t* rec,
+                               const int64_t* stride, void* H, hipStream_t s);
 
 }  // namespace cip

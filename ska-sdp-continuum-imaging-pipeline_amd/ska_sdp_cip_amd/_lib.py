@@ -56,6 +56,9 @@ EXPORTED_SYMBOLS = (
     "cip_strip_cols",
     "cip_strip_cols_wplane",
     "cip_strip_wfinal",
+    "cip_strip_pack_rows",
+    "cip_strip_rows_packed",
+    "cip_strip_unpack_rows",
     "cip_tile_runs",
     "cip_stokes_i",
     "cip_stokes",
@@ -147,6 +150,10 @@ def lib() -> ctypes.CDLL:
                                          _i64, _i32, _vp, _vp]
     so.cip_strip_wfinal.argtypes = [_vp, ctypes.POINTER(GridderParams), _i64, _i64, _f64, _f64, _i64, _i64, _vp,
                                     _vp]
+    so.cip_strip_pack_rows.argtypes = [_vp, _i64, _i64, _i32, _vp, _i64, _vp, _vp]
+    so.cip_strip_rows_packed.argtypes = [_vp, ctypes.POINTER(GridderParams), _i64, _i64, _i64, _i64, _i64, _vp,
+                                         _vp, _i64, _vp, _vp]
+    so.cip_strip_unpack_rows.argtypes = [_vp, _i64, _i64, _i32, _vp, _vp, _vp, _vp]
     so.cip_tile_runs.argtypes = [_vp, _i64, _vp, _i64, ctypes.POINTER(ctypes.c_double), _i64, _vp,
                                  ctypes.POINTER(ctypes.c_int64), _vp, _vp, _vp, _vp]
     so.cip_stokes_i.argtypes = [_vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp]
@@ -158,7 +165,7 @@ def lib() -> ctypes.CDLL:
     so.cip_last_error.restype = ctypes.c_char_p
     so.cip_build_info.restype = ctypes.c_char_p
     for name in ("cip_choose_params", "cip_ms2dirty", "cip_ms2dirty_stokes_i", "cip_grid_plane", "cip_grid_layout", "cip_plane_group", "cip_grid_ms", "cip_grid_ms_stokes_i",
-                 "cip_grid_tiles", "cip_grid_tiles_strip", "cip_ms2dirty_wplanes", "cip_grid_to_dirty", "cip_strip_rows", "cip_strip_rows_masked", "cip_strip_cols", "cip_strip_cols_wplane", "cip_strip_wfinal", "cip_tile_runs",
+                 "cip_grid_tiles", "cip_grid_tiles_strip", "cip_ms2dirty_wplanes", "cip_grid_to_dirty", "cip_strip_rows", "cip_strip_rows_masked", "cip_strip_cols", "cip_strip_cols_wplane", "cip_strip_wfinal", "cip_strip_pack_rows", "cip_strip_unpack_rows", "cip_strip_rows_packed", "cip_tile_runs",
                  "cip_stokes_i", "cip_stokes", "cip_facet_rephase", "cip_allreduce_grid", "cip_release_collectives",
                  "cip_release_workspace", "cip_profile_enable", "cip_profile_last"):
         getattr(so, name).restype = ctypes.c_int

@@ -434,6 +434,22 @@ class HipStripBackend:
                                                            int(y0), int(y1), self._stream(), H.data_ptr()))
         return H
 
+    def pass_rows_packed(self, grid, y0: int, y1: int, live, count: int, plane: int = 0):
+        """Pass A over buffer rows [y0, y1) keeping only the live rows (`live`:
+        bool over them, as live_rows gives; `count` Trues) -> H (npix_x / 4,
+        count, 4, 2): the sparse all-to-all's send buffer, written by pass A
+        itself (cip_strip_rows_packed) instead of packed after it."""
+        if not (self.masked and self._bits is not None and self.dirty):
+            return _pack_live(self.pass_rows(grid, y0, y1, plane), live, count)
+        slot = torch.cumsum(live.to(torch.int64), 0).sub_(1)
+        slot = torch.where(live, slot, torch.full_like(slot, -1))
+        H = torch.empty((self.npix_x // COL_BLOCK, count, COL_BLOCK, 2), dtype=torch.float64, device=self.device)
+        self._lib.check(self._lib.lib().cip_strip_rows_packed(
+            grid.data_ptr(), self.params, self.npix_x, self.npix_y, int(y0), int(y1), int(self.rows[0]),
+            self._bits[plane].data_ptr(), slot.data_ptr(), int(count), self._stream(),
+            H.data_ptr() if count else None))
+        return H
+
     def live_rows(self, h: int, plane: int = 0):
         """Buffer rows [0, h) of `plane` that may hold a non-zero cell (their
         tile row has a dirty tile in the gridded strip's mask), or None when
@@ -475,13 +491,30 @@ def _assemble_H(pieces: Sequence, nb: int, layout: StripLayout, device, dtype, i
     idx[r] of its strip: (nb, len(idx[r]), 4, 2), the other rows zero) ->
     (nb, nv, 4, 2)."""
     sparse = idx is not None and any(i is not None for i in idx)
-    H = (torch.zeros if sparse else torch.empty)((nb, layout.nv, COL_BLOCK, 2), dtype=dtype, device=device)
-    for r, piece in enumerate(pieces):
-        y0, y1 = layout.rows(r)
-        if idx is None or idx[r] is None:
+    H = torch.empty((nb, layout.nv, COL_BLOCK, 2), dtype=dtype, device=device)
+    if not sparse:
+        for r, piece in enumerate(pieces):
+            y0, y1 = layout.rows(r)
             H[:, y0:y1] = piece.reshape(nb, y1 - y0, COL_BLOCK, 2)
-        elif idx[r].numel():
-            H[:, y0 + idx[r]] = piece.reshape(nb, idx[r].numel(), COL_BLOCK, 2)
+        return H
+    # sparse: zero only the rows no rank sends, then one row-record copy per
+    # source (a record = one row of one 4-column block, 4 complex values; an
+    # advanced-index assignment of whole (nb, rows) slabs into a zeroed H cost
+    # 3-4x more: profiles/r05_assemble.txt)
+    nv = layout.nv
+    live = torch.zeros(nv, dtype=torch.bool, device=device)
+    glob = []
+    for r in range(len(pieces)):
+        y0, y1 = layout.rows(r)
+        g = (torch.arange(y0, y1, device=device) if idx[r] is None else idx[r].to(device) + y0)
+        live[g] = True
+        glob.append(g)
+    rec = H.view(nb * nv, COL_BLOCK * 2)
+    rec.view(nb, nv, COL_BLOCK * 2).index_fill_(1, torch.nonzero(~live).reshape(-1), 0)
+    base = torch.arange(nb, device=device).mul_(nv).reshape(nb, 1)
+    for piece, g in zip(pieces, glob):
+        if g.numel():
+            rec.index_copy_(0, (base + g.reshape(1, -1)).reshape(-1), piece.reshape(-1, COL_BLOCK * 2))
     return H
 
 
@@ -547,11 +580,17 @@ def invert_strips(data: StripData, freq, layout: StripLayout, backend, *, dst: i
         i0, i1 = layout.image_rows(rank)
         acc = torch.empty((i1 - i0, backend.npix_y), dtype=torch.float64, device=buf.device)
         for p in range(nplanes):
-            H = backend.pass_rows(buf[p], 0, h, plane=p)
-            mark("rows")
-            Hm = (_alltoall_H(_wire(H, backend), layout, rank, world, group,
-                              live=_live_of(backend, H, h, p) if sparse else None, stats=stages).to(torch.float64)
-                  if world > 1 else H)
+            snd = _packed_send(backend, buf[p], h, p, layout, rank, world, group) if (sparse and world > 1) else None
+            if snd is not None:
+                mark("rows")
+                Hm = _alltoall_rows(snd[0], layout, rank, world, group, snd[1], snd[2], snd[3],
+                                    stages).to(torch.float64)
+            else:
+                H = backend.pass_rows(buf[p], 0, h, plane=p)
+                mark("rows")
+                Hm = (_alltoall_H(_wire(H, backend), layout, rank, world, group,
+                                  live=_live_of(backend, H, h, p) if sparse else None, stats=stages).to(torch.float64)
+                      if world > 1 else H)
             mark("alltoall")
             backend.pass_cols_wplane(Hm, i0, i1, p, p == 0, acc)
             mark("cols")
@@ -559,13 +598,19 @@ def invert_strips(data: StripData, freq, layout: StripLayout, backend, *, dst: i
         rows_img = backend.finish_rows(acc, i0, i1, norm=sumw)
         mark("final")
         return _gather_rows(rows_img, layout, rank, world, dst, group, mark, async_op=gather_async)
-    H = backend.pass_rows(buf, 0, h)
-    live = _live_of(backend, H, h) if (sparse and world > 1) else None
-    backend.mark_clean()
-    mark("rows")
+    snd = _packed_send(backend, buf, h, 0, layout, rank, world, group) if (sparse and world > 1) else None
     i0, i1 = layout.image_rows(rank)
-    Hm = (_alltoall_H(_wire(H, backend), layout, rank, world, group, live=live, stats=stages).to(torch.float64)
-          if world > 1 else H)
+    if snd is not None:
+        backend.mark_clean()
+        mark("rows")
+        Hm = _alltoall_rows(snd[0], layout, rank, world, group, snd[1], snd[2], snd[3], stages).to(torch.float64)
+    else:
+        H = backend.pass_rows(buf, 0, h)
+        live = _live_of(backend, H, h) if (sparse and world > 1) else None
+        backend.mark_clean()
+        mark("rows")
+        Hm = (_alltoall_H(_wire(H, backend), layout, rank, world, group, live=live, stats=stages).to(torch.float64)
+              if world > 1 else H)
     mark("alltoall")
     rows_img = backend.pass_cols(Hm, i0, i1, norm=sumw)
     mark("cols")
@@ -589,6 +634,111 @@ def _live_of(backend, H, h: int, plane: int = 0):
     return live.to(torch.bool)
 
 
+def _elem_bytes(H) -> int:
+    """Bytes of one complex element of a (..., 2) real view."""
+    return 2 * H.element_size()
+
+
+def _pack_live(H, live, count: int):
+    """This rank's live pass-A rows, compacted: (nb, h, 4, 2) -> (nb, count,
+    4, 2) (`live`: bool (h); count = its number of Trues). On the GPU one
+    copy kernel (cip_strip_pack_rows); CPU tensors (the gloo tests' backend)
+    take the torch form."""
+    nb, h = int(H.shape[0]), int(H.shape[1])
+    if H.device.type != "cuda":
+        return H.index_select(1, torch.nonzero(live).reshape(-1))
+    from . import _lib  # pylint: disable=import-outside-toplevel
+
+    H = H.contiguous()
+    slot = torch.cumsum(live.to(torch.int64), 0).sub_(1)
+    slot = torch.where(live, slot, torch.full_like(slot, -1))
+    out = torch.empty((nb, count) + tuple(H.shape[2:]), dtype=H.dtype, device=H.device)
+    _lib.check(_lib.lib().cip_strip_pack_rows(H.data_ptr(), nb, h, _elem_bytes(H), slot.data_ptr(), count,
+                                              torch.cuda.current_stream(H.device).cuda_stream, out.data_ptr()))
+    return out
+
+
+_ROW_MAPS: dict = {}
+
+
+def _unpack_rows(recv, nb: int, layout: StripLayout, masks, counts, dtype, stacked=None):
+    """A receiver's pass-B input (nb, nv, 4, 2) from the flat received buffer:
+    rank r's piece (nb, counts[r], 4, 2) holds its live rows (masks[r], bool
+    over its strip rows; None: every row), in order; rows no rank sent are
+    zero. One copy kernel (cip_strip_unpack_rows); its row map - the record
+    of each grid row's block 0 and its source's row count - in a handful of
+    vectorised ops (`stacked`: the ranks' masks as one (world, >= max rows)
+    tensor, when the caller has it)."""
+    from . import _lib  # pylint: disable=import-outside-toplevel
+
+    dev = recv.device
+    nv, world = layout.nv, layout.world
+    hs = [layout.rows(r)[1] - layout.rows(r)[0] for r in range(world)]
+    if stacked is None:
+        stacked = torch.zeros((world, max(hs)), dtype=torch.uint8, device=dev)
+        for r, m in enumerate(masks):
+            stacked[r, :hs[r]] = 1 if m is None else m.to(torch.uint8)
+    M = stacked[:, :max(hs)].to(torch.int64)
+    key = (tuple(layout.y_bounds), str(dev))
+    if key not in _ROW_MAPS:  # grid row -> (its rank, its row in the rank's strip), per layout
+        rr = torch.repeat_interleave(torch.arange(world, device=dev), torch.tensor(hs, device=dev))
+        y0s = torch.tensor([layout.rows(r)[0] for r in range(world)], device=dev)
+        _ROW_MAPS.clear()
+        _ROW_MAPS[key] = (rr, torch.arange(nv, device=dev) - y0s[rr])
+    rr, jj = _ROW_MAPS[key]
+    cnt = M.sum(dim=1)  # = counts, on the device (no host copies)
+    base = (torch.cumsum(cnt, 0) - cnt) * nb
+    rec = torch.where(M[rr, jj] != 0, torch.cumsum(M, dim=1).sub_(1)[rr, jj] + base[rr],
+                      torch.full((nv,), -1, dtype=torch.int64, device=dev))
+    stride = cnt[rr]
+    H = torch.empty((nb, nv, COL_BLOCK, 2), dtype=dtype, device=dev)
+    _lib.check(_lib.lib().cip_strip_unpack_rows(recv.data_ptr(), nb, nv, 2 * H.element_size(), rec.data_ptr(),
+                                                stride.data_ptr(), torch.cuda.current_stream(dev).cuda_stream,
+                                                H.data_ptr()))
+    return H
+
+
+def _exchange_masks(live, layout: StripLayout, rank: int, world: int, group):
+    """All ranks' live-row masks of their pass-A output (one all-gather) ->
+    (stacked (world, max rows) uint8, counts, masks (bool over each rank's
+    rows)); the counts are the all-to-all's split sizes (one host wait)."""
+    import torch.distributed as dist  # pylint: disable=import-outside-toplevel
+
+    hs = [layout.rows(r)[1] - layout.rows(r)[0] for r in range(world)]
+    h = hs[rank]
+    mine = torch.zeros(max(hs), dtype=torch.uint8, device=live.device)
+    mine[:h] = live.to(torch.uint8)
+    allm = [torch.empty_like(mine) for _ in range(world)]
+    dist.all_gather(allm, mine, group=group)
+    stacked = torch.stack(allm)
+    counts = [int(c) for c in stacked.sum(dim=1).tolist()]
+    return stacked, counts, [allm[r][:hs[r]].to(torch.bool) for r in range(world)]
+
+
+def _alltoall_rows(Hsend, layout: StripLayout, rank: int, world: int, group, counts, masks, stacked=None,
+                   stats: Optional[dict] = None):
+    """The all-to-all of pass-A rows: `Hsend` (nb_all, counts[rank], 4, 2) is
+    this rank's send buffer (its live rows, or every row when masks[rank] is
+    None); rank s receives blocks [i0_s / 4, i1_s / 4) of every rank's rows ->
+    its pass-B input (nb, nv, 4, 2), rows nobody sent zero."""
+    import torch.distributed as dist  # pylint: disable=import-outside-toplevel
+
+    i0, i1 = layout.image_rows(rank)
+    nb = (i1 - i0) // COL_BLOCK
+    splits_in = [(layout.image_rows(s)[1] - layout.image_rows(s)[0]) // COL_BLOCK * counts[rank] * COL_BLOCK * 2
+                 for s in range(world)]
+    splits_out = [nb * counts[r] * COL_BLOCK * 2 for r in range(world)]
+    if stats is not None:
+        stats["a2a_send_bytes"] = stats.get("a2a_send_bytes", 0) + sum(splits_in) * Hsend.element_size()
+    recv = torch.empty(sum(splits_out), dtype=Hsend.dtype, device=Hsend.device)
+    dist.all_to_all_single(recv, Hsend.reshape(-1), splits_out, splits_in, group=group)
+    if Hsend.device.type == "cuda":
+        return _unpack_rows(recv, nb, layout, masks, counts, Hsend.dtype, stacked)
+    pieces = list(torch.split(recv, splits_out))
+    idx = [None if m is None else torch.nonzero(m).reshape(-1) for m in masks]
+    return _assemble_H(pieces, nb, layout, Hsend.device, Hsend.dtype, idx)
+
+
 def _alltoall_H(H, layout: StripLayout, rank: int, world: int, group, live=None, stats: Optional[dict] = None):
     """The all-to-all of pass-A blocks: rank s receives blocks [i0_s / 4,
     i1_s / 4) of every rank's rows -> its pass-B input (nb, nv, 4, 2).
@@ -596,33 +746,25 @@ def _alltoall_H(H, layout: StripLayout, rank: int, world: int, group, live=None,
     all-gather their live-row masks, then send only live rows; a receiver
     fills the others with zeros. The tall edge strips of C4's cost-balanced
     layout are mostly empty long-baseline rows."""
-    import torch.distributed as dist  # pylint: disable=import-outside-toplevel
-
-    h = layout.rows(rank)[1] - layout.rows(rank)[0]
-    i0, i1 = layout.image_rows(rank)
-    nb = (i1 - i0) // COL_BLOCK
-    hs = [layout.rows(r)[1] - layout.rows(r)[0] for r in range(world)]
     if live is None:
-        idx = [None] * world
-        counts = hs
-    else:
-        hmax = max(hs)
-        mine = torch.zeros(hmax, dtype=torch.uint8, device=H.device)
-        mine[:h] = live.to(torch.uint8)
-        allm = [torch.empty_like(mine) for _ in range(world)]
-        dist.all_gather(allm, mine, group=group)
-        idx = [torch.nonzero(allm[r][:hs[r]]).reshape(-1) for r in range(world)]
-        counts = [int(i.numel()) for i in idx]
-        H = H.index_select(1, idx[rank])  # (nb_all, live rows, 4, 2)
-    splits_in = [(layout.image_rows(s)[1] - layout.image_rows(s)[0]) // COL_BLOCK * counts[rank] * COL_BLOCK * 2
-                 for s in range(world)]
-    splits_out = [nb * counts[r] * COL_BLOCK * 2 for r in range(world)]
-    if stats is not None:
-        stats["a2a_send_bytes"] = stats.get("a2a_send_bytes", 0) + sum(splits_in) * H.element_size()
-    recv = torch.empty(sum(splits_out), dtype=H.dtype, device=H.device)
-    dist.all_to_all_single(recv, H.reshape(-1), splits_out, splits_in, group=group)
-    pieces = list(torch.split(recv, splits_out))
-    return _assemble_H(pieces, nb, layout, H.device, H.dtype, idx)
+        hs = [layout.rows(r)[1] - layout.rows(r)[0] for r in range(world)]
+        return _alltoall_rows(H, layout, rank, world, group, hs, [None] * world, stats=stats)
+    stacked, counts, masks = _exchange_masks(live, layout, rank, world, group)
+    return _alltoall_rows(_pack_live(H, masks[rank], counts[rank]), layout, rank, world, group, counts, masks,
+                          stacked, stats)
+
+
+def _packed_send(backend, buf, h: int, plane: int, layout: StripLayout, rank: int, world: int, group):
+    """Sparse exchange with pass A writing the send buffer (the backend knows
+    its live rows before pass A): (Hsend on the wire, counts, masks, stacked),
+    or None when it does not (then pass A runs dense and _alltoall_H packs)."""
+    fn = getattr(backend, "live_rows", None)
+    live = fn(h, plane) if fn is not None else None
+    if live is None or not hasattr(backend, "pass_rows_packed"):
+        return None
+    stacked, counts, masks = _exchange_masks(live, layout, rank, world, group)
+    Hs = backend.pass_rows_packed(buf, 0, h, masks[rank], counts[rank], plane=plane)
+    return _wire(Hs, backend), counts, masks, stacked
 
 
 class PendingGather:
@@ -695,6 +837,49 @@ def _local_pieces(Hs, b0: int, b1: int, backend, lives):
     return [_wire(H[b0:b1].index_select(1, i), backend) for H, i in zip(Hs, idx)], idx
 
 
+def _local_sends(Hs, lives, backend, timed):
+    """The emulated all-to-all's send side: every rank packs its live rows
+    once (timed as its "pack" stage, as _alltoall_H's sender does) ->
+    (sends, masks, counts, stacked masks); a receiver's buffer is the concatenation of the
+    sends' block ranges (the network: untimed), unpacked by _unpack_rows."""
+    wires = [_wire(H, backend) for H in Hs]
+    hs = [int(H.shape[1]) for H in Hs]
+    if lives is None:
+        return wires, [None] * len(Hs), hs, None
+    masks = [lv.to(torch.bool) for lv in lives]
+    counts = [int(c) for c in torch.stack([m.sum() for m in masks]).tolist()]
+    stacked = torch.zeros((len(Hs), max(hs)), dtype=torch.uint8, device=Hs[0].device)
+    for r, m in enumerate(masks):
+        stacked[r, :hs[r]] = m.to(torch.uint8)
+    sends = [timed(r, "pack", lambda r=r: _pack_live(wires[r], masks[r], counts[r])) for r in range(len(Hs))]
+    return sends, masks, counts, stacked
+
+
+def _local_pass_a(ranks, grids, hs, plane, sparse: bool, on_gpu: bool, timed, backend, layout, stages):
+    """Every rank's pass A in the emulation -> (Hs, lives, sends): with the
+    sparse exchange on the GPU and every rank's live rows known from its mask,
+    pass A writes the packed send buffer itself (Hs None; sends = (buffers,
+    masks, counts, stacked)), else dense pass A (sends from _local_sends)."""
+    world = len(ranks)
+    if sparse and world > 1 and on_gpu and all(hasattr(rk, "pass_rows_packed") for rk in ranks):
+        lives = [rk.live_rows(h, plane) for rk, h in zip(ranks, hs)]
+        if all(lv is not None for lv in lives):
+            masks = [lv.to(torch.bool) for lv in lives]
+            counts = [int(c) for c in torch.stack([m.sum() for m in masks]).tolist()]
+            stacked = torch.zeros((world, max(hs)), dtype=torch.uint8, device=masks[0].device)
+            for r, m in enumerate(masks):
+                stacked[r, :hs[r]] = m.to(torch.uint8)
+            bufs = [timed(r, "rows", lambda r=r: _wire(ranks[r].pass_rows_packed(
+                grids[r], 0, hs[r], masks[r], counts[r], plane=plane), backend)) for r in range(world)]
+            _count_a2a(stages, bufs, masks, layout, backend)
+            return None, masks, (bufs, masks, counts, stacked)
+    Hs = [timed(r, "rows", lambda r=r: ranks[r].pass_rows(grids[r], 0, hs[r], plane=plane)) for r in range(world)]
+    lives = [_live_of(ranks[r], Hs[r], hs[r], plane) for r in range(world)] if (sparse and world > 1) else None
+    _count_a2a(stages, Hs, lives, layout, backend)
+    sends = _local_sends(Hs, lives, backend, timed) if (world > 1 and on_gpu) else None
+    return Hs, lives, sends
+
+
 def invert_strips_local(datas: Sequence[StripData], freq, layout: StripLayout, backend,
                         stages: Optional[list] = None, sparse: bool = True):
     """All ranks' stages in ONE process on one device, the exchanges done in
@@ -707,8 +892,8 @@ def invert_strips_local(datas: Sequence[StripData], freq, layout: StripLayout, b
     image-row strip. `sparse`: the regrouping moves only each rank's live
     rows (as the distributed sparse all-to-all). `stages` (a list,
     diagnostic): filled with one dict per rank of synchronised seconds (grid,
-    halo, rows, assemble, cols) and the bytes the rank would send in the
-    all-to-all (a2a_send_bytes). Returns the normalised dirty image
+    halo, rows, pack, assemble, cols) and the bytes the rank would send in
+    the all-to-all (a2a_send_bytes). Returns the normalised dirty image
     (npix_x, npix_y)."""
     import time  # pylint: disable=import-outside-toplevel
 
@@ -762,15 +947,17 @@ def invert_strips_local(datas: Sequence[StripData], freq, layout: StripLayout, b
             i0, i1 = layout.image_rows(s)
             accs.append(torch.empty((i1 - i0, backend.npix_y), dtype=torch.float64, device=bufs[0].device))
         for p in range(nplanes):
-            Hs = [timed(r, "rows", lambda r=r: ranks[r].pass_rows(bufs[r][p], 0, hs[r], plane=p))
-                  for r in range(world)]
-            lives = [_live_of(ranks[r], Hs[r], hs[r], p) for r in range(world)] if (sparse and world > 1) else None
-            _count_a2a(stages, Hs, lives, layout, backend)
+            Hs, lives, sends = _local_pass_a(ranks, [b[p] for b in bufs], hs, p, sparse, on_gpu, timed, backend,
+                                             layout, stages)
             for s in range(world):
                 i0, i1 = layout.image_rows(s)
                 b0, b1 = i0 // COL_BLOCK, i1 // COL_BLOCK
                 if world == 1:
                     Hm = Hs[0]
+                elif sends is not None:
+                    recv = torch.cat([snd[b0:b1].reshape(-1) for snd in sends[0]])
+                    Hm = timed(s, "assemble", lambda b0=b0, b1=b1, recv=recv: _unpack_rows(
+                        recv, b1 - b0, layout, sends[1], sends[2], recv.dtype, sends[3]).to(torch.float64))
                 else:
                     def regroup(b0=b0, b1=b1):
                         pieces, idx = _local_pieces(Hs, b0, b1, backend, lives)
@@ -785,19 +972,19 @@ def invert_strips_local(datas: Sequence[StripData], freq, layout: StripLayout, b
             i0, i1 = layout.image_rows(s)
             out.append(timed(s, "final", lambda s=s, i0=i0, i1=i1: ranks[s].finish_rows(accs[s], i0, i1, norm=sumw)))
         return torch.cat(out, dim=0)
-    Hs, lives = [], []
+    Hs, lives, sends = _local_pass_a(ranks, bufs, hs, 0, sparse, on_gpu, timed, backend, layout, stages)
     for r in range(world):
-        Hs.append(timed(r, "rows", lambda r=r: ranks[r].pass_rows(bufs[r], 0, hs[r])))
-        lives.append(_live_of(ranks[r], Hs[r], hs[r]) if (sparse and world > 1) else None)
         ranks[r].mark_clean()
-    lives = lives if (sparse and world > 1) else None
-    _count_a2a(stages, Hs, lives, layout, backend)
     out = []
     for s in range(world):
         i0, i1 = layout.image_rows(s)
         b0, b1 = i0 // COL_BLOCK, i1 // COL_BLOCK
         if world == 1:
             Hm = Hs[0]
+        elif sends is not None:
+            recv = torch.cat([snd[b0:b1].reshape(-1) for snd in sends[0]])
+            Hm = timed(s, "assemble", lambda b0=b0, b1=b1, recv=recv: _unpack_rows(
+                recv, b1 - b0, layout, sends[1], sends[2], recv.dtype, sends[3]).to(torch.float64))
         else:
             def regroup(b0=b0, b1=b1):
                 pieces, idx = _local_pieces(Hs, b0, b1, backend, lives)

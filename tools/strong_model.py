@@ -98,7 +98,10 @@ def strips_model(args):
         torch.cuda.empty_cache()
     N = args.ranks
     pr = out[N]["per_rank_ms"]
-    stage_max = {k: max(p.get(k, 0.0) for p in pr) for k in ("grid", "halo", "rows", "cols")}
+    # pack / assemble: a sender's live-row compaction before the all-to-all and
+    # a receiver's row scatter after it (the distributed run pays both; on the
+    # critical path)
+    stage_max = {k: max(p.get(k, 0.0) for p in pr) for k in ("grid", "halo", "rows", "pack", "assemble", "cols")}
     t1 = sum(out[1]["per_rank_ms"][0].get(k, 0.0) for k in ("grid", "rows", "cols"))
     H_bytes = [(npix // 4) * (b - a) * 4 * 16 for a, b in out[N]["strip_rows"]]  # each rank's pass-A output
     # what each rank sends in the (sparse) all-to-all: its live pass-A rows'
@@ -117,14 +120,15 @@ def strips_model(args):
         # is across; the all-to-all waits for every rank's pass A, pass B for
         # the all-to-all, the gather for every pass B
         g = [p.get("grid", 0.0) for p in pr]
-        rows_end = [max(g[max(r - 1, 0):r + 2]) + (halo_ms if N > 1 else 0.0) + pr[r].get("rows", 0.0)
-                    for r in range(N)]
-        step = max(rows_end) + a2a_ms + stage_max["cols"] + gather_ms
+        rows_end = [max(g[max(r - 1, 0):r + 2]) + (halo_ms if N > 1 else 0.0) + pr[r].get("rows", 0.0) +
+                    pr[r].get("pack", 0.0) for r in range(N)]
+        step = max(rows_end) + a2a_ms + stage_max["assemble"] + stage_max["cols"] + gather_ms
         # bench.py --strong's pipelined steps: step k's gather on the
         # communicator's stream during step k + 1's gridding (hidden while it is
         # shorter than the grid stage)
-        step_ov = max(rows_end) + a2a_ms + stage_max["cols"] + max(0.0, gather_ms - min(g))
-        bound = stage_max["grid"] + stage_max["rows"] + stage_max["cols"] + halo_ms + a2a_ms + gather_ms
+        step_ov = max(rows_end) + a2a_ms + stage_max["assemble"] + stage_max["cols"] + max(0.0, gather_ms - min(g))
+        bound = (stage_max["grid"] + stage_max["rows"] + stage_max["pack"] + stage_max["assemble"] + stage_max["cols"] +
+                 halo_ms + a2a_ms + gather_ms)
         models[f"{link:g}GB/s"] = {"halo_ms": round(halo_ms, 3), "alltoall_ms": round(a2a_ms, 3),
                                    "gather_ms": round(gather_ms, 3), "step_ms": round(step, 3),
                                    "step_ms_stage_max_sum": round(bound, 3),
@@ -237,7 +241,7 @@ def wstrips_model(args):
         torch.cuda.empty_cache()
     N = args.ranks
     pr = out[N]["per_rank_ms"]
-    stage_max = {k: max(p.get(k, 0.0) for p in pr) for k in ("grid", "rows", "cols", "final")}
+    stage_max = {k: max(p.get(k, 0.0) for p in pr) for k in ("grid", "rows", "pack", "assemble", "cols", "final")}
     t1 = sum(out[1]["per_rank_ms"][0].get(k, 0.0) for k in ("grid", "rows", "cols", "final"))
     nplanes, W, nu = int(params.nplanes), int(params.support), int(params.nu)
     # one plane's pass-A output as it crosses the all-to-all (complex64 for the packed class, strips._wire)
@@ -253,8 +257,8 @@ def wstrips_model(args):
         # grid (+ halo) then the plane loop: each plane's pass A, all-to-all and
         # pass B in turn (the slowest rank's summed pass-A and pass-B times),
         # the final correction, the gather
-        step = (stage_max["grid"] + halo_ms + stage_max["rows"] + a2a_ms + stage_max["cols"] + stage_max["final"] +
-                gather_ms)
+        step = (stage_max["grid"] + halo_ms + stage_max["rows"] + stage_max["pack"] + a2a_ms + stage_max["assemble"] +
+                stage_max["cols"] + stage_max["final"] + gather_ms)
         models[f"{link:g}GB/s"] = {"halo_ms": round(halo_ms, 3), "alltoall_ms": round(a2a_ms, 3),
                                    "gather_ms": round(gather_ms, 3), "step_ms": round(step, 3),
                                    "speedup_vs_one_shot": round(one_ms / step, 2),
