@@ -489,32 +489,16 @@ def _assemble_H(pieces: Sequence, nb: int, layout: StripLayout, device, dtype, i
     """Rank s's pass-B input from every rank's pass-A blocks [i0_s / 4, i1_s / 4)
     (piece r: (nb, h_r, 4, 2), or with idx[r] (sparse) only rank r's rows
     idx[r] of its strip: (nb, len(idx[r]), 4, 2), the other rows zero) ->
-    (nb, nv, 4, 2)."""
+    (nb, nv, 4, 2). The torch form, for CPU tensors (the gloo tests' backend);
+    GPU buffers go through _unpack_rows (one copy kernel)."""
     sparse = idx is not None and any(i is not None for i in idx)
-    H = torch.empty((nb, layout.nv, COL_BLOCK, 2), dtype=dtype, device=device)
-    if not sparse:
-        for r, piece in enumerate(pieces):
-            y0, y1 = layout.rows(r)
-            H[:, y0:y1] = piece.reshape(nb, y1 - y0, COL_BLOCK, 2)
-        return H
-    # sparse: zero only the rows no rank sends, then one row-record copy per
-    # source (a record = one row of one 4-column block, 4 complex values; an
-    # advanced-index assignment of whole (nb, rows) slabs into a zeroed H cost
-    # 3-4x more: profiles/r05_assemble.txt)
-    nv = layout.nv
-    live = torch.zeros(nv, dtype=torch.bool, device=device)
-    glob = []
-    for r in range(len(pieces)):
+    H = (torch.zeros if sparse else torch.empty)((nb, layout.nv, COL_BLOCK, 2), dtype=dtype, device=device)
+    for r, piece in enumerate(pieces):
         y0, y1 = layout.rows(r)
-        g = (torch.arange(y0, y1, device=device) if idx[r] is None else idx[r].to(device) + y0)
-        live[g] = True
-        glob.append(g)
-    rec = H.view(nb * nv, COL_BLOCK * 2)
-    rec.view(nb, nv, COL_BLOCK * 2).index_fill_(1, torch.nonzero(~live).reshape(-1), 0)
-    base = torch.arange(nb, device=device).mul_(nv).reshape(nb, 1)
-    for piece, g in zip(pieces, glob):
-        if g.numel():
-            rec.index_copy_(0, (base + g.reshape(1, -1)).reshape(-1), piece.reshape(-1, COL_BLOCK * 2))
+        if idx is None or idx[r] is None:
+            H[:, y0:y1] = piece.reshape(nb, y1 - y0, COL_BLOCK, 2)
+        elif idx[r].numel():
+            H[:, y0 + idx[r]] = piece.reshape(nb, idx[r].numel(), COL_BLOCK, 2)
     return H
 
 
