@@ -870,15 +870,19 @@ static int wstack_group(const GridGeometry& g, bool packed) {
   static const int env = [] {
     const char* e = getenv("CIP_WSTACK_GROUP");
     const int v = e ? atoi(e) : 0;
-    return v < 0 ? 0 : (v > 5 ? 5 : v);
+    return v < 0 ? 0 : (v > 7 ? 7 : v);
   }();
   if (!g.do_wstacking || g.support > 16 || g.nplanes < 2) return 1;
   const int64_t P = kTile + g.support - 1;
   if (packed) {
-    // 8-byte cells: up to 5 sub-grids in one 512-thread block (<= 64 KB of
-    // static LDS, cip_scatter.h kFitG5 / kFitG4), two blocks per CU
-    int G = env ? env : 5;
-    while (G > 3 && G * P * P * 8 + 4200 > 65536) --G;
+    // 8-byte cells: up to 7 sub-grids in one 512-thread block, two blocks per
+    // CU (<= 80 KB of static LDS each; cip_scatter.h kFitG7 .. kFitG4). Round
+    // 5: G = 7 at W = 6 (the reference call: 14 planes in two groups, a
+    // visibility visits 1.6 groups instead of 2) scatter 7.15 -> 6.93 ms,
+    // call 7.35 -> 7.51-7.54 Gvis/s (profiles/r05ah_ab_wstack_group.txt)
+    int G = env ? env : 7;
+    while (G > 5 && G * P * P * 8 + 4200 > 81920) --G;
+    while (G > 3 && G <= 5 && G * P * P * 8 + 4200 > 65536) --G;
     return G;
   }
   // two 512-thread blocks per CU must fit their G sub-grids in 160 KB of LDS

@@ -811,8 +811,20 @@ inline hipError_t scatter_dispatch_ws(bool ws, int group, bool pack, unsigned ld
 #define LAUNCH_WS_PACKED(PRM)                                \
   {                                                          \
     bool hit = false;                                        \
+    if constexpr (kFitG7) {                                  \
+      if (ws && group == 7) {                                \
+        LAUNCH(true, PRM, true, 7);                          \
+        hit = true;                                          \
+      }                                                      \
+    }                                                        \
+    if constexpr (kFitG6) {                                  \
+      if (!hit && ws && group == 6) {                        \
+        LAUNCH(true, PRM, true, 6);                          \
+        hit = true;                                          \
+      }                                                      \
+    }                                                        \
     if constexpr (kFitG5) {                                  \
-      if (ws && group == 5) {                                \
+      if (!hit && ws && group == 5) {                        \
         LAUNCH(true, PRM, true, 5);                          \
         hit = true;                                          \
       }                                                      \
@@ -830,6 +842,9 @@ inline hipError_t scatter_dispatch_ws(bool ws, int group, bool pack, unsigned ld
   // plane groups of 4 / 5 packed sub-grids while they fit 64 KB of static LDS
   constexpr int P2 = (kTile + W - 1) * (kTile + W - 1);
   constexpr bool kFitG5 = 5 * P2 * 8 + 4200 <= 65536;
+  // 6 / 7 (CIP_WSTACK_GROUP, experiment): two blocks per CU in 160 KB
+  constexpr bool kFitG7 = 7 * P2 * 8 + 4200 <= 81920;
+  constexpr bool kFitG6 = 6 * P2 * 8 + 4200 <= 81920;
   constexpr bool kFitG4 = 4 * P2 * 8 + 4200 <= 65536;
   bool done = false;
   const bool wide = m.delta != nullptr;  // ragged row slices: u64 entries

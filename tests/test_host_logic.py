@@ -178,7 +178,7 @@ def test_params_match_oracle():
 
 def test_plane_group_and_wplane_split_on_its_lattice(monkeypatch):
     # cip_plane_group is the scatter's w-plane group (cip_api.hip wstack_group):
-    # 1 in 2-D and above W = 16, 5 packed at small W, 3 / 2 in the fp64 class;
+    # 1 in 2-D and above W = 16, 7 packed at W = 6 (6 at W = 8), 3 / 2 in the fp64 class;
     # split_planes with that group cuts only on group boundaries
     from ska_sdp_cip_amd import wplanes
 
@@ -187,7 +187,9 @@ def test_plane_group_and_wplane_split_on_its_lattice(monkeypatch):
     assert _lib.plane_group(p2d) == 1 and _lib.plane_group(p2d, packed=True) == 1
     pw = _lib.choose_params(4096, 4096, 3e-6, 3e-6, 1e-4, 0, True, -60000.0, 60000.0)
     assert pw.support == 6 and pw.nplanes > 10
-    assert _lib.plane_group(pw, packed=True) == 5 and _lib.plane_group(pw) == 3
+    assert _lib.plane_group(pw, packed=True) == 7 and _lib.plane_group(pw) == 3
+    pw8 = _lib.choose_params(4096, 4096, 3e-6, 3e-6, 1e-4, 8, True, -60000.0, 60000.0)
+    assert _lib.plane_group(pw8, packed=True) == 6
     pw12 = _lib.choose_params(4096, 4096, 3e-6, 3e-6, 1e-4, 12, True, -60000.0, 60000.0)
     assert _lib.plane_group(pw12) == 2
     g = _lib.plane_group(pw, packed=True)
