@@ -664,12 +664,15 @@ def _unpack_rows(recv, nb: int, layout: StripLayout, masks, counts, dtype, stack
             stacked[r, :hs[r]] = 1 if m is None else m.to(torch.uint8)
     M = stacked[:, :max(hs)].to(torch.int64)
     key = (tuple(layout.y_bounds), str(dev))
-    if key not in _ROW_MAPS:  # grid row -> (its rank, its row in the rank's strip), per layout
+    maps = _ROW_MAPS.get(key)
+    if maps is None:  # grid row -> (its rank, its row in the rank's strip), per layout
         rr = torch.repeat_interleave(torch.arange(world, device=dev), torch.tensor(hs, device=dev))
         y0s = torch.tensor([layout.rows(r)[0] for r in range(world)], device=dev)
-        _ROW_MAPS.clear()
-        _ROW_MAPS[key] = (rr, torch.arange(nv, device=dev) - y0s[rr])
-    rr, jj = _ROW_MAPS[key]
+        maps = (rr, torch.arange(nv, device=dev) - y0s[rr])
+        if len(_ROW_MAPS) > 16:
+            _ROW_MAPS.clear()
+        _ROW_MAPS[key] = maps
+    rr, jj = maps
     cnt = M.sum(dim=1)  # = counts, on the device (no host copies)
     base = (torch.cumsum(cnt, 0) - cnt) * nb
     rec = torch.where(M[rr, jj] != 0, torch.cumsum(M, dim=1).sub_(1)[rr, jj] + base[rr],
