@@ -645,11 +645,11 @@ def _pack_live(H, live, count: int):
 _ROW_MAPS: dict = {}
 
 
-def _unpack_rows(recv, nb: int, layout: StripLayout, masks, counts, dtype, stacked=None):
+def _unpack_rows(recv, nb: int, layout: StripLayout, masks, dtype, stacked=None):
     """A receiver's pass-B input (nb, nv, 4, 2) from the flat received buffer:
-    rank r's piece (nb, counts[r], 4, 2) holds its live rows (masks[r], bool
-    over its strip rows; None: every row), in order; rows no rank sent are
-    zero. One copy kernel (cip_strip_unpack_rows); its row map - the record
+    rank r's piece (nb, its live row count, 4, 2) holds its live rows
+    (masks[r], bool over its strip rows; None: every row), in order; rows no
+    rank sent are zero. One copy kernel (cip_strip_unpack_rows); its row map - the record
     of each grid row's block 0 and its source's row count - in a handful of
     vectorised ops (`stacked`: the ranks' masks as one (world, >= max rows)
     tensor, when the caller has it)."""
@@ -720,7 +720,7 @@ def _alltoall_rows(Hsend, layout: StripLayout, rank: int, world: int, group, cou
     recv = torch.empty(sum(splits_out), dtype=Hsend.dtype, device=Hsend.device)
     dist.all_to_all_single(recv, Hsend.reshape(-1), splits_out, splits_in, group=group)
     if Hsend.device.type == "cuda":
-        return _unpack_rows(recv, nb, layout, masks, counts, Hsend.dtype, stacked)
+        return _unpack_rows(recv, nb, layout, masks, Hsend.dtype, stacked)
     pieces = list(torch.split(recv, splits_out))
     idx = [None if m is None else torch.nonzero(m).reshape(-1) for m in masks]
     return _assemble_H(pieces, nb, layout, Hsend.device, Hsend.dtype, idx)
@@ -944,7 +944,7 @@ def invert_strips_local(datas: Sequence[StripData], freq, layout: StripLayout, b
                 elif sends is not None:
                     recv = torch.cat([snd[b0:b1].reshape(-1) for snd in sends[0]])
                     Hm = timed(s, "assemble", lambda b0=b0, b1=b1, recv=recv: _unpack_rows(
-                        recv, b1 - b0, layout, sends[1], sends[2], recv.dtype, sends[3]).to(torch.float64))
+                        recv, b1 - b0, layout, sends[1], recv.dtype, sends[3]).to(torch.float64))
                 else:
                     def regroup(b0=b0, b1=b1):
                         pieces, idx = _local_pieces(Hs, b0, b1, backend, lives)
@@ -971,7 +971,7 @@ def invert_strips_local(datas: Sequence[StripData], freq, layout: StripLayout, b
         elif sends is not None:
             recv = torch.cat([snd[b0:b1].reshape(-1) for snd in sends[0]])
             Hm = timed(s, "assemble", lambda b0=b0, b1=b1, recv=recv: _unpack_rows(
-                recv, b1 - b0, layout, sends[1], sends[2], recv.dtype, sends[3]).to(torch.float64))
+                recv, b1 - b0, layout, sends[1], recv.dtype, sends[3]).to(torch.float64))
         else:
             def regroup(b0=b0, b1=b1):
                 pieces, idx = _local_pieces(Hs, b0, b1, backend, lives)

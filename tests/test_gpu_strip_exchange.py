@@ -35,7 +35,7 @@ def test_pack_unpack_equal_index_forms(gpu_device, dtype):
         i0, i1 = layout.image_rows(s)
         b0, b1 = i0 // 4, i1 // 4
         recv = torch.cat([snd[b0:b1].reshape(-1) for snd in sends])
-        got = strips._unpack_rows(recv, b1 - b0, layout, masks, counts, dtype)  # pylint: disable=protected-access
+        got = strips._unpack_rows(recv, b1 - b0, layout, masks, dtype)  # pylint: disable=protected-access
         ref = torch.zeros((b1 - b0, nv, 4, 2), dtype=dtype, device=gpu_device)
         for r, H in enumerate(Hs):
             y0, _ = layout.rows(r)
@@ -44,7 +44,7 @@ def test_pack_unpack_equal_index_forms(gpu_device, dtype):
         assert torch.equal(got, ref)
     # dense ranks (no masks): every row sent
     recv = torch.cat([H[0:2].reshape(-1) for H in Hs])
-    got = strips._unpack_rows(recv, 2, layout, [None] * world, hs, dtype)  # pylint: disable=protected-access
+    got = strips._unpack_rows(recv, 2, layout, [None] * world, dtype)  # pylint: disable=protected-access
     assert torch.equal(got, torch.cat([H[0:2] for H in Hs], dim=1))
 
 
