@@ -147,5 +147,39 @@ def test_c4_full_eight_strips_equal_one_shot(gpu_device):
     err = float(np.abs(got - sums / sw).max())
     print(f"C4 8 strips vs DFT pixels: {err:.3e} of sum w")
     assert err < 1e-6
-    del be, datas, img, ref
+    del be, img
     torch.cuda.empty_cache()
+    _distributed_as_threads(datas, f, layout, prm, px, ref, world)
+    del datas, ref
+    torch.cuda.empty_cache()
+
+
+def _distributed_as_threads(datas, f, layout, prm, px, ref, world):
+    """The same split through the DISTRIBUTED function (strips.invert_strips:
+    halo send/recv, mask all-gather, packed pass A, sparse all-to-all, unpack
+    kernel, image gather) with the 8 ranks as host threads on this GPU and
+    torch.distributed's calls replaced by an in-memory stand-in
+    (tests/_thread_dist.py): the configs[3] 8-GPU leg's code path at its size."""
+    import torch
+
+    from _thread_dist import run_ranks
+    from ska_sdp_cip_amd import strips
+
+    mp = pytest.MonkeyPatch()
+    try:
+        def rank_fn(r):
+            be = strips.HipStripBackend(prm, px, px, NPIX, NPIX, device=torch.device("cuda", 0))
+            out = strips.invert_strips(datas[r], f, layout, be)
+            torch.cuda.synchronize()
+            assert float(be.grid.abs().max()) == 0.0 and not be.dirty
+            return out
+
+        results, errors = run_ranks(mp, world, rank_fn)
+    finally:
+        mp.undo()
+    assert not errors, errors
+    img = results[0]
+    peak = float(ref.abs().max())
+    diff = float((img - ref).abs().max())
+    print(f"C4 8 distributed ranks (threads) vs one-shot: max |diff| = {diff:.3e} (peak {peak:.3e})")
+    assert diff < 1e-12 * peak
