@@ -1251,6 +1251,16 @@ static bool scatter_on_plan_stream() {
   return e && e[0] == '1';
 }
 
+// CIP_WACC_F32=0: the packed class's w planes accumulate in the fp64 image
+// (A/B); default: a float accumulator
+static bool wacc_f32_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("CIP_WACC_F32");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 // CIP_SCATTER_SHARE=0: pipelined calls' scatters take every CU slot (A/B)
 static bool share_cus_enabled() {
   static const bool on = [] {
@@ -1303,7 +1313,8 @@ static bool fft_rowskip() {
 // after_rows (may be NULL): recorded on s once pass A has consumed the grid
 static int plane_to_dirty(const DirtyStage& st, const GridGeometry& g, int64_t p, double* grid, double* dirty_out,
                           hipStream_t s, const uint32_t* dmask = nullptr, const double* norm = nullptr,
-                          const uint32_t* rowbits = nullptr, int first = -1, hipEvent_t after_rows = nullptr) {
+                          const uint32_t* rowbits = nullptr, int first = -1, hipEvent_t after_rows = nullptr,
+                          bool acc_f32 = false) {
   if (first < 0) first = p == 0;  // the first plane overwrites the image, later ones add
   hipEvent_t f0 = g_prof.mark(s);
   if (st.fast) {
@@ -1320,7 +1331,7 @@ static int plane_to_dirty(const DirtyStage& st, const GridGeometry& g, int64_t p
   if (st.fast)
     CIP_HIP_CHECK(launch_fft_cols(st.fft_h, g.nv, st.npix_x, st.npix_y, st.tw_v, g.do_wstacking ? 1 : 0, dirty_out,
                                   st.cx, st.cy, st.px, st.py, w_plane, first, g.do_wstacking ? nullptr : norm,
-                                  dmask ? rowbits : nullptr, s, g.grid_f32 != 0));
+                                  dmask ? rowbits : nullptr, s, g.grid_f32 != 0, acc_f32));
   hipEvent_t f1 = g_prof.mark(s);
   g_prof.span(3, f0, f1);
   if (st.fast) {
@@ -1382,14 +1393,14 @@ static int w_correction_table(Workspace* ws, const cip_gridder_params& prm, cons
 }
 
 static int finish_dirty(Workspace* ws, const DirtyStage& st, const cip_gridder_params& prm, const GridGeometry& g,
-                        double* dirty_out, hipStream_t s) {
+                        double* dirty_out, hipStream_t s, const float* acc_f32 = nullptr) {
   if (!g.do_wstacking) return CIP_OK;
   double* fwd = nullptr;
   int64_t fw_n = 0;
   double dnu = 0.0;
   if (const int rc = w_correction_table(ws, prm, g, s, &fwd, &fw_n, &dnu); rc != CIP_OK) return rc;
   CIP_HIP_CHECK(launch_wfinal_correct(dirty_out, st.npix_x, st.npix_y, st.px, st.py, st.cx, st.cy, fwd, fw_n, dnu,
-                                      g.dw, s));
+                                      g.dw, s, 0, -1, nullptr, acc_f32));
   return CIP_OK;
 }
 
@@ -1646,6 +1657,14 @@ static int ms2dirty_impl(const double* uvw, int64_t nrow, const double* freq, in
   } else if (const int jr = plan_join.join(); jr != CIP_OK) {
     return jr;
   }
+  // the packed class's w planes accumulate in a float image (its own
+  // precision, one rounding per plane; the final correction writes the fp64
+  // image): half the per-plane read-modify-write of pass B
+  float* wacc = nullptr;
+  if (st.fast && g.do_wstacking && g.grid_f32 && !pair_b && p_lo < p_hi && wacc_f32_enabled()) {
+    wacc = buf<float>(ws, "wacc_f32", npix_x * npix_y);
+    if (!wacc) return CIP_ENOMEM;
+  }
   for (int64_t q = p_lo / G; !scatter_ps && q * G < p_hi; ++q) {
     // pipelined calls: leave CU slots to the next call's planner (profiles/r03_ab_scatter_share.txt)
     rc = scatter_plane(pp, q, uvw, vis, vis_dtype, wgt, wgt_dtype, st.fast, grid, s, clean,
@@ -1671,14 +1690,15 @@ static int ms2dirty_impl(const double* uvw, int64_t nrow, const double* freq, in
         g_prof.span(3, f0, g_prof.mark(s));
         continue;
       }
-      rc = plane_to_dirty(st, g, p, plane_p, dirty_out, s, dm, normalise ? pp.red : nullptr, rbp, p == p_lo);
+      rc = plane_to_dirty(st, g, p, plane_p, wacc ? (double*)wacc : dirty_out, s, dm, normalise ? pp.red : nullptr,
+                          rbp, p == p_lo, nullptr, wacc != nullptr);
       if (rc != CIP_OK) return rc;
     }
     // a group's planes outside the range were neither written (the scatter
     // skips them) nor read, so a masked pass A still leaves the group clean
     clean = dmask != nullptr;
   }
-  rc = finish_dirty(ws, st, pp.p, g, dirty_out, s);
+  rc = finish_dirty(ws, st, pp.p, g, dirty_out, s, wacc);
   if (rc != CIP_OK) return rc;
   // fused into pass B on the pruned 2-D path; a separate pass otherwise
   if (normalise && (!st.fast || g.do_wstacking))

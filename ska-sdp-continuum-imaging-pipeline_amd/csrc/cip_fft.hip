@@ -13,6 +13,8 @@
 // two workgroups per CU). HBM bytes per plane: pass A 16 nu nv read +
 // 16 nx nv written, pass B 16 nx nv read + 8 nx ny written (against 64 nu nv
 // for hipFFT's in-place 2-D c2c plus the crop pass).
+#include <type_traits>
+
 #include "cip_internal.h"
 
 namespace cip {
@@ -364,7 +366,9 @@ struct ColEpilogue {
 // rowbits (may be NULL: every H row is read): bit ty of the plane's tile-row
 // words - H rows y of clean tile rows (y / kTile) were not written by pass A
 // and are zero.
-template <int N, int MODE, typename HT = double2, typename CT = double2>
+// OT (MODE 1): the plane accumulator's type - double, or float for the packed
+// class (its own precision; one rounding per plane: acc = (float)(acc + val))
+template <int N, int MODE, typename HT = double2, typename CT = double2, typename OT = double>
 __global__ __launch_bounds__(N / 16, fft_waves<CT>()) void fft_cols_kernel(const HT* __restrict__ H, int64_t nx, int64_t ny,
                                                           const double2* __restrict__ tw, ColEpilogue ep,
                                                           int64_t i0 = 0, const uint32_t* __restrict__ rowbits = nullptr) {
@@ -404,7 +408,7 @@ __global__ __launch_bounds__(N / 16, fft_waves<CT>()) void fft_cols_kernel(const
   }
   fft_core<N>(v, t, lds, tw);
   const int64_t p = i - nx / 2;
-  double* orow = ep.out + il * ny;
+  OT* orow = reinterpret_cast<OT*>(ep.out) + il * ny;
   const double cxi = MODE == 0 ? (ep.norm ? ep.cx[i] / *ep.norm : ep.cx[i]) : 0.0;
 #pragma unroll
   for (int m = 0; m < 16 / S::RF; ++m)
@@ -440,8 +444,12 @@ __global__ __launch_bounds__(N / 16, fft_waves<CT>()) void fft_cols_kernel(const
             sincospi(ph, &sn, &cs);
           }
           const double val = sgn * (g.x * cs - g.y * sn);
-          if (ep.first) orow[j] = val;
-          else orow[j] += val;
+          if constexpr (std::is_same<OT, float>::value) {
+            orow[j] = ep.first ? (float)val : (float)((double)orow[j] + val);
+          } else {
+            if (ep.first) orow[j] = val;
+            else orow[j] += val;
+          }
         }
       }
     }
@@ -735,7 +743,8 @@ hipError_t launch_fft_cols_strip_wplane(const double* H, int64_t nv, int64_t nx,
 
 hipError_t launch_fft_cols(const double* H, int64_t nv, int64_t nx, int64_t ny, const double* tw_v, int mode,
                            double* out, const double* cx, const double* cy, double px, double py, double w_plane,
-                           int first, const double* norm, const uint32_t* rowbits, hipStream_t s, bool h_f32) {
+                           int first, const double* norm, const uint32_t* rowbits, hipStream_t s, bool h_f32,
+                           bool acc_f32) {
   const dim3 gd((unsigned)nx);
   const double2* h = (const double2*)H;
   const float2* hf = (const float2*)H;
@@ -744,7 +753,10 @@ hipError_t launch_fft_cols(const double* H, int64_t nv, int64_t nx, int64_t ny, 
   const bool fft_f32 = fft_f32_enabled();
 #define COLS(NN)                                                                                           \
   case NN:                                                                                                 \
-    if (h_f32 && fft_f32 && mode == 0)                                                                     \
+    if (h_f32 && fft_f32 && mode == 1 && acc_f32)                                                          \
+      fft_cols_kernel<NN, 1, float2, float2, float><<<gd, dim3(NN / 16), 0, s>>>(hf, nx, ny, tw, ep, 0,     \
+                                                                                 rowbits);                \
+    else if (h_f32 && fft_f32 && mode == 0)                                                                \
       fft_cols_kernel<NN, 0, float2, float2><<<gd, dim3(NN / 16), 0, s>>>(hf, nx, ny, tw, ep, 0, rowbits);  \
     else if (h_f32 && fft_f32)                                                                             \
       fft_cols_kernel<NN, 1, float2, float2><<<gd, dim3(NN / 16), 0, s>>>(hf, nx, ny, tw, ep, 0, rowbits);  \

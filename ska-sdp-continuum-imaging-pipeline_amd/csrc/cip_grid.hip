@@ -453,13 +453,17 @@ hipError_t launch_wplane_accumulate(const double* grid, const GridGeometry& g, i
 // acc *= cx[i] cy[j] / (F(dw |n-1|) n): F from a uniform table (cubic Lagrange).
 // Image rows i0 + blockIdx.y (acc row blockIdx.y: a uv strip's image rows,
 // DESIGN.md 7); norm (may be NULL): also / *norm (the weight sum).
-__global__ void wfinal_correct_kernel(double* __restrict__ acc, int64_t nx, int64_t ny, double px, double py,
-                                      const double* __restrict__ cx, const double* __restrict__ cy,
-                                      const double* __restrict__ fw, int64_t fw_n, double fw_dnu, double dw,
-                                      int64_t i0, const double* __restrict__ norm) {
+// AT: the plane accumulator's type (double: in place, out == acc; float: the
+// packed class's accumulator, corrected into the fp64 image `out`)
+template <typename AT>
+__global__ void wfinal_correct_kernel(const AT* __restrict__ acc, double* __restrict__ out, int64_t nx, int64_t ny,
+                                      double px, double py, const double* __restrict__ cx,
+                                      const double* __restrict__ cy, const double* __restrict__ fw, int64_t fw_n,
+                                      double fw_dnu, double dw, int64_t i0, const double* __restrict__ norm) {
   const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t i = i0 + blockIdx.y;
-  double* row = acc + (int64_t)blockIdx.y * ny;
+  const AT* arow = acc + (int64_t)blockIdx.y * ny;
+  double* row = out + (int64_t)blockIdx.y * ny;
   if (j >= ny) return;
   const double nm1 = nm1_of(i, j, nx, ny, px, py);
   const double t = fabs(dw * nm1) / fw_dnu;
@@ -471,17 +475,22 @@ __global__ void wfinal_correct_kernel(double* __restrict__ acc, int64_t nx, int6
   const double F = -x * (x - 1.0) * (x - 2.0) / 6.0 * f0 + (x + 1.0) * (x - 1.0) * (x - 2.0) / 2.0 * f1 -
                    (x + 1.0) * x * (x - 2.0) / 2.0 * f2 + (x + 1.0) * x * (x - 1.0) / 6.0 * f3;
   const double c = cx[i] * cy[j] / (F * (nm1 + 1.0));
-  row[j] *= norm ? c / *norm : c;
+  row[j] = (double)arow[j] * (norm ? c / *norm : c);
 }
 
 hipError_t launch_wfinal_correct(double* acc, int64_t npix_x, int64_t npix_y, double pixsize_x, double pixsize_y,
                                  const double* cx, const double* cy, const double* fw_table, int64_t fw_n,
                                  double fw_dnu, double dw, hipStream_t s, int64_t i0, int64_t nrows,
-                                 const double* norm) {
+                                 const double* norm, const float* acc_f32) {
   if (nrows < 0) nrows = npix_x - i0;
   if (nrows <= 0) return hipSuccess;
-  wfinal_correct_kernel<<<dim3((unsigned)((npix_y + 255) / 256), (unsigned)nrows), dim3(256), 0, s>>>(
-      acc, npix_x, npix_y, pixsize_x, pixsize_y, cx, cy, fw_table, fw_n, fw_dnu, dw, i0, norm);
+  const dim3 gd((unsigned)((npix_y + 255) / 256), (unsigned)nrows);
+  if (acc_f32)
+    wfinal_correct_kernel<float><<<gd, dim3(256), 0, s>>>(acc_f32, acc, npix_x, npix_y, pixsize_x, pixsize_y, cx,
+                                                          cy, fw_table, fw_n, fw_dnu, dw, i0, norm);
+  else
+    wfinal_correct_kernel<double><<<gd, dim3(256), 0, s>>>(acc, acc, npix_x, npix_y, pixsize_x, pixsize_y, cx, cy,
+                                                           fw_table, fw_n, fw_dnu, dw, i0, norm);
   return hipGetLastError();
 }
 

@@ -162,11 +162,12 @@ hipError_t launch_wplane_accumulate(const double* grid, const GridGeometry& g, i
                                     double pixsize_x, double pixsize_y, double w_plane, int first,
                                     double* acc, hipStream_t s);
 // image rows [i0, i0 + nrows) held as acc rows 0.. (nrows < 0: to npix_x);
-// norm (may be NULL): also / *norm
+// norm (may be NULL): also / *norm; acc_f32 (may be NULL): the planes were
+// accumulated in this float buffer (the packed class) - corrected into acc
 hipError_t launch_wfinal_correct(double* acc, int64_t npix_x, int64_t npix_y, double pixsize_x, double pixsize_y,
                                  const double* cx, const double* cy, const double* fw_table, int64_t fw_n,
                                  double fw_dnu, double dw, hipStream_t s, int64_t i0 = 0, int64_t nrows = -1,
-                                 const double* norm = nullptr);
+                                 const double* norm = nullptr, const float* acc_f32 = nullptr);
 
 // ---- pruned 2-D FFT (cip_fft.hip) -----------------------------------------
 // gT: the grid transposed (nv rows of nu cells); H: (nx / 8) x nv x 8 complex;
@@ -185,7 +186,7 @@ hipError_t launch_fft_rows(double* gT, int64_t nu, int64_t nv, int64_t nx, const
 hipError_t launch_fft_cols(const double* H, int64_t nv, int64_t nx, int64_t ny, const double* tw_v, int mode,
                            double* out, const double* cx, const double* cy, double px, double py, double w_plane,
                            int first, const double* norm, const uint32_t* rowbits, hipStream_t s,
-                           bool h_f32 = false);
+                           bool h_f32 = false, bool acc_f32 = false);
 // w-stacking pass B over nb consecutive planes (global pbase ..): their
 // pass-A outputs at H + q hstride_bytes, summed per image row in plane order
 // and written once (first: overwrite, else added to out's values); rowbits:

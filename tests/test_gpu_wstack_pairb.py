@@ -43,9 +43,11 @@ np.savez(out, **res)
 """
 
 
-def _run(tmp_path, on):
-    out = tmp_path / f"pairb{on}.npz"
-    env = dict(os.environ, CIP_WSTACK_PAIRB="1" if on else "0")
+def _run(tmp_path, on, wacc_f32="0"):
+    out = tmp_path / f"pairb{on}{wacc_f32}.npz"
+    # both forms accumulate the planes in the fp64 image (the pair kernel's
+    # form; the default packed-class path accumulates in float: CIP_WACC_F32)
+    env = dict(os.environ, CIP_WSTACK_PAIRB="1" if on else "0", CIP_WACC_F32=wacc_f32)
     subprocess.run([sys.executable, "-c", CHILD, str(ROOT), str(out)], env=env, check=True, timeout=180)
     return np.load(out)
 
@@ -57,3 +59,18 @@ def test_plane_pair_pass_b_is_bit_identical(gpu_device, tmp_path):
     for k in off.files:
         assert np.array_equal(off[k], on[k]), k
     assert counts  # (odd and even counts both exercised when the two differ in parity)
+
+
+def test_float_plane_accumulator_within_the_class_precision(gpu_device, tmp_path):
+    """The packed class's w planes accumulate in a float image by default
+    (CIP_WACC_F32; one rounding per plane, then the fp64 final correction):
+    within 1e-6 of the peak of the fp64-accumulated image (the class's own
+    fp32 taps already differ from fp64 at ~1e-7), w-plane ranges included."""
+    f64, f32 = _run(tmp_path, False, "0"), _run(tmp_path, False, "1")
+    for k in f64.files:
+        if k.startswith("planes"):
+            continue
+        peak = float(np.abs(f64[k]).max())
+        err = float(np.abs(f32[k] - f64[k]).max())
+        print(k, err / peak)
+        assert 0.0 < err < 1e-6 * peak, k
