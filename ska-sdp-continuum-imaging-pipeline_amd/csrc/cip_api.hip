@@ -1357,6 +1357,15 @@ static bool wstack_pair_b() {
   return e && e[0] == '1';
 }
 
+// CIP_WSTACK_GROUPB: the packed class's plane groups through one pass B each
+// (pass A of the group's planes into as many pass-A slots, then
+// fft_cols_wacc_kernel: one float-accumulator row read and write per group;
+// the same image bit for bit as the per-plane float accumulation)
+static bool wstack_group_b() {
+  const char* e = getenv("CIP_WSTACK_GROUPB");
+  return e && e[0] == '1';
+}
+
 // pass A of plane p into pass-A slot `slot` of the buffer (complex64 slots)
 static int plane_pass_a(const DirtyStage& st, const GridGeometry& g, double* grid, int slot, hipStream_t s,
                         const uint32_t* dmask, const uint32_t* rowbits) {
@@ -1665,11 +1674,34 @@ static int ms2dirty_impl(const double* uvw, int64_t nrow, const double* freq, in
     wacc = buf<float>(ws, "wacc_f32", npix_x * npix_y);
     if (!wacc) return CIP_ENOMEM;
   }
+  const bool group_b = wacc && wstack_group_b() && g.nv <= 8192 && npix_y <= g.nv / 2;
+  DirtyStage st_g = st;
+  if (group_b) {
+    st_g.fft_h = buf<double>(ws, "fft_pass_a_group", (int64_t)G * npix_x * g.nv);
+    if (!st_g.fft_h) return CIP_ENOMEM;
+  }
   for (int64_t q = p_lo / G; !scatter_ps && q * G < p_hi; ++q) {
     // pipelined calls: leave CU slots to the next call's planner (profiles/r03_ab_scatter_share.txt)
     rc = scatter_plane(pp, q, uvw, vis, vis_dtype, wgt, wgt_dtype, st.fast, grid, s, clean,
                        pipelined && share_cus_enabled());
     if (rc != CIP_OK) return rc;
+    if (group_b) {
+      const int64_t a = std::max(q * G, p_lo), b = std::min<int64_t>(q * G + G, p_hi);
+      hipEvent_t f0 = g_prof.mark(s);
+      for (int64_t p = a; p < b; ++p) {
+        double* plane_p = (double*)((char*)grid + (size_t)(p - q * G) * (size_t)plane_elems * cell_bytes);
+        const uint32_t* dm = dmask ? dmask + p * (g.ntx * g.nty / 32) : nullptr;
+        const uint32_t* rbp = rowbits0 ? rowbits0 + p * rb_stride : nullptr;
+        rc = plane_pass_a(st_g, g, plane_p, (int)(p - a), s, dm, rbp);
+        if (rc != CIP_OK) return rc;
+      }
+      CIP_HIP_CHECK(launch_fft_cols_wacc(st_g.fft_h, (int64_t)npix_x * g.nv * 8, (int)(b - a), a, g.nv, npix_x,
+                                         npix_y, st.tw_v, wacc, st.px, st.py, g.w0, g.dw, a == p_lo ? 1 : 0,
+                                         (dmask && fft_rowskip()) ? rowbits0 : nullptr, rb_stride, s));
+      g_prof.span(3, f0, g_prof.mark(s));
+      clean = dmask != nullptr;
+      continue;
+    }
     for (int64_t p = std::max(q * G, p_lo); p < std::min<int64_t>(q * G + G, p_hi); ++p) {
       double* plane_p = (double*)((char*)grid + (size_t)(p - q * G) * (size_t)plane_elems * cell_bytes);
       const uint32_t* dm = dmask ? dmask + p * (g.ntx * g.nty / 32) : nullptr;

@@ -147,15 +147,48 @@ __device__ __forceinline__ int in_pos(int t, int m, int r) {
   return t + m * T + r * (N / R);
 }
 
-// one padding double per 16: a thread's 16 consecutive outputs (first
-// exchange) then start 17 doubles apart, so 32 lanes cover all 64 banks
-__device__ __forceinline__ int pad(int p) { return p + (p >> 4); }
+// Exchange layout. CIP_FFT_XLDS=1 (round 5): fp32 transforms move whole
+// complex values (one ds_write_b64 / ds_read_b64 per element, one pass
+// instead of real then imaginary b32 halves), fp64 ones their two halves; both
+// at position p ^ ((p >> 4) & 15) (no padding). ds_read_b64 banks a wave's two
+// 32-lane groups by element mod 32, ds_write_b64 its four 16-lane groups by
+// element mod 16 (MI355X_MICROARCH.md, LDS): reads (32 consecutive, 32-aligned
+// positions) keep their 16-element blocks; the first exchange's writes
+// (positions 16 t + r) and the second's (256 (j >> 4) + 16 r + j % 16) land on
+// 16 distinct elements mod 16 per group. The padded layout (0: p + p / 16)
+// spans 34 elements for 32 consecutive reads, a 2-way conflict on every read,
+// and its b32 halves bank by dword mod 32: 40 % of the LDS cycles of the
+// refcall's fp32 transforms were conflict cycles (profiles/r05_sq_refcall.md).
+#ifndef CIP_FFT_XLDS
+#define CIP_FFT_XLDS 1
+#endif
+__device__ __forceinline__ int pad(int p) {
+  if constexpr (CIP_FFT_XLDS) return p ^ ((p >> 4) & 15);
+  return p + (p >> 4);
+}
+
+template <typename CT>
+using XT = std::conditional_t<CIP_FFT_XLDS && sizeof(CT) == 8, CT, typename Cx<CT>::R>;
+template <int N>
+constexpr int kXLen = CIP_FFT_XLDS ? N : N + N / 16;
 
 template <int N, int R, int R2, typename CT>
-__device__ __forceinline__ void exchange(CT* v, int t, int ns, typename Cx<CT>::R* lds) {
-  // real parts, then imaginary parts, through one N-double array
+__device__ __forceinline__ void exchange(CT* v, int t, int ns, XT<CT>* lds) {
+  if constexpr (!std::is_same<XT<CT>, typename Cx<CT>::R>::value) {
 #pragma unroll
-  for (int half = 0; half < 2; ++half) {
+    for (int m = 0; m < 16 / R; ++m)
+#pragma unroll
+      for (int r = 0; r < R; ++r) lds[pad(out_pos<N, R>(t, m, r, ns))] = v[m * R + r];
+    __syncthreads();
+#pragma unroll
+    for (int m = 0; m < 16 / R2; ++m)
+#pragma unroll
+      for (int r = 0; r < R2; ++r) v[m * R2 + r] = lds[pad(in_pos<N, R2>(t, m, r))];
+    __syncthreads();
+  } else {
+    // real parts, then imaginary parts, through one N-double array
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
 #pragma unroll
     for (int m = 0; m < 16 / R; ++m)
 #pragma unroll
@@ -170,6 +203,7 @@ __device__ __forceinline__ void exchange(CT* v, int t, int ns, typename Cx<CT>::
         else v[m * R2 + r].x = x;
       }
     __syncthreads();
+    }
   }
 }
 
@@ -219,7 +253,7 @@ struct FftShape {
 };
 
 template <int N, typename CT>
-__device__ __forceinline__ void fft_core(CT* v, int t, typename Cx<CT>::R* lds, const double2* __restrict__ tw) {
+__device__ __forceinline__ void fft_core(CT* v, int t, XT<CT>* lds, const double2* __restrict__ tw) {
   using S = FftShape<N>;
   int ns = 1;
   stockham_pass<N, 16>(v, t, ns, tw);
@@ -261,7 +295,7 @@ __global__ __launch_bounds__(N / 16, fft_waves_rows<CT>()) void fft_rows_kernel(
                                                           int64_t mrow0 = 0, int64_t mnv = 0,
                                                           const int64_t* __restrict__ row_slot = nullptr) {
   using S = FftShape<N>;
-  __shared__ typename Cx<CT>::R lds[N + N / 16];
+  __shared__ XT<CT> lds[kXLen<N>];
   const int t = threadIdx.x;
   // rows y .. y + kColBlock - 1 share their H lines (kColBlock-column rows of
   // 8 or 16 bytes): a group of 8 kColBlock consecutive workgroups (dispatched
@@ -373,7 +407,7 @@ __global__ __launch_bounds__(N / 16, fft_waves<CT>()) void fft_cols_kernel(const
                                                           const double2* __restrict__ tw, ColEpilogue ep,
                                                           int64_t i0 = 0, const uint32_t* __restrict__ rowbits = nullptr) {
   using S = FftShape<N>;
-  __shared__ typename Cx<CT>::R lds[N + N / 16];
+  __shared__ XT<CT> lds[kXLen<N>];
   const int t = threadIdx.x;
   const int64_t b = blockIdx.x;
   const int64_t nrows = gridDim.x;
@@ -481,7 +515,7 @@ __global__ __launch_bounds__(N / 16, fft_waves<CT>()) void fft_cols_wstack_kerne
     const uint32_t* __restrict__ rowbits, int64_t rb_stride) {
   using S = FftShape<N>;
   constexpr int NO = 16;  // outputs per thread (16 / RF blocks of RF)
-  __shared__ typename Cx<CT>::R lds[N + N / 16];
+  __shared__ XT<CT> lds[kXLen<N>];
   const int t = threadIdx.x;
   const int64_t b = blockIdx.x;
   const int64_t nrows = gridDim.x;
@@ -577,6 +611,114 @@ __global__ __launch_bounds__(N / 16, fft_waves<CT>()) void fft_cols_wstack_kerne
       const int64_t j = (int64_t)((k + (int)(ny / 2)) & (N - 1));
       if (j < ny) orow[j] = acc[m * S::RF + r];
     }
+}
+
+// Pass B of a packed-class w-stacking plane group into the float plane
+// accumulator (round 5): the nb planes' pass-A outputs (H + q hstride) one
+// after another in the same workgroup, each plane's screened contributions
+// added into an LDS copy of the image row, written once per group - one
+// read-modify-write of the accumulator row per group instead of one per
+// plane. The additions are the per-plane kernel's (acc = (float)(acc + val)
+// in plane order): the same image bit for bit. ny <= N / 2.
+template <int N, typename HT, typename CT>
+__global__ __launch_bounds__(N / 16, fft_waves<CT>()) void fft_cols_wacc_kernel(
+    const HT* __restrict__ H, int64_t hstride, int nb, int64_t pbase, int64_t nx, int64_t ny,
+    const double2* __restrict__ tw, float* __restrict__ out, double px, double py, double w0, double dw, int first,
+    const uint32_t* __restrict__ rowbits, int64_t rb_stride) {
+  using S = FftShape<N>;
+  __shared__ XT<CT> lds[kXLen<N>];
+  __shared__ float s_acc[N / 2];
+  const int t = threadIdx.x;
+  const int64_t b = blockIdx.x;
+  const int64_t nrows = gridDim.x;
+  int64_t il = b;
+  if (nrows % (8 * kColBlock) == 0)
+    il = (b / (8 * kColBlock)) * (8 * kColBlock) + (b % 8) * kColBlock + (b / 8) % kColBlock;
+  const int64_t p = il - nx / 2;
+  float* orow = out + il * ny;
+  for (int64_t jj = t; jj < ny; jj += S::T) s_acc[jj] = first ? 0.0f : orow[jj];
+  __syncthreads();
+  const HT* colb = H + ((il / kColBlock) * N) * kColBlock + (il % kColBlock);
+  for (int qp = 0; qp < nb; ++qp) {
+    const HT* col = colb + (int64_t)qp * hstride;
+    const uint32_t* rb = rowbits ? rowbits + (pbase + qp) * rb_stride : nullptr;
+    CT v[16];
+    HT raw[16];
+    if (rb) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int y = t + r * S::T;
+        const uint32_t word = rb[(r * S::T) >> 10];
+        raw[r] = HT{0, 0};
+        if ((word >> ((y >> 5) & 31)) & 1u) raw[r] = col[(int64_t)y * kColBlock];
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) raw[r] = col[(int64_t)(t + r * S::T) * kColBlock];
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      if constexpr (sizeof(HT) == 8) asm volatile("" : "+v"(raw[r].x), "+v"(raw[r].y));
+      v[r] = ccast<CT>(raw[r]);
+    }
+    fft_core<N>(v, t, lds, tw);
+    const double w_plane = w0 + (double)(pbase + qp) * dw;
+#pragma unroll
+    for (int m = 0; m < 16 / S::RF; ++m)
+#pragma unroll
+      for (int r = 0; r < S::RF; ++r) {
+        const int k = out_pos<N, S::RF>(t, m, r, N / S::RF);
+        const int64_t j = (int64_t)((k + (int)(ny / 2)) & (N - 1));
+        if (j < ny) {
+          const int64_t q = j - ny / 2;
+          const double sgn = ((p + q) & 1) ? -1.0 : 1.0;
+          const double2 g = ccast<double2>(v[m * S::RF + r]);
+          const double l = (double)p * px, mm = (double)q * py;
+          const double e = l * l + mm * mm;
+          const double nm1 = -e / (sqrt(1.0 - e) + 1.0);
+          const double ph = -2.0 * w_plane * nm1;
+          double sn, cs;
+          if constexpr (sizeof(CT) == 8 && CIP_SCREEN_F32 == 1) {
+            const float red = (float)(ph - 2.0 * rint(0.5 * ph));
+            float sf, cf;
+            sincospif(red, &sf, &cf);
+            sn = sf;
+            cs = cf;
+          } else {
+            sincospi(ph, &sn, &cs);
+          }
+          const double val = sgn * (g.x * cs - g.y * sn);
+          s_acc[j] = (float)((double)s_acc[j] + val);
+        }
+      }
+  }
+  __syncthreads();
+  for (int64_t jj = t; jj < ny; jj += S::T) orow[jj] = s_acc[jj];
+}
+
+hipError_t launch_fft_cols_wacc(const double* H, int64_t hstride_bytes, int nb, int64_t pbase, int64_t nv, int64_t nx,
+                                int64_t ny, const double* tw_v, float* out, double px, double py, double w0,
+                                double dw, int first, const uint32_t* rowbits, int64_t rb_stride, hipStream_t s) {
+  if (nb <= 0) return hipSuccess;
+  if (!fft_f32_enabled() || ny > nv / 2) return hipErrorInvalidValue;
+  const dim3 gd((unsigned)nx);
+  const double2* tw = (const double2*)tw_v;
+  const int64_t hs = hstride_bytes / (int64_t)sizeof(float2);
+#define COLSA(NN)                                                                                            \
+  case NN:                                                                                                   \
+    fft_cols_wacc_kernel<NN, float2, float2><<<gd, dim3(NN / 16), 0, s>>>(                                   \
+        (const float2*)H, hs, nb, pbase, nx, ny, tw, out, px, py, w0, dw, first, rowbits, rb_stride);        \
+    break;
+  switch (nv) {
+    COLSA(1024)
+    COLSA(2048)
+    COLSA(4096)
+    COLSA(8192)
+    default:
+      return hipErrorInvalidValue;
+  }
+#undef COLSA
+  return hipGetLastError();
 }
 
 hipError_t launch_fft_cols_wstack(const double* H, int64_t hstride_bytes, int nb, int64_t pbase, int64_t nv,

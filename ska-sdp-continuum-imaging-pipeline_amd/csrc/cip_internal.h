@@ -191,6 +191,12 @@ hipError_t launch_fft_cols(const double* H, int64_t nv, int64_t nx, int64_t ny, 
 // pass-A outputs at H + q hstride_bytes, summed per image row in plane order
 // and written once (first: overwrite, else added to out's values); rowbits:
 // plane p's tile-row words at rowbits + p rb_stride (NULL: dense)
+// packed-class plane group pass B into the float accumulator (cip_fft.hip):
+// nb planes' complex64 pass-A outputs hstride_bytes apart, one accumulator
+// row write per group (first: overwrite); nv <= 8192, ny <= nv / 2
+hipError_t launch_fft_cols_wacc(const double* H, int64_t hstride_bytes, int nb, int64_t pbase, int64_t nv, int64_t nx,
+                                int64_t ny, const double* tw_v, float* out, double px, double py, double w0,
+                                double dw, int first, const uint32_t* rowbits, int64_t rb_stride, hipStream_t s);
 hipError_t launch_fft_cols_wstack(const double* H, int64_t hstride_bytes, int nb, int64_t pbase, int64_t nv,
                                   int64_t nx, int64_t ny, const double* tw_v, double* out, double px, double py,
                                   double w0, double dw, int first, const uint32_t* rowbits, int64_t rb_stride,

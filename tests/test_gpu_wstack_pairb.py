@@ -5,6 +5,8 @@ contributions summed in registers and the image written once per pair, in the
 per-plane path's order of additions - the same image bit for bit, for odd and
 even plane counts and a w-plane range (cip_ms2dirty_wplanes). Each mode runs
 in a child process.
+CIP_WSTACK_GROUPB=1 does the same for a whole plane group into the float
+accumulator.
 """
 import os
 import subprocess
@@ -43,11 +45,11 @@ np.savez(out, **res)
 """
 
 
-def _run(tmp_path, on, wacc_f32="0"):
-    out = tmp_path / f"pairb{on}{wacc_f32}.npz"
+def _run(tmp_path, on, wacc_f32="0", group_b="0"):
+    out = tmp_path / f"pairb{on}{wacc_f32}{group_b}.npz"
     # both forms accumulate the planes in the fp64 image (the pair kernel's
     # form; the default packed-class path accumulates in float: CIP_WACC_F32)
-    env = dict(os.environ, CIP_WSTACK_PAIRB="1" if on else "0", CIP_WACC_F32=wacc_f32)
+    env = dict(os.environ, CIP_WSTACK_PAIRB="1" if on else "0", CIP_WACC_F32=wacc_f32, CIP_WSTACK_GROUPB=group_b)
     subprocess.run([sys.executable, "-c", CHILD, str(ROOT), str(out)], env=env, check=True, timeout=180)
     return np.load(out)
 
@@ -74,3 +76,19 @@ def test_float_plane_accumulator_within_the_class_precision(gpu_device, tmp_path
         err = float(np.abs(f32[k] - f64[k]).max())
         print(k, err / peak)
         assert 0.0 < err < 1e-6 * peak, k
+
+
+@pytest.mark.parametrize("group", ["3", "7"])
+def test_plane_group_pass_b_is_bit_identical(gpu_device, tmp_path, group):
+    """CIP_WSTACK_GROUPB=1 (cip_fft.hip fft_cols_wacc_kernel): a plane group's
+    planes through one pass B into an LDS copy of the float accumulator row -
+    the per-plane float accumulation bit for bit, whole stacks and w-plane
+    ranges that start and end inside a group."""
+    os.environ["CIP_WSTACK_GROUP"] = group
+    try:
+        per_plane = _run(tmp_path, False, "1", "0")
+        grouped = _run(tmp_path, False, "1", "1")
+    finally:
+        del os.environ["CIP_WSTACK_GROUP"]
+    for k in per_plane.files:
+        assert np.array_equal(per_plane[k], grouped[k]), k
