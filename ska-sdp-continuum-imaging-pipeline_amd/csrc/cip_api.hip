@@ -870,7 +870,7 @@ static int wstack_group(const GridGeometry& g, bool packed) {
   static const int env = [] {
     const char* e = getenv("CIP_WSTACK_GROUP");
     const int v = e ? atoi(e) : 0;
-    return v < 0 ? 0 : (v > 7 ? 7 : v);
+    return v < 0 ? 0 : (v == 14 ? 14 : (v > 7 ? 7 : v));
   }();
   if (!g.do_wstacking || g.support > 16 || g.nplanes < 2) return 1;
   const int64_t P = kTile + g.support - 1;
@@ -881,7 +881,9 @@ static int wstack_group(const GridGeometry& g, bool packed) {
     // visibility visits 1.6 groups instead of 2) scatter 7.15 -> 6.93 ms,
     // call 7.35 -> 7.51-7.54 Gvis/s (profiles/r05ah_ab_wstack_group.txt)
     int G = env ? env : 7;
-    while (G > 5 && G * P * P * 8 + 4200 > 81920) --G;
+    // 14 (experiment): one 512-thread block per CU holding a 14-plane group
+    if (G == 14 && G * P * P * 8 + 4200 > 163840) G = 7;
+    while (G > 5 && G <= 7 && G * P * P * 8 + 4200 > 81920) --G;
     while (G > 3 && G <= 5 && G * P * P * 8 + 4200 > 65536) --G;
     return G;
   }

@@ -811,6 +811,12 @@ inline hipError_t scatter_dispatch_ws(bool ws, int group, bool pack, unsigned ld
 #define LAUNCH_WS_PACKED(PRM)                                \
   {                                                          \
     bool hit = false;                                        \
+    if constexpr (kFitG14) {                                 \
+      if (ws && group == 14) {                               \
+        LAUNCH(true, PRM, true, 14);                         \
+        hit = true;                                          \
+      }                                                      \
+    }                                                        \
     if constexpr (kFitG7) {                                  \
       if (ws && group == 7) {                                \
         LAUNCH(true, PRM, true, 7);                          \
@@ -845,6 +851,8 @@ inline hipError_t scatter_dispatch_ws(bool ws, int group, bool pack, unsigned ld
   // 6 / 7 (CIP_WSTACK_GROUP, experiment): two blocks per CU in 160 KB
   constexpr bool kFitG7 = 7 * P2 * 8 + 4200 <= 81920;
   constexpr bool kFitG6 = 6 * P2 * 8 + 4200 <= 81920;
+  // 14 (CIP_WSTACK_GROUP=14, experiment): one block per CU in 160 KB (W <= 6)
+  constexpr bool kFitG14 = 14 * P2 * 8 + 4200 <= 163840;
   constexpr bool kFitG4 = 4 * P2 * 8 + 4200 <= 65536;
   bool done = false;
   const bool wide = m.delta != nullptr;  // ragged row slices: u64 entries
