@@ -704,8 +704,8 @@ def main():
                          "exchange + distributed FFT (DESIGN.md 7); with --wstacking: ONE C3 w-stacking image split "
                          "by w-plane groups + one image reduce (SURVEY 8(e) option 2); --config is ignored")
     ap.add_argument("--epsilon-call", action="store_true",
-                    help="with --strong --wstacking: epsilon = 1e-4 picks the support (the reference's call, W = 6) "
-                         "instead of --support")
+                    help="epsilon = 1e-4 picks the support (the reference's call, W = 6) instead of --support "
+                         "(with --wstacking --single: the reference's whole ms2dirty call as the main line)")
     ap.add_argument("--split", choices=("strips", "wplanes"), default="strips",
                     help="with --strong --wstacking: split the w-stacking image by uv strips (default; modelled "
                          "2.83x at 8 ranks on the C3 reference call against 2.49x for w-plane groups) or by "
@@ -786,6 +786,9 @@ def main():
     pending = [None, None]
     nstep = [0]
 
+    # --epsilon-call: epsilon = 1e-4 picks the support (invert.py:170-183)
+    sup_kw = {"epsilon": 1e-4} if args.epsilon_call else {"support": args.support}
+
     def step(sync=False):
         k = nstep[0] % 2
         nstep[0] += 1
@@ -796,7 +799,7 @@ def main():
         # the host prepares step k + 1 while the GPU finishes step k; the
         # inputs are resident and unchanged (CIP_PIPELINE), so step k + 1's
         # planner runs beside step k's scatter and FFT
-        invert(support=args.support, do_wstacking=args.wstacking, out=dirty, sum_weights=sumw,
+        invert(**sup_kw, do_wstacking=args.wstacking, out=dirty, sum_weights=sumw,
                single_precision_accumulation=args.single, normalise=world == 1, synchronize=sync,
                resident_inputs=not sync)
         # RCCL reduce of the partial images + weights to rank 0, normalised there
@@ -815,8 +818,9 @@ def main():
         step(sync=args.sync)
     drain()
     dirty, sumw = bufs[0]
-    _, params = invert(support=args.support, do_wstacking=args.wstacking, out=dirty, sum_weights=sumw,
+    _, params = invert(**sup_kw, do_wstacking=args.wstacking, out=dirty, sum_weights=sumw,
                        single_precision_accumulation=args.single)
+    args.support = params.support
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -909,9 +913,15 @@ def main():
     lds_bytes = vis_per_launch * params.support ** 2 * (8 if args.single else 16)  # packed: one u64 per tap
     lds_peak = 128.0 * 2.4e9 * 256 / 1e9  # GB/s: 128 B / CU-cycle, 256 CUs at 2.4 GHz
     lds_tap_peak = 64 * 8 / 8.12 * 2.4e9 * 256 / 1e9  # the tap pattern's rate (its conflicts included)
+    # the fastest rate any kernel here reaches: the conflict-free ("distinct"
+    # addresses) microbenchmark, 6.68 CU-cycles per wave-instruction
+    # (profiles/r05_lds_conflict_microbench.txt)
+    lds_measured_peak = 64 * 8 / 6.68 * 2.4e9 * 256 / 1e9
     lds_achieved = lds_bytes / (scatter_ms * 1e-3) / 1e9
     roofline["lds_atomic"] = {"achieved": round(lds_achieved, 1), "peak": round(lds_peak, 1), "unit": "GB/s",
                               "frac": round(lds_achieved / lds_peak, 4),
+                              "peak_measured": round(lds_measured_peak, 1),
+                              "frac_of_peak_measured": round(lds_achieved / lds_measured_peak, 4),
                               "frac_of_tap_pattern_rate": round(lds_achieved / lds_tap_peak, 4),
                               "basis": f"{8 if args.single else 16} B of ds_add_u64 per tap; peak = 4 LDS cycles per "
                                        "conflict-free wave-instr (128 B/CU-cycle); the scatter's own bank conflicts "

@@ -407,7 +407,7 @@ int cip_release_workspace(void);
  * stream around each phase; cip_profile_last fills
  *   ms[0..5]     = prep, plan, scatter, fft, correct, total  (milliseconds)
  *   counts[0..5] = visibilities, runs (row slices), chunks, planes, scatter launches,
- *                  time-pair row stride (0: the call gridded no time pairs)
+ *                  reserved (0)
  * of the most recent call. */
 #define CIP_PROFILE_PHASES 6
 #define CIP_PROFILE_COUNTS 6

@@ -184,7 +184,7 @@ static int64_t good_size(int64_t n) {
 static int support_for_epsilon(double eps) {
   // calibrated against the fp64 direct DFT (DESIGN.md "Accuracy")
   // max |err| / sum(w) vs the direct DFT measured 2e-3, 2e-5, 3e-7, 4e-9,
-  // 5e-11, 6e-13, 2e-14 for W = 4 .. 16 (tests/test_oracle.py)
+  // 5e-11, 6e-13, 2e-14 for W = 4 .. 16 (tests/test_oracle_accuracy.py)
   if (eps >= 2e-3) return 4;
   if (eps >= 2e-5) return 6;
   if (eps >= 3e-7) return 8;
@@ -292,8 +292,6 @@ struct PlanResult {
   Chunk* chunks = nullptr;
   void* perm = nullptr;  // bank-class ordered visibility stream (perm_encode entries), or NULL
   uint32_t* dmask = nullptr;  // grid tiles the scatter writes, per plane (bit-packed, ntx / 32 words per tile row)
-  const int64_t* pair_d = nullptr;  // time pairs: the dump stride the plan's pair flags were made with, or NULL
-  int64_t pair_stride = 0;          // its value (read back with the run count)
 };
 
 struct Workspace {
@@ -322,18 +320,10 @@ struct Workspace {
   // plan_stream beside call k's scatter and FFT; it only waits for
   // call k - 1's work on the caller's stream (ev_done[parity]: its scatter
   // read the plan, its FFT the masks and weight sum); the caller's stream
-  // waits for the plan (ev_planned).
-  // Two plan streams (one per parity): a 2-D pipelined call's scatter runs on
-  // its plan stream after its planner (scatter_on_plan_stream), so call k's
-  // pass B on s overlaps call k + 1's scatter while call k + 1's planner
-  // overlaps call k's scatter on the other plan stream.
+  // waits for the plan (ev_planned). One plan stream per parity.
   hipStream_t plan_stream = nullptr, plan_stream1 = nullptr;
   hipEvent_t ev_done[2] = {nullptr, nullptr}, ev_planned = nullptr, ev_entry = nullptr;
-  // the grid consumed (its pass A done) by the last call, if that call was a
-  // plan-stream-scatter call (grid_seq == its call_seq): the next such call's
-  // scatter waits for ev_grid only, not for the pass B queued after it on s
-  hipEvent_t ev_grid = nullptr, ev_scattered = nullptr, ev_gate = nullptr;
-  uint64_t call_seq = 0, grid_seq = ~0ull;
+  uint64_t call_seq = 0;
   int parity = 0;
   bool parity_scope = false;
   // a planner ran on a caller's stream (parity-0 buffer names) since the last
@@ -423,8 +413,6 @@ static void destroy_workspace(Workspace* ws) {
       (void)hipStreamDestroy(ps);
     }
   for (hipEvent_t e : ws->ev_done)
-    if (e) (void)hipEventDestroy(e);
-  for (hipEvent_t e : {ws->ev_grid, ws->ev_scattered, ws->ev_gate})
     if (e) (void)hipEventDestroy(e);
   if (ws->ev_planned) (void)hipEventDestroy(ws->ev_planned);
   if (ws->ev_entry) (void)hipEventDestroy(ws->ev_entry);
@@ -549,21 +537,14 @@ static int fft_twiddles(Workspace* ws, int64_t n, hipStream_t s, double** out) {
 
 // ------------------------------------------------------------- planner ----
 // Visibilities per scatter work unit: <= kChunkVis (64-bit fixed point) or
-// kChunkVisPacked (packed class, complex64 input); CIP_CHUNK_VIS lowers it for
-// tuning.
+// kChunkVisPacked (packed class, complex64 input); multiples of kOrderWindow,
+// so 2-D ordering windows never straddle chunks (w-stacking units: see
+// kOrderWindow in cip_common.h).
 static int64_t chunk_vis(bool packed, int64_t nu) {
-  static int64_t env = -2;
-  if (env == -2) {
-    const char* e = getenv("CIP_CHUNK_VIS");
-    env = e ? atoll(e) : -1;
-  }
   // grids of 16384+ cells per axis (C4): half-size work units - shorter slices
   // on finer cells, the scatter's tail matters more (interleaved A/B at C4:
   // scatter 4.76 vs 4.89 ms, profiles/r02_ab_c4.txt)
-  const int64_t cap = packed ? kChunkVisPacked : (nu >= 16384 ? kChunkVis / 2 : kChunkVis);
-  // a multiple of kOrderWindow, so 2-D ordering windows never straddle chunks
-  // (w-stacking units: see kOrderWindow in cip_common.h)
-  return (env >= kOrderWindow && env < cap) ? env / kOrderWindow * kOrderWindow : cap;
+  return packed ? kChunkVisPacked : (nu >= 16384 ? kChunkVis / 2 : kChunkVis);
 }
 
 
@@ -576,34 +557,6 @@ static bool fft_pruned() {
   return on;
 }
 
-// CIP_OVERLAP_ZERO=0 zeroes the first grid plane in stream order instead of on
-// the side stream beside the planner (A/B experiments)
-static bool overlap_zero() {
-  static const bool on = [] {
-    const char* e = getenv("CIP_OVERLAP_ZERO");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
-
-// How the order pass gets each visibility's bank class: default "gather" -
-// the place pass's per-visibility class bytes, gathered in tile order (~1 HBM
-// line per row slice, 1.24 GB at C3); CIP_ORDER_CLASS=runs recomputes them in
-// fp32 from the run's row (u, v), carried through the radix sort beside the
-// run record, and f / c (no class bytes, no gather - but 8 more bytes per run
-// in both radix passes: planner 1.82 vs 1.47 ms at C3, interleaved A/B,
-// profiles/r04_ab_order_place.txt); =compute recomputes from a uvw gather.
-enum { ORDER_RUNS = 0, ORDER_GATHER = 1, ORDER_UVW = 2 };
-static int order_class_mode() {
-  static const int mode = [] {
-    const char* e = getenv("CIP_ORDER_CLASS");
-    if (e && std::strcmp(e, "runs") == 0) return (int)ORDER_RUNS;
-    if (e && std::strcmp(e, "compute") == 0) return (int)ORDER_UVW;
-    return (int)ORDER_GATHER;
-  }();
-  return mode;
-}
-
 // CIP_GRID_MASK=0: no dirty-tile mask - the grid is zeroed in full before
 // every scatter and pass A reads all of it (A/B experiments)
 static bool grid_mask() {
@@ -612,26 +565,6 @@ static bool grid_mask() {
     return !(e && e[0] == '0');
   }();
   return on;
-}
-
-// CIP_CHUNK_ORDER=tile: 2-D work units in tile order instead of full chunks
-// first (A/B experiments)
-static bool chunks_full_first() {
-  static const bool on = [] {
-    const char* e = getenv("CIP_CHUNK_ORDER");
-    return !(e && std::strcmp(e, "tile") == 0);
-  }();
-  return on;
-}
-
-// CIP_PAIRS=1 enables the time pairs of the 2-D fp64 class (opt-in, read per
-// call). Measured at C3 (profiles/r05_pairs.md): the scatter 2.90 -> 2.58 ms,
-// but the planner 1.59 -> 1.91 ms (the partner placement in the place pass,
-// the two-group order pass), so the pipelined step is 4.62 -> 4.79 ms - off by
-// default.
-static bool pairs_enabled() {
-  const char* e = getenv("CIP_PAIRS");
-  return e && e[0] == '1';
 }
 
 // CIP_SCATTER_ORDER=0 skips the bank-class order (A/B experiments)
@@ -659,20 +592,8 @@ static bool ragged_pack() {
 }
 
 // sub-blocks per radix workgroup: pass 0 (place blocks of ~500 runs) and the
-// dense passes (4096 runs); CIP_RADIX_G0 / CIP_RADIX_G1 override (A/B)
-static int radix_group(int pass) {
-  static const int g[2] = {[] {
-                             const char* e = getenv("CIP_RADIX_G0");
-                             const int v = e ? atoi(e) : 0;
-                             return v > 0 ? v : 8;
-                           }(),
-                           [] {
-                             const char* e = getenv("CIP_RADIX_G1");
-                             const int v = e ? atoi(e) : 0;
-                             return v > 0 ? v : 1;
-                           }()};
-  return g[pass ? 1 : 0];
-}
+// dense passes (4096 runs)
+static int radix_group(int pass) { return pass ? 1 : 8; }
 
 // Also reduces {sum w, max |w V|} into red (device) and returns max |w V| in
 // *maxabs (the place pass reads the visibilities anyway).
@@ -696,18 +617,13 @@ static int make_plan(Workspace* ws, const double* uvw, const double* fx, const R
   const bool ragged = m.delta != nullptr;
   const bool order = scatter_order() && (ragged || nvis < ((int64_t)1 << 32));
   uint8_t* vis_class = nullptr;
-  uint64_t* park_uv = nullptr;
-  if (order && order_class_mode() == ORDER_GATHER) {
+  if (order) {
     vis_class = buf<uint8_t>(ws, "vis_class", nvis);
     if (!vis_class) return CIP_ENOMEM;
   }
   CIP_ALLOC(blk_cnt, int64_t, "blk_cnt", nblk)
   CIP_ALLOC(park_key, uint32_t, "park_key", (int64_t)nblk * 4096)
   CIP_ALLOC(park_run, uint64_t, "park_run", (int64_t)nblk * 4096)
-  if (order && order_class_mode() == ORDER_RUNS) {
-    park_uv = buf<uint64_t>(ws, "park_uv", (int64_t)nblk * 4096);
-    if (!park_uv) return CIP_ENOMEM;
-  }
   CIP_ALLOC(partial, double, "prep_partial", 2 * nblk)
   // the place pass also writes radix pass 0's histogram per place block; summed
   // per radix group of g0 blocks, its scan's last entry = runs
@@ -724,7 +640,7 @@ static int make_plan(Workspace* ws, const double* uvw, const double* fx, const R
   RowMap mp = m;
   mp.pk_runs = (ragged && m.pk_cbits && order && g.support <= 16 && 8 * npass <= kRunLenShift && packed_runs()) ? 1 : 0;
   CIP_HIP_CHECK(launch_plan_place(uvw, fx, mp, vis, vis_dtype, wgt, wgt_dtype, g, err, vis_class, blk_cnt, park_key,
-                                  park_run, partial, hist0, s, park_uv));
+                                  park_run, partial, hist0, s));
   CIP_HIP_CHECK(launch_prep_final(partial, nblk, red, s));
   CIP_HIP_CHECK(launch_radix_group_hist(hist0, nblk, g0, hist0g, s));
   CIP_HIP_CHECK(exclusive_scan_i64(hist0g, 256 * ng0 + 1, scan_h0, s));
@@ -733,11 +649,8 @@ static int make_plan(Workspace* ws, const double* uvw, const double* fx, const R
   CIP_HIP_CHECK(hipMemcpyAsync(&h[0], hist0g + 256 * ng0, sizeof(int64_t), hipMemcpyDeviceToHost, s));
   CIP_HIP_CHECK(hipMemcpyAsync(&h[1], err, sizeof(unsigned), hipMemcpyDeviceToHost, s));
   CIP_HIP_CHECK(hipMemcpyAsync(&h[2], red + 1, sizeof(double), hipMemcpyDeviceToHost, s));
-  h[3] = 0;
-  if (m.pair_d) CIP_HIP_CHECK(hipMemcpyAsync(&h[3], m.pair_d, sizeof(int64_t), hipMemcpyDeviceToHost, s));
   CIP_HIP_CHECK(hipStreamSynchronize(s));
   const int64_t nruns = h[0];
-  pr->pair_stride = h[3];
   const unsigned errbits = (unsigned)h[1];
   std::memcpy(maxabs, &h[2], sizeof(double));
   if (errbits & 4u) return set_error(CIP_EINVAL, "channel frequencies must be positive");
@@ -750,28 +663,19 @@ static int make_plan(Workspace* ws, const double* uvw, const double* fx, const R
   CIP_ALLOC(key_b, uint32_t, "sort_key_b", nruns)
   CIP_ALLOC(run_a, uint64_t, "sort_run_a", nruns)
   CIP_ALLOC(run_b, uint64_t, "sort_run_b", nruns)
-  uint64_t *uv_a = nullptr, *uv_b = nullptr;
-  if (park_uv) {
-    uv_a = buf<uint64_t>(ws, "sort_uv_a", nruns);
-    uv_b = buf<uint64_t>(ws, "sort_uv_b", nruns);
-    if (!uv_a || !uv_b) return CIP_ENOMEM;
-  }
   const int64_t nbd = radix_blocks(nruns);
   const int64_t ng1 = (nbd + g1 - 1) / g1;
   CIP_ALLOC(hist, int64_t, "radix_hist", 256 * ng1 + 1)
   CIP_ALLOC(scan_h, int64_t, "scan_hist", scan_tmp_elems(256 * ng1 + 1))
-  CIP_HIP_CHECK(launch_radix_scatter(park_key, park_run, 0, blk_cnt, nblk, g0, 0, hist0g, key_a, run_a, s, park_uv,
-                                     uv_a));
+  CIP_HIP_CHECK(launch_radix_scatter(park_key, park_run, 0, blk_cnt, nblk, g0, 0, hist0g, key_a, run_a, s));
   uint32_t *kin = key_a, *kout = key_b;
   uint64_t *rin = run_a, *rout = run_b;
-  uint64_t *uin = uv_a, *uout = uv_b;
   for (int p = 1; p < npass; ++p) {
     CIP_HIP_CHECK(launch_radix_hist(kin, nruns, nullptr, nbd, g1, 8 * p, hist, s));
     CIP_HIP_CHECK(exclusive_scan_i64(hist, 256 * ng1 + 1, scan_h, s));
-    CIP_HIP_CHECK(launch_radix_scatter(kin, rin, nruns, nullptr, nbd, g1, 8 * p, hist, kout, rout, s, uin, uout));
+    CIP_HIP_CHECK(launch_radix_scatter(kin, rin, nruns, nullptr, nbd, g1, 8 * p, hist, kout, rout, s));
     std::swap(kin, kout);
     std::swap(rin, rout);
-    std::swap(uin, uout);
   }
   uint64_t* runs = rin;
   CIP_HIP_CHECK(launch_tile_offsets(kin, nruns, ntiles, tile_runs, s, mp.pk_runs ? kRunKeyMask : 0xffffffffu));
@@ -797,7 +701,7 @@ static int make_plan(Workspace* ws, const double* uvw, const double* fx, const R
   pr->group = per_plane ? group : 1;
   const int64_t ngroups = per_plane ? (g.nplanes + group - 1) / group : 1;
   const int64_t nrange = ngroups;  // chunk ranges: per plane group, or the one 2-D layer
-  const int full_first = (!per_plane && chunks_full_first()) ? 1 : 0;
+  const int full_first = per_plane ? 0 : 1;
   CIP_ALLOC(layer_off, int64_t, "layer_off", nrange + 1)
   int64_t* pc_off = nullptr;
   if (per_plane) {
@@ -836,7 +740,6 @@ static int make_plan(Workspace* ws, const double* uvw, const double* fx, const R
   else
     CIP_HIP_CHECK(launch_chunk_emit(tile_vis_off, tile_vis, chunk_off, run_goff, tile_runs, ntiles, cv, full_first,
                                     pr->nchunks, chunks, s));
-  pr->pair_d = m.pair_d;
   pr->runs = runs;
   pr->run_goff = run_goff;
   pr->tile_run_off = tile_runs;
@@ -846,7 +749,7 @@ static int make_plan(Workspace* ws, const double* uvw, const double* fx, const R
     CIP_HIP_CHECK(launch_chunk_emit(tile_vis_off, tile_vis, win_off, run_goff, tile_runs, ntiles, kOrderWindow, 0, nwin,
                                     windows, s));
     CIP_ALLOC(perm, uint32_t, "perm", ragged ? 2 * nvis : nvis)
-    CIP_HIP_CHECK(launch_order(uvw, fx, vis_class, g, mp, runs, run_goff, tile_runs, windows, nwin, perm, s, uin));
+    CIP_HIP_CHECK(launch_order(vis_class, mp, runs, run_goff, windows, nwin, perm, s));
     pr->perm = perm;
   }
   return CIP_OK;
@@ -863,14 +766,16 @@ static bool wgt_dtype_ok(int d) { return d == CIP_NONE || d == CIP_F32 || d == C
 // placed and its u, v, w kernels evaluated once for three planes; the unit
 // holds G sub-grids in 512-thread blocks), fewer where two such blocks would
 // not fit a CU's LDS (W >= 10: 2); the packed class's 8-byte cells allow up to
-// 5 (round 4); CIP_WSTACK_GROUP=1..5 caps it (A/B); the large supports always
-// 1. Refcall C3 (round 3, fp64 taps): G = 1 / 2 / 3 -> 13.4 / 12.2 / 11.8 ms
-// of scatter (profiles/r03_ab_wstack_group*.txt).
+// 7 (round 5); CIP_WSTACK_GROUP=1..7 caps it (tests compare the groups with
+// G = 1); the large supports always 1. Refcall C3 (round 3, fp64 taps): G = 1
+// / 2 / 3 -> 13.4 / 12.2 / 11.8 ms of scatter (profiles/r03_ab_wstack_group*.txt).
+// One 14-plane group per CU (W = 6) measured slower: 6.94 -> 8.34 ms
+// (profiles/r05at_ab_wstack_g14.txt).
 static int wstack_group(const GridGeometry& g, bool packed) {
   static const int env = [] {
     const char* e = getenv("CIP_WSTACK_GROUP");
     const int v = e ? atoi(e) : 0;
-    return v < 0 ? 0 : (v == 14 ? 14 : (v > 7 ? 7 : v));
+    return v < 0 ? 0 : (v > 7 ? 7 : v);
   }();
   if (!g.do_wstacking || g.support > 16 || g.nplanes < 2) return 1;
   const int64_t P = kTile + g.support - 1;
@@ -881,8 +786,6 @@ static int wstack_group(const GridGeometry& g, bool packed) {
     // visibility visits 1.6 groups instead of 2) scatter 7.15 -> 6.93 ms,
     // call 7.35 -> 7.51-7.54 Gvis/s (profiles/r05ah_ab_wstack_group.txt)
     int G = env ? env : 7;
-    // 14 (experiment): one 512-thread block per CU holding a 14-plane group
-    if (G == 14 && G * P * P * 8 + 4200 > 163840) G = 7;
     while (G > 5 && G <= 7 && G * P * P * 8 + 4200 > 81920) --G;
     while (G > 3 && G <= 5 && G * P * P * 8 + 4200 > 65536) --G;
     return G;
@@ -1085,23 +988,6 @@ static int prepare(Workspace* ws, const double* uvw, int64_t nrow, const double*
     out->plan.plane_chunk_off.assign((out->g.do_wstacking ? out->g.nplanes : 1) + 1, 0);  // group 1
     return CIP_OK;
   }
-  // time pairs: 2-D fp64 class on dense complex rows through
-  // the gathered bank-class order; the dump stride is detected on the device
-  // (no host round trip), and a plan reused later keeps the stride it was
-  // made with
-  m.pair_d = nullptr;
-  const bool pairable = pairs_enabled() && !ragged && !packed && !out->g.do_wstacking && out->g.support <= 16 &&
-                        (vis_dtype == CIP_C64 || vis_dtype == CIP_C128) && nrow >= 2 &&
-                        m.nvis < ((int64_t)1 << 31) && scatter_order() && order_class_mode() == ORDER_GATHER &&
-                        (want_group ? wstack_group(out->g, packed) : 1) == 1;
-  if (reusing) {
-    m.pair_d = ws->saved_plan.pair_d;
-  } else if (pairable) {
-    int64_t* pd = buf<int64_t>(ws, "pair_d", 1);
-    if (!pd) return CIP_ENOMEM;
-    CIP_HIP_CHECK(launch_pair_stride(uvw, nrow, pd, s));
-    m.pair_d = pd;
-  }
   int rc;
   if (reusing) {
     // the plan's buffers are read-only here; only the weight reduction runs
@@ -1143,7 +1029,6 @@ static int prepare(Workspace* ws, const double* uvw, int64_t nrow, const double*
   g_prof.counts[1] = out->plan.nruns;
   g_prof.counts[2] = out->plan.nchunks;
   g_prof.counts[3] = out->g.nplanes;
-  g_prof.counts[5] = out->plan.pair_d ? out->plan.pair_stride : 0;
   return rc;
 }
 
@@ -1243,31 +1128,12 @@ static bool grid_f32_enabled() {
   return on;
 }
 
-// CIP_PIPE_SCATTER=1: a pipelined 2-D call's scatter runs on the plan stream
-// (after its planner and the previous call's pass A), so the previous call's
-// pass B overlaps it. Off by default: measured 21.11 vs 21.36 Gvis/s at C3
-// (profiles/r05t_ab_pipe_scatter.txt) - the co-running planner, starved of
-// wave slots beside the scatter, is the pipelined step's critical path either way.
-static bool scatter_on_plan_stream() {
-  const char* e = getenv("CIP_PIPE_SCATTER");  // read per call (tests switch it)
-  return e && e[0] == '1';
-}
-
 // CIP_WACC_F32=0: the packed class's w planes accumulate in the fp64 image
 // (A/B); default: a float accumulator
 static bool wacc_f32_enabled() {
   static const bool on = [] {
     const char* e = getenv("CIP_WACC_F32");
     return !(e && e[0] == '0');
-  }();
-  return on;
-}
-
-// CIP_SCATTER_SHARE=0: pipelined calls' scatters take every CU slot (A/B)
-static bool share_cus_enabled() {
-  static const bool on = [] {
-    const char* e = getenv("CIP_SCATTER_SHARE");
-    return !(e && std::strcmp(e, "0") == 0);
   }();
   return on;
 }
@@ -1312,11 +1178,10 @@ static bool fft_rowskip() {
 }
 
 // rowbits (with dmask): the plane's tile-row bits (row_bits_kernel)
-// after_rows (may be NULL): recorded on s once pass A has consumed the grid
+// acc_f32: dirty_out is the packed class's float plane accumulator
 static int plane_to_dirty(const DirtyStage& st, const GridGeometry& g, int64_t p, double* grid, double* dirty_out,
                           hipStream_t s, const uint32_t* dmask = nullptr, const double* norm = nullptr,
-                          const uint32_t* rowbits = nullptr, int first = -1, hipEvent_t after_rows = nullptr,
-                          bool acc_f32 = false) {
+                          const uint32_t* rowbits = nullptr, int first = -1, bool acc_f32 = false) {
   if (first < 0) first = p == 0;  // the first plane overwrites the image, later ones add
   hipEvent_t f0 = g_prof.mark(s);
   if (st.fast) {
@@ -1327,7 +1192,6 @@ static int plane_to_dirty(const DirtyStage& st, const GridGeometry& g, int64_t p
              HIPFFT_SUCCESS) {
     return set_error(CIP_EHIP, "hipfftExecZ2Z failed");
   }
-  if (after_rows) CIP_HIP_CHECK(hipEventRecord(after_rows, s));
   const double w_plane = g.w0 + (double)p * g.dw;
   // pass B carries the crop epilogue: it is booked under "fft"
   if (st.fast)
@@ -1344,36 +1208,6 @@ static int plane_to_dirty(const DirtyStage& st, const GridGeometry& g, int64_t p
     CIP_HIP_CHECK(launch_crop_correct_2d(grid, g, st.npix_x, st.npix_y, st.cx, st.cy, dirty_out, s));
   }
   g_prof.span(4, f1, g_prof.mark(s));
-  return CIP_OK;
-}
-
-// CIP_WSTACK_PAIRB=1: w-stacking pass B over plane pairs (the packed class's
-// complex64 pass-A outputs of two planes side by side in the pass-A buffer,
-// one image read-modify-write per pair; the same image bit for bit). Off by
-// default: measured on the C3 reference call FFT 5.33 vs 4.91 ms
-// (profiles/r05_ab_wstack_pairb.txt) - the pair kernel needs ~250 VGPRs, one
-// 512-thread block per CU instead of two, and the lost occupancy costs more
-// than the 134 MB image read-modify-write it saves per pair.
-static bool wstack_pair_b() {
-  const char* e = getenv("CIP_WSTACK_PAIRB");
-  return e && e[0] == '1';
-}
-
-// CIP_WSTACK_GROUPB: the packed class's plane groups through one pass B each
-// (pass A of the group's planes into as many pass-A slots, then
-// fft_cols_wacc_kernel: one float-accumulator row read and write per group;
-// the same image bit for bit as the per-plane float accumulation)
-static bool wstack_group_b() {
-  const char* e = getenv("CIP_WSTACK_GROUPB");
-  return e && e[0] == '1';
-}
-
-// pass A of plane p into pass-A slot `slot` of the buffer (complex64 slots)
-static int plane_pass_a(const DirtyStage& st, const GridGeometry& g, double* grid, int slot, hipStream_t s,
-                        const uint32_t* dmask, const uint32_t* rowbits) {
-  if (!fft_rowskip()) rowbits = nullptr;
-  double* h = st.fft_h + (size_t)slot * (size_t)st.npix_x * (size_t)g.nv;  // npix_x nv complex64 = as many doubles
-  CIP_HIP_CHECK(launch_fft_rows(grid, g.nu, g.nv, st.npix_x, st.tw_u, h, dmask, g.ntx, rowbits != nullptr, s, true));
   return CIP_OK;
 }
 
@@ -1536,18 +1370,13 @@ static int ms2dirty_impl(const double* uvw, int64_t nrow, const double* freq, in
       // the plan streams at the lowest priority: the scatter on s keeps first
       // call on freed wave slots (C3 pipelined 21.58-21.62 vs 21.46-21.53
       // Gvis/s at the default priority, 21.15-21.24 at the highest,
-      // profiles/r05v_ab_plan_priority.txt); CIP_PLAN_PRIORITY=default / high (A/B)
+      // profiles/r05v_ab_plan_priority.txt)
       int prio_lo = 0, prio_hi = 0;
       CIP_HIP_CHECK(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
-      const char* pe = getenv("CIP_PLAN_PRIORITY");
-      const int prio = (pe && std::strcmp(pe, "high") == 0) ? prio_hi : (pe && std::strcmp(pe, "default") == 0) ? 0 : prio_lo;
-      CIP_HIP_CHECK(hipStreamCreateWithPriority(&ws->plan_stream, hipStreamNonBlocking, prio));
-      CIP_HIP_CHECK(hipStreamCreateWithPriority(&ws->plan_stream1, hipStreamNonBlocking, prio));
+      CIP_HIP_CHECK(hipStreamCreateWithPriority(&ws->plan_stream, hipStreamNonBlocking, prio_lo));
+      CIP_HIP_CHECK(hipStreamCreateWithPriority(&ws->plan_stream1, hipStreamNonBlocking, prio_lo));
       CIP_HIP_CHECK(hipEventCreateWithFlags(&ws->ev_planned, hipEventDisableTiming));
       CIP_HIP_CHECK(hipEventCreateWithFlags(&ws->ev_entry, hipEventDisableTiming));
-      CIP_HIP_CHECK(hipEventCreateWithFlags(&ws->ev_grid, hipEventDisableTiming));
-      CIP_HIP_CHECK(hipEventCreateWithFlags(&ws->ev_scattered, hipEventDisableTiming));
-      CIP_HIP_CHECK(hipEventCreateWithFlags(&ws->ev_gate, hipEventDisableTiming));
       for (hipEvent_t& e : ws->ev_done) {
         CIP_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         // the first pipelined calls: the planner starts after the work already on s
@@ -1585,12 +1414,11 @@ static int ms2dirty_impl(const double* uvw, int64_t nrow, const double* freq, in
   ws->parity_scope = pipelined;
   int rc = prepare(ws, uvw, nrow, freq, nchan, vis, vis_dtype, wgt, wgt_dtype, npix_x, npix_y, pixsize_x, pixsize_y,
                    epsilon, support, do_wstacking, packed, nullptr, ps, &pp,
-                   (overlap_zero() && !pipelined) ? &grid : nullptr, nullptr, (flags & CIP_REUSE_PLAN) != 0, flags4,
+                   pipelined ? nullptr : &grid, nullptr, (flags & CIP_REUSE_PLAN) != 0, flags4,
                    true, plane_begin, plane_end);
   ws->parity_scope = false;
   // s continues once the plan exists (also after a failed one, or any early
-  // return: nothing then runs on it); a plan-stream scatter joins s after the
-  // scatter instead
+  // return: nothing then runs on it)
   struct PlanJoin {
     Workspace* ws;
     hipStream_t ps, s;
@@ -1636,96 +1464,28 @@ static int ms2dirty_impl(const double* uvw, int64_t nrow, const double* freq, in
   // unless cip_ms2dirty_wplanes); an empty range leaves a zero image
   const int64_t p_lo = g.plane_lo, p_hi = g.plane_hi;
   if (p_lo >= p_hi) CIP_HIP_CHECK(hipMemsetAsync(dirty_out, 0, sizeof(double) * npix_x * npix_y, s));
-  // plane pairs through pass B (CIP_WSTACK_PAIRB, packed class): the pass-A
-  // output of an odd plane waits in slot 0 for its partner
-  const bool pair_b = st.fast && g.do_wstacking && g.grid_f32 && wstack_pair_b() && g.nv <= 8192;
-  int64_t pending = -1;  // plane whose pass A sits in slot 0
   const int64_t rb_stride = (g.nty + 31) / 32;
   const uint32_t* rowbits0 = dmask ? dmask + g.nplanes * (g.ntx * g.nty / 32) : nullptr;
-  // pipelined 2-D calls: the scatter on the plan stream after the planner and
-  // after the grid is free (the previous call's pass A), s joins it before
-  // pass A, and this call's pass B then overlaps the next call's scatter
-  const bool scatter_ps = pipelined && st.fast && !g.do_wstacking && G == 1 && p_hi - p_lo == 1 && !pair_b &&
-                          scatter_on_plan_stream();
-  if (scatter_ps) {
-    if (ws->grid_seq != ~0ull && ws->grid_seq + 1 == ws->call_seq) {
-      CIP_HIP_CHECK(hipStreamWaitEvent(ps, ws->ev_grid, 0));
-    } else {  // another call used the workspace since: everything queued on s
-      CIP_HIP_CHECK(hipEventRecord(ws->ev_gate, s));
-      CIP_HIP_CHECK(hipStreamWaitEvent(ps, ws->ev_gate, 0));
-    }
-    plan_join.joined = true;  // s joins after the scatter
-    rc = scatter_plane(pp, p_lo, uvw, vis, vis_dtype, wgt, wgt_dtype, st.fast, grid, ps, clean, share_cus_enabled());
-    CIP_HIP_CHECK(hipEventRecord(ws->ev_scattered, ps));
-    CIP_HIP_CHECK(hipStreamWaitEvent(s, ws->ev_scattered, 0));
-    if (rc != CIP_OK) return rc;
-    const uint32_t* dm = dmask ? dmask + p_lo * (g.ntx * g.nty / 32) : nullptr;
-    const uint32_t* rbp = rowbits0 ? rowbits0 + p_lo * rb_stride : nullptr;
-    rc = plane_to_dirty(st, g, p_lo, grid, dirty_out, s, dm, normalise ? pp.red : nullptr, rbp, 1, ws->ev_grid);
-    if (rc != CIP_OK) return rc;
-    ws->grid_seq = ws->call_seq;
-    clean = dmask != nullptr;
-  } else if (const int jr = plan_join.join(); jr != CIP_OK) {
-    return jr;
-  }
+  if (const int jr = plan_join.join(); jr != CIP_OK) return jr;
   // the packed class's w planes accumulate in a float image (its own
   // precision, one rounding per plane; the final correction writes the fp64
-  // image): half the per-plane read-modify-write of pass B
+  // image): half the per-plane read-modify-write of pass B. Only beside fp32
+  // transforms of complex64 planes (launch_fft_cols refuses any other pairing).
   float* wacc = nullptr;
-  if (st.fast && g.do_wstacking && g.grid_f32 && !pair_b && p_lo < p_hi && wacc_f32_enabled()) {
+  if (st.fast && g.do_wstacking && g.grid_f32 && fft_f32_enabled() && p_lo < p_hi && wacc_f32_enabled()) {
     wacc = buf<float>(ws, "wacc_f32", npix_x * npix_y);
     if (!wacc) return CIP_ENOMEM;
   }
-  const bool group_b = wacc && wstack_group_b() && g.nv <= 8192 && npix_y <= g.nv / 2;
-  DirtyStage st_g = st;
-  if (group_b) {
-    st_g.fft_h = buf<double>(ws, "fft_pass_a_group", (int64_t)G * npix_x * g.nv);
-    if (!st_g.fft_h) return CIP_ENOMEM;
-  }
-  for (int64_t q = p_lo / G; !scatter_ps && q * G < p_hi; ++q) {
+  for (int64_t q = p_lo / G; q * G < p_hi; ++q) {
     // pipelined calls: leave CU slots to the next call's planner (profiles/r03_ab_scatter_share.txt)
-    rc = scatter_plane(pp, q, uvw, vis, vis_dtype, wgt, wgt_dtype, st.fast, grid, s, clean,
-                       pipelined && share_cus_enabled());
+    rc = scatter_plane(pp, q, uvw, vis, vis_dtype, wgt, wgt_dtype, st.fast, grid, s, clean, pipelined);
     if (rc != CIP_OK) return rc;
-    if (group_b) {
-      const int64_t a = std::max(q * G, p_lo), b = std::min<int64_t>(q * G + G, p_hi);
-      hipEvent_t f0 = g_prof.mark(s);
-      for (int64_t p = a; p < b; ++p) {
-        double* plane_p = (double*)((char*)grid + (size_t)(p - q * G) * (size_t)plane_elems * cell_bytes);
-        const uint32_t* dm = dmask ? dmask + p * (g.ntx * g.nty / 32) : nullptr;
-        const uint32_t* rbp = rowbits0 ? rowbits0 + p * rb_stride : nullptr;
-        rc = plane_pass_a(st_g, g, plane_p, (int)(p - a), s, dm, rbp);
-        if (rc != CIP_OK) return rc;
-      }
-      CIP_HIP_CHECK(launch_fft_cols_wacc(st_g.fft_h, (int64_t)npix_x * g.nv * 8, (int)(b - a), a, g.nv, npix_x,
-                                         npix_y, st.tw_v, wacc, st.px, st.py, g.w0, g.dw, a == p_lo ? 1 : 0,
-                                         (dmask && fft_rowskip()) ? rowbits0 : nullptr, rb_stride, s));
-      g_prof.span(3, f0, g_prof.mark(s));
-      clean = dmask != nullptr;
-      continue;
-    }
     for (int64_t p = std::max(q * G, p_lo); p < std::min<int64_t>(q * G + G, p_hi); ++p) {
       double* plane_p = (double*)((char*)grid + (size_t)(p - q * G) * (size_t)plane_elems * cell_bytes);
       const uint32_t* dm = dmask ? dmask + p * (g.ntx * g.nty / 32) : nullptr;
       const uint32_t* rbp = rowbits0 ? rowbits0 + p * rb_stride : nullptr;
-      if (pair_b && (pending >= 0 || p + 1 < p_hi)) {
-        hipEvent_t f0 = g_prof.mark(s);
-        rc = plane_pass_a(st, g, plane_p, pending >= 0 ? 1 : 0, s, dm, rbp);
-        if (rc != CIP_OK) return rc;
-        if (pending >= 0) {
-          CIP_HIP_CHECK(launch_fft_cols_wstack(st.fft_h, (int64_t)st.npix_x * g.nv * 8, 2, pending, g.nv, st.npix_x,
-                                               st.npix_y, st.tw_v, dirty_out, st.px, st.py, g.w0, g.dw,
-                                               pending == p_lo ? 1 : 0, fft_rowskip() ? rowbits0 : nullptr,
-                                               rb_stride, s, true));
-          pending = -1;
-        } else {
-          pending = p;
-        }
-        g_prof.span(3, f0, g_prof.mark(s));
-        continue;
-      }
       rc = plane_to_dirty(st, g, p, plane_p, wacc ? (double*)wacc : dirty_out, s, dm, normalise ? pp.red : nullptr,
-                          rbp, p == p_lo, nullptr, wacc != nullptr);
+                          rbp, p == p_lo, wacc != nullptr);
       if (rc != CIP_OK) return rc;
     }
     // a group's planes outside the range were neither written (the scatter

@@ -338,19 +338,6 @@ __device__ __forceinline__ bool place_vis(double u_m, double v_m, double w_m, do
   return ok;
 }
 
-// The unwrapped footprint-origin floors floor(x - W/2), floor(y - W/2) of a
-// visibility, in place_origin's operations and order (two visibilities with
-// equal floors have the same wrapped origin; the planner's time-pair test).
-__device__ __forceinline__ void origin_floors(double u_m, double v_m, double fx, const GridGeometry& g, double* flx,
-                                              double* fly) {
-#pragma clang fp contract(off)
-  const int hw = g.support / 2;
-  const double x = (u_m * fx) * g.scale_u + (double)(g.nu / 2);
-  const double y = (v_m * fx) * g.scale_v + (double)(g.nv / 2);
-  *flx = floor(x - (double)hw);
-  *fly = floor(y - (double)hw);
-}
-
 // The planner's placement: the footprint origins place_vis computes (the same
 // integers), without the kernel variables and without divergent branches in
 // the common case - |origin| < 2^30 and within one grid period of the grid,
@@ -454,26 +441,10 @@ struct RowMap {
   // 2^(cbits + rbits))) and its length - 1 rides in bits 26-31 of its sort key,
   // above the radix digits - so the order pass needs no delta[row] gather
   int pk_runs = 0;
-  // time pairs (2-D fp64 class, dense rows): device pointer to
-  // the detected row stride D of one dump (pair_stride_kernel), or NULL. Rows
-  // of even dump blocks (row / D even) pair with row + D at the same channel
-  // when both footprints start on the same cell: the planner marks the leader
-  // and the absorbed partner in the class byte, the order pass drops the
-  // absorbed entries, and the scatter grids a pair with ONE 64-bit atomic per
-  // tap and component for both visibilities.
-  const int64_t* pair_d = nullptr;
 };
 
 constexpr int kRunLenShift = 26;  // RowMap::pk_runs: run length - 1 in sort-key bits 26-31
 constexpr uint32_t kRunKeyMask = (1u << kRunLenShift) - 1u;
-
-// Class-byte flags of a time pair (planner -> order pass): the class is bits
-// 0-4; the ordered stream marks a pair leader in bit 31 of its dense entry and
-// fills the positions of absorbed partners with kPermNull at the window's end.
-constexpr uint8_t kClassLeader = 0x80u;
-constexpr uint8_t kClassAbsorbed = 0x40u;
-constexpr uint32_t kPermLeader = 0x80000000u;
-constexpr uint32_t kPermNull = 0xffffffffu;
 
 __device__ __forceinline__ int64_t vis_index(const RowMap& m, int64_t r, int64_t c) {
   return m.delta ? m.delta[r] + c : r * m.nchan + c;

@@ -8,9 +8,10 @@
 // image row i directly through the crop epilogue (grid correction, or the
 // w-plane screen and accumulation). Each workgroup holds one N-point
 // transform: N/16 threads x 16 complex values in registers, radix-16 (and a
-// last radix-2/4/8) Stockham passes exchanged through a "half" LDS array
-// (real parts, then imaginary parts; 17/16 N doubles = 68 KiB at N = 8192,
-// two workgroups per CU). HBM bytes per plane: pass A 16 nu nv read +
+// last radix-2/4/8) Stockham passes exchanged through one N-element LDS array
+// (fp64: real parts, then imaginary parts, N doubles; fp32: whole complex
+// values, N float2) - 64 KiB at N = 8192 (two workgroups per CU), 128 KiB at
+// N = 16384 (one per CU). HBM bytes per plane: pass A 16 nu nv read +
 // 16 nx nv written, pass B 16 nx nv read + 8 nx ny written (against 64 nu nv
 // for hipFFT's in-place 2-D c2c plus the crop pass).
 #include <type_traits>
@@ -38,9 +39,10 @@ __device__ __constant__ const double kW16c[16] = {1.0,
                                                   0.92387953251128674};
 
 // The transform's complex type CT: double2, or float2 for the packed class
-// (complex64 planes, CIP_FFT_F32): the same passes on fp32 values and a
-// float LDS exchange array - half the LDS, so four N = 8192 workgroups share a
-// CU instead of two.
+// (complex64 planes, CIP_FFT_F32): the same passes on fp32 values. Both
+// exchange N 8-byte elements through LDS (kXLen), so the fp32 form saves
+// registers and HBM bytes, not LDS: two N = 8192 workgroups per CU either way
+// (the register file allows no more: 90 VGPRs x 8 waves per SIMD).
 template <typename CT>
 struct Cx;
 template <>
@@ -147,7 +149,7 @@ __device__ __forceinline__ int in_pos(int t, int m, int r) {
   return t + m * T + r * (N / R);
 }
 
-// Exchange layout. CIP_FFT_XLDS=1 (round 5): fp32 transforms move whole
+// Exchange layout (round 5): fp32 transforms move whole
 // complex values (one ds_write_b64 / ds_read_b64 per element, one pass
 // instead of real then imaginary b32 halves), fp64 ones their two halves; both
 // at position p ^ ((p >> 4) & 15) (no padding). ds_read_b64 banks a wave's two
@@ -155,22 +157,21 @@ __device__ __forceinline__ int in_pos(int t, int m, int r) {
 // element mod 16 (MI355X_MICROARCH.md, LDS): reads (32 consecutive, 32-aligned
 // positions) keep their 16-element blocks; the first exchange's writes
 // (positions 16 t + r) and the second's (256 (j >> 4) + 16 r + j % 16) land on
-// 16 distinct elements mod 16 per group. The padded layout (0: p + p / 16)
-// spans 34 elements for 32 consecutive reads, a 2-way conflict on every read,
-// and its b32 halves bank by dword mod 32: 40 % of the LDS cycles of the
-// refcall's fp32 transforms were conflict cycles (profiles/r05_sq_refcall.md).
-#ifndef CIP_FFT_XLDS
-#define CIP_FFT_XLDS 1
-#endif
-__device__ __forceinline__ int pad(int p) {
-  if constexpr (CIP_FFT_XLDS) return p ^ ((p >> 4) & 15);
-  return p + (p >> 4);
-}
+// 16 distinct elements mod 16 per group. The round-4 padded layout (p + p /
+// 16, real / imaginary b32 halves) spanned 34 elements for 32 consecutive
+// reads, a 2-way conflict on every read: 40 % of the LDS cycles of the
+// refcall's fp32 transforms were conflict cycles (profiles/r05_sq_refcall.md),
+// 0 with this one (profiles/r05aq_sq_refcall_xlds.md).
+__device__ __forceinline__ int pad(int p) { return p ^ ((p >> 4) & 15); }
 
 template <typename CT>
-using XT = std::conditional_t<CIP_FFT_XLDS && sizeof(CT) == 8, CT, typename Cx<CT>::R>;
+using XT = std::conditional_t<sizeof(CT) == 8, CT, typename Cx<CT>::R>;
 template <int N>
-constexpr int kXLen = CIP_FFT_XLDS ? N : N + N / 16;
+constexpr int kXLen = N;
+// every instantiated transform's exchange array (plus the small per-block
+// tables) within the 160 KiB of LDS a CU has
+static_assert(kXLen<16384> * 8 + 4096 <= 160 * 1024, "N = 16384 exchange must fit one CU's LDS");
+static_assert(2 * (kXLen<8192> * 8 + 4096) <= 160 * 1024, "two N = 8192 transforms per CU");
 
 template <int N, int R, int R2, typename CT>
 __device__ __forceinline__ void exchange(CT* v, int t, int ns, XT<CT>* lds) {
@@ -491,263 +492,12 @@ __global__ __launch_bounds__(N / 16, fft_waves<CT>()) void fft_cols_kernel(const
 
 // CIP_FFT_F32=0: the packed class's complex64 planes transformed in fp64
 // (the round-4 form); default: in fp32, the class's own precision
-static bool fft_f32_enabled() {
+bool fft_f32_enabled() {
   static const bool on = [] {
     const char* e = getenv("CIP_FFT_F32");
     return !(e && e[0] == '0');
   }();
   return on;
-}
-
-// Pass B of a w-stacking batch (round 5): the screened contributions of nb
-// consecutive w planes (global planes pbase .. pbase + nb - 1, their pass-A
-// outputs H + q hstride) summed in registers per image row and written once:
-// one image write per batch instead of a read-modify-write per plane (the
-// C3 reference call: 14 planes -> one write of the 134 MB image instead of 13
-// read-modify-writes). The sum runs in plane order from the batch's first
-// plane (first: overwrite, else: the image row's current values first), the
-// per-plane kernel's additions in the same order - the same image bit for bit.
-// rowbits: plane p's tile-row words at rowbits + p rb_stride (NULL: dense).
-template <int N, typename HT, typename CT, int NB>
-__global__ __launch_bounds__(N / 16, fft_waves<CT>()) void fft_cols_wstack_kernel(
-    const HT* __restrict__ H, int64_t hstride, int64_t pbase, int64_t nx, int64_t ny,
-    const double2* __restrict__ tw, double* __restrict__ out, double px, double py, double w0, double dw, int first,
-    const uint32_t* __restrict__ rowbits, int64_t rb_stride) {
-  using S = FftShape<N>;
-  constexpr int NO = 16;  // outputs per thread (16 / RF blocks of RF)
-  __shared__ XT<CT> lds[kXLen<N>];
-  const int t = threadIdx.x;
-  const int64_t b = blockIdx.x;
-  const int64_t nrows = gridDim.x;
-  int64_t il = b;
-  if (nrows % (8 * kColBlock) == 0)
-    il = (b / (8 * kColBlock)) * (8 * kColBlock) + (b % 8) * kColBlock + (b / 8) % kColBlock;
-  const int64_t i = il;
-  const int64_t p = i - nx / 2;
-  double* orow = out + il * ny;
-  double acc[NO];
-  double nm1v[NO];
-  // the outputs this thread owns: j of element (m, r), kept when j < ny
-#pragma unroll
-  for (int m = 0; m < 16 / S::RF; ++m)
-#pragma unroll
-    for (int r = 0; r < S::RF; ++r) {
-      const int k = out_pos<N, S::RF>(t, m, r, N / S::RF);
-      const int64_t j = (int64_t)((k + (int)(ny / 2)) & (N - 1));
-      const int e_ = m * S::RF + r;
-      acc[e_] = 0.0;
-      nm1v[e_] = 0.0;
-      if (j < ny) {
-        const int64_t q = j - ny / 2;
-        const double l = (double)p * px, mm = (double)q * py;
-        const double e = l * l + mm * mm;
-        nm1v[e_] = -e / (sqrt(1.0 - e) + 1.0);
-        if (!first) acc[e_] = orow[j];
-      }
-    }
-  const HT* colb = H + ((il / kColBlock) * N) * kColBlock + (il % kColBlock);
-  // NB planes in straight-line code (a runtime plane loop around the
-  // transform made the compiler keep ~1300 VGPRs of loop state in scratch)
-#pragma unroll
-  for (int qp = 0; qp < NB; ++qp) {
-    const double2* twq = tw;
-    const int tq = t;
-    const HT* col = colb + (int64_t)qp * hstride;
-    const uint32_t* rb = rowbits ? rowbits + (pbase + qp) * rb_stride : nullptr;
-    CT v[16];
-    HT raw[16];
-    if (rb) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int y = tq + r * S::T;
-        const uint32_t word = rb[(r * S::T) >> 10];
-        raw[r] = HT{0, 0};
-        if ((word >> ((y >> 5) & 31)) & 1u) raw[r] = col[(int64_t)y * kColBlock];
-      }
-    } else {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) raw[r] = col[(int64_t)(tq + r * S::T) * kColBlock];
-    }
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      if constexpr (sizeof(HT) == 8) asm volatile("" : "+v"(raw[r].x), "+v"(raw[r].y));
-      v[r] = ccast<CT>(raw[r]);
-    }
-    fft_core<N>(v, tq, lds, twq);
-    const double w_plane = w0 + (double)(pbase + qp) * dw;
-    // every element's contribution computed branch-free (the outputs past ny
-    // too, then dropped): a divergent branch per element made the carried
-    // accumulators spill (~1300 VGPRs); the kept values are bit-identical
-#pragma unroll
-    for (int m = 0; m < 16 / S::RF; ++m)
-#pragma unroll
-      for (int r = 0; r < S::RF; ++r) {
-        const int k = out_pos<N, S::RF>(tq, m, r, N / S::RF);
-        const int64_t j = (int64_t)((k + (int)(ny / 2)) & (N - 1));
-        const int e_ = m * S::RF + r;
-        const int64_t q = j - ny / 2;
-        const double sgn = ((p + q) & 1) ? -1.0 : 1.0;
-        const double2 g = ccast<double2>(v[e_]);
-        const double ph = -2.0 * w_plane * nm1v[e_];  // the screen's phase / pi
-        double sn, cs;
-        if constexpr (sizeof(CT) == 8 && CIP_SCREEN_F32 == 1) {
-          const float red = (float)(ph - 2.0 * rint(0.5 * ph));
-          float sf, cf;
-          sincospif(red, &sf, &cf);
-          sn = sf;
-          cs = cf;
-        } else {
-          sincospi(ph, &sn, &cs);
-        }
-        const double val = sgn * (g.x * cs - g.y * sn);
-        acc[e_] = (first && qp == 0) ? val : acc[e_] + val;
-      }
-  }
-#pragma unroll
-  for (int m = 0; m < 16 / S::RF; ++m)
-#pragma unroll
-    for (int r = 0; r < S::RF; ++r) {
-      const int k = out_pos<N, S::RF>(t, m, r, N / S::RF);
-      const int64_t j = (int64_t)((k + (int)(ny / 2)) & (N - 1));
-      if (j < ny) orow[j] = acc[m * S::RF + r];
-    }
-}
-
-// Pass B of a packed-class w-stacking plane group into the float plane
-// accumulator (round 5): the nb planes' pass-A outputs (H + q hstride) one
-// after another in the same workgroup, each plane's screened contributions
-// added into an LDS copy of the image row, written once per group - one
-// read-modify-write of the accumulator row per group instead of one per
-// plane. The additions are the per-plane kernel's (acc = (float)(acc + val)
-// in plane order): the same image bit for bit. ny <= N / 2.
-template <int N, typename HT, typename CT>
-__global__ __launch_bounds__(N / 16, fft_waves<CT>()) void fft_cols_wacc_kernel(
-    const HT* __restrict__ H, int64_t hstride, int nb, int64_t pbase, int64_t nx, int64_t ny,
-    const double2* __restrict__ tw, float* __restrict__ out, double px, double py, double w0, double dw, int first,
-    const uint32_t* __restrict__ rowbits, int64_t rb_stride) {
-  using S = FftShape<N>;
-  __shared__ XT<CT> lds[kXLen<N>];
-  __shared__ float s_acc[N / 2];
-  const int t = threadIdx.x;
-  const int64_t b = blockIdx.x;
-  const int64_t nrows = gridDim.x;
-  int64_t il = b;
-  if (nrows % (8 * kColBlock) == 0)
-    il = (b / (8 * kColBlock)) * (8 * kColBlock) + (b % 8) * kColBlock + (b / 8) % kColBlock;
-  const int64_t p = il - nx / 2;
-  float* orow = out + il * ny;
-  for (int64_t jj = t; jj < ny; jj += S::T) s_acc[jj] = first ? 0.0f : orow[jj];
-  __syncthreads();
-  const HT* colb = H + ((il / kColBlock) * N) * kColBlock + (il % kColBlock);
-  for (int qp = 0; qp < nb; ++qp) {
-    const HT* col = colb + (int64_t)qp * hstride;
-    const uint32_t* rb = rowbits ? rowbits + (pbase + qp) * rb_stride : nullptr;
-    CT v[16];
-    HT raw[16];
-    if (rb) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int y = t + r * S::T;
-        const uint32_t word = rb[(r * S::T) >> 10];
-        raw[r] = HT{0, 0};
-        if ((word >> ((y >> 5) & 31)) & 1u) raw[r] = col[(int64_t)y * kColBlock];
-      }
-    } else {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) raw[r] = col[(int64_t)(t + r * S::T) * kColBlock];
-    }
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      if constexpr (sizeof(HT) == 8) asm volatile("" : "+v"(raw[r].x), "+v"(raw[r].y));
-      v[r] = ccast<CT>(raw[r]);
-    }
-    fft_core<N>(v, t, lds, tw);
-    const double w_plane = w0 + (double)(pbase + qp) * dw;
-#pragma unroll
-    for (int m = 0; m < 16 / S::RF; ++m)
-#pragma unroll
-      for (int r = 0; r < S::RF; ++r) {
-        const int k = out_pos<N, S::RF>(t, m, r, N / S::RF);
-        const int64_t j = (int64_t)((k + (int)(ny / 2)) & (N - 1));
-        if (j < ny) {
-          const int64_t q = j - ny / 2;
-          const double sgn = ((p + q) & 1) ? -1.0 : 1.0;
-          const double2 g = ccast<double2>(v[m * S::RF + r]);
-          const double l = (double)p * px, mm = (double)q * py;
-          const double e = l * l + mm * mm;
-          const double nm1 = -e / (sqrt(1.0 - e) + 1.0);
-          const double ph = -2.0 * w_plane * nm1;
-          double sn, cs;
-          if constexpr (sizeof(CT) == 8 && CIP_SCREEN_F32 == 1) {
-            const float red = (float)(ph - 2.0 * rint(0.5 * ph));
-            float sf, cf;
-            sincospif(red, &sf, &cf);
-            sn = sf;
-            cs = cf;
-          } else {
-            sincospi(ph, &sn, &cs);
-          }
-          const double val = sgn * (g.x * cs - g.y * sn);
-          s_acc[j] = (float)((double)s_acc[j] + val);
-        }
-      }
-  }
-  __syncthreads();
-  for (int64_t jj = t; jj < ny; jj += S::T) orow[jj] = s_acc[jj];
-}
-
-hipError_t launch_fft_cols_wacc(const double* H, int64_t hstride_bytes, int nb, int64_t pbase, int64_t nv, int64_t nx,
-                                int64_t ny, const double* tw_v, float* out, double px, double py, double w0,
-                                double dw, int first, const uint32_t* rowbits, int64_t rb_stride, hipStream_t s) {
-  if (nb <= 0) return hipSuccess;
-  if (!fft_f32_enabled() || ny > nv / 2) return hipErrorInvalidValue;
-  const dim3 gd((unsigned)nx);
-  const double2* tw = (const double2*)tw_v;
-  const int64_t hs = hstride_bytes / (int64_t)sizeof(float2);
-#define COLSA(NN)                                                                                            \
-  case NN:                                                                                                   \
-    fft_cols_wacc_kernel<NN, float2, float2><<<gd, dim3(NN / 16), 0, s>>>(                                   \
-        (const float2*)H, hs, nb, pbase, nx, ny, tw, out, px, py, w0, dw, first, rowbits, rb_stride);        \
-    break;
-  switch (nv) {
-    COLSA(1024)
-    COLSA(2048)
-    COLSA(4096)
-    COLSA(8192)
-    default:
-      return hipErrorInvalidValue;
-  }
-#undef COLSA
-  return hipGetLastError();
-}
-
-hipError_t launch_fft_cols_wstack(const double* H, int64_t hstride_bytes, int nb, int64_t pbase, int64_t nv,
-                                  int64_t nx, int64_t ny, const double* tw_v, double* out, double px, double py,
-                                  double w0, double dw, int first, const uint32_t* rowbits, int64_t rb_stride,
-                                  hipStream_t s, bool h_f32) {
-  if (nb <= 0) return hipSuccess;
-  const dim3 gd((unsigned)nx);
-  const double2* tw = (const double2*)tw_v;
-  const bool fft_f32 = fft_f32_enabled();
-  const int64_t hs = hstride_bytes / (h_f32 ? (int64_t)sizeof(float2) : (int64_t)sizeof(double2));
-  // the packed class's plane pairs, grids up to 8192 (16384: one 1024-thread
-  // block per CU would spill the pair's state)
-  if (nb != 2 || !h_f32 || !fft_f32 || nv > 8192) return hipErrorInvalidValue;
-#define COLSW(NN)                                                                                              \
-  case NN:                                                                                                     \
-    fft_cols_wstack_kernel<NN, float2, float2, 2><<<gd, dim3(NN / 16), 0, s>>>(                                \
-        (const float2*)H, hs, pbase, nx, ny, tw, out, px, py, w0, dw, first, rowbits, rb_stride);              \
-    break;
-  switch (nv) {
-    COLSW(1024)
-    COLSW(2048)
-    COLSW(4096)
-    COLSW(8192)
-    default:
-      return hipErrorInvalidValue;
-  }
-#undef COLSW
-  return hipGetLastError();
 }
 
 static bool fft_len_ok(int64_t n) { return n == 1024 || n == 2048 || n == 4096 || n == 8192 || n == 16384; }
@@ -893,6 +643,10 @@ hipError_t launch_fft_cols(const double* H, int64_t nv, int64_t nx, int64_t ny, 
   const double2* tw = (const double2*)tw_v;
   const ColEpilogue ep{out, cx, cy, px, py, w_plane, first, norm};
   const bool fft_f32 = fft_f32_enabled();
+  // the float plane accumulator exists only beside fp32 transforms of
+  // complex64 planes (with CIP_FFT_F32=0 the fp64-output kernel
+  // would write doubles across twice the float buffer's bytes)
+  if (acc_f32 && !(h_f32 && fft_f32 && mode == 1)) return hipErrorInvalidValue;
 #define COLS(NN)                                                                                           \
   case NN:                                                                                                 \
     if (h_f32 && fft_f32 && mode == 1 && acc_f32)                                                          \

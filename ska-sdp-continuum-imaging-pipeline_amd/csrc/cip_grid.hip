@@ -96,68 +96,35 @@ constexpr int kOrderPer = kOrderWindow / kOrderThreads;
 constexpr int kOrderBatch = kOrderThreads * kOrderPer;
 static_assert(kOrderBatch == kOrderWindow, "one order block per window");
 
-// Bank class of a visibility's footprint origin in its tile's LDS sub-grid,
-// recomputed in fp32 from the row's pre-scaled (u scale_u, v scale_v) and
-// f/c. The class only decides the ORDER of a window's visibilities (bank
-// spreading); the scatter places every visibility with its own fp64
-// arithmetic whatever position it gets, so a class that differs from the
-// exact one near a cell edge (fp32: ~1e-3 cells at |x| = 8192) costs at most a
-// bank conflict, never a different sum.
-__device__ __forceinline__ unsigned origin_class_f32(float us, float vs, float f, const GridGeometry& g) {
-  const int hw = g.support / 2;
-  const int P = kTile + g.support - 1;
-  const float x = fmaf(us, f, (float)(g.nu / 2) - (float)hw);
-  const float y = fmaf(vs, f, (float)(g.nv / 2) - (float)hw);
-  int ix0 = (int)floorf(x) + 1, iy0 = (int)floorf(y) + 1;
-  ix0 += ix0 < 0 ? (int)g.nu : 0;
-  ix0 -= ix0 >= (int)g.nu ? (int)g.nu : 0;
-  iy0 += iy0 < 0 ? (int)g.nv : 0;
-  iy0 -= iy0 >= (int)g.nv ? (int)g.nv : 0;
-  return (unsigned)(((ix0 % kTile) * P + iy0 % kTile) & 31);  // ix0, iy0 in [0, nu), [0, nv)
-}
-
 // One block per window (<= kOrderWindow consecutive tile-order positions).
-// The window's row slices are staged in LDS with their rows' (u, v)
-// (positions relative to the window start; the next window of the tile starts
-// in its last slice), each thread finds the slice of its 4 positions by binary
-// search, recomputes the bank class of each visibility (no per-visibility
-// class array: a gathered byte per visibility cost more HBM lines than the
-// whole perm stream) and the window is counting-sorted into level-major
-// order: perm[g] = perm_encode(row, channel).
-// PAIRS (dense rows, gathered classes with time-pair flags, RowMap::pair_d):
-// the window's pair leaders first (their own level-major class order, entry |
-// kPermLeader), then the single visibilities (level-major), then one kPermNull
-// entry per absorbed partner - so the scatter's waves are uniformly pairs or
-// singles (one mixed wave at the boundary) and the nulls fill whole waves at
-// the window's end.
-template <bool GATHER, int WIDE, bool PAIRS = false>
-__global__ __launch_bounds__(kOrderThreads, PAIRS ? 6 : 8) void order_kernel(const double* __restrict__ uvw,
-                                                              const double* __restrict__ fx,
-                                                              const uint8_t* __restrict__ vis_class, GridGeometry g,
-                                                              RowMap m, const uint64_t* __restrict__ runs,
-                                                              const int64_t* __restrict__ run_goff,
-                                                              const int64_t* __restrict__ tile_run_off,
-                                                              const Chunk* __restrict__ windows, int64_t nwindows,
-                                                              void* __restrict__ perm,
-                                                              const uint64_t* __restrict__ run_uv) {
-  static_assert(!PAIRS || (GATHER && WIDE == 0), "time pairs: dense rows with gathered classes");
-  constexpr int NCLS = PAIRS ? 64 : 32;  // PAIRS: leaders' classes 0..31, singles' 32..63
-  __shared__ __attribute__((aligned(16))) unsigned s_cnt[NCLS];
+// The window's row slices are staged in LDS (positions relative to the window
+// start; the next window of the tile starts in its last slice), each thread
+// finds the slice of its 4 positions, gathers the bank class the place pass
+// stored for each visibility, and the window is counting-sorted into
+// level-major order: perm[g] = perm_encode(row, channel). (Recomputing the
+// classes here instead - from a uvw gather, or from fp32 (u, v) carried with
+// each run through the radix sort - measured slower in rounds 2-5: the
+// gathered class byte costs fewer lines than either.)
+template <int WIDE>
+__global__ __launch_bounds__(kOrderThreads, 8) void order_kernel(const uint8_t* __restrict__ vis_class, RowMap m,
+                                                                 const uint64_t* __restrict__ runs,
+                                                                 const int64_t* __restrict__ run_goff,
+                                                                 const Chunk* __restrict__ windows,
+                                                                 void* __restrict__ perm) {
+  __shared__ __attribute__((aligned(16))) unsigned s_cnt[32];
   // the staged slices are dead once every position has its class: the level
   // tables reuse their space
   __shared__ union {
     struct {
-      float2 uv[GATHER ? 1 : kOrderBatch];  // (u scale_u, v scale_v) of each slice's row (recompute only)
       uint64_t rec[kOrderBatch];
       int64_t delta[WIDE == 1 ? kOrderBatch : 1];  // ragged: delta[row] of each slice (index = delta + channel)
       int off[kOrderBatch + 1];  // slice starts relative to the window start
       uint16_t idx[kOrderBatch];  // slice of each position
     } a;
     struct {
-      unsigned S[PAIRS ? 2 * kOrderBatch : kOrderBatch], M[PAIRS ? 2 * kOrderBatch : kOrderBatch];
+      unsigned S[kOrderBatch], M[kOrderBatch];
     } b;
   } sh;
-  float2* const s_uv = sh.a.uv;
   uint64_t* const s_rec = sh.a.rec;
   int* const s_off = sh.a.off;
   uint16_t* const s_idx = sh.a.idx;
@@ -184,17 +151,8 @@ __global__ __launch_bounds__(kOrderThreads, PAIRS ? 6 : 8) void order_kernel(con
       s_rec[k] = rec;
     }
     if constexpr (WIDE == 1) sh.a.delta[k] = m.delta[(int64_t)(rec >> 32)];
-    if constexpr (!GATHER) {
-      if (run_uv) {  // carried with the run through the sort: contiguous, no gather
-        s_uv[k] = __builtin_bit_cast(float2, run_uv[ch.first_run + k]);
-      } else {
-        const int64_t row = m.pk_runs ? (int64_t)((rec >> m.pk_cbits) & ((1ull << m.pk_rbits) - 1ull))
-                                      : (int64_t)(rec >> 32);
-        s_uv[k] = make_float2((float)(uvw[3 * row] * g.scale_u), (float)(uvw[3 * row + 1] * g.scale_v));
-      }
-    }
   }
-  if (threadIdx.x < NCLS) s_cnt[threadIdx.x] = 0u;
+  if (threadIdx.x < 32) s_cnt[threadIdx.x] = 0u;
   __syncthreads();
   // expand: every position learns its slice (slices are <= 64 positions long)
   for (int k = threadIdx.x; k < nst; k += kOrderThreads) {
@@ -234,66 +192,16 @@ __global__ __launch_bounds__(kOrderThreads, PAIRS ? 6 : 8) void order_kernel(con
   }
 #pragma unroll
   for (int k = 0; k < kOrderPer; ++k) {
-    cls[k] = (unsigned)NCLS;  // none (past the window)
-    if (threadIdx.x + k * kOrderThreads < nsb) {
-      if constexpr (PAIRS) {
-        // leaders -> 0..31, singles -> 32..63, absorbed partners -> none (64)
-        const unsigned b = vis_class[(int64_t)packed[k]];
-        cls[k] = (b & kClassAbsorbed) ? 64u : ((b & kClassLeader) ? (b & 31u) : 32u + (b & 31u));
-        if (b & kClassLeader) packed[k] |= (Entry)kPermLeader;
-      } else if constexpr (GATHER) {
-        cls[k] = vis_class[WIDE == 2   ? (int64_t)((uint64_t)packed[k] >> pk_shift)
-                           : WIDE == 1 ? sh.a.delta[slice[k]] + chan[k]
-                                       : (int64_t)packed[k]];
-      } else {
-        const float2 uv = s_uv[slice[k]];
-        cls[k] = origin_class_f32(uv.x, uv.y, (float)fx[chan[k]], g);
-      }
-    }
+    cls[k] = 32u;  // none (past the window)
+    if (threadIdx.x + k * kOrderThreads < nsb)
+      cls[k] = vis_class[WIDE == 2   ? (int64_t)((uint64_t)packed[k] >> pk_shift)
+                         : WIDE == 1 ? sh.a.delta[slice[k]] + chan[k]
+                                     : (int64_t)packed[k]];
   }
 #pragma unroll
   for (int k = 0; k < kOrderPer; ++k)
-    if (cls[k] < (unsigned)NCLS) rk[k] = atomicAdd(&s_cnt[cls[k]], 1u);
+    if (cls[k] < 32u) rk[k] = atomicAdd(&s_cnt[cls[k]], 1u);
   __syncthreads();
-  if constexpr (PAIRS) {
-    // two level-major groups (leaders, singles) and the nulls after them
-    unsigned maxl = 0, maxs = 0, nlead = 0, nsing = 0;
-#pragma unroll
-    for (int i = 0; i < 32; ++i) {
-      maxl = s_cnt[i] > maxl ? s_cnt[i] : maxl;
-      maxs = s_cnt[32 + i] > maxs ? s_cnt[32 + i] : maxs;
-      nlead += s_cnt[i];
-      nsing += s_cnt[32 + i];
-    }
-    // one group at a time (a compile-time offset: the 32 counts of one group
-    // live in registers, not both groups' 64)
-    auto tables = [&](const unsigned* cnt_g, unsigned* S_g, unsigned* M_g, unsigned nlev) {
-      for (unsigned r = threadIdx.x; r < nlev; r += kOrderThreads) {
-        unsigned S = 0, M = 0;
-#pragma unroll
-        for (int c2 = 0; c2 < 32; ++c2) {
-          const unsigned cnt = cnt_g[c2];
-          S += cnt < r ? cnt : r;
-          M |= (cnt > r ? 1u : 0u) << c2;
-        }
-        S_g[r] = S;
-        M_g[r] = M;
-      }
-    };
-    tables(s_cnt, s_S, s_M, maxl);
-    tables(s_cnt + 32, s_S + kOrderBatch, s_M + kOrderBatch, maxs);
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < kOrderPer; ++k) {
-      if (cls[k] < 64u) {
-        const unsigned grp = cls[k] >> 5, c = cls[k] & 31u;
-        const unsigned t = grp * (unsigned)kOrderBatch + rk[k];
-        ((Entry*)perm)[sb + (grp ? nlead : 0u) + s_S[t] + __popc(s_M[t] & ((1u << c) - 1u))] = packed[k];
-      }
-    }
-    for (int t = (int)(nlead + nsing) + threadIdx.x; t < nsb; t += kOrderThreads) ((Entry*)perm)[sb + t] = (Entry)kPermNull;
-    return;
-  }
   unsigned maxcnt = 0;
 #pragma unroll
   for (int i = 0; i < 32; ++i) maxcnt = s_cnt[i] > maxcnt ? s_cnt[i] : maxcnt;  // LDS broadcast reads
@@ -314,28 +222,18 @@ __global__ __launch_bounds__(kOrderThreads, PAIRS ? 6 : 8) void order_kernel(con
     if (cls[k] < 32u) ((Entry*)perm)[sb + s_S[rk[k]] + __popc(s_M[rk[k]] & ((1u << cls[k]) - 1u))] = packed[k];
 }
 
-hipError_t launch_order(const double* uvw, const double* fx, const uint8_t* vis_class, const GridGeometry& g,
-                        const RowMap& m, const uint64_t* runs, const int64_t* run_goff, const int64_t* tile_run_off,
-                        const Chunk* windows, int64_t nwindows, void* perm, hipStream_t s,
-                        const uint64_t* run_uv) {
+hipError_t launch_order(const uint8_t* vis_class, const RowMap& m, const uint64_t* runs, const int64_t* run_goff,
+                        const Chunk* windows, int64_t nwindows, void* perm, hipStream_t s) {
   if (nwindows <= 0) return hipSuccess;
-#define ORDER(GA, WI)                                                              \
-  order_kernel<GA, WI><<<dim3((unsigned)nwindows), dim3(kOrderThreads), 0, s>>>( \
-      uvw, fx, vis_class, g, m, runs, run_goff, tile_run_off, windows, nwindows, perm, run_uv)
+  if (!vis_class) return hipErrorInvalidValue;
+#define ORDER(WI)                                                                                            \
+  order_kernel<WI><<<dim3((unsigned)nwindows), dim3(kOrderThreads), 0, s>>>(vis_class, m, runs, run_goff,   \
+                                                                           windows, perm)
   // ragged row slices: u64 entries (2: packed (index, row, channel))
   const int wide = m.delta == nullptr ? 0 : (m.pk_cbits ? 2 : 1);
-  if (vis_class && m.pair_d != nullptr && !wide) {
-    order_kernel<true, 0, true><<<dim3((unsigned)nwindows), dim3(kOrderThreads), 0, s>>>(
-        uvw, fx, vis_class, g, m, runs, run_goff, tile_run_off, windows, nwindows, perm, run_uv);
-  } else if (vis_class) {
-    if (wide == 2) ORDER(true, 2);
-    else if (wide) ORDER(true, 1);
-    else ORDER(true, 0);
-  } else {
-    if (wide == 2) ORDER(false, 2);
-    else if (wide) ORDER(false, 1);
-    else ORDER(false, 0);
-  }
+  if (wide == 2) ORDER(2);
+  else if (wide) ORDER(1);
+  else ORDER(0);
 #undef ORDER
   return hipGetLastError();
 }
@@ -355,12 +253,8 @@ hipError_t launch_scatter(int support, int vis_dtype, int wgt_dtype, bool packed
   if (share_cus && group == 1 && support <= 16) {
     const unsigned P = (unsigned)(kTile + support - 1);
     const unsigned stat = P * P * (packed ? 8u : 16u) + 64u;
-    // CIP_SHARE_BLOCKS=1..3: the scatter blocks per CU beside the planner (A/B)
-    static const unsigned nb = [] {
-      const char* e = getenv("CIP_SHARE_BLOCKS");
-      const int v = e ? atoi(e) : 3;
-      return (unsigned)(v >= 1 && v <= 3 ? v : 3);
-    }();
+    // 3 blocks per CU: the optimum of 2 / 3 / 4 (profiles/r03_ab_scatter_share.txt, r05z_ab_share_blocks.txt)
+    const unsigned nb = 3u;
     const unsigned need = 160u * 1024u / (nb + 1u) + 256u;
     pad = stat < need ? need - stat : 0u;
   }

@@ -43,8 +43,6 @@ hipError_t launch_w_range(const double* uvw, int64_t nrow, double fxmin, double 
 // partials (2 * plan_place_blocks) and the radix pass-0 histogram of the parked
 // keys (hist0[d * nblocks + b], 256 * nblocks + 1 entries, last one zeroed);
 // vis_class (optional, nvis bytes): each visibility's LDS bank class.
-// park_uv (optional, beside park_run): each run's row as fp32 (u nu dx, v nv dy)
-// bit-cast to u64, for the order pass's class recompute.
 // err_flag: bit 0 non-finite uvw / w off the stack, bit 1 non-finite vis or weight.
 int plan_place_blocks(int64_t nvis);
 // the place pass's reduction alone (sum of weights, max |w V|, non-finite
@@ -54,11 +52,7 @@ hipError_t launch_prep_reduce(const RowMap& m, const void* vis, int vis_dtype, c
 hipError_t launch_plan_place(const double* uvw, const double* fx, const RowMap& m,
                              const void* vis, int vis_dtype, const void* wgt, int wgt_dtype, const GridGeometry& g,
                              unsigned* err_flag, uint8_t* vis_class, int64_t* blk_cnt, uint32_t* park_key,
-                             uint64_t* park_run, double* partial, int64_t* hist0, hipStream_t s,
-                             uint64_t* park_uv = nullptr);
-// time pairs: the row stride D of one dump (the same baseline one dump later)
-// detected from uvw on the device -> *out (0: none found; nothing pairs)
-hipError_t launch_pair_stride(const double* uvw, int64_t nrow, int64_t* out, hipStream_t s);
+                             uint64_t* park_run, double* partial, int64_t* hist0, hipStream_t s);
 // ragged rows: out[r] = chan_stop[r] - chan_start[r] (out[nrow] = 0; err bit
 // set for a range outside [0, nchan)); after the exclusive scan (off[r] = row
 // r's first visibility), launch_ragged_expand writes delta[r] = off[r] -
@@ -79,8 +73,7 @@ hipError_t launch_radix_hist(const uint32_t* keys, int64_t n, const int64_t* blk
 hipError_t launch_radix_group_hist(const int64_t* hist0, int64_t nsub, int G, int64_t* hg, hipStream_t s);
 hipError_t launch_radix_scatter(const uint32_t* keys, const uint64_t* vals, int64_t n, const int64_t* blk_cnt,
                                 int64_t nsub, int G, int shift, const int64_t* hist, uint32_t* keys_out,
-                                uint64_t* vals_out, hipStream_t s, const uint64_t* vals2 = nullptr,
-                                uint64_t* vals2_out = nullptr);
+                                uint64_t* vals_out, hipStream_t s);
 hipError_t launch_tile_offsets(const uint32_t* keys, int64_t nruns, int64_t ntiles, int64_t* tile_run_off,
                                hipStream_t s, uint32_t kmask = 0xffffffffu);
 // per grid plane (nplanes x ntx x nty bytes); bits (optional, ntx % 32 ==
@@ -148,14 +141,9 @@ hipError_t launch_scatter(int support, int vis_dtype, int wgt_dtype, bool packed
 // perm (nvis 32-bit records, nvis < 2^32): the tile-order visibilities as
 // row * nchan + channel, bank-class sorted within each window (the tiles split
 // into <= kOrderWindow pieces by chunk_emit with cv = kOrderWindow)
-// vis_class: classes from the place pass, or NULL (recomputed from u, v, f)
-// run_uv (optional): each sorted run's park_uv entry - classes recomputed from
-// it and f / c (no gather); else vis_class, else recomputed from uvw
-hipError_t launch_order(const double* uvw, const double* fx, const uint8_t* vis_class, const GridGeometry& g,
-                        const RowMap& m,
-                        const uint64_t* runs, const int64_t* run_goff, const int64_t* tile_run_off,
-                        const Chunk* windows, int64_t nwindows, void* perm, hipStream_t s,
-                        const uint64_t* run_uv = nullptr);
+// vis_class: the place pass's class byte per visibility (required)
+hipError_t launch_order(const uint8_t* vis_class, const RowMap& m, const uint64_t* runs, const int64_t* run_goff,
+                        const Chunk* windows, int64_t nwindows, void* perm, hipStream_t s);
 hipError_t launch_crop_correct_2d(const double* grid, const GridGeometry& g, int64_t npix_x, int64_t npix_y,
                                   const double* cx, const double* cy, double* dirty, hipStream_t s);
 hipError_t launch_wplane_accumulate(const double* grid, const GridGeometry& g, int64_t npix_x, int64_t npix_y,
@@ -187,20 +175,10 @@ hipError_t launch_fft_cols(const double* H, int64_t nv, int64_t nx, int64_t ny, 
                            double* out, const double* cx, const double* cy, double px, double py, double w_plane,
                            int first, const double* norm, const uint32_t* rowbits, hipStream_t s,
                            bool h_f32 = false, bool acc_f32 = false);
-// w-stacking pass B over nb consecutive planes (global pbase ..): their
-// pass-A outputs at H + q hstride_bytes, summed per image row in plane order
-// and written once (first: overwrite, else added to out's values); rowbits:
-// plane p's tile-row words at rowbits + p rb_stride (NULL: dense)
-// packed-class plane group pass B into the float accumulator (cip_fft.hip):
-// nb planes' complex64 pass-A outputs hstride_bytes apart, one accumulator
-// row write per group (first: overwrite); nv <= 8192, ny <= nv / 2
-hipError_t launch_fft_cols_wacc(const double* H, int64_t hstride_bytes, int nb, int64_t pbase, int64_t nv, int64_t nx,
-                                int64_t ny, const double* tw_v, float* out, double px, double py, double w0,
-                                double dw, int first, const uint32_t* rowbits, int64_t rb_stride, hipStream_t s);
-hipError_t launch_fft_cols_wstack(const double* H, int64_t hstride_bytes, int nb, int64_t pbase, int64_t nv,
-                                  int64_t nx, int64_t ny, const double* tw_v, double* out, double px, double py,
-                                  double w0, double dw, int first, const uint32_t* rowbits, int64_t rb_stride,
-                                  hipStream_t s, bool h_f32);
+// acc_f32: out is the packed class's float plane accumulator (mode 1, h_f32,
+// fp32 transforms only: hipErrorInvalidValue otherwise - the fp64-output
+// kernels would write doubles into a float buffer)
+bool fft_f32_enabled();
 // strips (multi-GPU strong scaling): pass A over rows [y0, y1)
 // of gT (zeroed after reading) into H with y1 - y0 rows per block; pass B for
 // image rows [i0, i1) (multiples of the column block) from an H holding those

@@ -186,51 +186,6 @@ hipError_t launch_w_range(const double* uvw, int64_t nrow, double fxmin, double 
   return hipGetLastError();
 }
 
-// ------------------------------------------------------- time pairs ----
-// The row stride D of one dump: rows of an MS are time-major, baseline-minor,
-// so row r + D is row r's baseline one dump later, whose uvw differs by the
-// earth's rotation over the dump (~6e-4 of |uvw| for 8 s). D = the smallest d
-// for which every sampled row k (0, 1, 2, 3, nrow / 3, nrow / 2, with k + d <
-// nrow and uvw_k != 0) has |uvw_{k+d} - uvw_k| <= 1 % of |uvw_k|, with at
-// least three such rows. A performance hint only: the place pass pairs two
-// visibilities when their footprints start on the same cell, whatever D is.
-// One workgroup; candidates in blocks of 256, smallest first, stopping at the
-// first block holding a match.
-__global__ __launch_bounds__(256) void pair_stride_kernel(const double* __restrict__ uvw, int64_t nrow,
-                                                          int64_t* __restrict__ out) {
-  __shared__ unsigned long long best;
-  if (threadIdx.x == 0) best = ~0ull;
-  __syncthreads();
-  const int64_t dmax = nrow / 2 < ((int64_t)1 << 20) ? nrow / 2 : ((int64_t)1 << 20);
-  const int64_t ks[6] = {0, 1, 2, 3, nrow / 3, nrow / 2};
-  for (int64_t d0 = 1; d0 <= dmax; d0 += 256) {
-    const int64_t d = d0 + threadIdx.x;
-    if (d <= dmax) {
-      int checked = 0;
-      bool ok = true;
-      for (int i = 0; i < 6 && ok; ++i) {
-        const int64_t k = ks[i];
-        if (k + d >= nrow) continue;
-        const double a0 = uvw[3 * k], a1 = uvw[3 * k + 1], a2 = uvw[3 * k + 2];
-        const double n2 = a0 * a0 + a1 * a1 + a2 * a2;
-        if (!(n2 > 0.0)) continue;
-        const double b0 = uvw[3 * (k + d)] - a0, b1 = uvw[3 * (k + d) + 1] - a1, b2 = uvw[3 * (k + d) + 2] - a2;
-        ok = b0 * b0 + b1 * b1 + b2 * b2 <= 1e-4 * n2;
-        ++checked;
-      }
-      if (ok && checked >= 3) atomicMin(&best, (unsigned long long)d);
-    }
-    __syncthreads();
-    if (best != ~0ull) break;  // block-uniform
-  }
-  if (threadIdx.x == 0) *out = best == ~0ull ? 0 : (int64_t)best;
-}
-
-hipError_t launch_pair_stride(const double* uvw, int64_t nrow, int64_t* out, hipStream_t s) {
-  pair_stride_kernel<<<dim3(1), dim3(256), 0, s>>>(uvw, nrow, out);
-  return hipGetLastError();
-}
-
 // ---------------------------------------------------------- planner ----
 // A run is a maximal range of consecutive channels of one row with constant
 // tile key (cf. the reference's row slices, tiling_plan.py:150-181). Each
@@ -252,30 +207,20 @@ __device__ __forceinline__ uint32_t wave_shr1(uint32_t v) {
 }
 constexpr uint32_t kNoKey = 0xffffffffu;  // visibility off the grid (tile keys are < 2^32 - 1)
 
-#ifndef CIP_PLACE_ABL
-#define CIP_PLACE_ABL 0  // experiment builds only: 1 no visibility load, 2 no run parking, 3 no class store, 4 no vis / weight load
-#endif
-#ifndef CIP_PLACE_WAVES
-#define CIP_PLACE_WAVES 1  // min waves per SIMD the place pass is compiled for
-#endif
 // PLACE = false: only the fused reduction (sum of weights, max |w V|,
 // non-finite check), in exactly the place pass's order - a call that reuses
 // its predecessor's plan (CIP_REUSE_PLAN) gets the same sums bit for bit.
-// LOADVIS = false (PLACE only): the placement without the reduction - no
-// visibility or weight loads, no partials (the split place pass: a separate
-// block of the same launch reduces the same visibilities, see
-// plan_place_split_kernel). blk / nblocks: this place block and their count.
+// blk / nblocks: this place block and their count.
 // RM: the row map, at compile time (each mode's registers only): 0 dense MS
-// rows, 1 dense rows that may pair (RowMap::pair_d), 2 ragged row slices
-template <typename VisT, int WK, bool PLACE, bool LOADVIS, int RM>
+// rows, 2 ragged row slices
+template <typename VisT, int WK, bool PLACE, int RM>
 __device__ __forceinline__ void place_body(const double* __restrict__ uvw, const double* __restrict__ fx,
                                            const RowMap& m, const VisT* __restrict__ vis,
                                            const void* __restrict__ wgt, const GridGeometry& g, unsigned* err_flag,
                                            uint8_t* __restrict__ vis_class, int64_t* __restrict__ blk_cnt,
                                            uint32_t* __restrict__ park_key, uint64_t* __restrict__ park_run,
-                                           double* partial, int64_t* __restrict__ hist0,
-                                           uint64_t* __restrict__ park_uv, const int64_t blk, const int64_t nblocks) {
-  static_assert(PLACE || LOADVIS, "a place body places or reduces");
+                                           double* partial, int64_t* __restrict__ hist0, const int64_t blk,
+                                           const int64_t nblocks) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   __shared__ unsigned s_nruns;
   __shared__ unsigned s_hist[256];
@@ -297,12 +242,6 @@ __device__ __forceinline__ void place_body(const double* __restrict__ uvw, const
   int64_t r0 = 0, c0 = 0;
   if (!ragged) split_index64((blk * kPlaceSegs + wave) * 64 + lane, nchan, m.inv_nchan, &r0, &c0);
   const int64_t step_r = 256 / nchan, step_c = 256 % nchan;
-  // time pairs (dense rows, m.pair_d): the dump stride D (0 = none)
-  int64_t pair_d = 0;
-  if constexpr (PLACE)
-    if (RM == 1 && m.pair_d != nullptr) pair_d = __builtin_amdgcn_readfirstlane((int)*m.pair_d);
-  const int64_t nrow_dense = ragged ? 0 : nvis / nchan;
-  const double inv_d = pair_d > 0 ? 1.0 / (double)pair_d : 0.0;
   // ragged rows: the first rows of the wave's kPlaceSegs / 4 segments and the
   // starts of the rows after them, loaded once (lane j: segment j), so the
   // loop's row lookup is a register read, not a chain of dependent loads
@@ -352,39 +291,16 @@ __device__ __forceinline__ void place_body(const double* __restrict__ uvw, const
     // position loads first: the visibility load of a PSF call is a branch,
     // and the wait inside it then covers every load (one memory round trip)
     double u = 0.0, v = 0.0, w = 0.0, f = 0.0;
-    // time pair partner: row rl + D in an even dump block, rl - D in an odd one
-    int64_t prow = rl;
-    bool pair_even = false, pair_has = false;
-    double pu = 0.0, pv = 0.0;
     if constexpr (PLACE) {
       u = uvw[3 * rl];
       v = uvw[3 * rl + 1];
       w = uvw[3 * rl + 2];
       f = fx[cl];
-      if (pair_d > 0) {
-        int64_t b = (int64_t)((double)rl * inv_d);
-        b -= (b * pair_d > rl) ? 1 : 0;
-        b += ((b + 1) * pair_d <= rl) ? 1 : 0;
-        pair_even = (b & 1) == 0;
-        const int64_t pr = pair_even ? rl + pair_d : rl - pair_d;
-        pair_has = valid && pr >= 0 && pr < nrow_dense;
-        prow = pair_has ? pr : rl;
-        pu = uvw[3 * prow];
-        pv = uvw[3 * prow + 1];
-      }
     }
-    if constexpr (LOADVIS) {
-#if CIP_PLACE_ABL == 4
-      const double wt = 1.0;  // ablation: neither weights nor visibilities read (uvw + fx only)
-#else
+    {
       const double wt = load_weight<WK>(wgt, m, il);
-#endif
       double vr, vi;
-#if CIP_PLACE_ABL == 1 || CIP_PLACE_ABL == 4
-      vr = 1.0; vi = 0.0;
-#else
       load_vis(vis, il, vr, vi);
-#endif
       // zero-weight visibilities are skipped by the scatter, whatever they hold
       const bool counted = valid & (wt != 0.0);
       const double a = counted ? fabs(wt) * fmax(fabs(vr), fabs(vi)) : 0.0;
@@ -407,24 +323,8 @@ __device__ __forceinline__ void place_body(const double* __restrict__ uvw, const
                                            (uint32_t)iw0)
                                         : kNoKey;
       const bool bad = valid & !ok;
-      // a time pair: both footprints start on the same cell (the scatter's
-      // placement, bit for bit) and both feed the call's planes; the even
-      // block's visibility leads, the odd block's is absorbed into it
-      uint8_t pair_flag = 0;
-      if (pair_d > 0) {  // wave-uniform; 2-D calls only (no w layer to compare)
-        // the unwrapped footprint-origin floors of both (place_origin's
-        // operations in its order: the own ones are common subexpressions)
-        double fxa, fya, fxb, fyb;
-        origin_floors(u, v, f, g, &fxa, &fya);
-        origin_floors(pu, pv, f, g, &fxb, &fyb);
-        const bool same = pair_has & ok & feeds & (fxa == fxb) & (fya == fyb);
-        pair_flag = same ? (pair_even ? kClassLeader : kClassAbsorbed) : (uint8_t)0;
-      }
-#if CIP_PLACE_ABL != 3
       if (vis_class && valid)
-        vis_class[i] = ok ? (uint8_t)(((((unsigned)ix0 % kTile) * P + (unsigned)iy0 % kTile) & 31u) | pair_flag)
-                          : (uint8_t)0;
-#endif
+        vis_class[i] = ok ? (uint8_t)((((unsigned)ix0 % kTile) * P + (unsigned)iy0 % kTile) & 31u) : (uint8_t)0;
       if (__ballot(bad) != 0ull && lane == 0) atomicOr(err_flag, 1u);
       // the previous lane's key and row: DPP wave_shr:1 (a VALU move; __shfl_up
       // is an LDS ds_bpermute with its own latency); lane 0 is a start anyway
@@ -439,11 +339,7 @@ __device__ __forceinline__ void place_body(const double* __restrict__ uvw, const
       unsigned wbase = 0;
       if (lane == 0 && emits) wbase = atomicAdd(&s_nruns, (unsigned)__popcll(emits));
       wbase = (unsigned)__builtin_amdgcn_readlane((int)wbase, 0);  // lane 0's slot base (scalar)
-#if CIP_PLACE_ABL == 2
-      if (emit && key == 0x7fffffffu) {
-#else
       if (emit) {
-#endif
         const unsigned long long above = starts & ~((2ull << lane) - 1ull);  // lane 63: 2 << 63 == 0
         const int next = above ? (__ffsll((long long)above) - 1) : nvalid;
         const int64_t slot = blk * kPlaceSegs * 64 + wbase + __popcll(emits & ((1ull << lane) - 1ull));
@@ -455,16 +351,11 @@ __device__ __forceinline__ void place_body(const double* __restrict__ uvw, const
           park_key[slot] = key;
           park_run[slot] = ((uint64_t)r << 32) | ((uint64_t)c << 16) | (uint64_t)(c + (next - lane));
         }
-        // the run's row pre-scaled (u nu dx, v nv dy) in fp32: the order pass
-        // recomputes each visibility's bank class from it and f / c, with no
-        // per-visibility class array and no uvw gather
-        if (park_uv)
-          park_uv[slot] = __builtin_bit_cast(uint64_t, make_float2((float)(u * g.scale_u), (float)(v * g.scale_v)));
       }
     }
   }
   __shared__ double ss[4], sm[4];
-  if constexpr (LOADVIS) {
+  {
     if (nonfinite) atomicOr(err_flag, 2u);
     for (int d = 32; d > 0; d >>= 1) {
       wsum += __shfl_xor(wsum, d, 64);
@@ -478,7 +369,7 @@ __device__ __forceinline__ void place_body(const double* __restrict__ uvw, const
   __syncthreads();
   if constexpr (PLACE) hist0[(int64_t)threadIdx.x * nblocks + blk] = s_hist[threadIdx.x];
   if (threadIdx.x == 0) {
-    if constexpr (LOADVIS) {
+    {
       partial[2 * blk] = (ss[0] + ss[1]) + (ss[2] + ss[3]);
       partial[2 * blk + 1] = fmax(fmax(sm[0], sm[1]), fmax(sm[2], sm[3]));
     }
@@ -492,7 +383,7 @@ __device__ __forceinline__ void place_body(const double* __restrict__ uvw, const
 // The place pass (reduction fused, the place block = this workgroup); PLACE =
 // false: the reduction alone (CIP_REUSE_PLAN calls).
 template <typename VisT, int WK, bool PLACE = true, int RM = 0>
-__global__ __launch_bounds__(256, CIP_PLACE_WAVES) void plan_place_kernel(const double* __restrict__ uvw,
+__global__ __launch_bounds__(256) void plan_place_kernel(const double* __restrict__ uvw,
                                                          const double* __restrict__ fx, RowMap m,
                                                          const VisT* __restrict__ vis, const void* __restrict__ wgt,
                                                          GridGeometry g, unsigned* err_flag,
@@ -500,32 +391,10 @@ __global__ __launch_bounds__(256, CIP_PLACE_WAVES) void plan_place_kernel(const 
                                                          int64_t* __restrict__ blk_cnt,
                                                          uint32_t* __restrict__ park_key,
                                                          uint64_t* __restrict__ park_run, double* partial,
-                                                         int64_t* __restrict__ hist0,
-                                                         uint64_t* __restrict__ park_uv = nullptr) {
-  place_body<VisT, WK, PLACE, true, RM>(uvw, fx, m, vis, wgt, g, err_flag, vis_class, blk_cnt, park_key, park_run,
-                                        partial, hist0, park_uv, blockIdx.x, gridDim.x);
+                                                         int64_t* __restrict__ hist0) {
+  place_body<VisT, WK, PLACE, RM>(uvw, fx, m, vis, wgt, g, err_flag, vis_class, blk_cnt, park_key, park_run, partial,
+                                  hist0, blockIdx.x, gridDim.x);
 }
-
-// The split place pass (CIP_PLACE_SPLIT=1): workgroup 2 b places place block
-// b (uvw + f / c only), workgroup 2 b + 1 reduces its visibilities' weights
-// and values in the fused pass's order (the same partials bit for bit): the
-// streaming read and the VALU-heavy placement run in different waves side by
-// side on the CUs instead of one memory round trip per placed segment.
-template <typename VisT, int WK, int RM>
-__global__ __launch_bounds__(256, CIP_PLACE_WAVES) void plan_place_split_kernel(
-    const double* __restrict__ uvw, const double* __restrict__ fx, RowMap m, const VisT* __restrict__ vis,
-    const void* __restrict__ wgt, GridGeometry g, unsigned* err_flag, uint8_t* __restrict__ vis_class,
-    int64_t* __restrict__ blk_cnt, uint32_t* __restrict__ park_key, uint64_t* __restrict__ park_run,
-    double* partial, int64_t* __restrict__ hist0, uint64_t* __restrict__ park_uv) {
-  const int64_t nb = gridDim.x / 2;
-  if (blockIdx.x & 1)
-    place_body<VisT, WK, false, true, RM>(uvw, fx, m, vis, wgt, g, err_flag, vis_class, blk_cnt, park_key, park_run,
-                                          partial, hist0, park_uv, blockIdx.x >> 1, nb);
-  else
-    place_body<VisT, WK, true, false, RM>(uvw, fx, m, vis, wgt, g, err_flag, vis_class, blk_cnt, park_key, park_run,
-                                          partial, hist0, park_uv, blockIdx.x >> 1, nb);
-}
-
 
 static unsigned plan_blocks(int64_t nvis) {
   const int64_t segs = (nvis + 63) / 64;
@@ -534,17 +403,6 @@ static unsigned plan_blocks(int64_t nvis) {
 }
 
 int plan_place_blocks(int64_t nvis) { return (int)plan_blocks(nvis); }
-
-// CIP_PLACE_SPLIT=1: the placement and the weight / visibility reduction in
-// separate workgroups of one launch (plan_place_split_kernel); 0 (default):
-// one fused pass
-static bool place_split() {
-  static const bool on = [] {
-    const char* e = getenv("CIP_PLACE_SPLIT");
-    return e && e[0] == '1';
-  }();
-  return on;
-}
 
 hipError_t launch_prep_reduce(const RowMap& m, const void* vis, int vis_dtype, const void* wgt, int wgt_dtype,
                               const GridGeometry& g, unsigned* err_flag, double* partial, hipStream_t s) {
@@ -571,26 +429,17 @@ hipError_t launch_prep_reduce(const RowMap& m, const void* vis, int vis_dtype, c
 hipError_t launch_plan_place(const double* uvw, const double* fx, const RowMap& m,
                              const void* vis, int vis_dtype, const void* wgt, int wgt_dtype, const GridGeometry& g,
                              unsigned* err_flag, uint8_t* vis_class, int64_t* blk_cnt, uint32_t* park_key,
-                             uint64_t* park_run, double* partial, int64_t* hist0, hipStream_t s,
-                             uint64_t* park_uv) {
+                             uint64_t* park_run, double* partial, int64_t* hist0, hipStream_t s) {
   const dim3 gd(plan_blocks(m.nvis));
-  const dim3 gd2(2 * plan_blocks(m.nvis));
-  const int rm = m.delta != nullptr ? 2 : (m.pair_d != nullptr ? 1 : 0);
+  const int rm = m.delta != nullptr ? 2 : 0;
 #define PLACE_RM(VT, WKV, RMV)                                                                                      \
-  if (place_split())                                                                                                \
-    plan_place_split_kernel<VT, WKV, RMV><<<gd2, dim3(256), 0, s>>>(uvw, fx, m, (const VT*)vis, wgt, g, err_flag,   \
-                                                                    vis_class, blk_cnt, park_key, park_run,         \
-                                                                    partial, hist0, park_uv);                       \
-  else                                                                                                              \
-    plan_place_kernel<VT, WKV, true, RMV><<<gd, dim3(256), 0, s>>>(uvw, fx, m, (const VT*)vis, wgt, g, err_flag,   \
-                                                                   vis_class, blk_cnt, park_key, park_run, partial, \
-                                                                   hist0, park_uv)
+  plan_place_kernel<VT, WKV, true, RMV><<<gd, dim3(256), 0, s>>>(uvw, fx, m, (const VT*)vis, wgt, g, err_flag,     \
+                                                                 vis_class, blk_cnt, park_key, park_run, partial,   \
+                                                                 hist0)
 #define PLACE(VT, WKV)            \
   do {                            \
     if (rm == 2) {                \
       PLACE_RM(VT, WKV, 2);       \
-    } else if (rm == 1) {         \
-      PLACE_RM(VT, WKV, 1);       \
     } else {                      \
       PLACE_RM(VT, WKV, 0);       \
     }                             \
@@ -724,15 +573,10 @@ __global__ void radix_group_hist_kernel(const int64_t* __restrict__ hist0, int64
   hg[t] = sum;
 }
 
-#ifndef CIP_RADIX_WAVES
-#define CIP_RADIX_WAVES 1  // min waves per SIMD the radix scatter is compiled for (experiment builds)
-#endif
-template <bool V2>
-__global__ __launch_bounds__(kRadixThreads, CIP_RADIX_WAVES) void radix_scatter_kernel(
+__global__ __launch_bounds__(kRadixThreads) void radix_scatter_kernel(
     const uint32_t* __restrict__ keys, const uint64_t* __restrict__ vals, int64_t n,
     const int64_t* __restrict__ blk_cnt, int64_t nsub, int G, int shift, int64_t ngroups,
-    const int64_t* __restrict__ hist, uint32_t* __restrict__ keys_out, uint64_t* __restrict__ vals_out,
-    const uint64_t* __restrict__ vals2 = nullptr, uint64_t* __restrict__ vals2_out = nullptr) {
+    const int64_t* __restrict__ hist, uint32_t* __restrict__ keys_out, uint64_t* __restrict__ vals_out) {
   __shared__ unsigned wcnt[4][256];  // per-wave running digit counts
   __shared__ int64_t dnext[256];     // the group's next position per digit
   __shared__ int64_t woff[4][256];   // global position of each wave's first item per digit
@@ -755,13 +599,12 @@ __global__ __launch_bounds__(kRadixThreads, CIP_RADIX_WAVES) void radix_scatter_
 #pragma unroll
     for (int w = 0; w < 4; ++w) wcnt[w][threadIdx.x] = 0u;
     uint32_t key[kRadixPer];
-    uint64_t val[kRadixPer], val2[kRadixPer];
+    uint64_t val[kRadixPer];
 #pragma unroll
     for (int k = 0; k < kRadixPer; ++k) {
       const int64_t i = i0 + k * 64;
       key[k] = (k < steps && i < lim) ? keys[i] : 0u;
       val[k] = (k < steps && i < lim) ? vals[i] : 0ull;
-      if constexpr (V2) val2[k] = (k < steps && i < lim) ? vals2[i] : 0ull;
     }
     __syncthreads();
     unsigned rank[kRadixPer];
@@ -800,7 +643,6 @@ __global__ __launch_bounds__(kRadixThreads, CIP_RADIX_WAVES) void radix_scatter_
         const int64_t pos = woff[wave][(key[k] >> shift) & 255u] + rank[k];
         keys_out[pos] = key[k];
         vals_out[pos] = val[k];
-        if constexpr (V2) vals2_out[pos] = val2[k];
       }
     __syncthreads();  // wcnt / woff are reused by the next sub-block
   }
@@ -841,16 +683,11 @@ hipError_t launch_radix_group_hist(const int64_t* hist0, int64_t nsub, int G, in
 
 hipError_t launch_radix_scatter(const uint32_t* keys, const uint64_t* vals, int64_t n, const int64_t* blk_cnt,
                                 int64_t nsub, int G, int shift, const int64_t* hist, uint32_t* keys_out,
-                                uint64_t* vals_out, hipStream_t s, const uint64_t* vals2, uint64_t* vals2_out) {
+                                uint64_t* vals_out, hipStream_t s) {
   if (nsub == 0) return hipSuccess;
   const int64_t ngroups = (nsub + G - 1) / G;
-  // vals2 (optional): a second 8-byte value per item moved with it
-  if (vals2)
-    radix_scatter_kernel<true><<<dim3((unsigned)ngroups), dim3(kRadixThreads), 0, s>>>(
-        keys, vals, n, blk_cnt, nsub, G, shift, ngroups, hist, keys_out, vals_out, vals2, vals2_out);
-  else
-    radix_scatter_kernel<false><<<dim3((unsigned)ngroups), dim3(kRadixThreads), 0, s>>>(
-        keys, vals, n, blk_cnt, nsub, G, shift, ngroups, hist, keys_out, vals_out);
+  radix_scatter_kernel<<<dim3((unsigned)ngroups), dim3(kRadixThreads), 0, s>>>(
+      keys, vals, n, blk_cnt, nsub, G, shift, ngroups, hist, keys_out, vals_out);
   return hipGetLastError();
 }
 

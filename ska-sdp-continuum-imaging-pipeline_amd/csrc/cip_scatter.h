@@ -18,24 +18,7 @@
 
 #include "cip_internal.h"
 
-// Experiment-only builds (tools/build_variant.sh): 1 = conflict-free LDS
-// addresses, 2 = no LDS atomics, 3 = no kernel evaluation, 4 = no flush to
-// HBM (timing only, wrong images). 0 in the library. Measured at C3
-// (profiles/microbench_r01.txt): kernel evaluation ~0.2 ms, flush ~0.1 ms of
-// the 3.1 ms scatter.
-#ifndef CIP_ABLATE
-#define CIP_ABLATE 0
-#endif
-
-// CIP_TAP_BIAS=1 (fp64 class, one plane per unit): the taps add the raw bits
-// of fma(k, v, 1.5 2^52) - the integer plus the constant bias 0x4338 << 48 -
-// with no per-tap subtraction; each item counts itself at its footprint
-// origin (one ds_add_u32), and the flush removes n x bias from a cell, n =
-// the items whose W x W footprint covers it (a box sum of the origin counts).
-// One VALU instruction per tap and component fewer; the same integers.
-#ifndef CIP_TAP_BIAS
-#define CIP_TAP_BIAS 0
-#endif
+// the bits of fma(k, v, 1.5 2^52) are the integer plus this bias
 constexpr unsigned long long kTapBias = 0x4338000000000000ull;
 
 namespace cip {
@@ -158,10 +141,6 @@ __device__ __forceinline__ VisFetch from_raw(const RawFetch<VisT, WK>& r, bool u
   return f;
 }
 
-#ifdef CIP_COUNT_KBLOCKS
-extern __device__ unsigned long long cip_kblock_count[192];
-#endif
-
 // One packed single-precision tap (CIP_ACC_SINGLE): the contributions
 // ku * kr and ku * ki rounded to integers in fp32 by one packed fma against
 // 1.5 * 2^23 (exact for |x| < 2^22, which packed_chunk_gain guarantees): the
@@ -223,24 +202,9 @@ __device__ __forceinline__ void grid_fetched_packed(const VisFetch& f, const Gri
   } else {
     float kwv[W];
     eval_kernel_f32<W>((float)yw, kwv);
-#ifdef CIP_COUNT_KBLOCKS
-    // experiment builds: per lane, slot lane counts the visits, slot 64 + lane
-    // the plane blocks it executes with work and slot 128 + lane those its
-    // wave executes (vector atomics on lane-indexed slots)
-    atomicAdd(&cip_kblock_count[threadIdx.x & 63u], 1ull);
-#endif
 #pragma unroll
     for (int k = 0; k < G; ++k) {
       const int64_t kw = plane + k - iw0;
-#ifdef CIP_COUNT_KBLOCKS
-      {
-        const unsigned ln = threadIdx.x & 63u;
-        const bool work = !(kw < 0 || kw >= W);
-        const unsigned long long any = __ballot(work);
-        if (any) atomicAdd(&cip_kblock_count[128 + ln], 1ull);
-        if (work) atomicAdd(&cip_kblock_count[64 + ln], 1ull);
-      }
-#endif
       if (kw < 0 || kw >= W) continue;  // the visibility does not feed plane + k
       if (plane + k < g.plane_lo || plane + k >= g.plane_hi) continue;  // outside the call's plane range
       float sel = 0.0f;
@@ -254,19 +218,15 @@ __device__ __forceinline__ void grid_fetched_packed(const VisFetch& f, const Gri
 // One visibility onto the unit's sub-grid(s). G > 1 (w-stacking): the unit
 // grids planes plane .. plane + G - 1 at once (G sub-grids, S u64 apart), the
 // visibility placed and its u, v, w kernels evaluated once for all of them.
-template <int W, bool WSTACK, bool PACK, int G = 1, bool BIAS = false>
+template <int W, bool WSTACK, bool PACK, int G = 1>
 __device__ __forceinline__ void grid_fetched(const VisFetch& f, const GridGeometry& g, int64_t plane, int64_t X0,
-                                             int64_t Y0, double fixed_scale, unsigned long long* sub,
-                                             unsigned* cnt = nullptr) {
-  static_assert(!BIAS || (!PACK && G == 1), "tap bias: fp64 class, one plane per unit");
+                                             int64_t Y0, double fixed_scale, unsigned long long* sub) {
   constexpr int T = kTile;
   constexpr int P = T + W - 1;
-#if CIP_ABLATE == 0 || CIP_ABLATE == 4
   if constexpr (PACK) {
     grid_fetched_packed<W, WSTACK, G>(f, g, plane, X0, Y0, fixed_scale, sub);
     return;
   }
-#endif
   if (f.wt == 0.0) return;
   int64_t ix0, iy0, iw0;
   double yu, yv, yw;
@@ -312,8 +272,8 @@ __device__ __forceinline__ void grid_fetched(const VisFetch& f, const GridGeomet
                 "s"(0u - kMagicHi));
             atomicAdd(bk + (i * P + j), __builtin_bit_cast(unsigned long long, make_uint2((unsigned)bi, hi)));
           } else {
-            atomicAdd(bk + (i * P + j), br - 0x4338000000000000ull);
-            atomicAdd(bk + P * P + (i * P + j), bi - 0x4338000000000000ull);
+            atomicAdd(bk + (i * P + j), br - kTapBias);
+            atomicAdd(bk + P * P + (i * P + j), bi - kTapBias);
           }
         }
       }
@@ -332,18 +292,9 @@ __device__ __forceinline__ void grid_fetched(const VisFetch& f, const GridGeomet
     sc *= sel;
   }
   const double vr = f.vr * sc, vi = f.vi * sc;
-  if constexpr (BIAS) atomicAdd(cnt + (lx * P + ly), 1u);  // the item's origin (its bias count)
   double ku[W], kv[W];
-#if CIP_ABLATE == 3
-#pragma unroll
-  for (int k = 0; k < W; ++k) {
-    ku[k] = yu + (double)k;
-    kv[k] = yv - (double)k;
-  }
-#else
   eval_kernel<W>(yu, ku);
   eval_kernel<W>(yv, kv);
-#endif
   double kr[W], ki[W];
 #pragma unroll
   for (int j = 0; j < W; ++j) {
@@ -353,15 +304,7 @@ __device__ __forceinline__ void grid_fetched(const VisFetch& f, const GridGeomet
   // separate re / im planes: a lane-scattered 8-byte add touches 2 of the 64
   // LDS banks, so 8-byte cells spread a wave over twice the bank pairs that
   // interleaved 16-byte (re, im) cells would
-#if CIP_ABLATE == 1
-  unsigned long long* base = sub + ((threadIdx.x & 31) + ((threadIdx.x & 32) ? 8 * P : 0));
-#else
   unsigned long long* base = sub + (lx * P + ly);
-#endif
-#if CIP_ABLATE == 2
-  unsigned long long acc = 0;
-#define atomicAdd(p, v) (acc += (v) ^ (unsigned long long)((p) - sub))
-#endif
 #pragma unroll
   for (int i = 0; i < W; ++i) {
 #pragma unroll
@@ -374,47 +317,26 @@ __device__ __forceinline__ void grid_fetched(const VisFetch& f, const GridGeomet
         // bits(kMagic + k) = 0x43380000'00000000 + k (two's complement), so
         // re * 2^32 + im = {lo32(br) + hi32(bi) - 0x43380000, lo32(bi)}
         unsigned hi;  // one v_add3_u32 (the compiler otherwise widens it to 64-bit adds)
-#if CIP_ABLATE == 2
-        hi = (unsigned)br + (unsigned)(bi >> 32) + (0u - kMagicHi);
-#else
         asm("v_add3_u32 %0, %1, %2, %3" : "=v"(hi) : "v"((unsigned)br), "v"((unsigned)(bi >> 32)),
             "s"(0u - kMagicHi));
-#endif
         atomicAdd(base + (i * P + j), __builtin_bit_cast(unsigned long long, make_uint2((unsigned)bi, hi)));
       } else {
-        atomicAdd(base + (i * P + j), BIAS ? br : br - kTapBias);
-        atomicAdd(base + P * P + (i * P + j), BIAS ? bi : bi - kTapBias);
+        atomicAdd(base + (i * P + j), br - kTapBias);
+        atomicAdd(base + P * P + (i * P + j), bi - kTapBias);
       }
     }
   }
-#if CIP_ABLATE == 2
-#undef atomicAdd
-  if (acc == 0x123456789ull) sub[0] = acc;
-#endif
 }
 
 // Flush the touched cells of a work unit's sub-grid(s) to the HBM grid(s)
 // (called after the unit's last LDS atomic and a barrier).
-template <int W, bool PACK, int G, int NT, bool BIAS = false>
+template <int W, bool PACK, int G, int NT>
 __device__ __forceinline__ void flush_subgrid(const unsigned long long* sub, const GridGeometry& g, int64_t plane,
                                               int64_t X0, int64_t Y0, const Chunk& ch, int store_private,
-                                              double inv_scale, double* __restrict__ grid, unsigned* cnt = nullptr) {
+                                              double inv_scale, double* __restrict__ grid) {
   constexpr int T = kTile;
   constexpr int P = T + W - 1;
   constexpr int S = P * P * (PACK ? 1 : 2);
-  if constexpr (BIAS) {
-    // n(x, y) = items with origin in [x - W + 1, x] x [y - W + 1, y]: the
-    // origin counts (cnt[0 .. P^2)) summed over x into cnt[P^2 ..), then over
-    // y per cell below
-    for (int cell = threadIdx.x; cell < P * P; cell += NT) {
-      const int lx = cell / P, ly = cell - lx * P;
-      unsigned a = 0u;
-#pragma unroll
-      for (int i = 0; i < W; ++i) a += (lx - i >= 0) ? cnt[(lx - i) * P + ly] : 0u;
-      cnt[P * P + cell] = a;
-    }
-    __syncthreads();
-  }
   // flush the touched cells of the sub-grid(s) to the fp64 HBM grid(s)
   // (lanes walk the HBM grid's contiguous axis: y, or x when it is stored
   // transposed for the pruned FFT); plane group: plane + k -> grid + k planes.
@@ -438,27 +360,15 @@ __device__ __forceinline__ void flush_subgrid(const unsigned long long* sub, con
     unsigned long long sv[G];  // PACK: re * 2^32 + im
     unsigned long long si[G];  // !PACK: the im plane
     bool any = false;
-    unsigned long long bias = 0ull;  // BIAS: n x kTapBias, removed from both planes
-    if constexpr (BIAS) {
-      const int lx = lcell / P, ly = lcell - (lcell / P) * P;
-      unsigned n = 0u;
-#pragma unroll
-      for (int j = 0; j < W; ++j) n += (ly - j >= 0) ? cnt[P * P + lx * P + ly - j] : 0u;
-      if (n == 0u) continue;  // no item's footprint covers the cell
-      bias = (unsigned long long)n * kTapBias;
-    }
 #pragma unroll
     for (int k = 0; k < G; ++k) {
       sv[k] = 0ull;
       si[k] = 0ull;
       if (G > 1 && (plane + k >= g.nplanes || plane + k < g.plane_lo || plane + k >= g.plane_hi)) continue;
-      sv[k] = sub[k * S + lcell] - bias;
-      if constexpr (!PACK) si[k] = sub[k * S + P * P + lcell] - bias;
+      sv[k] = sub[k * S + lcell];
+      if constexpr (!PACK) si[k] = sub[k * S + P * P + lcell];
       any |= (sv[k] | si[k]) != 0ull;
     }
-#if CIP_ABLATE == 4
-    any = any && sv[0] == 0x123456789ull;  // ablation: no flush (timing only)
-#endif
     if (!any) continue;
     // the sub-grid of an edge tile wraps around the periodic grid
     int64_t gx = X0 + lcell / P, gy = Y0 + lcell % P;
@@ -525,8 +435,6 @@ __global__ __launch_bounds__(scatter_threads<G>(), CIP_SCATTER_WAVES) void scatt
   constexpr int S = P * P * (PACK ? 1 : 2);
   constexpr int NT = scatter_threads<G>();
   __shared__ unsigned long long sub[G * S];
-  constexpr bool kBias = CIP_TAP_BIAS != 0 && !PACK && G == 1;
-  __shared__ unsigned s_cnt[kBias ? 2 * P * P : 1];  // origin counts, then their x sums
   __shared__ int64_t s_voff[PERM ? 1 : kRunBatch + 1];
   __shared__ uint64_t s_run[PERM ? 1 : kRunBatch];
   constexpr bool kWide = PERM == 2;
@@ -535,8 +443,6 @@ __global__ __launch_bounds__(scatter_threads<G>(), CIP_SCATTER_WAVES) void scatt
   int64_t X0, Y0;
   tile_origin(ch.tile, g, &X0, &Y0);
   for (int i = threadIdx.x; i < G * S; i += NT) sub[i] = 0ull;
-  if constexpr (kBias)
-    for (int i = threadIdx.x; i < P * P; i += NT) s_cnt[i] = 0u;
   if constexpr (PACK) {
     fixed_scale *= packed_chunk_gain(ch.g1 - ch.g0);
     inv_scale = 1.0 / fixed_scale;
@@ -563,8 +469,7 @@ __global__ __launch_bounds__(scatter_threads<G>(), CIP_SCATTER_WAVES) void scatt
       const uint64_t pnn = perm_entry_t<kWide>(perm, hnn ? qnn : q);
       RawFetch<VisT, WK> nxt;
       fetch_raw<VisT, WK, kWide>(pn, uvw, fx, vis_ld, unit_vis, wgt, m, nxt);
-      grid_fetched<W, WSTACK, PACK, G, kBias>(from_raw<VisT, WK>(cur, unit_vis), g, plane, X0, Y0, fixed_scale, sub,
-                                              s_cnt);
+      grid_fetched<W, WSTACK, PACK, G>(from_raw<VisT, WK>(cur, unit_vis), g, plane, X0, Y0, fixed_scale, sub);
       cur = nxt;
       q = qn;
       have = hn;
@@ -595,7 +500,7 @@ __global__ __launch_bounds__(scatter_threads<G>(), CIP_SCATTER_WAVES) void scatt
         const bool hn = qn < bend;
         VisFetch nxt;
         if (hn) fetch_vis<VisT, WK>(qn, s_voff, s_run, nst, uvw, fx, vis, wgt, m, nxt);
-        grid_fetched<W, WSTACK, PACK, G, kBias>(cur, g, plane, X0, Y0, fixed_scale, sub, s_cnt);
+        grid_fetched<W, WSTACK, PACK, G>(cur, g, plane, X0, Y0, fixed_scale, sub);
         cur = nxt;
         q = qn;
         have = hn;
@@ -605,182 +510,7 @@ __global__ __launch_bounds__(scatter_threads<G>(), CIP_SCATTER_WAVES) void scatt
     }
   }
   __syncthreads();
-  flush_subgrid<W, PACK, G, NT, kBias>(sub, g, plane, X0, Y0, ch, store_private, inv_scale, grid, s_cnt);
-}
-
-// ------------------------------------------------------- time pairs ----
-// The 2-D fp64-class scatter over the time-paired ordered stream (dense rows,
-// RowMap::pair_d). An entry is a single visibility, a pair
-// leader (kPermLeader: row r of an even dump block, whose row r + D at the
-// same channel starts its footprint on the same cell - the planner checked it
-// with this placement, bit for bit) or kPermNull (an absorbed partner's
-// position). A pair grids BOTH visibilities with one 64-bit fixed-point
-// atomic per tap and component: fma(ku_a, kr_a, fma(ku_b, kr_b, 1.5 2^52))
-// rounds each product to the integer grid in turn, so the item's integer is a
-// fixed function of its two visibilities (the sums stay exact and
-// order-independent; within one quantum of the two separately rounded
-// contributions). At C3 58 % of the visibilities pair: 0.71 LDS items per
-// visibility.
-template <typename VisT, int WK>
-struct PairFetch {
-  using WT = typename std::conditional<WK == WK_F64, double, float>::type;
-  double u, v, fx, u2, v2;  // 2-D only: no w
-  VisT vis, vis2;
-  WT wt, wt2;
-  int kind;  // 0 null, 1 single, 2 pair
-};
-
-template <typename VisT, int WK>
-__device__ __forceinline__ void fetch_pair(uint32_t e, int64_t pair_d, const double* __restrict__ uvw,
-                                           const double* __restrict__ fx, const VisT* __restrict__ vis_ld,
-                                           bool unit_vis, const void* __restrict__ wgt, const RowMap& m,
-                                           PairFetch<VisT, WK>& f) {
-  using WT = typename PairFetch<VisT, WK>::WT;
-  // branch-free: a null entry loads visibility 0, a single its own row twice
-  f.kind = e == kPermNull ? 0 : ((e & kPermLeader) ? 2 : 1);
-  const int64_t il = e == kPermNull ? 0 : (int64_t)(e & ~kPermLeader);
-  int64_t r, c;
-  split_index64(il, m.nchan, m.inv_nchan, &r, &c);
-  const int64_t r2 = f.kind == 2 ? r + pair_d : r;
-  const int64_t il2 = f.kind == 2 ? il + pair_d * m.nchan : il;
-  f.u = uvw[3 * r];
-  f.v = uvw[3 * r + 1];
-  f.u2 = uvw[3 * r2];
-  f.v2 = uvw[3 * r2 + 1];
-  f.fx = fx[c];
-  f.vis = vis_ld[unit_vis ? 0 : il];
-  f.vis2 = vis_ld[unit_vis ? 0 : il2];
-  if constexpr (WK != WK_NONE) {
-    f.wt = ((const WT*)wgt)[il];
-    f.wt2 = ((const WT*)wgt)[il2];
-  }
-}
-
-template <int W, typename VisT, int WK, bool BIAS>
-__device__ __forceinline__ void grid_pair(const PairFetch<VisT, WK>& f, bool unit_vis, const GridGeometry& g,
-                                          int64_t X0, int64_t Y0, double fixed_scale, unsigned long long* sub,
-                                          unsigned* cnt) {
-  constexpr int T = kTile;
-  constexpr int P = T + W - 1;
-  const bool pr = f.kind == 2;
-  const double wa = WK == WK_NONE ? 1.0 : (double)f.wt, wb = WK == WK_NONE ? 1.0 : (double)f.wt2;
-  if (f.kind == 0 || (wa == 0.0 && !(pr && wb != 0.0))) return;
-  int64_t ix0, iy0, iw0;
-  double yu, yv, yw;
-  if (!place_vis(f.u, f.v, 0.0, f.fx, g, &ix0, &yu, &iy0, &yv, &iw0, &yw)) return;
-  const int64_t lx = ix0 - X0, ly = iy0 - Y0;
-  if (lx < 0 || lx >= T || ly < 0 || ly >= T) return;  // never for a consistent plan
-  // the visibilities' values scaled to the fixed point (zero-weight members
-  // contribute an exact zero, whatever their values hold)
-  const double vra = wa == 0.0 ? 0.0 : (unit_vis ? 1.0 : (double)f.vis.x) * (wa * fixed_scale);
-  const double via = wa == 0.0 ? 0.0 : (unit_vis ? 0.0 : (double)f.vis.y) * (wa * fixed_scale);
-  double vrb = 0.0, vib = 0.0, yub = yu, yvb = yv;
-  if (__ballot(pr) != 0ull) {
-    int64_t jx0, jy0, jw0;
-    double ywb;
-    const bool okb = place_vis(f.u2, f.v2, 0.0, f.fx, g, &jx0, &yub, &jy0, &yvb, &jw0, &ywb);
-    const bool same = pr && okb && jx0 == ix0 && jy0 == iy0;
-    if (pr && !same && g.oob) atomicOr(g.oob, 2u);  // a plan / scatter placement mismatch (never)
-    vrb = (same && wb != 0.0) ? (unit_vis ? 1.0 : (double)f.vis2.x) * (wb * fixed_scale) : 0.0;
-    vib = (same && wb != 0.0) ? (unit_vis ? 0.0 : (double)f.vis2.y) * (wb * fixed_scale) : 0.0;
-    yub = same ? yub : yu;
-    yvb = same ? yvb : yv;
-  } else {
-    // a wave of single visibilities: the plain lane kernel
-    VisFetch a;
-    a.u = f.u;
-    a.v = f.v;
-    a.w = 0.0;
-    a.fx = f.fx;
-    a.vr = unit_vis ? 1.0 : (double)f.vis.x;
-    a.vi = unit_vis ? 0.0 : (double)f.vis.y;
-    a.wt = wa;
-    grid_fetched<W, false, false, 1, BIAS>(a, g, 0, X0, Y0, fixed_scale, sub, cnt);
-    return;
-  }
-  if constexpr (BIAS) atomicAdd(cnt + (lx * P + ly), 1u);  // one bias per item (the pair's nested fma)
-  // the u kernels of both visibilities held (2 W values); the v kernels
-  // streamed in mirrored pairs of columns j = k, W - 1 - k (the even / odd
-  // halves of eval_kernel) - 48 live fp64 registers of taps instead of 72
-  double kua[W], kub[W];
-  eval_kernel<W>(yu, kua);
-  eval_kernel<W>(yub, kub);
-  unsigned long long* base = sub + (lx * P + ly);
-  const double za = yv * yv, zb = yvb * yvb;
-#pragma unroll
-  for (int k = 0; k < W / 2; ++k) {
-    double va[2], vb[2];
-    eval_piece_pair<W>(k, yv, za, va);
-    eval_piece_pair<W>(k, yvb, zb, vb);
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int j = h ? W - 1 - k : k;
-      const double kra = va[h] * vra, kia = va[h] * via, krb = vb[h] * vrb, kib = vb[h] * vib;
-#pragma unroll
-      for (int i = 0; i < W; ++i) {
-        const double qr = fma(kua[i], kra, fma(kub[i], krb, kMagic));
-        const double qi = fma(kua[i], kia, fma(kub[i], kib, kMagic));
-        atomicAdd(base + (i * P + j), (unsigned long long)__double_as_longlong(qr) - (BIAS ? 0ull : kTapBias));
-        atomicAdd(base + P * P + (i * P + j), (unsigned long long)__double_as_longlong(qi) - (BIAS ? 0ull : kTapBias));
-      }
-    }
-  }
-}
-
-#ifndef CIP_PAIR_WAVES
-#define CIP_PAIR_WAVES 4  // min waves per SIMD (the lane kernel's 4; share_cus caps pipelined calls at 3 blocks per CU)
-#endif
-template <int W, typename VisT, int WK>
-__global__ __launch_bounds__(kScatterThreads, CIP_PAIR_WAVES) void scatter_pair_kernel(
-    const double* __restrict__ uvw, const double* __restrict__ fx, const VisT* __restrict__ vis,
-    const void* __restrict__ wgt, RowMap m, const uint32_t* __restrict__ perm, const Chunk* __restrict__ chunks,
-    int64_t chunk_begin, GridGeometry g, double fixed_scale, double inv_scale, double* __restrict__ grid,
-    int store_private) {
-  constexpr int T = kTile;
-  constexpr int P = T + W - 1;
-  constexpr int S = P * P * 2;
-  constexpr int NT = kScatterThreads;
-  __shared__ unsigned long long sub[S];
-  constexpr bool kBias = CIP_TAP_BIAS != 0;
-  __shared__ unsigned s_cnt[kBias ? 2 * P * P : 1];
-  const Chunk ch = chunks[chunk_begin + blockIdx.x];
-  int64_t X0, Y0;
-  tile_origin(ch.tile, g, &X0, &Y0);
-  for (int i = threadIdx.x; i < S; i += NT) sub[i] = 0ull;
-  if constexpr (kBias)
-    for (int i = threadIdx.x; i < P * P; i += NT) s_cnt[i] = 0u;
-  const int64_t pair_d = (int64_t)__builtin_amdgcn_readfirstlane((int)*m.pair_d);
-  __syncthreads();
-  const bool unit_vis = vis == nullptr;
-  const VisT* vis_ld = unit_vis ? (const VisT*)uvw : vis;
-  // software pipeline as scatter_kernel's: the entry of q + 512 and the data
-  // of q + 256 in flight while q grids
-  int64_t q = ch.g0 + threadIdx.x;
-  bool have = q < ch.g1;
-  PairFetch<VisT, WK> cur;
-  int64_t qn = q + NT;
-  bool hn = qn < ch.g1;
-  uint32_t pn = kPermNull;
-  if (have) {
-    fetch_pair<VisT, WK>(perm[q], pair_d, uvw, fx, vis_ld, unit_vis, wgt, m, cur);
-    pn = perm[hn ? qn : q];
-  }
-  while (have) {
-    const int64_t qnn = qn + NT;
-    const bool hnn = qnn < ch.g1;
-    const uint32_t pnn = perm[hnn ? qnn : q];
-    PairFetch<VisT, WK> nxt;
-    fetch_pair<VisT, WK>(hn ? pn : kPermNull, pair_d, uvw, fx, vis_ld, unit_vis, wgt, m, nxt);
-    grid_pair<W, VisT, WK, kBias>(cur, unit_vis, g, X0, Y0, fixed_scale, sub, s_cnt);
-    cur = nxt;
-    q = qn;
-    have = hn;
-    qn = qnn;
-    hn = hnn;
-    pn = pnn;
-  }
-  __syncthreads();
-  flush_subgrid<W, false, 1, NT, kBias>(sub, g, 0, X0, Y0, ch, store_private, inv_scale, grid, s_cnt);
+  flush_subgrid<W, PACK, G, NT>(sub, g, plane, X0, Y0, ch, store_private, inv_scale, grid);
 }
 
 template <int W, typename VisT, int WK>
@@ -811,12 +541,6 @@ inline hipError_t scatter_dispatch_ws(bool ws, int group, bool pack, unsigned ld
 #define LAUNCH_WS_PACKED(PRM)                                \
   {                                                          \
     bool hit = false;                                        \
-    if constexpr (kFitG14) {                                 \
-      if (ws && group == 14) {                               \
-        LAUNCH(true, PRM, true, 14);                         \
-        hit = true;                                          \
-      }                                                      \
-    }                                                        \
     if constexpr (kFitG7) {                                  \
       if (ws && group == 7) {                                \
         LAUNCH(true, PRM, true, 7);                          \
@@ -848,23 +572,12 @@ inline hipError_t scatter_dispatch_ws(bool ws, int group, bool pack, unsigned ld
   // plane groups of 4 / 5 packed sub-grids while they fit 64 KB of static LDS
   constexpr int P2 = (kTile + W - 1) * (kTile + W - 1);
   constexpr bool kFitG5 = 5 * P2 * 8 + 4200 <= 65536;
-  // 6 / 7 (CIP_WSTACK_GROUP, experiment): two blocks per CU in 160 KB
+  // 6 / 7: two blocks per CU in 160 KB
   constexpr bool kFitG7 = 7 * P2 * 8 + 4200 <= 81920;
   constexpr bool kFitG6 = 6 * P2 * 8 + 4200 <= 81920;
-  // 14 (CIP_WSTACK_GROUP=14, experiment): one block per CU in 160 KB (W <= 6)
-  constexpr bool kFitG14 = 14 * P2 * 8 + 4200 <= 163840;
   constexpr bool kFitG4 = 4 * P2 * 8 + 4200 <= 65536;
   bool done = false;
   const bool wide = m.delta != nullptr;  // ragged row slices: u64 entries
-  if constexpr (std::is_same<VisT, float2>::value || std::is_same<VisT, double2>::value) {
-    // time pairs: 2-D fp64 class over the paired dense ordered stream
-    if (m.pair_d != nullptr && perm && !wide && !ws && !pack && group == 1) {
-      scatter_pair_kernel<W, VisT, WK><<<grid_dim, dim3(kScatterThreads), lds_extra, s>>>(
-          uvw, fx, (const VisT*)vis, wgt, m, (const uint32_t*)perm, chunks, chunk_begin, g, fs, 1.0 / fs, grid,
-          store_private);
-      return hipGetLastError();
-    }
-  }
   if constexpr (std::is_same<VisT, float2>::value || std::is_same<VisT, Pol4>::value) {
     if (pack) {
       if (perm && wide) {

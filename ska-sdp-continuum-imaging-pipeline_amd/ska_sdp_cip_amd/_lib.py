@@ -73,7 +73,7 @@ EXPORTED_SYMBOLS = (
 )
 
 PROFILE_PHASES = ("prep", "plan", "scatter", "fft", "correct", "total")
-PROFILE_COUNTS = ("visibilities", "runs", "chunks", "planes", "scatter_launches", "pair_stride")
+PROFILE_COUNTS = ("visibilities", "runs", "chunks", "planes", "scatter_launches", "reserved")
 
 
 class GridderParams(ctypes.Structure):

@@ -141,17 +141,13 @@ def test_async_call_matches_synchronous(gpu_device, wstack, resident):
         assert float(sw.item()) == float(sets[k % 2][3].double().sum().item())
 
 
-@pytest.mark.parametrize("pipe_scatter", ["0", "1"])
-def test_pipelined_calls_interleaved_with_other_calls(gpu_device, monkeypatch, pipe_scatter):
-    """With CIP_PIPE_SCATTER=1 a pipelined 2-D call grids on its plan stream
-    once the previous call's pass A has consumed the workspace grid, so its
-    scatter overlaps that call's pass B (cip_api.hip scatter_on_plan_stream). Calls of another kind
-    in between - synchronous, asynchronous without resident inputs, pipelined
-    w-stacking - also use the grid: the next plan-stream scatter must wait
-    for all of their work. Every image equals its synchronous reference."""
+def test_pipelined_calls_interleaved_with_other_calls(gpu_device):
+    """Pipelined calls (planner on the plan streams) interleaved with calls of
+    another kind - synchronous, asynchronous without resident inputs,
+    pipelined w-stacking - that also use the workspace grid and planner
+    buffers. Every image equals its synchronous reference."""
     import torch
 
-    monkeypatch.setenv("CIP_PIPE_SCATTER", pipe_scatter)  # read per call
     a = _inputs(512)
     b = (a[0], a[1], a[2] * (0.5 - 2.0j), a[3] * 0.25 + 1.0) + a[4:]
     ref = {}

@@ -99,18 +99,3 @@ def test_2d_after_wstacking_same_workspace(gpu_device):
     device_ms2dirty(uvw, f, vis, w, npix, npix, px, px, support=8, do_wstacking=True)
     b, _ = device_ms2dirty(uvw, f, vis, w, npix, npix, px, px, support=8)
     assert torch.equal(a, b)
-
-
-@pytest.mark.parametrize("W", [4, 6])
-def test_fourteen_plane_groups_equal_single_plane_units(gpu_device, W, tmp_path):
-    """CIP_WSTACK_GROUP=14 (the packed class at W <= 6: one 153 KB block per CU
-    holding 14 sub-grids) against one plane per unit, repeated calls included."""
-    imgs = {}
-    for g in ("1", "14"):
-        out = tmp_path / f"g{g}.npy"
-        subprocess.run([sys.executable, "-c", CHILD + "\nimg, _ = device_ms2dirty(t(uvw), t(f), t(vis), t(w), npix, "
-                        "npix, px, px, support=W, do_wstacking=True, single_precision_accumulation=single)\n"
-                        "np.save(out, img.cpu().numpy())\n", str(ROOT), str(W), "512", "1", str(out)],
-                       env=dict(os.environ, CIP_WSTACK_GROUP=g), check=True, timeout=120)
-        imgs[g] = np.load(out)
-    assert np.abs(imgs["14"] - imgs["1"]).max() <= 1e-6 * np.abs(imgs["1"]).max()

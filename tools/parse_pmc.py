@@ -5,6 +5,11 @@ roofline.traffic. gfx950 corrections (MI355X_MICROARCH.md, HBM section):
 FETCH_SIZE (KB) counts exactly half the bytes of wide coalesced reads -> x2;
 WRITE_SIZE (KB) reads the bytes exactly for 16-B stores and float atomics.
 Usage: python tools/parse_pmc.py <round> <config> <dir>...
+Only full-size dispatches are averaged: a dispatch whose counter is below a
+quarter of the kernel's largest (a max|err| sample call on 1/50 of the rows,
+say) is dropped and counted. Rounds 3 and 4 averaged such a sample into the
+per-launch figures (10 dispatches, one of them 2M visibilities): their
+scatter / order / place reads read 10 % low (profiles/r06_pmc_delta.md).
 """
 import csv
 import json
@@ -32,6 +37,14 @@ def main():
     lines = [f"# PMC summary {rnd} ({config}); per-dispatch averages", "",
              "| kernel | dispatches | FETCH_SIZE KB (raw) | HBM read bytes (x2) | WRITE_SIZE KB | TCC_EA0_ATOMIC |",
              "|---|---|---|---|---|---|"]
+    dropped = {}
+    for k, cs in list(vals.items()):
+        for c, v in cs.items():
+            top = max(v) if v else 0.0
+            keep = [x for x in v if x >= 0.25 * top] if top > 0 else v
+            if len(keep) < len(v):
+                dropped[f"{k}/{c}"] = len(v) - len(keep)
+            cs[c] = keep
     for k, cs in sorted(vals.items(), key=lambda kv: -sum(kv[1].get("FETCH_SIZE", [0]))):
         avg = {c: sum(v) / len(v) for c, v in cs.items()}
         n = max(len(v) for v in cs.values())
@@ -52,6 +65,9 @@ def main():
                    "source": f"profiles/{rnd}_pmc_summary.md"}
         Path("profiles").mkdir(exist_ok=True)
         Path(f"profiles/traffic_{config}.json").write_text(json.dumps(traffic, indent=1))
+    if dropped:
+        lines += ["", "Dropped small dispatches (below 1/4 of the kernel's largest): " +
+                  ", ".join(f"{k} x{n}" for k, n in sorted(dropped.items()))]
     Path(f"profiles/{rnd}_pmc_summary.md").write_text("\n".join(lines) + "\n")
     print("\n".join(lines))
 
