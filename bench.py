@@ -271,24 +271,35 @@ def run_strong(args, world, rank, device, steps=None, warmup=None):
     uvw = torch.from_numpy(uvw_h).to(device)
     freq = torch.from_numpy(freq_h).to(device)
     params = _lib.choose_params(npix, npix, px, px, 1e-4, args.support)
+    # the MS's dense (rows, nchan) columns, resident: counter-based values -
+    # every visibility's value and weight are a pure function of its global
+    # (row, channel) index, so every rank count grids the SAME 1G visibilities
+    # into the same image (parity across N)
+    r_all = torch.arange(rows, device=device)
+    vis_all, wgt_all = syn.counter_columns_slices(r_all, torch.zeros_like(r_all), torch.full_like(r_all, nchan), nchan,
+                                                  seed)
+    del r_all
+    # the strip split on the device (cip_strips.hip): the per-row cost
+    # histogram -> balanced strip bounds, then this rank's row slices with its
+    # visibilities and weights gathered into the Tile layout (the reference's
+    # offline reorder_by_uvw_tile step, cut by strip) - once per data set,
+    # timed and reported as plan_ms
+    torch.cuda.synchronize()
     t0 = time.perf_counter()
     layout = strips.plan_strips(uvw, freq, params, px, npix, npix, world)
-    rws, c0, c1 = strips.strip_slices(uvw, freq, params, px, *layout.rows(rank))
+    data = strips.split_strip(uvw, freq, vis_all, wgt_all, params, px, *layout.rows(rank))
+    torch.cuda.synchronize()
     t_plan = time.perf_counter() - t0
-    lengths = (c1 - c0)
-    nvis = int(lengths.sum())
-    # counter-based columns: every visibility's value and weight are a pure
-    # function of its global (row, channel) index, so every rank count grids
-    # the SAME 1G visibilities into the same image (parity across N)
-    vis, wgt = syn.counter_columns_slices(rws, c0, c1, nchan, seed)
-    data = strips.StripData(uvw[rws].contiguous(), c0.to(torch.int32), c1.to(torch.int32), vis, wgt, rws)
-    del uvw
+    del vis_all, wgt_all, uvw
+    torch.cuda.empty_cache()
+    vis, wgt = data.vis, data.wgt
+    nvis = data.nvis
     # this rank's strip + W - 1 halo rows only (1/N of the grid per rank)
     backend = strips.HipStripBackend(params, px, px, npix, npix, device=device,
                                      rows=strips.strip_buffer_rows(layout, rank))
     y0, y1 = layout.rows(rank)
     log(f"[bench --strong] rank {rank}/{world}: strip rows [{y0}, {y1}) of {params.nv}, {nvis:,} vis "
-        f"({data.slice_uvw.shape[0]:,} slices), plan {t_plan:.2f} s")
+        f"({data.slice_uvw.shape[0]:,} slices), strip plan + split {t_plan * 1e3:.1f} ms")
 
     # step k's image-row gather runs on the communicator's stream while step
     # k + 1 grids (its buffers are not touched by the next step); it is waited
@@ -383,6 +394,11 @@ def run_strong(args, world, rank, device, steps=None, warmup=None):
             "grid_rows_per_rank": [strips.strip_buffer_rows(layout, r)[1] for r in range(world)],
         },
         "stages_ms_rank0": {k: round(v / nprof * 1e3, 3) for k, v in stages.items()},
+        # the strip split (cip_strip_histogram + plan_strips' bounds +
+        # cip_strip_split with the gather), once per data set, rank 0; the rate
+        # if every step re-split its data beside it
+        "plan_ms": round(t_plan * 1e3, 3),
+        "value_with_plan_per_step": round(total * steps / (elapsed + steps * t_plan) / 1e6, 2),
         "parity": parity,
         "roofline": None,
         "cpu_baseline": None,
@@ -561,8 +577,7 @@ def run_strong_wstrips(args, world, rank, device):
     params = wplanes.HipWPlaneBackend(uvw_d, freq_d, vis_d, wgt_d, npix, npix, px, px, epsilon=1e-4,
                                       support=support, single_precision_accumulation=args.single).params()
     layout = strips.plan_strips(uvw_d, freq_d, params, px, npix, npix, world)
-    rws, c0, c1 = strips.strip_slices(uvw_d, freq_d, params, px, *layout.rows(rank))
-    data = strips.gather_strip(uvw_d, vis_d, wgt_d, rws, c0, c1)
+    data = strips.split_strip(uvw_d, freq_d, vis_d, wgt_d, params, px, *layout.rows(rank))
     backend = strips.HipStripBackend(params, px, px, npix, npix, device=device,
                                      rows=strips.strip_buffer_rows(layout, rank),
                                      single_precision_accumulation=args.single)
@@ -989,7 +1004,8 @@ def main():
         torch.cuda.empty_cache()
         st = run_strong(args, world, rank, device, steps=max(3, min(args.steps, 10)), warmup=2)
         secondary["strong_c4"] = {k: st[k] for k in ("metric", "value", "unit", "n_gpus", "steps", "ms_per_step",
-                                                     "scaling", "stages_ms_rank0", "parity")}
+                                                     "scaling", "stages_ms_rank0", "plan_ms",
+                                                     "value_with_plan_per_step", "parity")}
         secondary["strong_c4"]["workload"] = st["config"]["workload"]
         secondary["strong_c4"]["parallelism"] = st["config"]["parallelism"]
         secondary["strong_c4"]["grid_rows_per_rank"] = st["config"]["grid_rows_per_rank"]

@@ -257,6 +257,53 @@ int cip_grid_tiles_strip(const double* slice_uvw, const int32_t* chan_start,
                          int64_t npix_y, int64_t row0, int64_t nrows, int flags,
                          void* hip_stream, double* strip, double* sum_wgt);
 
+/* cip_grid_tiles_strip that also writes the strip's dirty-tile bits for its
+ * masked pass A (cip_strip_rows_masked / _packed): tile_bits (device, per w
+ * plane (nv / 32) x (nu / 1024) uint32 words, the layout those calls read) =
+ * the tiles this call's own planner marks for its flush (the one-shot path's
+ * dirty mask) plus every tile of the tile rows holding grid rows row0 ..
+ * row0 + W - 2 (the previous rank's halo is added there). Replaces
+ * strips.py's torch restatement of the mask (round 5) - every call computes
+ * its own. */
+int cip_grid_tiles_strip_mask(const double* slice_uvw, const int32_t* chan_start,
+                              const int32_t* chan_stop, int64_t nslices,
+                              const double* freq, int64_t nchan, const void* vis,
+                              int64_t nvis, int vis_dtype, const void* wgt,
+                              int wgt_dtype, const cip_gridder_params* params,
+                              double pixsize_x, double pixsize_y, int64_t npix_x,
+                              int64_t npix_y, int64_t row0, int64_t nrows, int flags,
+                              void* hip_stream, double* strip, double* sum_wgt,
+                              uint32_t* tile_bits);
+
+/* The uv-strip split of the strong-scaling path on the device (round 6;
+ * the reference's offline bucket step, uvw_tiling/tiling_plan.py:29-61 and
+ * reorder.py:19-111, cut by footprint-origin grid row). Power-of-two grids
+ * of 32 .. 16384 rows; uvw (nrow, 3), freq (nchan) DEVICE pointers; every
+ * visibility is placed with the gridder's own fp64 arithmetic.
+ * cip_strip_histogram: hist (device int64, 2 nv) = per grid row the
+ *   visibilities whose footprint origin lies in it, then the row slices
+ *   starting there (a slice starts at channel 0 and wherever the origin's
+ *   32-cell tile changes) - the strip cost model's inputs. Stream-ordered.
+ * cip_strip_split: the strip of origin rows [y0, y1) in the Tile layout
+ *   (uvw_tiling/tile.py:14-124): maximal channel runs per MS row, slices in
+ *   (row, channel) order. Two-phase: slice_uvw == NULL -> counts[0] = slices,
+ *   counts[1] = visibilities (host, one stream wait); then with device
+ *   buffers of those sizes: slice_uvw (n, 3) f64, chan_start / chan_stop (n)
+ *   int32, slice_row (n) int64 (the MS row), and, when vis != NULL (dense
+ *   (nrow, nchan) complex64 / complex128), vis_out (nvis) and - wgt != NULL
+ *   (float32 / float64) - wgt_out gathered into slice order. */
+int cip_strip_histogram(const double* uvw, int64_t nrow, const double* freq,
+                        int64_t nchan, const cip_gridder_params* params,
+                        double pixsize_x, double pixsize_y, void* hip_stream,
+                        int64_t* hist);
+int cip_strip_split(const double* uvw, int64_t nrow, const double* freq,
+                    int64_t nchan, const void* vis, int vis_dtype, const void* wgt,
+                    int wgt_dtype, const cip_gridder_params* params,
+                    double pixsize_y, int64_t y0, int64_t y1, void* hip_stream,
+                    int64_t* counts, double* slice_uvw, int32_t* chan_start,
+                    int32_t* chan_stop, int64_t* slice_row, void* vis_out,
+                    void* wgt_out);
+
 /* The accumulated planes -> dirty image (device (npix_x,npix_y) f64, not
  * normalised): FFT, w-screens and grid correction as in cip_ms2dirty. The
  * planes are consumed (used as FFT scratch). */

@@ -1256,7 +1256,8 @@ static int grid_accumulate(const double* uvw, int64_t nrow, const double* freq, 
                            int vis_dtype, const void* wgt, int wgt_dtype, const cip_gridder_params* params,
                            double pixsize_x, double pixsize_y, int64_t npix_x, int64_t npix_y, int flags,
                            void* hip_stream, double* grids, double* sum_wgt, const RaggedRows* ragged,
-                           const uint8_t* flags4 = nullptr, int64_t row0 = 0, int64_t nrows = 0) {
+                           const uint8_t* flags4 = nullptr, int64_t row0 = 0, int64_t nrows = 0,
+                           uint32_t* strip_bits = nullptr) {
   g_last_error.clear();
   if (flags & ~(CIP_ACC_SINGLE | CIP_PSF | CIP_GRID_ZEROED)) return set_error(CIP_EINVAL, "unknown flags");
   if (!params || !grids) return set_error(CIP_EINVAL, "NULL params or grids");
@@ -1293,6 +1294,13 @@ static int grid_accumulate(const double* uvw, int64_t nrow, const double* freq, 
     pp.g.oob = oob;
   }
   const GridGeometry& g = pp.g;
+  if (strip_bits) {
+    // the strip's dirty-tile bits for its masked pass A: this plan's own mask
+    // (the tiles this call's flush may write) + the tile rows receiving the
+    // previous rank's halo
+    if (g.ntx % 32 != 0) return set_error(CIP_EINVAL, "tile masks need nu / 32 to be a multiple of 32 tiles");
+    CIP_HIP_CHECK(launch_strip_mask(pp.plan.dmask, g, row0, g.support - 1, strip_bits, s));
+  }
   const int64_t plane_elems = 2 * g.nu * g.rows;
   const int G = pp.plan.group;
   for (int64_t q = 0; q * G < g.nplanes; ++q) {
@@ -1614,6 +1622,110 @@ int cip_grid_tiles_strip(const double* slice_uvw, const int32_t* chan_start, con
   const RaggedRows rr{chan_start, chan_stop, nvis};
   return grid_accumulate(slice_uvw, nslices, freq, nchan, vis, vis_dtype, wgt, wgt_dtype, params, pixsize_x,
                          pixsize_y, npix_x, npix_y, flags, hip_stream, strip, sum_wgt, &rr, nullptr, row0, nrows);
+}
+
+int cip_grid_tiles_strip_mask(const double* slice_uvw, const int32_t* chan_start, const int32_t* chan_stop,
+                              int64_t nslices, const double* freq, int64_t nchan, const void* vis, int64_t nvis,
+                              int vis_dtype, const void* wgt, int wgt_dtype, const cip_gridder_params* params,
+                              double pixsize_x, double pixsize_y, int64_t npix_x, int64_t npix_y, int64_t row0,
+                              int64_t nrows, int flags, void* hip_stream, double* strip, double* sum_wgt,
+                              uint32_t* tile_bits) {
+  if (nslices < 0 || nvis < 0) return set_error(CIP_EINVAL, "nslices and nvis must be >= 0");
+  if (nslices > 0 && (!chan_start || !chan_stop)) return set_error(CIP_EINVAL, "NULL channel ranges");
+  if (nslices >= ((int64_t)1 << 32) - 1) return set_error(CIP_EINVAL, "nslices must be < 2^32 - 1");
+  if (nrows < 1) return set_error(CIP_EINVAL, "nrows must be >= 1");
+  if (!tile_bits) return set_error(CIP_EINVAL, "NULL tile_bits");
+  if (!public_dtypes(vis_dtype, wgt_dtype)) return set_error(CIP_EINVAL, "vis dtype must be complex64 or complex128");
+  const RaggedRows rr{chan_start, chan_stop, nvis};
+  return grid_accumulate(slice_uvw, nslices, freq, nchan, vis, vis_dtype, wgt, wgt_dtype, params, pixsize_x,
+                         pixsize_y, npix_x, npix_y, flags, hip_stream, strip, sum_wgt, &rr, nullptr, row0, nrows,
+                         tile_bits);
+}
+
+// ---- the uv-strip split on the device (cip_strips.hip) ----
+static int strip_split_check(const cip_gridder_params* params, const double* uvw, int64_t nrow, const double* freq,
+                             int64_t nchan, GridGeometry* g) {
+  if (!params) return set_error(CIP_EINVAL, "params is NULL");
+  if (nrow < 0 || nchan < 1 || nchan > 65535) return set_error(CIP_EINVAL, "need nrow >= 0 and 1 <= nchan <= 65535");
+  if (nrow > 0 && (!uvw || !freq)) return set_error(CIP_EINVAL, "NULL uvw or freq");
+  const bool pow2 = params->nu > 0 && params->nv > 0 && (params->nu & (params->nu - 1)) == 0 &&
+                    (params->nv & (params->nv - 1)) == 0;
+  if (!pow2 || params->nv < 32 || params->nv > 16384)
+    return set_error(CIP_EINVAL, "strips need a power-of-two grid of 32 .. 16384 rows");
+  *g = geometry(*params, 1.0, 1.0);
+  return CIP_OK;
+}
+
+int cip_strip_histogram(const double* uvw, int64_t nrow, const double* freq, int64_t nchan,
+                        const cip_gridder_params* params, double pixsize_x, double pixsize_y, void* hip_stream,
+                        int64_t* hist) {
+  g_last_error.clear();
+  GridGeometry g;
+  if (const int rc = strip_split_check(params, uvw, nrow, freq, nchan, &g); rc != CIP_OK) return rc;
+  if (!hist) return set_error(CIP_EINVAL, "NULL hist");
+  g = geometry(*params, pixsize_x, pixsize_y);
+  hipStream_t s = (hipStream_t)hip_stream;
+  Workspace* ws = workspace();
+  if (!ws) return set_error(CIP_EHIP, "no HIP device");
+  if (const int sr = settle_async(ws, s); sr != CIP_OK) return sr;
+  if (nrow == 0) {
+    CIP_HIP_CHECK(hipMemsetAsync(hist, 0, sizeof(int64_t) * 2 * g.nv, s));
+    return CIP_OK;
+  }
+  CIP_ALLOC(fx, double, "strip_fx", nchan)
+  CIP_HIP_CHECK(launch_freq_scale(freq, nchan, fx, nullptr, s));
+  const int nb = strip_hist_blocks(nrow);
+  CIP_ALLOC(partial, uint32_t, "strip_hist_partial", (int64_t)nb * 2 * g.nv)
+  CIP_HIP_CHECK(launch_strip_hist(uvw, nrow, fx, nchan, g, partial, nb, hist, s));
+  return CIP_OK;
+}
+
+int cip_strip_split(const double* uvw, int64_t nrow, const double* freq, int64_t nchan, const void* vis,
+                    int vis_dtype, const void* wgt, int wgt_dtype, const cip_gridder_params* params, double pixsize_y,
+                    int64_t y0, int64_t y1, void* hip_stream, int64_t* counts, double* slice_uvw,
+                    int32_t* chan_start, int32_t* chan_stop, int64_t* slice_row, void* vis_out, void* wgt_out) {
+  g_last_error.clear();
+  GridGeometry g;
+  if (const int rc = strip_split_check(params, uvw, nrow, freq, nchan, &g); rc != CIP_OK) return rc;
+  g = geometry(*params, 1.0, pixsize_y);
+  if (!counts) return set_error(CIP_EINVAL, "NULL counts");
+  if (y0 < 0 || y1 > g.nv || y1 <= y0) return set_error(CIP_EINVAL, "strip rows outside the grid");
+  const int vb = vis ? (vis_dtype == CIP_C64 ? 8 : (vis_dtype == CIP_C128 ? 16 : -1)) : 0;
+  const int wb = (vis && wgt) ? (wgt_dtype == CIP_F32 ? 4 : (wgt_dtype == CIP_F64 ? 8 : -1)) : 0;
+  if (vb < 0) return set_error(CIP_EINVAL, "vis dtype must be complex64 or complex128");
+  if (wb < 0) return set_error(CIP_EINVAL, "wgt dtype must be float32 or float64");
+  hipStream_t s = (hipStream_t)hip_stream;
+  Workspace* ws = workspace();
+  if (!ws) return set_error(CIP_EHIP, "no HIP device");
+  if (const int sr = settle_async(ws, s); sr != CIP_OK) return sr;
+  CIP_ALLOC(fx, double, "strip_fx", nchan)
+  CIP_ALLOC(row_runs, int64_t, "strip_row_runs", nrow + 1)
+  CIP_ALLOC(row_vis, int64_t, "strip_row_vis", nrow + 1)
+  CIP_ALLOC(scan_tmp, int64_t, "strip_scan_tmp", scan_tmp_elems(nrow + 1))
+  CIP_HIP_CHECK(launch_freq_scale(freq, nchan, fx, nullptr, s));
+  // the counts and their scans: phase 1 (slice_uvw == NULL) reports the totals;
+  // phase 2 recounts (the same arithmetic, the same numbers) and emits
+  CIP_HIP_CHECK(launch_strip_count(uvw, nrow, fx, nchan, g, y0, y1, row_runs, row_vis, s));
+  CIP_HIP_CHECK(exclusive_scan_i64(row_runs, nrow + 1, scan_tmp, s));
+  CIP_HIP_CHECK(exclusive_scan_i64(row_vis, nrow + 1, scan_tmp, s));
+  if (!slice_uvw) {
+    int64_t* h = (int64_t*)pinned(ws, 2 * sizeof(int64_t));
+    if (!h) return set_error(CIP_ENOMEM, "hipHostMalloc failed");
+    CIP_HIP_CHECK(hipMemcpyAsync(&h[0], row_runs + nrow, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    CIP_HIP_CHECK(hipMemcpyAsync(&h[1], row_vis + nrow, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    CIP_HIP_CHECK(hipStreamSynchronize(s));
+    counts[0] = h[0];
+    counts[1] = h[1];
+    return CIP_OK;
+  }
+  if (!chan_start || !chan_stop || !slice_row) return set_error(CIP_EINVAL, "NULL slice outputs");
+  if (vb > 0 && !vis_out) return set_error(CIP_EINVAL, "NULL vis_out");
+  if (wb > 0 && !wgt_out) return set_error(CIP_EINVAL, "NULL wgt_out");
+  if (nrow > 0)
+    CIP_HIP_CHECK(launch_strip_emit(uvw, nrow, fx, nchan, g, y0, y1, row_runs, row_vis, vis, vb, wgt, wb, slice_uvw,
+                                    chan_start, chan_stop, slice_row, vb ? vis_out : nullptr, wb ? wgt_out : nullptr,
+                                    s));
+  return CIP_OK;
 }
 
 int cip_grid_to_dirty(double* grids, const cip_gridder_params* params, int64_t npix_x, int64_t npix_y,

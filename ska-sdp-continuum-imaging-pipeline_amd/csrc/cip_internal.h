@@ -217,6 +217,28 @@ hipError_t launch_facet_rephase(const double* uvw, int64_t nrow, const double* f
 hipError_t launch_stokes(int stokes, const void* vis4, const uint8_t* flags4, const float* wgt4, int64_t n,
                          void* vis_i, uint8_t* flag_i, float* wgt_i, float* eff_w, hipStream_t s);
 
+// the uv-strip split (cip_strips.hip): per grid row, the visibilities whose
+// footprint origin lies in it and the row slices starting there (hist: 2 nv
+// int64, stream-ordered; partial: strip_hist_blocks(nrow) * 2 nv uint32); per
+// MS row the strip [y0, y1)'s runs and visibilities (row_runs / row_vis,
+// nrow + 1 entries, exclusive-scanned by the caller); the runs as row slices
+// with the visibilities (vis_bytes 8 / 16, 0: none) and weights (wgt_bytes
+// 4 / 8, 0: none) gathered into slice order
+int strip_hist_blocks(int64_t nrow);
+hipError_t launch_strip_hist(const double* uvw, int64_t nrow, const double* fx, int64_t nchan,
+                             const GridGeometry& g, uint32_t* partial, int nblocks, int64_t* hist, hipStream_t s);
+hipError_t launch_strip_count(const double* uvw, int64_t nrow, const double* fx, int64_t nchan,
+                              const GridGeometry& g, int64_t y0, int64_t y1, int64_t* row_runs, int64_t* row_vis,
+                              hipStream_t s);
+hipError_t launch_strip_emit(const double* uvw, int64_t nrow, const double* fx, int64_t nchan, const GridGeometry& g,
+                             int64_t y0, int64_t y1, const int64_t* run_off, const int64_t* vis_off, const void* vis,
+                             int vis_bytes, const void* wgt, int wgt_bytes, double* slice_uvw, int32_t* chan_start,
+                             int32_t* chan_stop, int64_t* slice_row, void* vis_out, void* wgt_out, hipStream_t s);
+// a strip's dirty-tile bits: the plan's mask (may be NULL) | the tile rows of
+// grid rows row0 .. row0 + halo - 1 (nplanes * nty * ntx / 32 words)
+hipError_t launch_strip_mask(const uint32_t* dmask, const GridGeometry& g, int64_t row0, int64_t halo, uint32_t* out,
+                             hipStream_t s);
+
 // the strips' sparse all-to-all: pack this rank's live pass-A rows / unpack
 // a receiver's pass-B input (cip_grid.hip; units = 16-B units per record)
 hipError_t launch_strip_pack(const void* H, int64_t nb, int64_t h, int units, const int64_t* slot, int64_t nlive,

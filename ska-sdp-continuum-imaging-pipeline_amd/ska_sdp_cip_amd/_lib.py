@@ -49,6 +49,9 @@ EXPORTED_SYMBOLS = (
     "cip_grid_ms_stokes_i",
     "cip_grid_tiles",
     "cip_grid_tiles_strip",
+    "cip_grid_tiles_strip_mask",
+    "cip_strip_histogram",
+    "cip_strip_split",
     "cip_ms2dirty_wplanes",
     "cip_grid_to_dirty",
     "cip_strip_rows",
@@ -141,6 +144,12 @@ def lib() -> ctypes.CDLL:
     so.cip_grid_tiles_strip.argtypes = [_vp, _vp, _vp, _i64, _vp, _i64, _vp, _i64, _i32, _vp, _i32,
                                         ctypes.POINTER(GridderParams), _f64, _f64, _i64, _i64, _i64, _i64, _i32,
                                         _vp, _vp, _vp]
+    so.cip_grid_tiles_strip_mask.argtypes = [_vp, _vp, _vp, _i64, _vp, _i64, _vp, _i64, _i32, _vp, _i32,
+                                             ctypes.POINTER(GridderParams), _f64, _f64, _i64, _i64, _i64, _i64, _i32,
+                                             _vp, _vp, _vp, _vp]
+    so.cip_strip_histogram.argtypes = [_vp, _i64, _vp, _i64, ctypes.POINTER(GridderParams), _f64, _f64, _vp, _vp]
+    so.cip_strip_split.argtypes = [_vp, _i64, _vp, _i64, _vp, _i32, _vp, _i32, ctypes.POINTER(GridderParams), _f64,
+                                   _i64, _i64, _vp, ctypes.POINTER(ctypes.c_int64), _vp, _vp, _vp, _vp, _vp, _vp]
     so.cip_grid_to_dirty.argtypes = [_vp, ctypes.POINTER(GridderParams), _i64, _i64, _f64, _f64, _vp, _vp]
     so.cip_strip_rows.argtypes = [_vp, ctypes.POINTER(GridderParams), _i64, _i64, _i64, _i64, _vp, _vp]
     so.cip_strip_cols.argtypes = [_vp, ctypes.POINTER(GridderParams), _i64, _i64, _i64, _i64, _vp, _vp, _vp]
@@ -165,7 +174,8 @@ def lib() -> ctypes.CDLL:
     so.cip_last_error.restype = ctypes.c_char_p
     so.cip_build_info.restype = ctypes.c_char_p
     for name in ("cip_choose_params", "cip_ms2dirty", "cip_ms2dirty_stokes_i", "cip_grid_plane", "cip_grid_layout", "cip_plane_group", "cip_grid_ms", "cip_grid_ms_stokes_i",
-                 "cip_grid_tiles", "cip_grid_tiles_strip", "cip_ms2dirty_wplanes", "cip_grid_to_dirty", "cip_strip_rows", "cip_strip_rows_masked", "cip_strip_cols", "cip_strip_cols_wplane", "cip_strip_wfinal", "cip_strip_pack_rows", "cip_strip_unpack_rows", "cip_strip_rows_packed", "cip_tile_runs",
+                 "cip_grid_tiles", "cip_grid_tiles_strip", "cip_grid_tiles_strip_mask", "cip_strip_histogram",
+                 "cip_strip_split", "cip_ms2dirty_wplanes", "cip_grid_to_dirty", "cip_strip_rows", "cip_strip_rows_masked", "cip_strip_cols", "cip_strip_cols_wplane", "cip_strip_wfinal", "cip_strip_pack_rows", "cip_strip_unpack_rows", "cip_strip_rows_packed", "cip_tile_runs",
                  "cip_stokes_i", "cip_stokes", "cip_facet_rephase", "cip_allreduce_grid", "cip_release_collectives",
                  "cip_release_workspace", "cip_profile_enable", "cip_profile_last"):
         getattr(so, name).restype = ctypes.c_int

@@ -33,10 +33,13 @@ import os
 from dataclasses import dataclass
 from typing import Optional, Sequence
 
+import ctypes
+
 import numpy as np
 
 SPEED_OF_LIGHT = 299792458.0
 COL_BLOCK = 4  # pass-A output block width (cip_fft.hip kColBlock)
+ctypes_i64 = ctypes.c_int64
 
 try:
     import torch
@@ -89,68 +92,57 @@ def origin_rows(v_m, fx, scale_v: float, nv: int, support: int):
 TILE = 32  # the scatter's tile edge (cip_common.h kTile): the dirty-tile mask's unit
 
 
-def strip_tile_bits(data: "StripData", freq, params, pixsize_x: float, pixsize_y: float, y0: int,
-                    halo: int, chunk: int = 1 << 22):
-    """Dirty-tile bits of one rank's strip buffer after its gridding and the
-    halo add: (nplanes, nv / 32, nu / 1024) int32 words, bit tx % 32 of word
-    [p, ty, tx / 32] set when tile (tx, ty) of w plane p may hold a non-zero
-    cell (cip_strip_rows_masked then reads and zeroes only those tiles). The
-    footprint origins come from the gridder's own fp64 placement (place_vis:
-    the same operations in the same order, bit for bit), a footprint marks the
-    (up to) 2 x 2 tiles its W x W cells reach, a w layer iw0 marks planes
-    iw0 .. iw0 + W - 1; every tile of the tile rows holding the strip's first
-    W - 1 grid rows [y0, y0 + halo) is marked too (the previous rank's halo is
-    added there)."""
+def _on_device(t) -> bool:
+    """CUDA tensors take the HIP split (cip_strips.hip); CPU tensors (the gloo
+    tests' ranks) the torch restatement of the same arithmetic."""
+    return t is not None and getattr(t, "is_cuda", False)
+
+
+def _gridder_params(params):
+    """The ctypes cip_gridder_params of `params` (a GridderParams, or any object
+    with its fields - the CPU tests' stand-in)."""
+    from . import _lib  # pylint: disable=import-outside-toplevel
+
+    if isinstance(params, _lib.GridderParams):
+        return params
+    out = _lib.GridderParams()
+    for name, _ in _lib.GridderParams._fields_:
+        setattr(out, name, type(getattr(out, name))(getattr(params, name, 32 if name == "tile" else 0)))
+    return out
+
+
+def _stream(t):
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def strip_histogram(uvw, freq, params, pixsize_x: float, pixsize_y: float):
+    """(visibilities, row slices) per grid row (int64 (nv,) tensors each): by
+    footprint-origin row, a slice starting at each row's first channel and
+    wherever the origin's 32-cell tile changes along the channels. CUDA
+    tensors: one HIP pass (cip_strip_histogram, block-private LDS histograms);
+    CPU tensors: the torch restatement below."""
     nu, nv, W = int(params.nu), int(params.nv), int(params.support)
-    ntx, nty = nu // TILE, nv // TILE
-    wstack = bool(int(params.do_wstacking))
-    nplanes = int(params.nplanes) if wstack else 1
-    nlayers = nplanes - W + 1 if wstack else 1
-    dev = data.slice_uvw.device
-    fx = freq.to(torch.float64) / SPEED_OF_LIGHT
-    su, sv = float(nu) * pixsize_x, float(nv) * pixsize_y
-    hw = float(W // 2)
-    occ = torch.zeros((nlayers, nty, ntx), dtype=torch.bool, device=dev)
-    c0 = data.chan_start.to(torch.int64)
-    lengths = data.chan_stop.to(torch.int64) - c0
-    ends = torch.cumsum(lengths, 0)
-    total = int(ends[-1]) if ends.numel() else 0
-    for a in range(0, total, chunk):
-        b = min(total, a + chunk)
-        k = torch.arange(a, b, device=dev)
-        sl = torch.searchsorted(ends, k, right=True)  # the slice of visibility k
-        ch = c0[sl] + (k - (ends[sl] - lengths[sl]))
-        f = fx[ch]
-        uvw = data.slice_uvw[sl]
-        ix0 = torch.remainder(torch.floor(((uvw[:, 0] * f) * su + float(nu // 2)) - hw).to(torch.int64) + 1, nu)
-        iy0 = torch.remainder(torch.floor(((uvw[:, 1] * f) * sv + float(nv // 2)) - hw).to(torch.int64) + 1, nv)
-        if wstack:
-            xw = ((uvw[:, 2] * f) - float(params.w0)) * (1.0 / float(params.dw))
-            iw0 = (torch.floor(xw - hw).to(torch.int64) + 1).clamp(0, nlayers - 1)
-        else:
-            iw0 = torch.zeros_like(ix0)
-        # every tile the W cells from the origin reach: offsets 0, 32, 64, ...
-        # below W, and W - 1 (a footprint of W >= 34 cells crosses 3+ tiles)
-        offs = sorted(set(range(0, W, TILE)) | {W - 1})
-        txs = [torch.remainder(ix0 + d, nu) // TILE for d in offs]
-        tys = [torch.remainder(iy0 + d, nv) // TILE for d in offs]
-        for tx in txs:
-            for ty in tys:
-                occ[iw0, ty, tx] = True
-    if wstack:
-        # plane p is fed by layers max(0, p - W + 1) .. min(p, nlayers - 1)
-        cs = torch.cumsum(torch.nn.functional.pad(occ.to(torch.int32), (0, 0, 0, 0, 1, 0)), 0)
-        pl = torch.arange(nplanes, device=dev)
-        hi = torch.clamp(pl, max=nlayers - 1) + 1
-        lo = torch.clamp(pl - W + 1, min=0)
-        mask = (cs[hi] - cs[lo]) > 0
-    else:
-        mask = occ
-    rows = torch.remainder(torch.arange(y0, y0 + max(halo, 1), device=dev), nv) // TILE
-    mask[:, rows, :] = True
-    bits = mask.view(nplanes, nty, ntx // 32, 32).to(torch.int64) << torch.arange(32, device=dev)
-    words = bits.sum(-1)
-    return torch.where(words >= (1 << 31), words - (1 << 32), words).to(torch.int32).contiguous()
+    if _on_device(uvw):
+        from . import _lib  # pylint: disable=import-outside-toplevel
+
+        hist = torch.empty(2 * nv, dtype=torch.int64, device=uvw.device)
+        uvw_c, f_c = uvw.contiguous().to(torch.float64), freq.contiguous().to(torch.float64)
+        _lib.check(_lib.lib().cip_strip_histogram(uvw_c.data_ptr(), int(uvw_c.shape[0]), f_c.data_ptr(),
+                                                  int(f_c.shape[0]), _gridder_params(params), float(pixsize_x),
+                                                  float(pixsize_y), _stream(uvw_c), hist.data_ptr()))
+        return hist[:nv], hist[nv:]
+    fx = freq / SPEED_OF_LIGHT
+    vis = torch.zeros(nv, dtype=torch.int64, device=uvw.device)
+    runs = torch.zeros(nv, dtype=torch.int64, device=uvw.device)
+    for a, b in _row_chunks(uvw.shape[0]):
+        iy = origin_rows(uvw[a:b, 1], fx, float(params.nv) * pixsize_y, nv, W)
+        ix = origin_rows(uvw[a:b, 0], fx, float(params.nu) * pixsize_x, nu, W)
+        key = torch.div(iy, 32, rounding_mode="floor") * (nu // 32 + 1) + torch.div(ix, 32, rounding_mode="floor")
+        start = torch.ones_like(key, dtype=torch.bool)
+        start[:, 1:] = key[:, 1:] != key[:, :-1]
+        vis += torch.bincount(iy.reshape(-1), minlength=nv)
+        runs += torch.bincount(iy[start], minlength=nv)
+    return vis, runs
 
 
 def _row_chunks(nrow: int, chunk: int = 65536):
@@ -177,21 +169,11 @@ def row_costs(uvw, freq, params, pixsize_x: float, pixsize_y: float, a2a_ps_per_
     tile changes along the channels) and its pass-A cells (one pass per w
     plane), plus `a2a_ps_per_row` per row and plane: the row's pass-A output
     crossing the all-to-all (a rank's exchange time grows with its rows)."""
-    nu, nv, W = int(params.nu), int(params.nv), int(params.support)
+    nu, W = int(params.nu), int(params.support)
     wstack = bool(int(getattr(params, "do_wstacking", 0)))
     taps = W * W * (W if wstack else 1)
     nplanes = int(params.nplanes) if wstack else 1
-    fx = freq / SPEED_OF_LIGHT
-    vis = torch.zeros(nv, dtype=torch.int64, device=uvw.device)
-    runs = torch.zeros(nv, dtype=torch.int64, device=uvw.device)
-    for a, b in _row_chunks(uvw.shape[0]):
-        iy = origin_rows(uvw[a:b, 1], fx, float(params.nv) * pixsize_y, nv, W)
-        ix = origin_rows(uvw[a:b, 0], fx, float(params.nu) * pixsize_x, nu, W)
-        key = torch.div(iy, 32, rounding_mode="floor") * (nu // 32 + 1) + torch.div(ix, 32, rounding_mode="floor")
-        start = torch.ones_like(key, dtype=torch.bool)
-        start[:, 1:] = key[:, 1:] != key[:, :-1]
-        vis += torch.bincount(iy.reshape(-1), minlength=nv)
-        runs += torch.bincount(iy[start], minlength=nv)
+    vis, runs = strip_histogram(uvw, freq, params, pixsize_x, pixsize_y)
     cost = (COST_PS_PER_VIS * (taps / 64.0) * vis.double() + COST_PS_PER_SLICE * runs.double() +
             (COST_PS_PER_CELL * nu + a2a_ps_per_row) * nplanes)
     return cost.cpu().numpy()
@@ -228,12 +210,8 @@ def plan_strips(uvw, freq, params, pixsize_y: float, npix_x: int, npix_y: int, w
         hist = row_costs(uvw, freq, params, pixsize_y if pixsize_x is None else pixsize_x, pixsize_y,
                          a2a_ps_per_row=a2a)
     elif balance == "vis":
-        fx = freq / SPEED_OF_LIGHT
-        scale_v = float(params.nv) * pixsize_y
-        h = torch.zeros(nv, dtype=torch.int64, device=uvw.device)
-        for a, b in _row_chunks(uvw.shape[0]):
-            h += torch.bincount(origin_rows(uvw[a:b, 1], fx, scale_v, nv, W).reshape(-1), minlength=nv)
-        hist = h.cpu().numpy()
+        hist = strip_histogram(uvw, freq, params, pixsize_y if pixsize_x is None else pixsize_x,
+                               pixsize_y)[0].cpu().numpy()
     else:
         raise ValueError("balance must be 'cost' or 'vis'")
     cum = np.cumsum(hist)
@@ -268,10 +246,64 @@ class StripData:
         return int(self.vis.shape[0])
 
 
+def _split_device(uvw, freq, params, pixsize_y: float, y0: int, y1: int, vis=None, wgt=None):
+    """cip_strip_split: (slice_uvw, c0, c1 (int32), rows (int64), vis, wgt)
+    of the strip [y0, y1) - one count pass + scans, then one emit pass that
+    writes the slices and gathers the strip's visibilities (when given)."""
+    from . import _lib  # pylint: disable=import-outside-toplevel
+    from .gridder import _codes  # pylint: disable=import-outside-toplevel
+
+    dev = uvw.device
+    uvw_c, f_c = uvw.contiguous().to(torch.float64), freq.contiguous().to(torch.float64)
+    nrow, nchan = int(uvw_c.shape[0]), int(f_c.shape[0])
+    prm = _gridder_params(params)
+    vis_codes, wgt_codes = _codes()
+    if vis is not None:
+        vis = vis.reshape(nrow, nchan).contiguous()
+        wgt = None if wgt is None else wgt.reshape(nrow, nchan).contiguous()
+    vp = vis.data_ptr() if vis is not None else None
+    vc = vis_codes[vis.dtype] if vis is not None else _lib.CIP_C64
+    wp = wgt.data_ptr() if wgt is not None else None
+    wc = wgt_codes[wgt.dtype] if wgt is not None else _lib.CIP_NONE
+    counts = (ctypes_i64 * 2)()
+    lib = _lib.lib()
+    args = (uvw_c.data_ptr(), nrow, f_c.data_ptr(), nchan, vp, vc, wp, wc, prm, float(pixsize_y), int(y0), int(y1),
+            _stream(uvw_c), counts)
+    _lib.check(lib.cip_strip_split(*args, None, None, None, None, None, None))
+    ns, nvis = int(counts[0]), int(counts[1])
+    suvw = torch.empty((ns, 3), dtype=torch.float64, device=dev)
+    c0 = torch.empty(ns, dtype=torch.int32, device=dev)
+    c1 = torch.empty(ns, dtype=torch.int32, device=dev)
+    rows = torch.empty(ns, dtype=torch.int64, device=dev)
+    vout = torch.empty(nvis, dtype=vis.dtype, device=dev) if vis is not None else None
+    wout = torch.empty(nvis, dtype=wgt.dtype, device=dev) if wgt is not None else None
+    _lib.check(lib.cip_strip_split(*args, suvw.data_ptr(), c0.data_ptr(), c1.data_ptr(), rows.data_ptr(),
+                                   vout.data_ptr() if vout is not None and nvis else None,
+                                   wout.data_ptr() if wout is not None and nvis else None))
+    return suvw, c0, c1, rows, vout, wout
+
+
+def split_strip(uvw, freq, vis, wgt, params, pixsize_y: float, y0: int, y1: int) -> "StripData":
+    """Rank-local strip data from dense (nrow, nchan) columns: the row slices
+    whose footprint-origin rows lie in [y0, y1) and their visibilities /
+    weights, in the Tile layout (the reference's reorder_by_uvw_tile output,
+    reorder.py:19-111, cut by strip). CUDA tensors: cip_strip_split (one
+    count pass, one emit + gather pass); CPU tensors: strip_slices +
+    gather_strip (the same slices and order)."""
+    if _on_device(uvw):
+        suvw, c0, c1, rows, v, w = _split_device(uvw, freq, params, pixsize_y, y0, y1, vis, wgt)
+        return StripData(suvw, c0, c1, v, w, rows)
+    rows, c0, c1 = strip_slices(uvw, freq, params, pixsize_y, y0, y1)
+    return gather_strip(uvw, vis, wgt, rows, c0, c1)
+
+
 def strip_slices(uvw, freq, params, pixsize_y: float, y0: int, y1: int):
     """(rows, c0, c1) int64 tensors: the maximal channel runs of each row whose
     origin row lies in [y0, y1) (one run per row unless a row's v track wraps
-    or leaves and re-enters the strip)."""
+    or leaves and re-enters the strip). CUDA tensors: cip_strip_split."""
+    if _on_device(uvw):
+        _, c0, c1, rows, _, _ = _split_device(uvw, freq, params, pixsize_y, y0, y1)
+        return rows, c0.to(torch.int64), c1.to(torch.int64)
     nv, W = int(params.nv), int(params.support)
     fx = freq / SPEED_OF_LIGHT
     scale_v = float(params.nv) * pixsize_y
@@ -348,11 +380,12 @@ class HipStripBackend:
             raise ValueError("strips need a grid in the pruned-FFT layout (power-of-two grids)")
         self.nplanes = int(params.nplanes) if int(params.do_wstacking) else 1
         self.single = bool(single_precision_accumulation)
-        # dirty-tile masks of the gridded strip (strip_tile_bits), cached per
-        # strip data object; CIP_STRIP_MASK=0 runs pass A over every cell
+        # the gridded strip's dirty-tile bits, written by every grid_strip call
+        # (cip_grid_tiles_strip_mask: the call's own planner mask + the halo
+        # tile rows); CIP_STRIP_MASK=0 runs pass A over every cell
         self.masked = os.environ.get("CIP_STRIP_MASK", "1") != "0"
         self._bits = None
-        self._bits_key = None
+        self._bits_valid = False
         self.rows = None
         self.grid = None
         self.dirty = False
@@ -392,29 +425,31 @@ class HipStripBackend:
         if self.dirty:  # a previous invert did not finish: the buffer may hold partial sums
             self.grid.zero_()
         self.dirty = True
-        if self.masked:
-            # the mask depends on the data object, the strip rows AND the
-            # frequencies: a kept copy of freq is compared by value (nchan values)
-            key = (id(data), self.rows)
-            fresh = (self._bits_key is None or self._bits_key[0] != key or self._bits_key[1] is not data
-                     or self._bits_key[2].shape != freq.shape or self._bits_key[2].dtype != freq.dtype
-                     or not torch.equal(self._bits_key[2], freq.detach().to(self._bits_key[2].device)))
-            if fresh:
-                self._bits = strip_tile_bits(data, freq, self.params, self.px, self.py, self.rows[0],
-                                             int(self.params.support) - 1)
-                self._bits_key = (key, data, freq.detach().clone())
+        self._bits_valid = False
         vis_codes, wgt_codes = _codes()
         sumw = torch.zeros(1, dtype=torch.float64, device=self.device)
         ns = int(data.slice_uvw.shape[0])
-        if ns:
-            self._lib.check(self._lib.lib().cip_grid_tiles_strip(
-                data.slice_uvw.data_ptr(), data.chan_start.data_ptr(), data.chan_stop.data_ptr(), ns,
-                freq.data_ptr(), int(freq.shape[0]), data.vis.data_ptr(), data.nvis, vis_codes[data.vis.dtype],
-                data.wgt.data_ptr() if data.wgt is not None else None,
+        nu, nv = int(self.params.nu), int(self.params.nv)
+        mask = self.masked and nu % 1024 == 0
+        if mask:
+            shape = (self.nplanes, nv // TILE, nu // TILE // 32)
+            if self._bits is None or tuple(self._bits.shape) != shape:
+                self._bits = torch.empty(shape, dtype=torch.int32, device=self.device)
+        fn = self._lib.lib().cip_grid_tiles_strip_mask if mask else self._lib.lib().cip_grid_tiles_strip
+        extra = (self._bits.data_ptr(),) if mask else ()
+        if ns or mask:
+            # an empty strip still writes its mask (the halo rows it receives)
+            self._lib.check(fn(
+                data.slice_uvw.data_ptr() if ns else None, data.chan_start.data_ptr() if ns else None,
+                data.chan_stop.data_ptr() if ns else None, ns,
+                freq.data_ptr(), int(freq.shape[0]), data.vis.data_ptr() if data.nvis else None, data.nvis,
+                vis_codes[data.vis.dtype],
+                data.wgt.data_ptr() if data.wgt is not None and data.nvis else None,
                 wgt_codes[data.wgt.dtype] if data.wgt is not None else self._lib.CIP_NONE,
                 self.params, self.px, self.py, self.npix_x, self.npix_y, self.rows[0], self.rows[1],
                 self._lib.CIP_GRID_ZEROED | (self._lib.CIP_ACC_SINGLE if self.single else 0), self._stream(),
-                self.grid.data_ptr(), sumw.data_ptr()))
+                self.grid.data_ptr(), sumw.data_ptr(), *extra))
+        self._bits_valid = mask
         return self.grid, sumw
 
     def mark_clean(self) -> None:
@@ -425,7 +460,7 @@ class HipStripBackend:
         """Pass A over buffer rows [y0, y1) of w plane `plane` -> H (npix_x / 4, y1 - y0, 4, 2); zeroes the
         rows (only the dirty tiles' cells are read when the gridded strip's mask is known)."""
         H = torch.empty((self.npix_x // COL_BLOCK, y1 - y0, COL_BLOCK, 2), dtype=torch.float64, device=self.device)
-        if self.masked and self._bits is not None and self.dirty:
+        if self._bits_valid and self.dirty:
             self._lib.check(self._lib.lib().cip_strip_rows_masked(
                 grid.data_ptr(), self.params, self.npix_x, self.npix_y, int(y0), int(y1), int(self.rows[0]),
                 self._bits[plane].data_ptr(), self._stream(), H.data_ptr()))
@@ -439,7 +474,7 @@ class HipStripBackend:
         bool over them, as live_rows gives; `count` Trues) -> H (npix_x / 4,
         count, 4, 2): the sparse all-to-all's send buffer, written by pass A
         itself (cip_strip_rows_packed) instead of packed after it."""
-        if not (self.masked and self._bits is not None and self.dirty):
+        if not (self._bits_valid and self.dirty):
             return _pack_live(self.pass_rows(grid, y0, y1, plane), live, count)
         slot = torch.cumsum(live.to(torch.int64), 0).sub_(1)
         slot = torch.where(live, slot, torch.full_like(slot, -1))
@@ -454,7 +489,7 @@ class HipStripBackend:
         """Buffer rows [0, h) of `plane` that may hold a non-zero cell (their
         tile row has a dirty tile in the gridded strip's mask), or None when
         no mask is known: pass A of every other row is exactly zero."""
-        if not (self.masked and self._bits is not None):
+        if not self._bits_valid:
             return None
         words = self._bits[plane]  # (nty, ntx / 32) int32
         tile_live = (words != 0).any(dim=1)

@@ -2,6 +2,19 @@
 In-memory stand-in for the torch.distributed calls strips.py makes, for ranks
 that are host threads on one GPU (test infrastructure: tests/
 test_gpu_strips_threads.py, tests/test_gpu_c4.py).
+
+Asynchronous like RCCL (round 6): every rank thread runs on its own current
+stream, and a collective neither synchronises the device nor blocks the host
+beyond the ranks' host rendezvous. Each rank stages its input on its own
+communicator stream after the work already queued on its current stream (an
+event), the ranks exchange the staged tensors and their events on the host,
+and each rank's communicator stream waits for every peer's staging event and
+copies the peers' data into its outputs. A collective returns a work object
+whose wait() makes the caller's CURRENT STREAM wait for that copy (a device
+wait, as `Work.wait()` does for NCCL/RCCL); the blocking forms wait at once.
+So an asynchronous gather (`invert_strips(..., gather_async=True)`) really is
+still in flight while the caller queues its next invert, and buffer reuse or
+stream ordering mistakes show up as wrong images.
 """
 import threading
 
@@ -13,8 +26,17 @@ NAMES = ("is_available", "is_initialized", "get_world_size", "get_rank", "isend"
 
 
 class _Work:
+    """A collective in flight on the rank's communicator stream."""
+
+    def __init__(self, done):
+        self._done = done
+
     def wait(self):
+        torch.cuda.current_stream().wait_event(self._done)
         return True
+
+    def is_completed(self):
+        return self._done.query()
 
 
 class ThreadDist:
@@ -22,20 +44,48 @@ class ThreadDist:
 
     def __init__(self, world):
         self.world = world
-        self.barrier = threading.Barrier(world, timeout=120)
+        self.barrier = threading.Barrier(world, timeout=300)
         self.slots = [None] * world
         self.local = threading.local()
+        self.keep = []  # staged tensors: alive until the ranks finish (peers' streams read them)
+        self.lock = threading.Lock()
+        self.calls = [0] * world  # collectives per rank (the tests check they ran)
 
     def rank(self):
         return self.local.rank
 
-    def _exchange(self, obj):
-        self.slots[self.rank()] = obj
-        torch.cuda.synchronize()
+    def _comm(self):
+        if getattr(self.local, "comm", None) is None:
+            self.local.comm = torch.cuda.Stream()
+        return self.local.comm
+
+    def _collective(self, stage, deliver):
+        """stage(): this rank's payload (tensors cloned on the communicator
+        stream after the caller's queued work); deliver(vals): copy the peers'
+        staged payloads into this rank's outputs (on the communicator stream,
+        after every peer's staging). Returns the work object."""
+        cur, comm = torch.cuda.current_stream(), self._comm()
+        ready = torch.cuda.Event()
+        ready.record(cur)
+        comm.wait_event(ready)
+        with torch.cuda.stream(comm):
+            payload = stage()
+            staged = torch.cuda.Event()
+            staged.record(comm)
+        with self.lock:
+            self.keep.append(payload)
+            self.calls[self.rank()] += 1
+        self.slots[self.rank()] = (payload, staged)
         self.barrier.wait()
         vals = list(self.slots)
         self.barrier.wait()
-        return vals
+        for _, ev in vals:
+            comm.wait_event(ev)
+        with torch.cuda.stream(comm):
+            deliver([v for v, _ in vals])
+            done = torch.cuda.Event()
+            done.record(comm)
+        return _Work(done)
 
     # -- the API surface
     def is_available(self):
@@ -60,41 +110,69 @@ class ThreadDist:
         return (op, tensor, peer)
 
     def batch_isend_irecv(self, ops):
-        sends = {peer: t.clone() for op, t, peer in ops if op == self.isend}
-        vals = self._exchange(sends)
-        for op, t, peer in ops:
-            if op == self.irecv:
-                t.copy_(vals[peer][self.rank()])
-        torch.cuda.synchronize()
-        return [_Work()]
+        def stage():
+            return {peer: t.clone() for op, t, peer in ops if op == self.isend}
 
-    def all_reduce(self, t, group=None, op=None):
-        vals = self._exchange(t.clone())
-        acc = vals[0].clone()
-        for v in vals[1:]:
-            acc += v
-        t.copy_(acc)
+        def deliver(vals):
+            for op, t, peer in ops:
+                if op == self.irecv:
+                    t.copy_(vals[peer][self.rank()], non_blocking=True)
 
-    def all_gather(self, out, t, group=None):
-        vals = self._exchange(t.clone())
-        for o, v in zip(out, vals):
-            o.copy_(v)
+        return [self._collective(stage, deliver)]
 
-    def all_to_all_single(self, out, inp, output_split_sizes=None, input_split_sizes=None, group=None):
-        vals = self._exchange([c.clone() for c in torch.split(inp, input_split_sizes)])
-        out.copy_(torch.cat([vals[s][self.rank()] for s in range(self.world)]))
+    def all_reduce(self, t, group=None, op=None, async_op=False):
+        def deliver(vals):
+            acc = vals[0].clone()
+            for v in vals[1:]:
+                acc += v
+            t.copy_(acc)
+
+        w = self._collective(lambda: t.clone(), deliver)
+        if async_op:
+            return w
+        w.wait()
+        return None
+
+    def all_gather(self, out, t, group=None, async_op=False):
+        def deliver(vals):
+            for o, v in zip(out, vals):
+                o.copy_(v, non_blocking=True)
+
+        w = self._collective(lambda: t.clone(), deliver)
+        if async_op:
+            return w
+        w.wait()
+        return None
+
+    def all_to_all_single(self, out, inp, output_split_sizes=None, input_split_sizes=None, group=None,
+                          async_op=False):
+        def deliver(vals):
+            out.copy_(torch.cat([vals[s][self.rank()] for s in range(self.world)]), non_blocking=True)
+
+        w = self._collective(lambda: [c.clone() for c in torch.split(inp, input_split_sizes)], deliver)
+        if async_op:
+            return w
+        w.wait()
+        return None
 
     def gather(self, t, gather_list=None, dst=0, group=None, async_op=False):
-        vals = self._exchange(t.clone())
-        if self.rank() == dst:
-            for o, v in zip(gather_list, vals):
-                o.copy_(v)
-        return _Work() if async_op else None
+        me = self.rank()
 
+        def deliver(vals):
+            if me == dst:
+                for o, v in zip(gather_list, vals):
+                    o.copy_(v, non_blocking=True)
+
+        w = self._collective(lambda: t.clone(), deliver)
+        if async_op:
+            return w
+        w.wait()
+        return None
 
 
 def run_ranks(monkeypatch, world, fn):
-    """fn(rank) on `world` threads with torch.distributed replaced -> (results, errors)."""
+    """fn(rank) on `world` threads with torch.distributed replaced, each rank
+    on its own current stream -> (results, errors)."""
     fake = ThreadDist(world)
     for name in NAMES:
         monkeypatch.setattr(tdist, name, getattr(fake, name))
@@ -103,7 +181,9 @@ def run_ranks(monkeypatch, world, fn):
     def run(r):
         try:
             fake.local.rank = r
-            results[r] = fn(r)
+            with torch.cuda.stream(torch.cuda.Stream()):
+                results[r] = fn(r)
+                torch.cuda.current_stream().synchronize()
         except Exception as e:  # pylint: disable=broad-except
             errors.append((r, repr(e)))
             fake.barrier.abort()
@@ -112,5 +192,7 @@ def run_ranks(monkeypatch, world, fn):
     for th in threads:
         th.start()
     for th in threads:
-        th.join(timeout=600)
+        th.join(timeout=900)
+    torch.cuda.synchronize()
+    run_ranks.last = fake
     return results, errors

@@ -121,8 +121,7 @@ def test_c4_full_eight_strips_equal_one_shot(gpu_device):
     layout = strips.plan_strips(uvw, f, prm, px, NPIX, NPIX, world)
     datas = []
     for k in range(world):
-        rws, c0, c1 = strips.strip_slices(uvw, f, prm, px, *layout.rows(k))
-        datas.append(strips.gather_strip(uvw, vis, wgt, rws, c0, c1))
+        datas.append(strips.split_strip(uvw, f, vis, wgt, prm, px, *layout.rows(k)))
     assert sum(d.nvis for d in datas) == rows * NCHAN
     del vis, wgt
     torch.cuda.empty_cache()

@@ -51,8 +51,7 @@ def _images():
         layout = strips.plan_strips(tu, tf, prm, px, npix, npix, world)
         datas = []
         for r in range(world):
-            rows, c0, c1 = strips.strip_slices(tu, tf, prm, px, *layout.rows(r))
-            datas.append(strips.gather_strip(tu, tv, tw, rows, c0, c1))
+            datas.append(strips.split_strip(tu, tf, tv, tw, prm, px, *layout.rows(r)))
         be = strips.HipStripBackend(prm, px, px, npix, npix, device=dev)
         out[f"strips_{world}"] = strips.invert_strips_local(datas, tf, layout, be).cpu().numpy()
     acc = GridAccumulator(npix, npix, px, px, support=8, do_wstacking=False, w_range=w_range_rows(uvw, f))

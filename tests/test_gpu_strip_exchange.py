@@ -71,8 +71,7 @@ def test_packed_pass_a_equals_pass_a_then_pack(gpu_device, wstack):
     tu, tf, tv, tw = t(uvw), t(f), t(vis.astype(np.complex64)), t(w.astype(np.float32))
     _, prm = device_ms2dirty(tu, tf, tv, tw, npix, npix, px, px, support=8, do_wstacking=wstack)
     layout = strips.plan_strips(tu, tf, prm, px, npix, npix, 2)
-    rows, c0, c1 = strips.strip_slices(tu, tf, prm, px, *layout.rows(1))
-    data = strips.gather_strip(tu, tv, tw, rows, c0, c1)
+    data = strips.split_strip(tu, tf, tv, tw, prm, px, *layout.rows(1))
     outs = []
     for packed in (False, True):
         be = strips.HipStripBackend(prm, px, px, npix, npix, device=gpu_device)

@@ -68,8 +68,7 @@ def test_strip_decomposition_equals_one_shot(gpu_device, world, W, npix):
     layout = strips.plan_strips(tu, tf, prm, px, npix, npix, world)
     datas = []
     for r in range(world):
-        rows, c0, c1 = strips.strip_slices(tu, tf, prm, px, *layout.rows(r))
-        datas.append(strips.gather_strip(tu, tv, tw, rows, c0, c1))
+        datas.append(strips.split_strip(tu, tf, tv, tw, prm, px, *layout.rows(r)))
     assert sum(d.nvis for d in datas) == vis.size
     be = strips.HipStripBackend(prm, px, px, npix, npix, device=gpu_device)
     stages = []
@@ -107,8 +106,7 @@ def test_wstacking_strip_decomposition_equals_one_shot(gpu_device, world, W, sin
     layout = strips.plan_strips(tu, tf, prm, px, npix, npix, world)
     datas = []
     for r in range(world):
-        rows, c0, c1 = strips.strip_slices(tu, tf, prm, px, *layout.rows(r))
-        datas.append(strips.gather_strip(tu, tv, tw, rows, c0, c1))
+        datas.append(strips.split_strip(tu, tf, tv, tw, prm, px, *layout.rows(r)))
     be = strips.HipStripBackend(prm, px, px, npix, npix, device=gpu_device, single_precision_accumulation=single)
     stages = []
     img = strips.invert_strips_local(datas, tf, layout, be, stages=stages)
@@ -134,8 +132,7 @@ def test_strip_buffer_rejects_footprints_outside_its_rows(gpu_device):
     tu, tf, tv, tw = _to(gpu_device, uvw, f, vis.astype(np.complex64), w.astype(np.float32))
     prm = _lib.choose_params(npix, npix, px, px, 1e-4, 8)
     layout = strips.plan_strips(tu, tf, prm, px, npix, npix, 4)
-    rows, c0, c1 = strips.strip_slices(tu, tf, prm, px, *layout.rows(2))
-    data = strips.gather_strip(tu, tv, tw, rows, c0, c1)
+    data = strips.split_strip(tu, tf, tv, tw, prm, px, *layout.rows(2))
     assert data.nvis > 0
     be = strips.HipStripBackend(prm, px, px, npix, npix, device=gpu_device)
     be.bind(layout, 1)  # another rank's rows
@@ -159,8 +156,7 @@ def test_strip_backend_recovers_from_an_interrupted_invert(gpu_device):
     tu, tf, tv, tw = _to(gpu_device, uvw, f, vis.astype(np.complex64), w.astype(np.float32))
     ref, prm = device_ms2dirty(tu, tf, tv, tw, npix, npix, px, px, support=8, normalise=True)
     layout = strips.plan_strips(tu, tf, prm, px, npix, npix, 1)
-    rows, c0, c1 = strips.strip_slices(tu, tf, prm, px, *layout.rows(0))
-    data = strips.gather_strip(tu, tv, tw, rows, c0, c1)
+    data = strips.split_strip(tu, tf, tv, tw, prm, px, *layout.rows(0))
     be = strips.HipStripBackend(prm, px, px, npix, npix, device=gpu_device)
     be.grid_strip(data, tf)  # interrupted: no pass A
     assert be.dirty
@@ -203,8 +199,7 @@ def test_masked_strip_pass_a_equals_dense(gpu_device, monkeypatch, wstack, suppo
     layout = strips.plan_strips(tu, tf, prm, px, npix, npix, world)
     datas = []
     for r in range(world):
-        rows, c0, c1 = strips.strip_slices(tu, tf, prm, px, *layout.rows(r))
-        datas.append(strips.gather_strip(tu, tv, tw, rows, c0, c1))
+        datas.append(strips.split_strip(tu, tf, tv, tw, prm, px, *layout.rows(r)))
     imgs = {}
     for masked in ("1", "0"):
         monkeypatch.setenv("CIP_STRIP_MASK", masked)
@@ -228,8 +223,7 @@ def test_strip_mask_follows_the_frequencies(gpu_device):
     tu, tf, tv, tw = _to(gpu_device, uvw, f, vis.astype(np.complex64), w.astype(np.float32))
     _, prm = device_ms2dirty(tu, tf, tv, tw, npix, npix, px, px, support=W, normalise=True)
     layout = strips.plan_strips(tu, tf, prm, px, npix, npix, 1)
-    rows, c0, c1 = strips.strip_slices(tu, tf, prm, px, *layout.rows(0))
-    datas = [strips.gather_strip(tu, tv, tw, rows, c0, c1)]
+    datas = [strips.split_strip(tu, tf, tv, tw, prm, px, *layout.rows(0))]
     be = strips.HipStripBackend(prm, px, px, npix, npix, device=gpu_device)
     assert be.masked
     strips.invert_strips_local(datas, tf, layout, be)
@@ -259,8 +253,7 @@ def test_ragged_stream_forms_are_bit_identical(gpu_device, monkeypatch, wstack, 
     layout = strips.plan_strips(tu, tf, prm, px, npix, npix, 3)
     datas = []
     for r in range(3):
-        rows, c0, c1 = strips.strip_slices(tu, tf, prm, px, *layout.rows(r))
-        datas.append(strips.gather_strip(tu, tv, tw, rows, c0, c1))
+        datas.append(strips.split_strip(tu, tf, tv, tw, prm, px, *layout.rows(r)))
     imgs = []
     for env in ({}, {"CIP_PACKED_RUNS": "0"}, {"CIP_RAGGED_PACK": "0"}):
         for k in ("CIP_PACKED_RUNS", "CIP_RAGGED_PACK"):

@@ -42,8 +42,7 @@ def test_distributed_strips_as_threads_equal_one_shot(gpu_device, monkeypatch, w
     layout = strips.plan_strips(tu, tf, prm, px, npix, npix, world)
     datas = []
     for r in range(world):
-        rows, c0, c1 = strips.strip_slices(tu, tf, prm, px, *layout.rows(r))
-        datas.append(strips.gather_strip(tu, tv, tw, rows, c0, c1))
+        datas.append(strips.split_strip(tu, tf, tv, tw, prm, px, *layout.rows(r)))
     torch.cuda.synchronize()
     stages = [dict() for _ in range(world)]
 
@@ -65,3 +64,52 @@ def test_distributed_strips_as_threads_equal_one_shot(gpu_device, monkeypatch, w
     assert float((img - ref).abs().max()) < 1e-12 * peak
     # the sparse exchange ran (pass A wrote the packed send buffers)
     assert all(st.get("a2a_send_bytes", 0) > 0 for st in stages)
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_back_to_back_async_gathers_equal_one_shot(gpu_device, monkeypatch, world):
+    """bench.py --strong's step pattern with real stream ordering: each rank
+    queues invert k + 1 (gridding into the same strip buffer, halo and
+    all-to-all collectives) while invert k's image-row gather is still in
+    flight on its communicator stream (tests/_thread_dist.py: asynchronous
+    collectives, a stream per rank, no device synchronisation), then waits
+    for both. Two different data sets alternate, so a gather that read a
+    later step's rows, or a buffer reused too early, gives a wrong image."""
+    npix = 512
+    uvw, f, vis, w, px = _case(30000, 32, npix)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(gpu_device)  # noqa: E731
+    tu, tf, tw = t(uvw), t(f), t(w.astype(np.float32))
+    tvs = [t(vis.astype(np.complex64)), t((vis * (0.25 - 1.5j)).astype(np.complex64))]
+    refs, prm = [], None
+    for tv in tvs:
+        ref, prm = device_ms2dirty(tu, tf, tv, tw, npix, npix, px, px, support=8, normalise=True)
+        refs.append(ref)
+    layout = strips.plan_strips(tu, tf, prm, px, npix, npix, world)
+    datas = [[strips.split_strip(tu, tf, tv, tw, prm, px, *layout.rows(r)) for r in range(world)] for tv in tvs]
+    torch.cuda.synchronize()
+    nsteps = 4
+
+    def rank_fn(r):
+        be = strips.HipStripBackend(prm, px, px, npix, npix, device=gpu_device)
+        pend, imgs = None, []
+        for k in range(nsteps):
+            nxt = strips.invert_strips(datas[k % 2][r], tf, layout, be, gather_async=True)
+            if pend is not None:
+                imgs.append(pend.wait())
+            pend = nxt
+        imgs.append(pend.wait())
+        torch.cuda.current_stream().synchronize()
+        assert float(be.grid.abs().max()) == 0.0 and not be.dirty
+        return imgs
+
+    results, errors = run_ranks(monkeypatch, world, rank_fn)
+    assert not errors, errors
+    assert all(img is None for res in results[1:] for img in res)
+    imgs = results[0]
+    assert len(imgs) == nsteps
+    for k, img in enumerate(imgs):
+        ref = refs[k % 2]
+        assert float((img - ref).abs().max()) < 1e-12 * float(ref.abs().max()), k
+    # every collective went through the asynchronous stand-in
+    from _thread_dist import run_ranks as rr
+    assert min(rr.last.calls) >= nsteps * 4

@@ -245,55 +245,6 @@ def test_strip_plan_balances_the_cost_model(world):
     assert sum(d.nvis for d in datas) == vis.size
 
 
-class _PW(_P):  # + the w-stacking fields strip_tile_bits reads
-    def __init__(self, prm):
-        super().__init__(prm)
-        self.do_wstacking = int(prm.get("do_wstacking", 0))
-        self.nplanes, self.w0, self.dw = prm["nplanes"], prm["w0"], prm["dw"]
-
-
-@pytest.mark.parametrize("wstack,support", [(False, 8), (True, 6), (False, 48), (False, 64)])
-def test_strip_tile_mask_covers_every_gridded_cell(wstack, support):
-    # cip_strip_rows_masked reads only the marked tiles: every non-zero cell of
-    # a rank's gridded strip buffer (and the halo rows it receives) must lie in
-    # a marked tile of its plane, and the mask must be sparse. W = 48 / 64
-    # footprints cross three 32-cell tiles per axis (the middle one included).
-    from _strip_np import NumpyStripBackend
-
-    npix = 512
-    uvw, f, vis, w, _ = _case(nrow=900, nchan=12)
-    px = syn.pixel_size_for_grid(uvw, f, npix)
-    if wstack:
-        uvw = uvw * np.array([1.0, 1.0, 40.0])
-        wmin, wmax = oracle.w_range(uvw, f)
-        prm = oracle.choose_params(npix, npix, px, px, support=support, do_wstacking=True, wmin=wmin, wmax=wmax)
-    else:
-        prm = oracle.choose_params(npix, npix, px, px, support=support)
-    world = 3
-    tu, tf = torch.from_numpy(uvw), torch.from_numpy(f)
-    layout = strips.plan_strips(tu, tf, _P(prm), px, npix, npix, world)
-    tv = torch.from_numpy(vis.astype(np.complex128))
-    tw = torch.from_numpy(w.astype(np.float64))
-    nu, nv = prm["nu"], prm["nv"]
-    for r in range(world):
-        y0, y1 = layout.rows(r)
-        rows, c0, c1 = strips.strip_slices(tu, tf, _P(prm), px, y0, y1)
-        data = strips.gather_strip(tu, tv, tw, rows, c0, c1)
-        be = NumpyStripBackend(prm, px, px, npix, npix).bind(layout, r)
-        grid, _ = be.grid_strip(data, tf)
-        bits = strips.strip_tile_bits(data, tf, _PW(prm), px, px, be.rows[0], prm["support"] - 1).numpy()
-        planes = grid.numpy() if grid.dim() == 4 else grid.numpy()[None]
-        assert bits.shape == (planes.shape[0], nv // 32, nu // 1024)
-        marked = 0
-        for p in range(planes.shape[0]):
-            k, x = np.nonzero(np.abs(planes[p]).sum(-1))
-            gy = (be.rows[0] + k) % nv
-            words = bits[p][gy // 32, x // 1024].astype(np.int64) & 0xFFFFFFFF
-            assert np.all((words >> ((x // 32) % 32)) & 1), (r, p)
-            marked += int(np.unpackbits(bits[p].view(np.uint8)).sum())
-        assert marked < (0.5 if support <= 16 else 0.8) * planes.shape[0] * (nu // 32) * (nv // 32)
-
-
 @pytest.mark.parametrize("wstack", [False, True])
 def test_sparse_alltoall_equals_dense_and_sends_less(wstack):
     # the all-to-all carries only each rank's live pass-A rows (rows of an empty
