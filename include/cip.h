@@ -260,9 +260,9 @@ int cip_grid_tiles_strip(const double* slice_uvw, const int32_t* chan_start,
 /* cip_grid_tiles_strip that also writes the strip's dirty-tile bits for its
  * masked pass A (cip_strip_rows_masked / _packed): tile_bits (device, per w
  * plane (nv / 32) x (nu / 1024) uint32 words, the layout those calls read) =
- * the tiles this call's own planner marks for its flush (the one-shot path's
- * dirty mask) plus every tile of the tile rows holding grid rows row0 ..
- * row0 + W - 2 (the previous rank's halo is added there). Replaces
+ * the tiles this call's scatter flush writes a cell of (exact: reported by
+ * each work unit's flush) plus every tile of the tile rows holding grid rows
+ * row0 .. row0 + W - 2 (the previous rank's halo is added there). Replaces
  * strips.py's torch restatement of the mask (round 5) - every call computes
  * its own. */
 int cip_grid_tiles_strip_mask(const double* slice_uvw, const int32_t* chan_start,

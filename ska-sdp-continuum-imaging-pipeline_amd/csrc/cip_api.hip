@@ -268,6 +268,7 @@ static GridGeometry geometry(const cip_gridder_params& p, double px, double py) 
   g.plane_lo = 0;
   g.plane_hi = p.nplanes;
   g.grid_f32 = 0;
+  g.wmask = nullptr;
   return g;
 }
 
@@ -1293,14 +1294,19 @@ static int grid_accumulate(const double* uvw, int64_t nrow, const double* freq, 
     pp.g.rows = nrows;
     pp.g.oob = oob;
   }
-  const GridGeometry& g = pp.g;
+  uint32_t* wmask = nullptr;
   if (strip_bits) {
-    // the strip's dirty-tile bits for its masked pass A: this plan's own mask
-    // (the tiles this call's flush may write) + the tile rows receiving the
-    // previous rank's halo
-    if (g.ntx % 32 != 0) return set_error(CIP_EINVAL, "tile masks need nu / 32 to be a multiple of 32 tiles");
-    CIP_HIP_CHECK(launch_strip_mask(pp.plan.dmask, g, row0, g.support - 1, strip_bits, s));
+    // the strip's dirty-tile bits for its masked pass A: the tiles this
+    // call's flush writes (GridGeometry::wmask, exact) + the tile rows
+    // receiving the previous rank's halo (after the scatter, below)
+    if (pp.g.ntx % 32 != 0) return set_error(CIP_EINVAL, "tile masks need nu / 32 to be a multiple of 32 tiles");
+    const int64_t words = pp.g.nplanes * pp.g.nty * (pp.g.ntx / 32);
+    wmask = buf<uint32_t>(ws, "strip_wmask", words);
+    if (!wmask) return CIP_ENOMEM;
+    CIP_HIP_CHECK(hipMemsetAsync(wmask, 0, sizeof(uint32_t) * words, s));
+    pp.g.wmask = wmask;
   }
+  const GridGeometry& g = pp.g;
   const int64_t plane_elems = 2 * g.nu * g.rows;
   const int G = pp.plan.group;
   for (int64_t q = 0; q * G < g.nplanes; ++q) {
@@ -1309,6 +1315,7 @@ static int grid_accumulate(const double* uvw, int64_t nrow, const double* freq, 
     if (rc != CIP_OK) return rc;
   }
   if (sum_wgt) CIP_HIP_CHECK(launch_add_scalar(pp.red, sum_wgt, s));
+  if (strip_bits) CIP_HIP_CHECK(launch_strip_mask(wmask, g, row0, g.support - 1, strip_bits, s));
   g_prof.span(5, t_start, g_prof.mark(s));
   unsigned* h_oob = nullptr;
   if (oob) {

@@ -240,7 +240,31 @@ struct GridGeometry {
   // packed single class's own planes on the pruned-FFT path (cip_ms2dirty),
   // half the flush and pass-A bytes (ducc0's float class grids in float32)
   int grid_f32;
+  // written-tile mask (optional, zeroed by the caller): the scatter's flush
+  // sets bit tx % 32 of word [p][ty][tx / 32] for every 32 x 32 tile (tx, ty)
+  // of plane p it writes a cell of - the exact dirty tiles of the gridded
+  // planes (the uv-strip ranks' masked pass A, cip_grid_tiles_strip_mask)
+  uint32_t* wmask;
 };
+
+// The flush's report to GridGeometry::wmask: `bits` = the tiles of one work
+// unit's sub-grid its flush wrote, bit dx * 3 + dy for tile (X0 / T + dx,
+// Y0 / T + dy) (wrapped; dx, dy <= 2: the sub-grid spans T + W - 1 <= 95
+// cells), plane p. A handful of device atomics per work unit.
+__device__ __forceinline__ void wmask_report(const GridGeometry& g, int64_t p, int64_t X0, int64_t Y0,
+                                             unsigned bits) {
+  const int64_t tx0 = X0 / kTile, ty0 = Y0 / kTile;
+  const int64_t wpr = g.ntx / 32;
+  uint32_t* m = g.wmask + p * g.nty * wpr;
+  while (bits) {
+    const int b = __builtin_ctz(bits);
+    bits &= bits - 1u;
+    int64_t tx = tx0 + b / 3, ty = ty0 + b % 3;
+    tx -= tx >= g.ntx ? g.ntx : 0;
+    ty -= ty >= g.nty ? g.nty : 0;
+    atomicOr(m + ty * wpr + tx / 32, 1u << (unsigned)(tx % 32));
+  }
+}
 
 // Buffer offset (complex cells) of grid cell (gx, gy) in wrapped coordinates,
 // or -1 outside the buffer's row window.

@@ -212,7 +212,10 @@ constexpr uint32_t kNoKey = 0xffffffffu;  // visibility off the grid (tile keys 
 // its predecessor's plan (CIP_REUSE_PLAN) gets the same sums bit for bit.
 // blk / nblocks: this place block and their count.
 // RM: the row map, at compile time (each mode's registers only): 0 dense MS
-// rows, 2 ragged row slices
+// rows, 1 dense rows of a multiple of 64 channels (every wave's 64
+// visibilities are channels of ONE row: the row, its uvw and the run
+// detection's row check are wave-uniform - scalar registers and loads), 2
+// ragged row slices
 template <typename VisT, int WK, bool PLACE, int RM>
 __device__ __forceinline__ void place_body(const double* __restrict__ uvw, const double* __restrict__ fx,
                                            const RowMap& m, const VisT* __restrict__ vis,
@@ -221,7 +224,8 @@ __device__ __forceinline__ void place_body(const double* __restrict__ uvw, const
                                            uint32_t* __restrict__ park_key, uint64_t* __restrict__ park_run,
                                            double* partial, int64_t* __restrict__ hist0, const int64_t blk,
                                            const int64_t nblocks) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   __shared__ unsigned s_nruns;
   __shared__ unsigned s_hist[256];
   if (threadIdx.x == 0) s_nruns = 0u;
@@ -230,8 +234,10 @@ __device__ __forceinline__ void place_body(const double* __restrict__ uvw, const
   // fused prep reduction (sum of weights, max |w V|), fixed order
   double wsum = 0.0, wvmax = 0.0;
   bool nonfinite = false;
+  bool bad_any = false;  // a placement failed (reported once, after the loop)
   const int64_t nvis = m.nvis, nchan = m.nchan;
   constexpr bool ragged = RM == 2;
+  constexpr bool rowwave = RM == 1;
   const int64_t nseg = (nvis + 63) / 64;
   const int P = kTile + g.support - 1;
   // block b owns segments [64 b, 64 b + 64): wave w takes every 4th
@@ -240,7 +246,14 @@ __device__ __forceinline__ void place_body(const double* __restrict__ uvw, const
   // step without a division
   // (ragged rows: from the segment's first row, ragged_row_of)
   int64_t r0 = 0, c0 = 0;
-  if (!ragged) split_index64((blk * kPlaceSegs + wave) * 64 + lane, nchan, m.inv_nchan, &r0, &c0);
+  if (rowwave) {
+    // the wave's row and first channel (wave-uniform: the lane adds its own)
+    const int64_t i0 = (blk * kPlaceSegs + wave) * 64;
+    r0 = i0 / nchan;
+    c0 = i0 - r0 * nchan;
+  } else if (!ragged) {
+    split_index64((blk * kPlaceSegs + wave) * 64 + lane, nchan, m.inv_nchan, &r0, &c0);
+  }
   const int64_t step_r = 256 / nchan, step_c = 256 % nchan;
   // ragged rows: the first rows of the wave's kPlaceSegs / 4 segments and the
   // starts of the rows after them, loaded once (lane j: segment j), so the
@@ -260,8 +273,9 @@ __device__ __forceinline__ void place_body(const double* __restrict__ uvw, const
   int it = 0;
   for (int64_t seg = blk * kPlaceSegs + wave; seg < seg_end; seg += 4, ++it) {
     const int64_t i = seg * 64 + lane;
-    const bool valid = i < nvis;
-    int64_t r = r0, c = c0;
+    // rowwave: nvis = nrow nchan is a multiple of 64, every segment is whole
+    const bool valid = rowwave ? true : i < nvis;
+    int64_t r = r0, c = rowwave ? c0 + lane : c0;
     // lanes past the end load index 0's data (no divergent branch around the
     // loads); their results are masked by `valid`
     const int64_t il = valid ? i : 0;
@@ -294,7 +308,7 @@ __device__ __forceinline__ void place_body(const double* __restrict__ uvw, const
     if constexpr (PLACE) {
       u = uvw[3 * rl];
       v = uvw[3 * rl + 1];
-      w = uvw[3 * rl + 2];
+      if (g.do_wstacking) w = uvw[3 * rl + 2];  // (uniform)
       f = fx[cl];
     }
     {
@@ -313,8 +327,9 @@ __device__ __forceinline__ void place_body(const double* __restrict__ uvw, const
       int64_t iw0;
       const bool ok = place_origin(u, v, w, f, g, &ix0, &iy0, &iw0);
       // a w layer feeds planes [iw0, iw0 + W): dropped when none is in the
-      // call's plane range (plane groups split over GPUs)
-      const bool feeds = (iw0 + g.support > g.plane_lo) & (iw0 < g.plane_hi);
+      // call's plane range (plane groups split over GPUs; 2-D: the one plane)
+      bool feeds = true;
+      if (g.do_wstacking) feeds = (iw0 + g.support > g.plane_lo) & (iw0 < g.plane_hi);
       // the tile key modulo 2^32 (keys are < 2^32 - 1)
       // tile_key(): tile-major, the w layers of a uv tile adjacent
       const uint32_t key = (valid & ok & feeds) ? ((((uint32_t)iy0 / (uint32_t)kTile) * (uint32_t)g.ntx +
@@ -322,15 +337,20 @@ __device__ __forceinline__ void place_body(const double* __restrict__ uvw, const
                                                (uint32_t)g.ntw +
                                            (uint32_t)iw0)
                                         : kNoKey;
-      const bool bad = valid & !ok;
+      bad_any = bad_any | (valid & !ok);
+      // the bank class ((ix0 % T) P + iy0 % T) % 32 (T = 32)
       if (vis_class && valid)
-        vis_class[i] = ok ? (uint8_t)((((unsigned)ix0 % kTile) * P + (unsigned)iy0 % kTile) & 31u) : (uint8_t)0;
-      if (__ballot(bad) != 0ull && lane == 0) atomicOr(err_flag, 1u);
+        vis_class[i] = ok ? (uint8_t)(((unsigned)ix0 * (unsigned)P + (unsigned)iy0) & 31u) : (uint8_t)0;
       // the previous lane's key and row: DPP wave_shr:1 (a VALU move; __shfl_up
       // is an LDS ds_bpermute with its own latency); lane 0 is a start anyway
       const uint32_t prev = wave_shr1(key);
-      const uint32_t prev_r = wave_shr1((uint32_t)r);  // rows < 2^32
-      const bool start = valid && (lane == 0 || (uint32_t)r != prev_r || key != prev);
+      bool start;
+      if constexpr (rowwave) {
+        start = lane == 0 || key != prev;  // one row per wave
+      } else {
+        const uint32_t prev_r = wave_shr1((uint32_t)r);  // rows < 2^32
+        start = valid && (lane == 0 || (uint32_t)r != prev_r || key != prev);
+      }
       const unsigned long long starts = __ballot(start);
       const bool emit = start && key != kNoKey;
       const unsigned long long emits = __ballot(emit);
@@ -357,6 +377,7 @@ __device__ __forceinline__ void place_body(const double* __restrict__ uvw, const
   __shared__ double ss[4], sm[4];
   {
     if (nonfinite) atomicOr(err_flag, 2u);
+    if (bad_any) atomicOr(err_flag, 1u);
     for (int d = 32; d > 0; d >>= 1) {
       wsum += __shfl_xor(wsum, d, 64);
       wvmax = fmax(wvmax, __shfl_xor(wvmax, d, 64));
@@ -431,7 +452,7 @@ hipError_t launch_plan_place(const double* uvw, const double* fx, const RowMap& 
                              unsigned* err_flag, uint8_t* vis_class, int64_t* blk_cnt, uint32_t* park_key,
                              uint64_t* park_run, double* partial, int64_t* hist0, hipStream_t s) {
   const dim3 gd(plan_blocks(m.nvis));
-  const int rm = m.delta != nullptr ? 2 : 0;
+  const int rm = m.delta != nullptr ? 2 : (m.nchan % 64 == 0 ? 1 : 0);
 #define PLACE_RM(VT, WKV, RMV)                                                                                      \
   plan_place_kernel<VT, WKV, true, RMV><<<gd, dim3(256), 0, s>>>(uvw, fx, m, (const VT*)vis, wgt, g, err_flag,     \
                                                                  vis_class, blk_cnt, park_key, park_run, partial,   \
@@ -440,6 +461,8 @@ hipError_t launch_plan_place(const double* uvw, const double* fx, const RowMap& 
   do {                            \
     if (rm == 2) {                \
       PLACE_RM(VT, WKV, 2);       \
+    } else if (rm == 1) {         \
+      PLACE_RM(VT, WKV, 1);       \
     } else {                      \
       PLACE_RM(VT, WKV, 0);       \
     }                             \

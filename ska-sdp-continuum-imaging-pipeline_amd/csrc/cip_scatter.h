@@ -350,6 +350,15 @@ __device__ __forceinline__ void flush_subgrid(const unsigned long long* sub, con
   const bool own = store_private != 0 && ch.sole != 0;
   // packed class on complex64 planes (GridGeometry::grid_f32)
   const bool f32 = PACK && g.grid_f32 != 0;
+  // the tiles this unit writes, per plane (GridGeometry::wmask; uniform branch)
+  __shared__ unsigned s_wm[G];
+  unsigned wm[G];
+#pragma unroll
+  for (int k = 0; k < G; ++k) wm[k] = 0u;
+  if (g.wmask) {
+    if (threadIdx.x < G) s_wm[threadIdx.x] = 0u;
+    __syncthreads();
+  }
   // one pass over the cells for all G planes: a cell's G sub-grid values are
   // read together and its HBM offset (the wrap, the strip's row map, the
   // transposed layout: ~45 VALU) is computed once, not once per plane - on the
@@ -381,9 +390,11 @@ __device__ __forceinline__ void flush_subgrid(const unsigned long long* sub, con
     }
     const int lx = lcell / P, ly = lcell % P;
     const bool priv = own && lx >= W - 1 && lx < T && ly >= W - 1 && ly < T;
+    const unsigned tbit = 1u << ((lx / T) * 3 + ly / T);
 #pragma unroll
     for (int k = 0; k < G; ++k) {
       if ((sv[k] | si[k]) == 0ull) continue;  // (also every plane outside the call's range)
+      wm[k] |= tbit;
       long long re, im;
       if constexpr (PACK) {
         im = (long long)(int)(unsigned)sv[k];
@@ -413,6 +424,13 @@ __device__ __forceinline__ void flush_subgrid(const unsigned long long* sub, con
         unsafeAtomicAdd(dst + 1, (double)im * inv_scale);
       }
     }
+  }
+  if (g.wmask) {
+#pragma unroll
+    for (int k = 0; k < G; ++k)
+      if (wm[k]) atomicOr(&s_wm[k], wm[k]);
+    __syncthreads();
+    if (threadIdx.x < G && s_wm[threadIdx.x]) wmask_report(g, plane + threadIdx.x, X0, Y0, s_wm[threadIdx.x]);
   }
 }
 

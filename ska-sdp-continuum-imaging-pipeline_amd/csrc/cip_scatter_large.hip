@@ -161,7 +161,10 @@ __global__ __launch_bounds__(kLargeThreads) void scatter_large_kernel(
       }
     }
   }
+  __shared__ unsigned s_wm;  // the tiles the flush writes (GridGeometry::wmask)
+  if (threadIdx.x == 0) s_wm = 0u;
   __syncthreads();
+  unsigned wm = 0u;
   for (int cell = threadIdx.x; cell < PP; cell += kLargeThreads) {
     const int lcell = g.transposed ? (cell % P) * P + cell / P : cell;  // lx * P + ly
     const long long re = (long long)sub[lcell];
@@ -175,10 +178,16 @@ __global__ __launch_bounds__(kLargeThreads) void scatter_large_kernel(
         if (g.oob) atomicOr(g.oob, 1u);
         continue;
       }
+      wm |= 1u << ((lcell / P / T) * 3 + (lcell % P) / T);
       double* dst = grid + 2 * off;
       unsafeAtomicAdd(dst, (double)re * inv_scale);
       unsafeAtomicAdd(dst + 1, (double)im * inv_scale);
     }
+  }
+  if (g.wmask) {
+    if (wm) atomicOr(&s_wm, wm);
+    __syncthreads();
+    if (threadIdx.x == 0 && s_wm) wmask_report(g, plane, X0, Y0, s_wm);
   }
 }
 
