@@ -12,7 +12,7 @@ case $unit in scatter_w*) src=cip_scatter_w.hip; extra="-DCIP_SCATTER_W=${unit#s
 /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -fPIC -munsafe-fp-atomics -I../../include -I. \
   $extra "$@" -c $src -o build/variant_$name.o
 objs=""
-for u in api plan grid tiling fft collective scatter_w4 scatter_w6 scatter_w8 scatter_w10 scatter_w12 scatter_w14 scatter_w16 \
+for u in api plan grid tiling fft collective strips scatter_w4 scatter_w6 scatter_w8 scatter_w10 scatter_w12 scatter_w14 scatter_w16 \
          scatter_large_w24 scatter_large_w32 scatter_large_w48 scatter_large_w64; do
   [ "$u" = "$unit" ] || objs="$objs build/cip_$u.o"
 done
