@@ -14,6 +14,7 @@
 #   strong           bench --strong (C4 strong split at N = 1)
 #   refcall          the reference call alone (--wstacking --single --epsilon-call)
 #   ab=ENVSPEC       interleaved A/B of the quick line: ENVSPEC "K=V,K2=V2" vs the default (3 pairs)
+#   abrc=ENVSPEC     the same for the reference call (w-stacking, eps 1e-4, packed class)
 #   py=SCRIPT[:ARGS] python SCRIPT ARGS (tools), 300 s limit
 # Output: gpurun_out/<TAG>_<step>.{log,json,md}
 set -o pipefail
@@ -63,6 +64,12 @@ for step in "$@"; do
       for i in 1 2 3; do
         run 300 "ab_base$i" python bench.py $QUICK || exit 1
         run 300 "ab_var$i" env ${spec//,/ } python bench.py $QUICK || exit 1
+      done ;;
+    abrc=*)
+      spec=${step#abrc=}
+      for i in 1 2 3; do
+        run 300 "abrc_base$i" python bench.py --wstacking --single --epsilon-call $QUICK || exit 1
+        run 300 "abrc_var$i" env ${spec//,/ } python bench.py --wstacking --single --epsilon-call $QUICK || exit 1
       done ;;
     py=*)
       s=${step#py=}
