@@ -395,6 +395,53 @@ struct ColEpilogue {
   const double* norm;  // MODE 0: divide by *norm (the weight sum), NULL = no
 };
 
+// The packed class's w screen (fp32 transforms), round 6. Pass B of the
+// reference call was VALU-bound on its epilogue (~130 instructions an image
+// cell: fp64 sqrt with denormal scaling, an fp64 divide, ocml's general
+// sincospif). Three cheaper steps with the same phase accuracy:
+//  - n - 1 = sqrt(1 - e) - 1 directly: only its ABSOLUTE error enters the
+//    phase (2 pi w (n - 1)), and that is one ulp of 1 (1.1e-16) whichever
+//    form is used - the -e / (sqrt(1 - e) + 1) form only buys relative
+//    accuracy for tiny e, which the phase does not need;
+//  - sqrt(x), x = 1 - e in (0, 1]: hardware rsq_f64 and one Newton-Raphson
+//    correction (no scaling: x is never denormal or huge);
+//  - sin / cos (pi x) for the already-reduced |x| <= 1 (half turns): quadrant
+//    n = rint(2 x), |y| = |x - n / 2| <= 1/4, Taylor polynomials of degree 9 /
+//    10 (truncation < 2e-9), then the quadrant's swap and signs.
+// The n - 1 and phase stay fp64 (|phase| reaches hundreds of half turns),
+// only the reduced angle's sine and cosine are fp32, as before.
+__device__ __forceinline__ double screen_nm1(double e) {
+  const double x = 1.0 - e;
+  const double y = __builtin_amdgcn_rsq(x);
+  double s = x * y, h = 0.5 * y;
+  const double r = fma(-h, s, 0.5);
+  s = fma(s, r, s);
+  h = fma(h, r, h);
+  s = fma(fma(-s, s, x), h, s);
+  return s - 1.0;
+}
+
+__device__ __forceinline__ void screen_sincospi(float x, float* sn, float* cs) {
+  const float n = rintf(2.0f * x);
+  const float y = fmaf(-0.5f, n, x);
+  const float y2 = y * y;
+  // pi^(2k+1) / (2k+1)! and pi^(2k) / (2k)!, alternating signs
+  float ps = fmaf(y2, 0.0821458866111282f, -0.599264529320792f);
+  ps = fmaf(y2, ps, 2.55016403987735f);
+  ps = fmaf(y2, ps, -5.16771278004997f);
+  ps = fmaf(y2, ps, 3.14159265358979f);
+  float pc = fmaf(y2, -0.0258068913900140f, 0.235330630358893f);
+  pc = fmaf(y2, pc, -1.33526276885459f);
+  pc = fmaf(y2, pc, 4.05871212641677f);
+  pc = fmaf(y2, pc, -4.93480220054468f);
+  const float sv = y * ps, cv = fmaf(y2, pc, 1.0f);
+  // sin / cos (pi y + n pi / 2): n mod 4 = 0 (s, c), 1 (c, -s), 2 (-s, -c), 3 (-c, s)
+  const int q = (int)n & 3;
+  const float a = (q & 1) ? cv : sv, b = (q & 1) ? sv : cv;
+  *sn = (q & 2) ? -a : a;
+  *cs = ((q + 1) & 2) ? -b : b;
+}
+
 // A strip of image rows [i0, i0 + gridDim.x): H holds the
 // blocks from i0 / kColBlock on (i0 a multiple of kColBlock), and image row i
 // goes to ep.out row i - i0. The whole image: i0 = 0.
@@ -442,49 +489,69 @@ __global__ __launch_bounds__(N / 16, fft_waves<CT>()) void fft_cols_kernel(const
     v[r] = ccast<CT>(raw[r]);
   }
   fft_core<N>(v, t, lds, tw);
-  const int64_t p = i - nx / 2;
+  // (nx, ny <= N <= 16384: the crop indices are 32-bit)
+  const int p = (int)(i - nx / 2);
+  const int nyi = (int)ny;
   OT* orow = reinterpret_cast<OT*>(ep.out) + il * ny;
   const double cxi = MODE == 0 ? (ep.norm ? ep.cx[i] / *ep.norm : ep.cx[i]) : 0.0;
+  const double l = (double)p * ep.px;
+  const double l2 = l * l;
+  // MODE 1 accumulating into float planes: the accumulator's old values,
+  // every load issued before the first is used (a load inside the loop below
+  // is waited for before its own add, 8 serialised HBM round trips a lane);
+  // the loads come before every store, so no aliasing holds them back. (fp64
+  // planes load in the loop: 16 more doubles live would cost the fp64
+  // transform its second workgroup per CU, 124 -> 154 VGPRs)
+  constexpr bool kHoist = std::is_same<OT, float>::value;
+  OT old[16];
+  if (MODE == 1 && kHoist && !ep.first) {
+#pragma unroll
+    for (int m = 0; m < 16 / S::RF; ++m)
+#pragma unroll
+      for (int r = 0; r < S::RF; ++r) {
+        const int j = (out_pos<N, S::RF>(t, m, r, N / S::RF) + nyi / 2) & (N - 1);
+        old[m * S::RF + r] = j < nyi ? orow[j] : OT(0);
+      }
+  }
 #pragma unroll
   for (int m = 0; m < 16 / S::RF; ++m)
 #pragma unroll
     for (int r = 0; r < S::RF; ++r) {
       const int k = out_pos<N, S::RF>(t, m, r, N / S::RF);
-      const int64_t j = (int64_t)((k + (int)(ny / 2)) & (N - 1));
-      if (j < ny) {
-        const int64_t q = j - ny / 2;
+      const int j = (k + nyi / 2) & (N - 1);
+      if (j < nyi) {
+        const int q = j - nyi / 2;
         const double sgn = ((p + q) & 1) ? -1.0 : 1.0;
         const double2 g = ccast<double2>(v[m * S::RF + r]);
         if constexpr (MODE == 0) {
           orow[j] = sgn * g.x * cxi * ep.cy[j];
         } else {
-          const double l = (double)p * ep.px, mm = (double)q * ep.py;
-          const double e = l * l + mm * mm;
-          const double nm1 = -e / (sqrt(1.0 - e) + 1.0);
+          const double mm = (double)q * ep.py;
+          const double e = fma(mm, mm, l2);
           double sn, cs;
-          const double ph = -2.0 * ep.w_plane * nm1;  // the screen's phase / pi
           if constexpr (sizeof(CT) == 8 && CIP_SCREEN_F32 == 1) {
-            // fp32 transforms (the packed class): the phase is reduced exactly
-            // in fp64 to [-1, 1] (period 2) and only its sine and cosine are
-            // fp32 - ~1e-7, the class's own rounding of the plane values
+            // fp32 transforms (the packed class): the phase / pi is reduced
+            // exactly in fp64 to [-1, 1] (period 2) and only its sine and
+            // cosine are fp32 - ~1e-7, the class's own rounding of the plane
+            // values (screen_nm1 / screen_sincospi above)
+            const double ph = -2.0 * ep.w_plane * screen_nm1(e);
             const float red = (float)(ph - 2.0 * rint(0.5 * ph));
             float sf, cf;
-            sincospif(red, &sf, &cf);
+            screen_sincospi(red, &sf, &cf);
             sn = sf;
             cs = cf;
           } else if constexpr (sizeof(CT) == 8 && CIP_SCREEN_F32 == 2) {
-            sn = 0.0 * ph;  // ablation (timing only, wrong images)
+            sn = 0.0 * e;  // ablation (timing only, wrong images)
             cs = 1.0;
           } else {
+            const double nm1 = -e / (sqrt(1.0 - e) + 1.0);
+            const double ph = -2.0 * ep.w_plane * nm1;  // the screen's phase / pi
             sincospi(ph, &sn, &cs);
           }
+          // one rounding per plane for float planes: acc = (OT)((double)acc + val)
           const double val = sgn * (g.x * cs - g.y * sn);
-          if constexpr (std::is_same<OT, float>::value) {
-            orow[j] = ep.first ? (float)val : (float)((double)orow[j] + val);
-          } else {
-            if (ep.first) orow[j] = val;
-            else orow[j] += val;
-          }
+          if (ep.first) orow[j] = (OT)val;
+          else orow[j] = (OT)((double)(kHoist ? old[m * S::RF + r] : orow[j]) + val);
         }
       }
     }
