@@ -9,12 +9,14 @@
 #   quick            bench without CPU baseline / max|err| / secondaries
 #   prof             rocprofv3 kernel trace of the headline + summary
 #   profrc           rocprofv3 kernel trace of the reference call (w-stacking, eps 1e-4)
+#   profc4           rocprofv3 kernel trace of the C4 line (synchronous calls)
 #   pmc              FETCH_SIZE / WRITE_SIZE / TCC_EA0_ATOMIC passes (synchronous steps)
 #   c4               the C4 shard line
 #   strong           bench --strong (C4 strong split at N = 1)
 #   refcall          the reference call alone (--wstacking --single --epsilon-call)
 #   ab=ENVSPEC       interleaved A/B of the quick line: ENVSPEC "K=V,K2=V2" vs the default (3 pairs)
 #   abrc=ENVSPEC     the same for the reference call (w-stacking, eps 1e-4, packed class)
+#   abc4=ENVSPEC     the same for the C4 line (one-shot calls timed synchronously too)
 #   py=SCRIPT[:ARGS] python SCRIPT ARGS (tools), 300 s limit
 # Output: gpurun_out/<TAG>_<step>.{log,json,md}
 set -o pipefail
@@ -50,6 +52,11 @@ for step in "$@"; do
         python3 bench.py --wstacking --single --epsilon-call --sync $QUICK || exit 1
       python3 tools/trace_summary.py "$OUT/profrc_${TAG}/${TAG}rc_kernel_trace.csv" 10 \
         "$OUT/${TAG}_refcall_kernel_summary.md" > /dev/null || exit 1 ;;
+    profc4)
+      run 400 profc4 rocprofv3 --kernel-trace --stats -d "$PWD/$OUT/profc4_${TAG}" -o "${TAG}c4" --output-format csv -- \
+        python3 bench.py --config c4 --sync --steps 6 --warmup 2 $QUICK || exit 1
+      python3 tools/trace_summary.py "$OUT/profc4_${TAG}/${TAG}c4_kernel_trace.csv" 5 \
+        "$OUT/${TAG}_c4_kernel_summary.md" > /dev/null || exit 1 ;;
     pmc)
       A="--steps 2 --warmup 1 --sync $QUICK"
       for c in FETCH_SIZE WRITE_SIZE TCC_EA0_ATOMIC_sum; do
@@ -70,6 +77,12 @@ for step in "$@"; do
       for i in 1 2 3; do
         run 300 "abrc_base$i" python bench.py --wstacking --single --epsilon-call $QUICK || exit 1
         run 300 "abrc_var$i" env ${spec//,/ } python bench.py --wstacking --single --epsilon-call $QUICK || exit 1
+      done ;;
+    abc4=*)
+      spec=${step#abc4=}
+      for i in 1 2 3; do
+        run 300 "abc4_base$i" python bench.py --config c4 $QUICK || exit 1
+        run 300 "abc4_var$i" env ${spec//,/ } python bench.py --config c4 $QUICK || exit 1
       done ;;
     py=*)
       s=${step#py=}
