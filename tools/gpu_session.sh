@@ -11,6 +11,7 @@
 #   profrc           rocprofv3 kernel trace of the reference call (w-stacking, eps 1e-4)
 #   profc4           rocprofv3 kernel trace of the C4 line (synchronous calls)
 #   pmc              FETCH_SIZE / WRITE_SIZE / TCC_EA0_ATOMIC passes (synchronous steps)
+#   pmcc4            FETCH_SIZE / WRITE_SIZE passes of the C4 line
 #   c4               the C4 shard line
 #   strong           bench --strong (C4 strong split at N = 1)
 #   refcall          the reference call alone (--wstacking --single --epsilon-call)
@@ -61,6 +62,12 @@ for step in "$@"; do
       A="--steps 2 --warmup 1 --sync $QUICK"
       for c in FETCH_SIZE WRITE_SIZE TCC_EA0_ATOMIC_sum; do
         run 300 "pmc_$c" rocprofv3 --pmc $c -d "$PWD/$OUT/pmc_${TAG}_$c" -o "pmc_$c" --output-format csv -- \
+          python3 bench.py $A || exit 1
+      done ;;
+    pmcc4)
+      A="--config c4 --steps 2 --warmup 1 --sync $QUICK"
+      for c in FETCH_SIZE WRITE_SIZE; do
+        run 300 "pmcc4_$c" rocprofv3 --pmc $c -d "$PWD/$OUT/pmcc4_${TAG}_$c" -o "pmc_$c" --output-format csv -- \
           python3 bench.py $A || exit 1
       done ;;
     c4) run 400 c4 python bench.py --config c4 --no-cpu-baseline --no-secondary --no-strong-secondary || exit 1 ;;
