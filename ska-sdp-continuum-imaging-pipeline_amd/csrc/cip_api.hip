@@ -1185,10 +1185,13 @@ static int plane_to_dirty(const DirtyStage& st, const GridGeometry& g, int64_t p
                           const uint32_t* rowbits = nullptr, int first = -1, bool acc_f32 = false) {
   if (first < 0) first = p == 0;  // the first plane overwrites the image, later ones add
   hipEvent_t f0 = g_prof.mark(s);
+  // 16384-point fp64 columns of a 2-D image: pass B by even / odd halves
+  // (cip_fft.hip fft_cols_eo_kernel), pass A writing H in that order
+  const bool eo = st.fast && fft_cols_eo(g.nv, st.npix_y, g.grid_f32 != 0, g.do_wstacking ? 1 : 0);
   if (st.fast) {
     if (!fft_rowskip()) rowbits = nullptr;
     CIP_HIP_CHECK(launch_fft_rows(grid, g.nu, g.nv, st.npix_x, st.tw_u, st.fft_h, dmask, g.ntx, rowbits != nullptr, s,
-                                  g.grid_f32 != 0));
+                                  g.grid_f32 != 0, eo));
   } else if (hipfftExecZ2Z(st.plan, (hipfftDoubleComplex*)grid, (hipfftDoubleComplex*)grid, HIPFFT_BACKWARD) !=
              HIPFFT_SUCCESS) {
     return set_error(CIP_EHIP, "hipfftExecZ2Z failed");
@@ -1198,7 +1201,7 @@ static int plane_to_dirty(const DirtyStage& st, const GridGeometry& g, int64_t p
   if (st.fast)
     CIP_HIP_CHECK(launch_fft_cols(st.fft_h, g.nv, st.npix_x, st.npix_y, st.tw_v, g.do_wstacking ? 1 : 0, dirty_out,
                                   st.cx, st.cy, st.px, st.py, w_plane, first, g.do_wstacking ? nullptr : norm,
-                                  dmask ? rowbits : nullptr, s, g.grid_f32 != 0, acc_f32));
+                                  dmask ? rowbits : nullptr, s, g.grid_f32 != 0, acc_f32, eo));
   hipEvent_t f1 = g_prof.mark(s);
   g_prof.span(3, f0, f1);
   if (st.fast) {

@@ -111,9 +111,15 @@ __device__ __forceinline__ void dft(CT* v) {
 
 // One Stockham pass of radix R over the thread's 16 values (16 / R
 // butterflies j_m = t + m T), twiddles from the table tw[m] = exp(+2 pi i m / N).
-template <int N, int R, typename CT>
+// TWS: the table's stride (tw holds exp(+2 pi i m / (TWS N)): the even / odd
+// halves of a 2N-point column transform their N points with the 2N table)
+// LASTW: the last pass's twiddles (ns R = N: w = tw[t + m T]) as tw[t] W16^m,
+// one table load per lane instead of one per butterfly (16 / R loads in
+// flight at once: the registers the even / odd pass B needs)
+template <int N, int R, typename CT, int TWS = 1, bool LASTW = false>
 __device__ __forceinline__ void stockham_pass(CT* v, int t, int ns, const double2* __restrict__ tw) {
   constexpr int T = N / 16;
+  const double2 wlast = (LASTW && ns * R == N) ? tw[t * TWS] : make_double2(1.0, 0.0);
 #pragma unroll
   for (int m = 0; m < 16 / R; ++m) {
     const int j = t + m * T;
@@ -122,7 +128,11 @@ __device__ __forceinline__ void stockham_pass(CT* v, int t, int ns, const double
       // exp(+2 pi i r k / (ns R)) = w^r, w = tw[k N / (ns R)]: one table load
       // per butterfly (the loads were latency on the critical path), powers by
       // repeated products (error grows by ~1 ulp per power, R <= 16)
-      const CT w = ccast<CT>(tw[(k * (N / (ns * R))) & (N - 1)]);
+      CT w;
+      if (LASTW && ns * R == N)
+        w = ccast<CT>(m == 0 ? wlast : cmul(wlast, make_double2(kW16c[m & 15], kW16c[(m + 12) & 15])));
+      else
+        w = ccast<CT>(tw[((k * (N / (ns * R))) & (N - 1)) * TWS]);
       CT wr = w;
 #pragma unroll
       for (int r = 1; r < R; ++r) {
@@ -219,6 +229,9 @@ constexpr int kColBlock = CIP_FFT_COLBLOCK;
 #ifndef CIP_SCREEN_F32
 #define CIP_SCREEN_F32 1  // 0: fp64 w-screen sine / cosine on fp32 transforms too (A/B builds)
 #endif
+#ifndef CIP_FFT_EO
+#define CIP_FFT_EO 1  // 0: 16384-point fp64 pass B as one transform per workgroup (A/B builds)
+#endif
 #ifndef CIP_FFT_ROWS_XCD
 #define CIP_FFT_ROWS_XCD 1  // 0: pass A's workgroup b transforms row b (A/B builds)
 #endif
@@ -253,21 +266,21 @@ struct FftShape {
   static constexpr int RF = B ? (1 << B) : 16;  // radix of the final pass
 };
 
-template <int N, typename CT>
+template <int N, typename CT, int TWS = 1, bool LASTW = false>
 __device__ __forceinline__ void fft_core(CT* v, int t, XT<CT>* lds, const double2* __restrict__ tw) {
   using S = FftShape<N>;
   int ns = 1;
-  stockham_pass<N, 16>(v, t, ns, tw);
+  stockham_pass<N, 16, CT, TWS, LASTW>(v, t, ns, tw);
 #pragma unroll
   for (int p = 1; p < S::P; ++p) {
     exchange<N, 16, 16>(v, t, ns, lds);
     ns *= 16;
-    stockham_pass<N, 16>(v, t, ns, tw);
+    stockham_pass<N, 16, CT, TWS, LASTW>(v, t, ns, tw);
   }
   if constexpr (S::B != 0) {
     exchange<N, 16, S::RF>(v, t, ns, lds);
     ns *= 16;
-    stockham_pass<N, S::RF>(v, t, ns, tw);
+    stockham_pass<N, S::RF, CT, TWS, LASTW>(v, t, ns, tw);
   }
 }
 
@@ -287,8 +300,11 @@ __device__ __forceinline__ void fft_core(CT* v, int t, XT<CT>* lds, const double
 // pass A's output as stored (HT = double2, or float2 beside complex64 planes:
 // the packed class's precision, half the pass-A write and pass-B read bytes)
 
+// EO (the whole grid, pass B by even / odd halves: fft_cols_eo_kernel): grid
+// row y goes to H row (y mod 2) nv / 2 + y / 2, so each half's rows are
+// contiguous.
 template <int N, bool MASKED, bool ZERO = false, typename GT = double2, typename HT = double2,
-          typename CT = double2>
+          typename CT = double2, bool EO = false>
 __global__ __launch_bounds__(N / 16, fft_waves_rows<CT>()) void fft_rows_kernel(GT* __restrict__ gT, int64_t hrows, int64_t nx,
                                                           const double2* __restrict__ tw, HT* __restrict__ H,
                                                           const uint32_t* __restrict__ dmask, int64_t ntx,
@@ -315,6 +331,7 @@ __global__ __launch_bounds__(N / 16, fft_waves_rows<CT>()) void fft_rows_kernel(
   // rows - H holds those only, in order; a dead row (no dirty tile in its
   // tile row: nothing to read or zero) is skipped
   int64_t orow = y - hy0;
+  if constexpr (EO) orow = (orow & 1) * (hrows >> 1) + (orow >> 1);
   if (row_slot) {
     orow = row_slot[y - hy0];
     if (orow < 0) return;
@@ -557,6 +574,131 @@ __global__ __launch_bounds__(N / 16, fft_waves<CT>()) void fft_cols_kernel(const
     }
 }
 
+// Pass B of the 2-D crop for fp64 columns of N = 2 NH points (C4's 16384;
+// round 6) as their even and odd halves in one workgroup, one after the other:
+//   X[k] = E[k'] + w^k' O[k'],  X[k + NH] = E[k'] - w^k' O[k'],  w = exp(2 pi i / N)
+// (E, O: the NH-point transforms of the column's even / odd rows, which pass A
+// wrote as the contiguous H halves: fft_rows_kernel EO). One N-point fp64
+// transform is 256 KiB of registers and 128 KiB of LDS, so fft_cols_kernel
+// runs ONE workgroup per CU, and a CU alternates between loading its column
+// (HBM busy, ALUs idle) and transforming it (the reverse): pass B ran at ~33 %
+// of the HBM roof. The NH-point halves need 64 KiB of LDS and <= 128 VGPRs:
+// two workgroups per CU, one loading while the other transforms.
+// With ny <= N / 2 (the host checks) at most one of k', k' + NH is kept. The
+// even half stores Re E[k'] into its output cell, the odd half reads it back
+// (the same lane: both halves use one output mapping) and finishes
+//   dirty[i, j] = (-1)^(p+q) (Re E[k'] +- Re(w^k' O[k'])) cx[i] cy[j].
+// Loads before stores, batches of 8 (see the MODE 1 epilogue).
+template <int NH>
+__global__ __launch_bounds__(NH / 16, 4) void fft_cols_eo_kernel(const double2* __restrict__ H, int64_t nx,
+                                                              int64_t ny, const double2* __restrict__ tw,
+                                                              ColEpilogue ep, const uint32_t* __restrict__ rowbits) {
+  constexpr int N = 2 * NH;
+  using S = FftShape<NH>;
+  // k' = t + m T + r NH / 2 (out_pos with a final radix-2 pass)
+  static_assert(S::RF == 2 && NH / 16 <= 1024 && kTile == 32, "even / odd pass B layout");
+  __shared__ double lds[kXLen<NH>];
+  const int64_t b = blockIdx.x;
+  int64_t il = b;
+  if (gridDim.x % (8 * kColBlock) == 0)
+    il = (b / (8 * kColBlock)) * (8 * kColBlock) + (b % 8) * kColBlock + (b / 8) % kColBlock;
+  const int64_t i = il;
+  const double2* col = H + ((il / kColBlock) * N) * kColBlock + (il % kColBlock);
+  const int p = (int)(i - nx / 2);
+  const int nyi = (int)ny;
+  double* orow = ep.out + il * ny;
+  const double cxi = ep.norm ? ep.cx[i] / *ep.norm : ep.cx[i];
+  // the output cell of element x (mod N: the kept one of k', k' + NH), or -1;
+  // tt / nyy: t and ny re-issued after each transform (below), so the
+  // compiler cannot compute the 16 cells ahead, inside the transform, where
+  // their registers spill
+  int tt = threadIdx.x, nyy = nyi;
+  auto cell = [&](int x, bool* plus) {
+    const int kp = out_pos<NH, 2>(tt, x / 2, x % 2, NH / 2);
+    const int j0 = (kp + nyy / 2) & (N - 1), j1 = (kp + NH + nyy / 2) & (N - 1);
+    *plus = j0 < nyy;
+    return j0 < nyy ? j0 : (j1 < nyy ? j1 : -1);
+  };
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {
+    const double2* hc = col + (int64_t)half * NH * kColBlock;
+    // the lane index re-issued per half: the compiler kept the transform's
+    // t-derived LDS addresses live from the first half to the second, and they
+    // spilled
+    int t = threadIdx.x;
+    asm volatile("" : "+v"(t));
+    double2 v[16];
+    if (rowbits) {
+      // H row n of a half is grid row 2 n + half, tile row n / 16: the word of
+      // element r ((t + r T) / 512 = r) is uniform over the block
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int n = t + r * S::T;
+        const uint32_t word = rowbits[(r * S::T) >> 9];
+        v[r] = make_double2(0.0, 0.0);
+        if ((word >> ((n >> 4) & 31)) & 1u) v[r] = hc[(int64_t)n * kColBlock];
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) v[r] = hc[(int64_t)(t + r * S::T) * kColBlock];
+    }
+    fft_core<NH, double2, 2, true>(v, t, lds, tw);
+    asm volatile("" : "+v"(tt), "+s"(nyy)::"memory");
+    if (half == 0) {
+#pragma unroll
+      for (int x = 0; x < 16; ++x) {
+        bool plus;
+        const int j = cell(x, &plus);
+        if (j >= 0) orow[j] = v[x].x;
+      }
+    } else {
+      // z = Re(w^k' O[k']), w^k' = w^t (w^T)^m i^r: one table load per lane
+      // and the 8 constants w^(m T) = exp(2 pi i m / 32) (immediates: loaded
+      // from the table, the compiler hoisted them into the transform, where
+      // they spilled); formed for all 16 elements first, so the transform's
+      // registers are free for the loads below
+      static_assert(N / S::T == 32, "w^T = exp(2 pi i / 32)");
+      constexpr double kc[8] = {1.0, 0.9807852804032304, 0.9238795325112867, 0.8314696123025452,
+                                0.7071067811865476, 0.5555702330196023, 0.38268343236508984, 0.19509032201612833};
+      constexpr double ks[8] = {0.0, 0.19509032201612825, 0.3826834323650898, 0.5555702330196022,
+                                0.7071067811865475, 0.8314696123025452, 0.9238795325112867, 0.9807852804032304};
+      const double2 wt = tw[t];
+      double z[16];
+#pragma unroll
+      for (int x = 0; x < 16; ++x) {
+        const double2 wm = cmul(wt, make_double2(kc[x / 2], ks[x / 2]));
+        const double2 w = (x % 2) ? make_double2(-wm.y, wm.x) : wm;  // times i^r, r = x % 2
+        z[x] = fma(w.x, v[x].x, -w.y * v[x].y);
+      }
+#pragma unroll
+      for (int c = 0; c < 16; c += 4) {
+        double e[4], cyv[4];
+#pragma unroll
+        for (int x = c; x < c + 4; ++x) {
+          bool plus;
+          const int j = cell(x, &plus);
+          e[x - c] = orow[j >= 0 ? j : 0];
+          cyv[x - c] = ep.cy[j >= 0 ? j : 0];
+        }
+#pragma unroll
+        for (int x = c; x < c + 4; ++x) {
+          bool plus;
+          const int j = cell(x, &plus);
+          const int q = j - nyi / 2;
+          const double sgn = ((p + q) & 1) ? -1.0 : 1.0;
+          e[x - c] = sgn * (plus ? e[x - c] + z[x] : e[x - c] - z[x]) * cxi * cyv[x - c];
+        }
+#pragma unroll
+        for (int x = c; x < c + 4; ++x) {
+          bool plus;
+          const int j = cell(x, &plus);
+          if (j >= 0) orow[j] = e[x - c];
+        }
+      }
+    }
+  }
+}
+
 // CIP_FFT_F32=0: the packed class's complex64 planes transformed in fp64
 // (the round-4 form); default: in fp32, the class's own precision
 bool fft_f32_enabled() {
@@ -574,9 +716,15 @@ bool fast_fft_supported(int64_t nu, int64_t nv, int64_t nx, int64_t ny) {
          ny % 2 == 0;
 }
 
+bool fft_cols_eo(int64_t nv, int64_t ny, bool grid_f32, int mode) {
+  return CIP_FFT_EO && nv == 16384 && ny <= nv / 2 && !grid_f32 && mode == 0;
+}
+
 hipError_t launch_fft_rows(double* gT, int64_t nu, int64_t nv, int64_t nx, const double* tw_u, double* H,
-                           const uint32_t* dmask, int64_t ntx, bool skip_clean, hipStream_t s, bool grid_f32) {
+                           const uint32_t* dmask, int64_t ntx, bool skip_clean, hipStream_t s, bool grid_f32,
+                           bool eo) {
   if (!fft_len_ok(nu) || !fft_len_ok(nv) || nx > nu) return hipErrorInvalidValue;
+  if (eo && (grid_f32 || nv % 2 != 0)) return hipErrorInvalidValue;
   if (dmask && (nu % kTile != 0 || nv % kTile != 0 || ntx * kTile != nu || ntx % 32 != 0))
     return hipErrorInvalidValue;
   const dim3 gd((unsigned)nv);
@@ -600,6 +748,12 @@ hipError_t launch_fft_rows(double* gT, int64_t nu, int64_t nv, int64_t nx, const
     else if (grid_f32)                                                                                        \
       fft_rows_kernel<NN, false, false, float2, float2><<<gd, dim3(NN / 16), 0, s>>>(gf, nv, nx, tw, hf,      \
                                                                                      nullptr, 0);             \
+    else if (dmask && eo)                                                                                     \
+      fft_rows_kernel<NN, true, false, double2, double2, double2, true><<<gd, dim3(NN / 16), 0, s>>>(         \
+          g, nv, nx, tw, h, dmask, ntx, 0, 0, skip_clean);                                                    \
+    else if (eo)                                                                                              \
+      fft_rows_kernel<NN, false, false, double2, double2, double2, true><<<gd, dim3(NN / 16), 0, s>>>(        \
+          g, nv, nx, tw, h, nullptr, 0);                                                                      \
     else if (dmask)                                                                                           \
       fft_rows_kernel<NN, true><<<gd, dim3(NN / 16), 0, s>>>(g, nv, nx, tw, h, dmask, ntx, 0, 0, skip_clean); \
     else                                                                                                      \
@@ -703,12 +857,18 @@ hipError_t launch_fft_cols_strip_wplane(const double* H, int64_t nv, int64_t nx,
 hipError_t launch_fft_cols(const double* H, int64_t nv, int64_t nx, int64_t ny, const double* tw_v, int mode,
                            double* out, const double* cx, const double* cy, double px, double py, double w_plane,
                            int first, const double* norm, const uint32_t* rowbits, hipStream_t s, bool h_f32,
-                           bool acc_f32) {
+                           bool acc_f32, bool eo) {
   const dim3 gd((unsigned)nx);
   const double2* h = (const double2*)H;
   const float2* hf = (const float2*)H;
   const double2* tw = (const double2*)tw_v;
   const ColEpilogue ep{out, cx, cy, px, py, w_plane, first, norm};
+  if (eo) {
+    // pass A wrote the even / odd H halves (launch_fft_rows eo)
+    if (!fft_cols_eo(nv, ny, h_f32, mode)) return hipErrorInvalidValue;
+    fft_cols_eo_kernel<8192><<<gd, dim3(8192 / 16), 0, s>>>(h, nx, ny, tw, ep, rowbits);
+    return hipGetLastError();
+  }
   const bool fft_f32 = fft_f32_enabled();
   // the float plane accumulator exists only beside fp32 transforms of
   // complex64 planes (with CIP_FFT_F32=0 the fp64-output kernel

@@ -170,11 +170,14 @@ bool fast_fft_supported(int64_t nu, int64_t nv, int64_t nx, int64_t ny);
 // and H complex64 values (pass A's output; launch_fft_cols with h_f32)
 hipError_t launch_fft_rows(double* gT, int64_t nu, int64_t nv, int64_t nx, const double* tw_u, double* H,
                            const uint32_t* dmask, int64_t ntx, bool skip_clean, hipStream_t s,
-                           bool grid_f32 = false);
+                           bool grid_f32 = false, bool eo = false);
 hipError_t launch_fft_cols(const double* H, int64_t nv, int64_t nx, int64_t ny, const double* tw_v, int mode,
                            double* out, const double* cx, const double* cy, double px, double py, double w_plane,
                            int first, const double* norm, const uint32_t* rowbits, hipStream_t s,
-                           bool h_f32 = false, bool acc_f32 = false);
+                           bool h_f32 = false, bool acc_f32 = false, bool eo = false);
+// pass B of a 2-D crop by even / odd column halves (fp64, nv = 16384, ny <=
+// nv / 2): pass A and pass B of one plane both take eo = fft_cols_eo(...)
+bool fft_cols_eo(int64_t nv, int64_t ny, bool grid_f32, int mode);
 // acc_f32: out is the packed class's float plane accumulator (mode 1, h_f32,
 // fp32 transforms only: hipErrorInvalidValue otherwise - the fp64-output
 // kernels would write doubles into a float buffer)

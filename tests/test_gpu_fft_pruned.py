@@ -82,3 +82,30 @@ def test_pruned_fft_16k_grid_matches_dft(gpu_device, wstack):
     got = gpu[torch.from_numpy(ii).cuda(), torch.from_numpy(jj).cuda()].cpu().numpy()
     sumw = float(w.astype(np.float64).sum())
     assert float(np.abs(got - ref).max()) / sumw < 1e-10
+
+
+def test_pruned_fft_16k_even_odd_pass_b_whole_rows(gpu_device):
+    # 2-D at nv = 16384: pass B by even / odd column halves
+    # (cip_fft.hip fft_cols_eo_kernel; pass A writes H by row parity). Whole
+    # image rows - every output cell of their columns, both halves' k' mapping,
+    # the +- combination, the crop's both wrapped ranges and (few
+    # visibilities: most tile rows are clean) the skipped H rows - against the
+    # direct fp64 DFT.
+    import torch
+
+    uvw, f, vis, w = _case(400, 4, seed=9)
+    npix = 8192
+    px = syn.pixel_size_for_grid(uvw, f, npix, fill=0.4)
+    args = [torch.from_numpy(a).cuda() for a in (uvw, f, vis.astype(np.complex128), w.astype(np.float64))]
+    gpu, prm = gridder.device_ms2dirty(*args, npix, npix, px, px, support=16)
+    assert (prm.nu, prm.nv) == (16384, 16384)
+    flat = uvw.copy()
+    flat[:, 2] = 0.0
+    sumw = float(w.astype(np.float64).sum())
+    jj = np.arange(npix)
+    for i in (0, 1, npix // 2 - 1, npix // 2, 5001, npix - 1):
+        l = np.full(npix, (i - npix // 2) * px)
+        m = (jj - npix // 2) * px
+        ref = oracle.dft_directions(flat, f, vis, w, l, m)
+        got = gpu[i].cpu().numpy()
+        assert float(np.abs(got - ref).max()) / sumw < 1e-10, i
