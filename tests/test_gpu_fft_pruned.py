@@ -109,3 +109,25 @@ def test_pruned_fft_16k_even_odd_pass_b_whole_rows(gpu_device):
         ref = oracle.dft_directions(flat, f, vis, w, l, m)
         got = gpu[i].cpu().numpy()
         assert float(np.abs(got - ref).max()) / sumw < 1e-10, i
+
+
+def test_pruned_fft_16k_even_odd_rectangular(gpu_device):
+    # the even / odd pass B beside an 8192-point pass A (npix_x = 4096: nu =
+    # 8192, nv = 16384), i.e. nx != ny: whole image rows against the direct DFT
+    import torch
+
+    uvw, f, vis, w = _case(300, 3, seed=13)
+    npix_x, npix_y = 4096, 8192
+    px = syn.pixel_size_for_grid(uvw, f, npix_y, fill=0.4)
+    args = [torch.from_numpy(a).cuda() for a in (uvw, f, vis.astype(np.complex128), w.astype(np.float64))]
+    gpu, prm = gridder.device_ms2dirty(*args, npix_x, npix_y, px, px, support=16)
+    assert (prm.nu, prm.nv) == (8192, 16384) and tuple(gpu.shape) == (npix_x, npix_y)
+    flat = uvw.copy()
+    flat[:, 2] = 0.0
+    sumw = float(w.astype(np.float64).sum())
+    jj = np.arange(npix_y)
+    for i in (0, npix_x // 2, npix_x - 1):
+        l = np.full(npix_y, (i - npix_x // 2) * px)
+        m = (jj - npix_y // 2) * px
+        ref = oracle.dft_directions(flat, f, vis, w, l, m)
+        assert float(np.abs(gpu[i].cpu().numpy() - ref).max()) / sumw < 1e-10, i

@@ -17,6 +17,7 @@
 #   refcall          the reference call alone (--wstacking --single --epsilon-call)
 #   ab=ENVSPEC       interleaved A/B of the quick line: ENVSPEC "K=V,K2=V2" vs the default (3 pairs)
 #   abrc=ENVSPEC     the same for the reference call (w-stacking, eps 1e-4, packed class)
+#   abrc2=SPEC_A;SPEC_B  two variants of the reference call against the default, interleaved
 #   abc4=ENVSPEC     the same for the C4 line (one-shot calls timed synchronously too)
 #   py=SCRIPT[:ARGS] python SCRIPT ARGS (tools), 300 s limit
 # Output: gpurun_out/<TAG>_<step>.{log,json,md}
@@ -84,6 +85,16 @@ for step in "$@"; do
       for i in 1 2 3; do
         run 300 "abrc_base$i" python bench.py --wstacking --single --epsilon-call $QUICK || exit 1
         run 300 "abrc_var$i" env ${spec//,/ } python bench.py --wstacking --single --epsilon-call $QUICK || exit 1
+      done ;;
+    abrc2=*)
+      # two variants against the default, interleaved: abrc2=SPEC_A;SPEC_B
+      spec=${step#abrc2=}
+      sa=${spec%%;*}
+      sb=${spec#*;}
+      for i in 1 2 3; do
+        run 300 "abrc2_base$i" python bench.py --wstacking --single --epsilon-call $QUICK || exit 1
+        run 300 "abrc2_a$i" env ${sa//,/ } python bench.py --wstacking --single --epsilon-call $QUICK || exit 1
+        run 300 "abrc2_b$i" env ${sb//,/ } python bench.py --wstacking --single --epsilon-call $QUICK || exit 1
       done ;;
     abc4=*)
       spec=${step#abc4=}
