@@ -364,9 +364,12 @@ __device__ __forceinline__ bool place_vis(double u_m, double v_m, double w_m, do
 
 // The planner's placement: the footprint origins place_vis computes (the same
 // integers), without the kernel variables and without divergent branches in
-// the common case - |origin| < 2^30 and within one grid period of the grid,
-// so one select-add per axis wraps it; a wave with any other lane takes
-// place_vis itself (a wave-uniform branch).
+// the common case - the origin inside the grid, no wrap (one unsigned compare
+// per axis; |origin| < 2^30 first, so the conversion is exact); a wave with
+// any other lane (off the grid by a period or more, not finite) takes
+// place_vis itself (a wave-uniform branch). WS: w-stacking at compile time
+// (0 / 1; -1: g.do_wstacking).
+template <int WS = -1>
 __device__ __forceinline__ bool place_origin(double u_m, double v_m, double w_m, double fx, const GridGeometry& g,
                                              int* ix0, int* iy0, int64_t* iw0) {
 #pragma clang fp contract(off)
@@ -374,14 +377,9 @@ __device__ __forceinline__ bool place_origin(double u_m, double v_m, double w_m,
   const double x = (u_m * fx) * g.scale_u + (double)(g.nu / 2);
   const double y = (v_m * fx) * g.scale_v + (double)(g.nv / 2);
   const double flx = floor(x - (double)hw), fly = floor(y - (double)hw);
-  const int nu = (int)g.nu, nv = (int)g.nv;
   const bool small = fabs(flx) < 1073741824.0 && fabs(fly) < 1073741824.0;
-  int ix = small ? (int)flx + 1 : 0, iy = small ? (int)fly + 1 : 0;
-  ix = ix >= nu ? ix - nu : ix;
-  ix = ix < 0 ? ix + nu : ix;
-  iy = iy >= nv ? iy - nv : iy;
-  iy = iy < 0 ? iy + nv : iy;
-  const bool fits = small & (ix >= 0) & (ix < nu) & (iy >= 0) & (iy < nv);
+  const int ix = small ? (int)flx + 1 : -1, iy = small ? (int)fly + 1 : -1;
+  const bool fits = ((unsigned)ix < (unsigned)g.nu) & ((unsigned)iy < (unsigned)g.nv);
   if (__ballot(!fits) != 0ull) {
     int64_t a, b, c;
     double ya, yb, yc;
@@ -393,7 +391,7 @@ __device__ __forceinline__ bool place_origin(double u_m, double v_m, double w_m,
   }
   *ix0 = ix;
   *iy0 = iy;
-  if (g.do_wstacking) {
+  if (WS > 0 || (WS < 0 && g.do_wstacking)) {
     const double xw = ((w_m * fx) - g.w0) * g.inv_dw;
     double yw;
     footprint(xw, hw, iw0, &yw);

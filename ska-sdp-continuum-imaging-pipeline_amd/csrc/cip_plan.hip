@@ -3,6 +3,8 @@
 // (histogram -> exclusive scan -> scatter), and the chunk table that splits hot
 // tiles into <= kChunkVis-visibility work units (the role of split_tile,
 // reference uvw_tiling/tile.py:155-211, for the device gridder).
+#include <type_traits>
+
 #include "cip_internal.h"
 
 namespace cip {
@@ -401,8 +403,214 @@ __device__ __forceinline__ void place_body(const double* __restrict__ uvw, const
   }
 }
 
+// p in scalar registers: an opaque wave-uniform pointer, so p[lane] keeps the
+// scalar-base load form (the compiler otherwise reassociates p + lane into a
+// hoisted per-lane 64-bit pointer plus a VALU add per access)
+template <typename T>
+__device__ __forceinline__ T* uniform_ptr(T* p) {
+  const uint64_t a = (uint64_t)p;
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)a);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(a >> 32));
+  return (T*)(((uint64_t)hi << 32) | lo);
+}
+
+// base[lane] / base[lane] = x with base wave-uniform: the global access's
+// scalar-base form (base in scalar registers + the lane's 32-bit byte offset,
+// laundered through an empty asm inside the loop so the offset's zero
+// extension is not hoisted out of the loop body, where instruction selection
+// would no longer see it)
+template <typename T>
+__device__ __forceinline__ T seg_ld(const T* base, int lane) {
+  // loaded as a same-size integer (vector types have no constructor from an
+  // address-space-qualified object)
+  using U = typename std::conditional<sizeof(T) == 16, __uint128_t,
+                                      typename std::conditional<sizeof(T) == 8, uint64_t, uint32_t>::type>::type;
+  static_assert(sizeof(T) == sizeof(U), "4-, 8- or 16-byte elements");
+  unsigned off = (unsigned)lane * (unsigned)sizeof(T);
+  asm volatile("" : "+v"(off));
+  const __attribute__((address_space(1))) char* b = (const __attribute__((address_space(1))) char*)uniform_ptr(base);
+  return __builtin_bit_cast(T, *(const __attribute__((address_space(1))) U*)(b + off));
+}
+template <typename T>
+__device__ __forceinline__ void seg_st(T* base, unsigned idx, T x) {
+  unsigned off = idx * (unsigned)sizeof(T);
+  asm volatile("" : "+v"(off));
+  __attribute__((address_space(1))) char* b = (__attribute__((address_space(1))) char*)uniform_ptr(base);
+  *(__attribute__((address_space(1))) T*)(b + off) = x;
+}
+
+// Lane loads of the dense-row place pass: a wave-uniform base (the segment's
+// first visibility i0, scalar registers) plus the lane's 32-bit offset, so the
+// loads take the scalar-base form with no per-lane 64-bit address arithmetic.
+template <int WK>
+__device__ __forceinline__ double seg_weight(const void* __restrict__ w, const RowMap& m, int64_t i0, int lane) {
+  if constexpr (WK == WK_F32) return (double)seg_ld((const float*)w + i0, lane);
+  if constexpr (WK == WK_F64) return seg_ld((const double*)w + i0, lane);
+  if constexpr (WK == WK_POL4I) return load_weight<WK>(w, m, i0 + lane);
+  return 1.0;
+}
+// max(|re|, |im|) of a visibility and whether both parts are finite: complex64
+// in fp32 (the max of the exact fp32 magnitudes converts to the same double as
+// the max of the converted parts; the finite test is the same too)
+__device__ __forceinline__ double seg_vis_abs(const float2* __restrict__ p, int64_t i0, int lane, bool* finite) {
+  if (p == nullptr) {  // PSF: the unit visibility
+    *finite = true;
+    return 1.0;
+  }
+  const float2 v = seg_ld(p + i0, lane);
+  *finite = isfinite(v.x) && isfinite(v.y);
+  return (double)fmaxf(fabsf(v.x), fabsf(v.y));
+}
+__device__ __forceinline__ double seg_vis_abs(const double2* __restrict__ p, int64_t i0, int lane, bool* finite) {
+  const double2 v = seg_ld(p + i0, lane);
+  *finite = isfinite(v.x) && isfinite(v.y);
+  return fmax(fabs(v.x), fabs(v.y));
+}
+__device__ __forceinline__ double seg_vis_abs(const Pol4* __restrict__ p, int64_t i0, int lane, bool* finite) {
+  double re, im;
+  load_vis(p, i0 + lane, re, im);
+  *finite = isfinite(re) && isfinite(im);
+  return fmax(fabs(re), fabs(im));
+}
+
+// The place pass over dense rows of a multiple of 64 channels (RM = 1, the
+// MS layout of the benchmark): every wave's 64 visibilities are channels
+// c0 .. c0 + 63 of ONE row r, so the row, its uvw, the segment's load bases,
+// the park slots' base and the run detection's row check are wave-uniform
+// (scalar registers and loads), the key and class arithmetic is 32-bit, and
+// the per-lane work is the placement, the run detection and the stores.
+// Bit-identical to place_body<.., RM = 1>: the same sums in the same order,
+// the same keys, classes and park records.
+template <typename VisT, int WK, bool WS>
+__device__ __forceinline__ void place_rows64_body(const double* __restrict__ uvw, const double* __restrict__ fx,
+                                                  const RowMap& m, const VisT* __restrict__ vis,
+                                                  const void* __restrict__ wgt, const GridGeometry& g,
+                                                  unsigned* err_flag, uint8_t* __restrict__ vis_class,
+                                                  int64_t* __restrict__ blk_cnt, uint32_t* __restrict__ park_key,
+                                                  uint64_t* __restrict__ park_run, double* partial,
+                                                  int64_t* __restrict__ hist0, const int64_t blk,
+                                                  const int64_t nblocks) {
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  __shared__ unsigned s_nruns;
+  __shared__ unsigned s_hist[256];
+  if (threadIdx.x == 0) s_nruns = 0u;
+  s_hist[threadIdx.x] = 0u;
+  __syncthreads();
+  double wsum = 0.0, wvmax = 0.0;
+  // non-finite visibility / weight, failed placement: any lane, ever (scalar)
+  unsigned long long nonfinite = 0ull, bad_any = 0ull;
+  // 32-bit uniform row / channel / segment counters (launch_plan_place picks
+  // this body for nrow < 2^31 and nvis < 2^37): scalar compares, so the row
+  // and the loop stay in scalar registers
+  const int nchan = (int)m.nchan;
+  const int nseg = (int)(m.nvis / 64);  // nvis = nrow nchan: whole segments
+  const int blk32 = (int)blk;
+  const int seg_end = (blk32 + 1) * kPlaceSegs < nseg ? (blk32 + 1) * kPlaceSegs : nseg;
+  const unsigned P = (unsigned)(kTile + g.support - 1);
+  const uint32_t ntx = (uint32_t)g.ntx, ntw = (uint32_t)g.ntw;
+  constexpr bool wstack = WS;
+  // the wave's first segment: row r, channels c0 .. c0 + 63; then 256
+  // visibilities per step
+  const int64_t i00 = ((int64_t)blk32 * kPlaceSegs + wave) * 64;
+  int r = (int)(i00 / nchan);
+  int c0 = (int)(i00 - (int64_t)r * nchan);
+  const int step_r = 256 / nchan, step_c = 256 % nchan;
+  // this block's park region
+  uint32_t* const pkey = park_key + blk * kPlaceSegs * 64;
+  uint64_t* const prun = park_run + blk * kPlaceSegs * 64;
+  const unsigned long long upto = (2ull << lane) - 1ull;   // lane 63: 2 << 63 == 0 - 1 = all
+  for (int seg = blk32 * kPlaceSegs + wave; seg < seg_end; seg += 4) {
+    // readfirstlane: an opaque uniform base, so the loads below keep the
+    // scalar-base form (no per-lane pointer induction variables)
+    const int64_t i0 = (int64_t)__builtin_amdgcn_readfirstlane(seg) * 64;
+    const int64_t ru = (int64_t)__builtin_amdgcn_readfirstlane(r);
+    // loads first (one memory round trip per iteration)
+    const double u = uvw[3 * ru], v = uvw[3 * ru + 1];
+    const double w = wstack ? uvw[3 * ru + 2] : 0.0;
+    const double f = seg_ld(fx + c0, lane);
+    const double wt = seg_weight<WK>(wgt, m, i0, lane);
+    bool vfin;
+    const double vabs = seg_vis_abs(vis, i0, lane, &vfin);
+    // the fused reduction (place_body's order: every lane is valid here). A
+    // zero weight adds 0 * |V| = 0 or NaN (|V| not finite) to the max, which
+    // fmax ignores as it ignores place_body's 0 - the same max either way.
+    const bool counted = wt != 0.0;
+    nonfinite |= __ballot(counted && !(isfinite(wt) && vfin));
+    wsum = wsum + wt;
+    wvmax = fmax(wvmax, fabs(wt) * vabs);
+    int ix0, iy0;
+    int64_t iw0;
+    const bool ok = place_origin<WS ? 1 : 0>(u, v, w, f, g, &ix0, &iy0, &iw0);
+    bool feeds = true;
+    if constexpr (WS) feeds = (iw0 + g.support > g.plane_lo) & (iw0 < g.plane_hi);
+    const uint32_t tk = ((uint32_t)iy0 / (uint32_t)kTile) * ntx + (uint32_t)ix0 / (uint32_t)kTile;
+    const uint32_t key = (ok & feeds) ? (WS ? tk * ntw + (uint32_t)iw0 : tk) : kNoKey;
+    bad_any |= __ballot(!ok);
+    if (vis_class)
+      seg_st(vis_class + i0, (unsigned)lane, ok ? (uint8_t)(((unsigned)ix0 * P + (unsigned)iy0) & 31u) : (uint8_t)0);
+    // runs: a lane starts one where its key differs from the previous lane's
+    // (DPP shift; lane 0 always), and emits it unless off the grid (masks in
+    // scalar registers: the ballots are the compares themselves)
+    const uint32_t prev = wave_shr1(key);
+    const unsigned long long starts = __ballot(key != prev) | 1ull;
+    const bool emit = key != kNoKey && (key != prev || lane == 0);
+    const unsigned long long emits = __ballot(emit);
+    unsigned wbase = 0;
+    if (lane == 0 && emits) wbase = atomicAdd(&s_nruns, (unsigned)__popcll(emits));
+    wbase = (unsigned)__builtin_amdgcn_readlane((int)wbase, 0);
+    if (emit) {
+      const unsigned long long above = starts & ~upto;
+      const int next = above ? (__ffsll((long long)above) - 1) : 64;
+      const unsigned slot = wbase + __builtin_amdgcn_mbcnt_hi((unsigned)(emits >> 32),
+                                                              __builtin_amdgcn_mbcnt_lo((unsigned)emits, 0u));
+      atomicAdd(&s_hist[key & 255u], 1u);
+      seg_st(pkey, slot, key);
+      const uint32_t c = (uint32_t)(c0 + lane);
+      // (row << 32) | (c << 16) | channel stop, as two 32-bit words
+      const uint32_t lo = (c << 16) | (uint32_t)(c0 + next);
+      seg_st(prun, slot, ((uint64_t)(uint32_t)ru << 32) | (uint64_t)lo);
+    }
+    c0 += step_c;
+    r += step_r;
+    if (c0 >= nchan) {
+      c0 -= nchan;
+      ++r;
+    }
+  }
+  __shared__ double ss[4], sm[4];
+  if (lane == 0 && nonfinite) atomicOr(err_flag, 2u);
+  if (lane == 0 && bad_any) atomicOr(err_flag, 1u);
+  for (int d = 32; d > 0; d >>= 1) {
+    wsum += __shfl_xor(wsum, d, 64);
+    wvmax = fmax(wvmax, __shfl_xor(wvmax, d, 64));
+  }
+  if (lane == 0) {
+    ss[threadIdx.x >> 6] = wsum;
+    sm[threadIdx.x >> 6] = wvmax;
+  }
+  __syncthreads();
+  hist0[(int64_t)threadIdx.x * nblocks + blk] = s_hist[threadIdx.x];
+  if (threadIdx.x == 0) {
+    partial[2 * blk] = (ss[0] + ss[1]) + (ss[2] + ss[3]);
+    partial[2 * blk + 1] = fmax(fmax(sm[0], sm[1]), fmax(sm[2], sm[3]));
+    blk_cnt[blk] = s_nruns;
+    if (blk == 0) hist0[256 * nblocks] = 0;
+  }
+}
+
+// CIP_PLACE_ROWS64=0: dense 64-channel rows through place_body (A/B)
+static bool place_rows64() {
+  static const bool on = [] {
+    const char* e = getenv("CIP_PLACE_ROWS64");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 // The place pass (reduction fused, the place block = this workgroup); PLACE =
-// false: the reduction alone (CIP_REUSE_PLAN calls).
+// false: the reduction alone (CIP_REUSE_PLAN calls). RM = 3 / 4: dense rows of
+// a multiple of 64 channels through place_rows64_body (2-D / w-stacking).
 template <typename VisT, int WK, bool PLACE = true, int RM = 0>
 __global__ __launch_bounds__(256) void plan_place_kernel(const double* __restrict__ uvw,
                                                          const double* __restrict__ fx, RowMap m,
@@ -413,8 +621,12 @@ __global__ __launch_bounds__(256) void plan_place_kernel(const double* __restric
                                                          uint32_t* __restrict__ park_key,
                                                          uint64_t* __restrict__ park_run, double* partial,
                                                          int64_t* __restrict__ hist0) {
-  place_body<VisT, WK, PLACE, RM>(uvw, fx, m, vis, wgt, g, err_flag, vis_class, blk_cnt, park_key, park_run, partial,
-                                  hist0, blockIdx.x, gridDim.x);
+  if constexpr (PLACE && (RM == 3 || RM == 4))
+    place_rows64_body<VisT, WK, RM == 4>(uvw, fx, m, vis, wgt, g, err_flag, vis_class, blk_cnt, park_key, park_run, partial,
+                                hist0, blockIdx.x, gridDim.x);
+  else
+    place_body<VisT, WK, PLACE, RM>(uvw, fx, m, vis, wgt, g, err_flag, vis_class, blk_cnt, park_key, park_run,
+                                    partial, hist0, blockIdx.x, gridDim.x);
 }
 
 static unsigned plan_blocks(int64_t nvis) {
@@ -452,14 +664,19 @@ hipError_t launch_plan_place(const double* uvw, const double* fx, const RowMap& 
                              unsigned* err_flag, uint8_t* vis_class, int64_t* blk_cnt, uint32_t* park_key,
                              uint64_t* park_run, double* partial, int64_t* hist0, hipStream_t s) {
   const dim3 gd(plan_blocks(m.nvis));
-  const int rm = m.delta != nullptr ? 2 : (m.nchan % 64 == 0 ? 1 : 0);
+  const bool rows64 = place_rows64() && m.nchan > 0 && m.nvis / m.nchan < ((int64_t)1 << 31) && m.nvis < ((int64_t)1 << 37);
+  const int rm = m.delta != nullptr ? 2 : (m.nchan % 64 == 0 ? (rows64 ? (g.do_wstacking ? 4 : 3) : 1) : 0);
 #define PLACE_RM(VT, WKV, RMV)                                                                                      \
   plan_place_kernel<VT, WKV, true, RMV><<<gd, dim3(256), 0, s>>>(uvw, fx, m, (const VT*)vis, wgt, g, err_flag,     \
                                                                  vis_class, blk_cnt, park_key, park_run, partial,   \
                                                                  hist0)
 #define PLACE(VT, WKV)            \
   do {                            \
-    if (rm == 2) {                \
+    if (rm == 4) {                \
+      PLACE_RM(VT, WKV, 4);       \
+    } else if (rm == 3) {         \
+      PLACE_RM(VT, WKV, 3);       \
+    } else if (rm == 2) {         \
       PLACE_RM(VT, WKV, 2);       \
     } else if (rm == 1) {         \
       PLACE_RM(VT, WKV, 1);       \
