@@ -76,9 +76,10 @@ for step in "$@"; do
     refcall) run 400 refcall python bench.py --wstacking --single --epsilon-call $QUICK || exit 1 ;;
     ab=*)
       spec=${step#ab=}
+      sn=$(echo "$spec" | tr -c 'A-Za-z0-9\n' '_')  # the files of each ab step apart
       for i in 1 2 3; do
-        run 300 "ab_base$i" python bench.py $QUICK || exit 1
-        run 300 "ab_var$i" env ${spec//,/ } python bench.py $QUICK || exit 1
+        run 300 "ab_${sn}_base$i" python bench.py $QUICK || exit 1
+        run 300 "ab_${sn}_var$i" env ${spec//,/ } python bench.py $QUICK || exit 1
       done ;;
     abrc=*)
       spec=${step#abrc=}
