@@ -292,7 +292,6 @@ struct PlanResult {
   int64_t* tile_run_off = nullptr;
   Chunk* chunks = nullptr;
   void* perm = nullptr;  // bank-class ordered visibility stream (perm_encode entries), or NULL
-  bool sort = false;     // no ordered stream: the scatter class-sorts each window itself (PERM = 3)
   uint32_t* dmask = nullptr;  // grid tiles the scatter writes, per plane (bit-packed, ntx / 32 words per tile row)
 };
 
@@ -593,16 +592,6 @@ static bool ragged_pack() {
   return !(e && e[0] == '0');
 }
 
-// CIP_SCATTER_SORT=0: 2-D dense plans keep the planner's order pass (perm)
-// instead of the scatter's in-unit class sort (A/B experiments)
-static bool scatter_sort() {
-  static const bool on = [] {
-    const char* e = getenv("CIP_SCATTER_SORT");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
-
 // sub-blocks per radix workgroup: pass 0 (place blocks of ~500 runs) and the
 // dense passes (4096 runs)
 static int radix_group(int pass) { return pass ? 1 : 8; }
@@ -627,12 +616,7 @@ static int make_plan(Workspace* ws, const double* uvw, const double* fx, const R
   // inputs grid in plain tile order); ragged row slices store 64-bit
   // (row, channel) entries
   const bool ragged = m.delta != nullptr;
-  bool order = scatter_order() && (ragged || nvis < ((int64_t)1 << 32));
-  // 2-D dense rows, one plane per unit, the lane scatter: the scatter sorts
-  // each window by class itself - no class bytes, windows or order pass
-  const bool sort = order && !ragged && !g.do_wstacking && group == 1 && g.support <= 16 && scatter_sort();
-  pr->sort = sort;
-  if (sort) order = false;
+  const bool order = scatter_order() && (ragged || nvis < ((int64_t)1 << 32));
   uint8_t* vis_class = nullptr;
   if (order) {
     vis_class = buf<uint8_t>(ws, "vis_class", nvis);
@@ -1086,7 +1070,7 @@ static int scatter_plane(const Prepared& pp, int64_t q, const double* uvw, const
   CIP_HIP_CHECK(launch_scatter(g.support, vis_dtype, wgt_dtype, pp.packed, G, share_cus,
                                !accumulate && flush_store_enabled(g), uvw, pp.fx, vis, wgt, pp.m,
                                pp.plan.runs, pp.plan.run_goff, pp.plan.tile_run_off, pp.plan.perm, pp.plan.chunks, cb,
-                               ce - cb, g, p0, pp.fixed_scale, grid, s, pp.plan.sort));
+                               ce - cb, g, p0, pp.fixed_scale, grid, s));
   g_prof.span(2, a, g_prof.mark(s));
   if (ce > cb) g_prof.counts[4] += 1;
   return CIP_OK;

@@ -61,10 +61,6 @@ constexpr int kTile = CIP_TILE;
 #define CIP_ORDER_WINDOW 1024  // experiment builds: 2048 (tools/build_variant_all.sh)
 #endif
 constexpr int kOrderWindow = CIP_ORDER_WINDOW;
-// LDS of the scatter's in-unit class sort (cip_scatter.h, PERM = 3) beyond the
-// sub-grid: the staged row slices (first index, start) or the level tables,
-// the window's position -> index list (then slot -> index), 32 class counters
-constexpr unsigned kSortLds = (unsigned)(8 * (kOrderWindow + 2) + 4 * kOrderWindow + 4 * 32 + 16);
 
 __host__ __device__ inline int64_t floor_div(int64_t a, int64_t b) {
   int64_t q = a / b;

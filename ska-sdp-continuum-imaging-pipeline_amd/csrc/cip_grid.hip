@@ -243,9 +243,8 @@ hipError_t launch_scatter(int support, int vis_dtype, int wgt_dtype, bool packed
                           const double* fx, const void* vis, const void* wgt, const RowMap& m, const uint64_t* runs,
                           const int64_t* run_goff, const int64_t* tile_run_off, const void* perm,
                           const Chunk* chunks, int64_t chunk_begin, int64_t nchunks, const GridGeometry& g,
-                          int64_t plane, double fixed_scale, double* grid, hipStream_t s, bool sort) {
+                          int64_t plane, double fixed_scale, double* grid, hipStream_t s) {
   if (nchunks <= 0) return hipSuccess;
-  if (sort && support > 16) return hipErrorInvalidValue;
   if (packed && vis_dtype != CIP_C64 && vis_dtype != CIP_POL4I) return hipErrorInvalidValue;
   const dim3 gd((unsigned)nchunks);
   // three blocks per CU: each needs > 160 KB / 4 of LDS (static sub-grid +
@@ -253,7 +252,7 @@ hipError_t launch_scatter(int support, int vis_dtype, int wgt_dtype, bool packed
   unsigned pad = 0;
   if (share_cus && group == 1 && support <= 16) {
     const unsigned P = (unsigned)(kTile + support - 1);
-    const unsigned stat = P * P * (packed ? 8u : 16u) + 64u + (sort ? kSortLds : 0u);
+    const unsigned stat = P * P * (packed ? 8u : 16u) + 64u;
     // 3 blocks per CU: the optimum of 2 / 3 / 4 (profiles/r03_ab_scatter_share.txt, r05z_ab_share_blocks.txt)
     const unsigned nb = 3u;
     const unsigned need = 160u * 1024u / (nb + 1u) + 256u;
@@ -263,7 +262,7 @@ hipError_t launch_scatter(int support, int vis_dtype, int wgt_dtype, bool packed
   case WW:                                                                                                   \
     return launch_scatter_w<WW>(vis_dtype, wgt_dtype, packed, group, pad, store_private ? 1 : 0, gd, s, uvw, fx,  \
                                 vis, wgt, m, runs, \
-                                  run_goff, tile_run_off, perm, chunks, chunk_begin, g, plane, fixed_scale, grid, sort);
+                                  run_goff, tile_run_off, perm, chunks, chunk_begin, g, plane, fixed_scale, grid);
   switch (support) {
     CASE(4)
     CASE(6)

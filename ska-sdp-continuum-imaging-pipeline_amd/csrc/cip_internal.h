@@ -115,7 +115,7 @@ hipError_t launch_scatter_w(int vis_dtype, int wgt_dtype, bool pack, int group, 
                             const double* fx, const void* vis, const void* wgt, const RowMap& m,
                             const uint64_t* runs, const int64_t* run_goff, const int64_t* tile_run_off,
                             const void* perm, const Chunk* chunks, int64_t cb, const GridGeometry& g,
-                            int64_t plane, double fs, double* grid, bool sort);
+                            int64_t plane, double fs, double* grid);
 // the large supports W = 24, 32, 48, 64 (cip_scatter_large.hip, wave per
 // visibility; one translation unit per W)
 template <int W>
@@ -131,16 +131,13 @@ hipError_t launch_scatter_large_w(int vis_dtype, int wgt_dtype, dim3 gd, hipStre
 // beside it
 // store_private: the grid planes are zero (a cip_ms2dirty plane, not an
 // accumulating one), so a tile's only work unit stores its private cells
-// sort: the bank-class order inside the work unit (2-D, dense rows, G = 1,
-// W <= 16; perm unused): the plan's runs in tile order, class-sorted per
-// window by the scatter (cip_scatter.h scatter_sorted_windows)
 hipError_t launch_scatter(int support, int vis_dtype, int wgt_dtype, bool packed, int group, bool share_cus,
                           bool store_private,
                           const double* uvw,
                           const double* fx, const void* vis, const void* wgt, const RowMap& m, const uint64_t* runs,
                           const int64_t* run_goff, const int64_t* tile_run_off, const void* perm,
                           const Chunk* chunks, int64_t chunk_begin, int64_t nchunks, const GridGeometry& g,
-                          int64_t plane, double fixed_scale, double* grid, hipStream_t s, bool sort = false);
+                          int64_t plane, double fixed_scale, double* grid, hipStream_t s);
 // perm (nvis 32-bit records, nvis < 2^32): the tile-order visibilities as
 // row * nchan + channel, bank-class sorted within each window (the tiles split
 // into <= kOrderWindow pieces by chunk_emit with cv = kOrderWindow)

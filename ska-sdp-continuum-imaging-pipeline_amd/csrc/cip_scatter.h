@@ -434,147 +434,8 @@ __device__ __forceinline__ void flush_subgrid(const unsigned long long* sub, con
   }
 }
 
-// PERM = 3 (2-D, dense rows < 2^32 visibilities): the bank-class order made
-// inside the work unit instead of by the planner's order pass (no class bytes,
-// no windows, no ordered stream in HBM). Each aligned window of kOrderWindow
-// tile-order positions (the order pass's windows) is gridded in three steps:
-// (1) its row slices are staged in LDS and expanded into the flattened index
-// of every position; (2) each position's LDS bank class ((ix0 P + iy0) mod 32
-// of its footprint origin, placed in fp32 - a rare wrong class near a cell
-// edge costs a bank conflict, not a result) is ranked with an LDS counter and
-// the window counting-sorted into level-major order (order_kernel's
-// S[r] = sum_c min(cnt[c], r), M[r] = {c : cnt[c] > r} tables), the indices
-// written to their slots; (3) the slots are gridded in order as the PERM = 1
-// stream is, loads of slot q + NT in flight while q grids. The integer sums
-// are order-independent: the same sub-grid sums as the ordered stream's.
-template <int W, typename VisT, int WK, bool PACK, int NT>
-__device__ __forceinline__ void scatter_sorted_windows(const double* __restrict__ uvw, const double* __restrict__ fx,
-                                                       const VisT* __restrict__ vis, const void* __restrict__ wgt,
-                                                       const RowMap& m, const uint64_t* __restrict__ runs,
-                                                       const int64_t* __restrict__ run_goff, const Chunk& ch,
-                                                       const GridGeometry& g, int64_t plane, int64_t X0, int64_t Y0,
-                                                       double fixed_scale, unsigned long long* sub) {
-  constexpr int kWin = kOrderWindow;
-  constexpr int kPer = kWin / NT;
-  static_assert(kPer * NT == kWin, "a window is kPer positions per thread");
-  constexpr unsigned P = (unsigned)(kTile + W - 1);
-  __shared__ union {
-    struct {
-      uint32_t base[kWin + 1];  // flattened index of each staged slice's first visibility
-      int32_t off[kWin + 1];    // its start relative to the window (the first may be < 0)
-    } st;
-    struct {
-      uint32_t S[kWin], M[kWin];
-    } tb;
-  } su;
-  __shared__ uint32_t s_list[kWin];
-  __shared__ uint32_t s_cnt[32];
-  const bool unit_vis = vis == nullptr;
-  const VisT* vis_ld = unit_vis ? (const VisT*)uvw : vis;
-  const int hw = W / 2;
-  const float scale_u = (float)g.scale_u, scale_v = (float)g.scale_v;
-  const float cu = (float)(g.nu / 2) - (float)hw, cv = (float)(g.nv / 2) - (float)hw;
-  int64_t r0 = ch.first_run;
-  for (int64_t w0 = ch.g0; w0 < ch.g1; w0 += kWin) {
-    const int wn = (int)(ch.g1 - w0 < kWin ? ch.g1 - w0 : kWin);
-    const int64_t w1 = w0 + wn;
-    // (1) the window's slices r0, r0 + 1, ... (a prefix: run_goff is sorted;
-    // at most wn + 1 of them - the first may end at w0)
-    int nst = 0;
-    __syncthreads();  // the previous window's slots are gridded
-    if (threadIdx.x < 32) s_cnt[threadIdx.x] = 0u;
-    for (int kb = 0;; kb += NT) {
-      const int k = kb + (int)threadIdx.x;
-      const int64_t r = r0 + k;
-      bool in = false;
-      if (k <= kWin && r <= ch.last_run) {
-        const int64_t go = run_goff[r];
-        if (go < w1) {
-          const uint64_t rec = runs[r];
-          su.st.off[k] = (int)(go - w0);
-          su.st.base[k] = (uint32_t)((int64_t)(rec >> 32) * m.nchan + (int64_t)((rec >> 16) & 0xffff));
-          in = true;
-        }
-      }
-      const int cnt = __syncthreads_count(in);
-      nst += cnt;
-      if (cnt < NT) break;
-    }
-    // expand: every position's flattened index (slices are <= 64 long)
-    for (int k = threadIdx.x; k < nst; k += NT) {
-      const int o = su.st.off[k];
-      const int a = o > 0 ? o : 0;
-      const int b = k + 1 < nst ? su.st.off[k + 1] : wn;
-      const uint32_t base = su.st.base[k] - (uint32_t)o;
-      for (int p = a; p < b; ++p) s_list[p] = base + (uint32_t)p;
-    }
-    // the next window starts in this one's last slice (or the one after it)
-    r0 += nst > 0 ? nst - 1 : 0;
-    __syncthreads();
-    // (2) classes and ranks
-    uint32_t idx[kPer];
-    unsigned cls[kPer], rk[kPer];
-#pragma unroll
-    for (int k = 0; k < kPer; ++k) {
-      const int p = (int)threadIdx.x + k * NT;
-      idx[k] = p < wn ? s_list[p] : 0u;
-    }
-#pragma unroll
-    for (int k = 0; k < kPer; ++k) {
-      int64_t r, c;
-      split_index64((int64_t)idx[k], m.nchan, m.inv_nchan, &r, &c);
-      const float f = (float)fx[c];
-      const float x = fmaf((float)uvw[3 * r] * f, scale_u, cu);
-      const float y = fmaf((float)uvw[3 * r + 1] * f, scale_v, cv);
-      const int ix = (int)floorf(x) + 1, iy = (int)floorf(y) + 1;
-      cls[k] = ((unsigned)ix * P + (unsigned)iy) & 31u;
-    }
-#pragma unroll
-    for (int k = 0; k < kPer; ++k)
-      if ((int)threadIdx.x + k * NT < wn) rk[k] = atomicAdd(&s_cnt[cls[k]], 1u);
-    __syncthreads();
-    unsigned maxcnt = 0;
-#pragma unroll
-    for (int i = 0; i < 32; ++i) maxcnt = s_cnt[i] > maxcnt ? s_cnt[i] : maxcnt;  // LDS broadcast reads
-    for (unsigned r = threadIdx.x; r < maxcnt; r += NT) {
-      unsigned S = 0, M = 0;
-#pragma unroll
-      for (int c2 = 0; c2 < 32; ++c2) {
-        const unsigned cn = s_cnt[c2];
-        S += cn < r ? cn : r;
-        M |= (cn > r ? 1u : 0u) << c2;
-      }
-      su.tb.S[r] = S;
-      su.tb.M[r] = M;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < kPer; ++k)
-      if ((int)threadIdx.x + k * NT < wn)
-        s_list[su.tb.S[rk[k]] + __popc(su.tb.M[rk[k]] & ((1u << cls[k]) - 1u))] = idx[k];
-    __syncthreads();
-    // (3) the slots in order, the next slot's loads in flight
-    int q = (int)threadIdx.x;
-    if (q < wn) {
-      RawFetch<VisT, WK> cur;
-      fetch_raw<VisT, WK, 0>((uint64_t)s_list[q], uvw, fx, vis_ld, unit_vis, wgt, m, cur);
-      while (true) {
-        const int qn = q + NT;
-        const bool hn = qn < wn;
-        RawFetch<VisT, WK> nxt;
-        fetch_raw<VisT, WK, 0>((uint64_t)s_list[hn ? qn : q], uvw, fx, vis_ld, unit_vis, wgt, m, nxt);
-        grid_fetched<W, false, PACK, 1>(from_raw<VisT, WK>(cur, unit_vis), g, plane, X0, Y0, fixed_scale, sub);
-        if (!hn) break;
-        cur = nxt;
-        q = qn;
-      }
-    }
-  }
-}
-
 // PERM: 0 = tile order through the row slices, 1 / 2 = the bank-class ordered
-// stream of dense (u32) / ragged (u64) entries, 3 = tile order class-sorted
-// inside the work unit (scatter_sorted_windows). G: w planes per work unit
+// stream of dense (u32) / ragged (u64) entries. G: w planes per work unit
 // (w-stacking plane groups; G > 1 runs 512-thread blocks holding G sub-grids).
 template <int G>
 constexpr int scatter_threads() {
@@ -604,10 +465,7 @@ __global__ __launch_bounds__(scatter_threads<G>(), CIP_SCATTER_WAVES) void scatt
     fixed_scale *= packed_chunk_gain(ch.g1 - ch.g0);
     inv_scale = 1.0 / fixed_scale;
   }
-  if constexpr (PERM == 3) {
-    scatter_sorted_windows<W, VisT, WK, PACK, NT>(uvw, fx, vis, wgt, m, runs, run_goff, ch, g, plane, X0, Y0,
-                                                   fixed_scale, sub);
-  } else if constexpr (PERM) {
+  if constexpr (PERM) {
     // bank-class ordered stream (order_kernel); software pipeline, two
     // deep: perm record of q + 512 and data of q + 256 in flight while q grids
     __syncthreads();
@@ -680,7 +538,7 @@ inline hipError_t scatter_dispatch_ws(bool ws, int group, bool pack, unsigned ld
                                       const double* fx, const void* vis, const void* wgt, const RowMap& m,
                                       const uint64_t* runs, const int64_t* run_goff, const int64_t* tile_run_off,
                                       const void* perm, const Chunk* chunks, int64_t chunk_begin,
-                                      const GridGeometry& g, int64_t plane, double fs, double* grid, bool sort) {
+                                      const GridGeometry& g, int64_t plane, double fs, double* grid) {
 #define LAUNCH(WSV, PRM, PK, GG)                                                                            \
   scatter_kernel<W, VisT, WK, WSV, PRM, PK, GG><<<grid_dim, dim3(scatter_threads<GG>()), lds_extra, s>>>(   \
       uvw, fx, (const VisT*)vis, wgt, m, runs, run_goff, tile_run_off, perm, chunks, chunk_begin, g, plane,    \
@@ -738,13 +596,8 @@ inline hipError_t scatter_dispatch_ws(bool ws, int group, bool pack, unsigned ld
   constexpr bool kFitG4 = 4 * P2 * 8 + 4200 <= 65536;
   bool done = false;
   const bool wide = m.delta != nullptr;  // ragged row slices: u64 entries
-  // the in-unit class sort: 2-D, dense rows, one plane per unit
-  if (sort && (ws || wide || group != 1)) return hipErrorInvalidValue;
   if constexpr (std::is_same<VisT, float2>::value || std::is_same<VisT, Pol4>::value) {
-    if (pack && sort) {
-      LAUNCH(false, 3, true, 1);
-      done = true;
-    } else if (pack) {
+    if (pack) {
       if (perm && wide) {
         LAUNCH_WS_PACKED(2)
       } else if (perm) {
@@ -756,9 +609,7 @@ inline hipError_t scatter_dispatch_ws(bool ws, int group, bool pack, unsigned ld
     }
   }
   if (!done) {
-    if (sort) {
-      LAUNCH(false, 3, false, 1);
-    } else if (perm && wide) {
+    if (perm && wide) {
       LAUNCH_WS(2, false)
     } else if (perm) {
       LAUNCH_WS(1, false)
@@ -778,12 +629,11 @@ hipError_t launch_scatter_w(int vis_dtype, int wgt_dtype, bool pack, int group, 
                                      const double* uvw, const double* fx, const void* vis, const void* wgt,
                                      const RowMap& m, const uint64_t* runs, const int64_t* run_goff,
                                      const int64_t* tile_run_off, const void* perm, const Chunk* chunks,
-                                     int64_t cb, const GridGeometry& g, int64_t plane, double fs, double* grid,
-                                     bool sort) {
+                                     int64_t cb, const GridGeometry& g, int64_t plane, double fs, double* grid) {
   const bool ws = g.do_wstacking != 0;
 #define ARGS \
   ws, group, pack, lds_extra, store_private, gd, s, uvw, fx, vis, wgt, m, runs, run_goff, tile_run_off, perm, \
-      chunks, cb, g, plane, fs, grid, sort
+      chunks, cb, g, plane, fs, grid
   if (vis_dtype == CIP_POL4I) return scatter_dispatch_ws<W, Pol4, WK_POL4I>(ARGS);
   if (vis_dtype == CIP_C64) {
     if (wgt_dtype == CIP_F32) return scatter_dispatch_ws<W, float2, WK_F32>(ARGS);

@@ -12,5 +12,5 @@ template hipError_t launch_scatter_w<CIP_SCATTER_W>(int, int, bool, int, unsigne
                                                     const void*, const void*, const RowMap&, const uint64_t*,
                                                     const int64_t*, const int64_t*, const void*,
                                                     const Chunk*, int64_t, const GridGeometry&, int64_t, double,
-                                                    double*, bool);
+                                                    double*);
 }  // namespace cip
