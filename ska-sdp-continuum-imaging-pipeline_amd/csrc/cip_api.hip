@@ -592,17 +592,6 @@ static bool ragged_pack() {
   return !(e && e[0] == '0');
 }
 
-// CIP_ORDER_GEO=0: the order pass gathers the place pass's class byte per
-// visibility instead of interpolating each run's classes from its geometry
-// word (A/B experiments)
-static bool order_geo() {
-  static const bool on = [] {
-    const char* e = getenv("CIP_ORDER_GEO");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
-
 // sub-blocks per radix workgroup: pass 0 (place blocks of ~500 runs) and the
 // dense passes (4096 runs)
 static int radix_group(int pass) { return pass ? 1 : 8; }
@@ -628,22 +617,14 @@ static int make_plan(Workspace* ws, const double* uvw, const double* fx, const R
   // (row, channel) entries
   const bool ragged = m.delta != nullptr;
   const bool order = scatter_order() && (ragged || nvis < ((int64_t)1 << 32));
-  // the order pass's classes: each run's geometry word, moved through the
-  // radix sort beside the run (order_geo), or a class byte per visibility
-  const bool geo = order && order_geo();
   uint8_t* vis_class = nullptr;
-  if (order && !geo) {
+  if (order) {
     vis_class = buf<uint8_t>(ws, "vis_class", nvis);
     if (!vis_class) return CIP_ENOMEM;
   }
   CIP_ALLOC(blk_cnt, int64_t, "blk_cnt", nblk)
   CIP_ALLOC(park_key, uint32_t, "park_key", (int64_t)nblk * 4096)
   CIP_ALLOC(park_run, uint64_t, "park_run", (int64_t)nblk * 4096)
-  uint64_t* park_geo = nullptr;
-  if (geo) {
-    park_geo = buf<uint64_t>(ws, "park_geo", (int64_t)nblk * 4096);
-    if (!park_geo) return CIP_ENOMEM;
-  }
   CIP_ALLOC(partial, double, "prep_partial", 2 * nblk)
   // the place pass also writes radix pass 0's histogram per place block; summed
   // per radix group of g0 blocks, its scan's last entry = runs
@@ -660,7 +641,7 @@ static int make_plan(Workspace* ws, const double* uvw, const double* fx, const R
   RowMap mp = m;
   mp.pk_runs = (ragged && m.pk_cbits && order && g.support <= 16 && 8 * npass <= kRunLenShift && packed_runs()) ? 1 : 0;
   CIP_HIP_CHECK(launch_plan_place(uvw, fx, mp, vis, vis_dtype, wgt, wgt_dtype, g, err, vis_class, blk_cnt, park_key,
-                                  park_run, park_geo, partial, hist0, s));
+                                  park_run, partial, hist0, s));
   CIP_HIP_CHECK(launch_prep_final(partial, nblk, red, s));
   CIP_HIP_CHECK(launch_radix_group_hist(hist0, nblk, g0, hist0g, s));
   CIP_HIP_CHECK(exclusive_scan_i64(hist0g, 256 * ng0 + 1, scan_h0, s));
@@ -683,28 +664,19 @@ static int make_plan(Workspace* ws, const double* uvw, const double* fx, const R
   CIP_ALLOC(key_b, uint32_t, "sort_key_b", nruns)
   CIP_ALLOC(run_a, uint64_t, "sort_run_a", nruns)
   CIP_ALLOC(run_b, uint64_t, "sort_run_b", nruns)
-  uint64_t *geo_a = nullptr, *geo_b = nullptr;
-  if (geo) {
-    geo_a = buf<uint64_t>(ws, "sort_geo_a", nruns);
-    geo_b = buf<uint64_t>(ws, "sort_geo_b", nruns);
-    if (!geo_a || !geo_b) return CIP_ENOMEM;
-  }
   const int64_t nbd = radix_blocks(nruns);
   const int64_t ng1 = (nbd + g1 - 1) / g1;
   CIP_ALLOC(hist, int64_t, "radix_hist", 256 * ng1 + 1)
   CIP_ALLOC(scan_h, int64_t, "scan_hist", scan_tmp_elems(256 * ng1 + 1))
-  CIP_HIP_CHECK(launch_radix_scatter(park_key, park_run, 0, blk_cnt, nblk, g0, 0, hist0g, key_a, run_a, s, park_geo,
-                                     geo_a));
+  CIP_HIP_CHECK(launch_radix_scatter(park_key, park_run, 0, blk_cnt, nblk, g0, 0, hist0g, key_a, run_a, s));
   uint32_t *kin = key_a, *kout = key_b;
   uint64_t *rin = run_a, *rout = run_b;
-  uint64_t *gin = geo_a, *gout = geo_b;
   for (int p = 1; p < npass; ++p) {
     CIP_HIP_CHECK(launch_radix_hist(kin, nruns, nullptr, nbd, g1, 8 * p, hist, s));
     CIP_HIP_CHECK(exclusive_scan_i64(hist, 256 * ng1 + 1, scan_h, s));
-    CIP_HIP_CHECK(launch_radix_scatter(kin, rin, nruns, nullptr, nbd, g1, 8 * p, hist, kout, rout, s, gin, gout));
+    CIP_HIP_CHECK(launch_radix_scatter(kin, rin, nruns, nullptr, nbd, g1, 8 * p, hist, kout, rout, s));
     std::swap(kin, kout);
     std::swap(rin, rout);
-    std::swap(gin, gout);
   }
   uint64_t* runs = rin;
   CIP_HIP_CHECK(launch_tile_offsets(kin, nruns, ntiles, tile_runs, s, mp.pk_runs ? kRunKeyMask : 0xffffffffu));
@@ -778,7 +750,7 @@ static int make_plan(Workspace* ws, const double* uvw, const double* fx, const R
     CIP_HIP_CHECK(launch_chunk_emit(tile_vis_off, tile_vis, win_off, run_goff, tile_runs, ntiles, kOrderWindow, 0, nwin,
                                     windows, s));
     CIP_ALLOC(perm, uint32_t, "perm", ragged ? 2 * nvis : nvis)
-    CIP_HIP_CHECK(launch_order(vis_class, mp, runs, run_goff, windows, nwin, perm, s, gin, g.support));
+    CIP_HIP_CHECK(launch_order(vis_class, mp, runs, run_goff, windows, nwin, perm, s));
     pr->perm = perm;
   }
   return CIP_OK;

@@ -369,25 +369,14 @@ __device__ __forceinline__ bool place_vis(double u_m, double v_m, double w_m, do
 // any other lane (off the grid by a period or more, not finite) takes
 // place_vis itself (a wave-uniform branch). WS: w-stacking at compile time
 // (0 / 1; -1: g.do_wstacking).
-// Tile-local footprint geometry of a visibility, 16 bits per axis: the
-// origin cell within its T x T tile (5 bits) and the fraction of the
-// continuous origin coordinate (11 bits), (x << 16) | y. The order pass
-// interpolates a run's classes between its first and last visibility's
-// (run_class below).
-static_assert(kTile <= 32, "5 bits of tile-local cell");
-__device__ __forceinline__ uint32_t geo_axis(int i0, double frac) {
-  return (((uint32_t)i0 % (uint32_t)kTile) << 11) | (uint32_t)(frac * 2048.0);
-}
-
 template <int WS = -1>
 __device__ __forceinline__ bool place_origin(double u_m, double v_m, double w_m, double fx, const GridGeometry& g,
-                                             int* ix0, int* iy0, int64_t* iw0, uint32_t* geo = nullptr) {
+                                             int* ix0, int* iy0, int64_t* iw0) {
 #pragma clang fp contract(off)
   const int hw = g.support / 2;
   const double x = (u_m * fx) * g.scale_u + (double)(g.nu / 2);
   const double y = (v_m * fx) * g.scale_v + (double)(g.nv / 2);
-  const double sx = x - (double)hw, sy = y - (double)hw;
-  const double flx = floor(sx), fly = floor(sy);
+  const double flx = floor(x - (double)hw), fly = floor(y - (double)hw);
   const bool small = fabs(flx) < 1073741824.0 && fabs(fly) < 1073741824.0;
   const int ix = small ? (int)flx + 1 : -1, iy = small ? (int)fly + 1 : -1;
   const bool fits = ((unsigned)ix < (unsigned)g.nu) & ((unsigned)iy < (unsigned)g.nv);
@@ -398,13 +387,10 @@ __device__ __forceinline__ bool place_origin(double u_m, double v_m, double w_m,
     *ix0 = (int)a;
     *iy0 = (int)b;
     *iw0 = c;
-    // (the kernel variable y = 2 frac - 1)
-    if (geo) *geo = (geo_axis((int)a, 0.5 * (ya + 1.0)) << 16) | geo_axis((int)b, 0.5 * (yb + 1.0));
     return ok;
   }
   *ix0 = ix;
   *iy0 = iy;
-  if (geo) *geo = (geo_axis(ix, sx - flx) << 16) | geo_axis(iy, sy - fly);
   if (WS > 0 || (WS < 0 && g.do_wstacking)) {
     const double xw = ((w_m * fx) - g.w0) * g.inv_dw;
     double yw;
@@ -414,20 +400,6 @@ __device__ __forceinline__ bool place_origin(double u_m, double v_m, double w_m,
   }
   *iw0 = 0;
   return true;
-}
-
-// The LDS bank class ((ix0 % T) P + iy0 % T) % 32 of position d of a run of
-// len visibilities from its first / last visibility's geometry (geo_axis):
-// the tile-local origin coordinates interpolated linearly in d (exact for
-// equally spaced channels up to the 2^-11 quantisation; a wrong class only
-// costs a bank conflict in the scatter, never a result)
-__device__ __forceinline__ unsigned run_class(uint64_t geo, int d, int len, unsigned P) {
-  const uint32_t a = (uint32_t)geo, b = (uint32_t)(geo >> 32);
-  const float t = len > 1 ? (float)d * __frcp_rn((float)(len - 1)) : 0.0f;
-  const float xa = (float)(a >> 16), ya = (float)(a & 0xffffu);
-  const float xb = (float)(b >> 16), yb = (float)(b & 0xffffu);
-  const int lx = (int)fmaf(xb - xa, t, xa) >> 11, ly = (int)fmaf(yb - ya, t, ya) >> 11;
-  return ((unsigned)lx * P + (unsigned)ly) & 31u;
 }
 
 // Flattened MS index i = row * nchan + c (< 2^52) -> (row, c): i * (1/nchan)

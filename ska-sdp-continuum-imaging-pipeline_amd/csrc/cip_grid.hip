@@ -105,17 +105,12 @@ static_assert(kOrderBatch == kOrderWindow, "one order block per window");
 // classes here instead - from a uvw gather, or from fp32 (u, v) carried with
 // each run through the radix sort - measured slower in rounds 2-5: the
 // gathered class byte costs fewer lines than either.)
-// GEO: the classes from the runs' geometry words (run_class: each run's first
-// and last visibility's tile-local origin, carried through the radix sort; P =
-// T + W - 1) instead of the place pass's class byte per visibility - a few
-// VALU per position instead of a gathered byte (one cache line per run).
-template <int WIDE, bool GEO>
+template <int WIDE>
 __global__ __launch_bounds__(kOrderThreads, 8) void order_kernel(const uint8_t* __restrict__ vis_class, RowMap m,
                                                                  const uint64_t* __restrict__ runs,
                                                                  const int64_t* __restrict__ run_goff,
                                                                  const Chunk* __restrict__ windows,
-                                                                 void* __restrict__ perm,
-                                                                 const uint64_t* __restrict__ geo, unsigned P) {
+                                                                 void* __restrict__ perm) {
   __shared__ __attribute__((aligned(16))) unsigned s_cnt[32];
   // the staged slices are dead once every position has its class: the level
   // tables reuse their space
@@ -125,8 +120,6 @@ __global__ __launch_bounds__(kOrderThreads, 8) void order_kernel(const uint8_t* 
       int64_t delta[WIDE == 1 ? kOrderBatch : 1];  // ragged: delta[row] of each slice (index = delta + channel)
       int off[kOrderBatch + 1];  // slice starts relative to the window start
       uint16_t idx[kOrderBatch];  // slice of each position
-      uint64_t geo[GEO ? kOrderBatch : 1];  // GEO: each slice's geometry word
-      uint8_t len[GEO ? kOrderBatch : 1];   // GEO: each slice's run length (<= 64)
     } a;
     struct {
       unsigned S[kOrderBatch], M[kOrderBatch];
@@ -158,10 +151,6 @@ __global__ __launch_bounds__(kOrderThreads, 8) void order_kernel(const uint8_t* 
       s_rec[k] = rec;
     }
     if constexpr (WIDE == 1) sh.a.delta[k] = m.delta[(int64_t)(rec >> 32)];
-    if constexpr (GEO) {
-      sh.a.geo[k] = geo[ch.first_run + k];
-      sh.a.len[k] = (uint8_t)(run_goff[ch.first_run + k + 1] - run_goff[ch.first_run + k]);
-    }
   }
   if (threadIdx.x < 32) s_cnt[threadIdx.x] = 0u;
   __syncthreads();
@@ -204,17 +193,10 @@ __global__ __launch_bounds__(kOrderThreads, 8) void order_kernel(const uint8_t* 
 #pragma unroll
   for (int k = 0; k < kOrderPer; ++k) {
     cls[k] = 32u;  // none (past the window)
-    const int qi = threadIdx.x + k * kOrderThreads;
-    if (qi < nsb) {
-      if constexpr (GEO) {
-        const int lo = slice[k];
-        cls[k] = run_class(sh.a.geo[lo], qi - s_off[lo], (int)sh.a.len[lo], P);
-      } else {
-        cls[k] = vis_class[WIDE == 2   ? (int64_t)((uint64_t)packed[k] >> pk_shift)
-                           : WIDE == 1 ? sh.a.delta[slice[k]] + chan[k]
-                                       : (int64_t)packed[k]];
-      }
-    }
+    if (threadIdx.x + k * kOrderThreads < nsb)
+      cls[k] = vis_class[WIDE == 2   ? (int64_t)((uint64_t)packed[k] >> pk_shift)
+                         : WIDE == 1 ? sh.a.delta[slice[k]] + chan[k]
+                                     : (int64_t)packed[k]];
   }
 #pragma unroll
   for (int k = 0; k < kOrderPer; ++k)
@@ -241,25 +223,17 @@ __global__ __launch_bounds__(kOrderThreads, 8) void order_kernel(const uint8_t* 
 }
 
 hipError_t launch_order(const uint8_t* vis_class, const RowMap& m, const uint64_t* runs, const int64_t* run_goff,
-                        const Chunk* windows, int64_t nwindows, void* perm, hipStream_t s, const uint64_t* geo,
-                        int support) {
+                        const Chunk* windows, int64_t nwindows, void* perm, hipStream_t s) {
   if (nwindows <= 0) return hipSuccess;
-  if (!vis_class && !geo) return hipErrorInvalidValue;
-  const unsigned P = (unsigned)(kTile + support - 1);
-#define ORDER(WI, GE)                                                                                        \
-  order_kernel<WI, GE><<<dim3((unsigned)nwindows), dim3(kOrderThreads), 0, s>>>(vis_class, m, runs,         \
-                                                                               run_goff, windows, perm, geo, P)
+  if (!vis_class) return hipErrorInvalidValue;
+#define ORDER(WI)                                                                                            \
+  order_kernel<WI><<<dim3((unsigned)nwindows), dim3(kOrderThreads), 0, s>>>(vis_class, m, runs, run_goff,   \
+                                                                           windows, perm)
   // ragged row slices: u64 entries (2: packed (index, row, channel))
   const int wide = m.delta == nullptr ? 0 : (m.pk_cbits ? 2 : 1);
-  if (geo) {
-    if (wide == 2) ORDER(2, true);
-    else if (wide) ORDER(1, true);
-    else ORDER(0, true);
-  } else {
-    if (wide == 2) ORDER(2, false);
-    else if (wide) ORDER(1, false);
-    else ORDER(0, false);
-  }
+  if (wide == 2) ORDER(2);
+  else if (wide) ORDER(1);
+  else ORDER(0);
 #undef ORDER
   return hipGetLastError();
 }

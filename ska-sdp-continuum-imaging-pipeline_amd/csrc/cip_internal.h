@@ -43,8 +43,6 @@ hipError_t launch_w_range(const double* uvw, int64_t nrow, double fxmin, double 
 // partials (2 * plan_place_blocks) and the radix pass-0 histogram of the parked
 // keys (hist0[d * nblocks + b], 256 * nblocks + 1 entries, last one zeroed);
 // vis_class (optional, nvis bytes): each visibility's LDS bank class.
-// park_geo (optional, beside park_run): each run's first and last
-// visibility's tile-local geometry (geo_axis, cip_common.h) for run_class.
 // err_flag: bit 0 non-finite uvw / w off the stack, bit 1 non-finite vis or weight.
 int plan_place_blocks(int64_t nvis);
 // the place pass's reduction alone (sum of weights, max |w V|, non-finite
@@ -54,8 +52,7 @@ hipError_t launch_prep_reduce(const RowMap& m, const void* vis, int vis_dtype, c
 hipError_t launch_plan_place(const double* uvw, const double* fx, const RowMap& m,
                              const void* vis, int vis_dtype, const void* wgt, int wgt_dtype, const GridGeometry& g,
                              unsigned* err_flag, uint8_t* vis_class, int64_t* blk_cnt, uint32_t* park_key,
-                             uint64_t* park_run, uint64_t* park_geo, double* partial, int64_t* hist0,
-                             hipStream_t s);
+                             uint64_t* park_run, double* partial, int64_t* hist0, hipStream_t s);
 // ragged rows: out[r] = chan_stop[r] - chan_start[r] (out[nrow] = 0; err bit
 // set for a range outside [0, nchan)); after the exclusive scan (off[r] = row
 // r's first visibility), launch_ragged_expand writes delta[r] = off[r] -
@@ -74,11 +71,9 @@ int64_t radix_blocks(int64_t n);
 hipError_t launch_radix_hist(const uint32_t* keys, int64_t n, const int64_t* blk_cnt, int64_t nsub, int G, int shift,
                              int64_t* hist, hipStream_t s);
 hipError_t launch_radix_group_hist(const int64_t* hist0, int64_t nsub, int G, int64_t* hg, hipStream_t s);
-// geo / geo_out (optional): a second 8-byte payload moved with the values
 hipError_t launch_radix_scatter(const uint32_t* keys, const uint64_t* vals, int64_t n, const int64_t* blk_cnt,
                                 int64_t nsub, int G, int shift, const int64_t* hist, uint32_t* keys_out,
-                                uint64_t* vals_out, hipStream_t s, const uint64_t* geo = nullptr,
-                                uint64_t* geo_out = nullptr);
+                                uint64_t* vals_out, hipStream_t s);
 hipError_t launch_tile_offsets(const uint32_t* keys, int64_t nruns, int64_t ntiles, int64_t* tile_run_off,
                                hipStream_t s, uint32_t kmask = 0xffffffffu);
 // per grid plane (nplanes x ntx x nty bytes); bits (optional, ntx % 32 ==
@@ -146,11 +141,9 @@ hipError_t launch_scatter(int support, int vis_dtype, int wgt_dtype, bool packed
 // perm (nvis 32-bit records, nvis < 2^32): the tile-order visibilities as
 // row * nchan + channel, bank-class sorted within each window (the tiles split
 // into <= kOrderWindow pieces by chunk_emit with cv = kOrderWindow)
-// vis_class: the place pass's class byte per visibility, or (geo, support)
-// the sorted runs' geometry words (park_geo through the radix sort)
+// vis_class: the place pass's class byte per visibility (required)
 hipError_t launch_order(const uint8_t* vis_class, const RowMap& m, const uint64_t* runs, const int64_t* run_goff,
-                        const Chunk* windows, int64_t nwindows, void* perm, hipStream_t s,
-                        const uint64_t* geo = nullptr, int support = 0);
+                        const Chunk* windows, int64_t nwindows, void* perm, hipStream_t s);
 hipError_t launch_crop_correct_2d(const double* grid, const GridGeometry& g, int64_t npix_x, int64_t npix_y,
                                   const double* cx, const double* cy, double* dirty, hipStream_t s);
 hipError_t launch_wplane_accumulate(const double* grid, const GridGeometry& g, int64_t npix_x, int64_t npix_y,

@@ -224,8 +224,8 @@ __device__ __forceinline__ void place_body(const double* __restrict__ uvw, const
                                            const void* __restrict__ wgt, const GridGeometry& g, unsigned* err_flag,
                                            uint8_t* __restrict__ vis_class, int64_t* __restrict__ blk_cnt,
                                            uint32_t* __restrict__ park_key, uint64_t* __restrict__ park_run,
-                                           uint64_t* __restrict__ park_geo, double* partial,
-                                           int64_t* __restrict__ hist0, const int64_t blk, const int64_t nblocks) {
+                                           double* partial, int64_t* __restrict__ hist0, const int64_t blk,
+                                           const int64_t nblocks) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   __shared__ unsigned s_nruns;
@@ -327,8 +327,7 @@ __device__ __forceinline__ void place_body(const double* __restrict__ uvw, const
     if constexpr (PLACE) {
       int ix0, iy0;
       int64_t iw0;
-      uint32_t geo = 0u;
-      const bool ok = place_origin(u, v, w, f, g, &ix0, &iy0, &iw0, &geo);
+      const bool ok = place_origin(u, v, w, f, g, &ix0, &iy0, &iw0);
       // a w layer feeds planes [iw0, iw0 + W): dropped when none is in the
       // call's plane range (plane groups split over GPUs; 2-D: the one plane)
       bool feeds = true;
@@ -362,14 +361,10 @@ __device__ __forceinline__ void place_body(const double* __restrict__ uvw, const
       unsigned wbase = 0;
       if (lane == 0 && emits) wbase = atomicAdd(&s_nruns, (unsigned)__popcll(emits));
       wbase = (unsigned)__builtin_amdgcn_readlane((int)wbase, 0);  // lane 0's slot base (scalar)
-      // the lane after this one's run: the next start above it (or the end)
-      const unsigned long long above = starts & ~((2ull << lane) - 1ull);  // lane 63: 2 << 63 == 0
-      const int next = above ? (__ffsll((long long)above) - 1) : nvalid;
-      // the run's last visibility's geometry (every lane takes part)
-      const uint32_t geo_last = park_geo ? (uint32_t)__shfl((int)geo, next - 1, 64) : 0u;
       if (emit) {
+        const unsigned long long above = starts & ~((2ull << lane) - 1ull);  // lane 63: 2 << 63 == 0
+        const int next = above ? (__ffsll((long long)above) - 1) : nvalid;
         const int64_t slot = blk * kPlaceSegs * 64 + wbase + __popcll(emits & ((1ull << lane) - 1ull));
-        if (park_geo) park_geo[slot] = ((uint64_t)geo_last << 32) | geo;
         atomicAdd(&s_hist[key & 255u], 1u);
         if (ragged && m.pk_runs) {  // wave-uniform
           park_key[slot] = key | ((uint32_t)(next - lane - 1) << kRunLenShift);
@@ -492,8 +487,8 @@ __device__ __forceinline__ void place_rows64_body(const double* __restrict__ uvw
                                                   const void* __restrict__ wgt, const GridGeometry& g,
                                                   unsigned* err_flag, uint8_t* __restrict__ vis_class,
                                                   int64_t* __restrict__ blk_cnt, uint32_t* __restrict__ park_key,
-                                                  uint64_t* __restrict__ park_run, uint64_t* __restrict__ park_geo,
-                                                  double* partial, int64_t* __restrict__ hist0, const int64_t blk,
+                                                  uint64_t* __restrict__ park_run, double* partial,
+                                                  int64_t* __restrict__ hist0, const int64_t blk,
                                                   const int64_t nblocks) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
@@ -524,7 +519,6 @@ __device__ __forceinline__ void place_rows64_body(const double* __restrict__ uvw
   // this block's park region
   uint32_t* const pkey = park_key + blk * kPlaceSegs * 64;
   uint64_t* const prun = park_run + blk * kPlaceSegs * 64;
-  uint64_t* const pgeo = park_geo ? park_geo + blk * kPlaceSegs * 64 : nullptr;
   const unsigned long long upto = (2ull << lane) - 1ull;   // lane 63: 2 << 63 == 0 - 1 = all
   for (int seg = blk32 * kPlaceSegs + wave; seg < seg_end; seg += 4) {
     // readfirstlane: an opaque uniform base, so the loads below keep the
@@ -547,8 +541,7 @@ __device__ __forceinline__ void place_rows64_body(const double* __restrict__ uvw
     wvmax = fmax(wvmax, fabs(wt) * vabs);
     int ix0, iy0;
     int64_t iw0;
-    uint32_t geo = 0u;
-    const bool ok = place_origin<WS ? 1 : 0>(u, v, w, f, g, &ix0, &iy0, &iw0, &geo);
+    const bool ok = place_origin<WS ? 1 : 0>(u, v, w, f, g, &ix0, &iy0, &iw0);
     bool feeds = true;
     if constexpr (WS) feeds = (iw0 + g.support > g.plane_lo) & (iw0 < g.plane_hi);
     const uint32_t tk = ((uint32_t)iy0 / (uint32_t)kTile) * ntx + (uint32_t)ix0 / (uint32_t)kTile;
@@ -566,16 +559,13 @@ __device__ __forceinline__ void place_rows64_body(const double* __restrict__ uvw
     unsigned wbase = 0;
     if (lane == 0 && emits) wbase = atomicAdd(&s_nruns, (unsigned)__popcll(emits));
     wbase = (unsigned)__builtin_amdgcn_readlane((int)wbase, 0);
-    const unsigned long long above = starts & ~upto;
-    const int next = above ? (__ffsll((long long)above) - 1) : 64;
-    // the run's last visibility's geometry (every lane takes part)
-    const uint32_t geo_last = park_geo ? (uint32_t)__shfl((int)geo, next - 1, 64) : 0u;
     if (emit) {
+      const unsigned long long above = starts & ~upto;
+      const int next = above ? (__ffsll((long long)above) - 1) : 64;
       const unsigned slot = wbase + __builtin_amdgcn_mbcnt_hi((unsigned)(emits >> 32),
                                                               __builtin_amdgcn_mbcnt_lo((unsigned)emits, 0u));
       atomicAdd(&s_hist[key & 255u], 1u);
       seg_st(pkey, slot, key);
-      if (park_geo) seg_st(pgeo, slot, ((uint64_t)geo_last << 32) | geo);
       const uint32_t c = (uint32_t)(c0 + lane);
       // (row << 32) | (c << 16) | channel stop, as two 32-bit words
       const uint32_t lo = (c << 16) | (uint32_t)(c0 + next);
@@ -629,16 +619,14 @@ __global__ __launch_bounds__(256) void plan_place_kernel(const double* __restric
                                                          uint8_t* __restrict__ vis_class,
                                                          int64_t* __restrict__ blk_cnt,
                                                          uint32_t* __restrict__ park_key,
-                                                         uint64_t* __restrict__ park_run,
-                                                         uint64_t* __restrict__ park_geo, double* partial,
+                                                         uint64_t* __restrict__ park_run, double* partial,
                                                          int64_t* __restrict__ hist0) {
   if constexpr (PLACE && (RM == 3 || RM == 4))
-    place_rows64_body<VisT, WK, RM == 4>(uvw, fx, m, vis, wgt, g, err_flag, vis_class, blk_cnt, park_key, park_run,
-                                         park_geo, partial,
+    place_rows64_body<VisT, WK, RM == 4>(uvw, fx, m, vis, wgt, g, err_flag, vis_class, blk_cnt, park_key, park_run, partial,
                                 hist0, blockIdx.x, gridDim.x);
   else
     place_body<VisT, WK, PLACE, RM>(uvw, fx, m, vis, wgt, g, err_flag, vis_class, blk_cnt, park_key, park_run,
-                                    park_geo, partial, hist0, blockIdx.x, gridDim.x);
+                                    partial, hist0, blockIdx.x, gridDim.x);
 }
 
 static unsigned plan_blocks(int64_t nvis) {
@@ -655,7 +643,7 @@ hipError_t launch_prep_reduce(const RowMap& m, const void* vis, int vis_dtype, c
 #define REDUCE(VT, WKV)                                                                                      \
   plan_place_kernel<VT, WKV, false><<<gd, dim3(256), 0, s>>>(nullptr, nullptr, m, (const VT*)vis, wgt, g,    \
                                                             err_flag, nullptr, nullptr, nullptr, nullptr,   \
-                                                            nullptr, partial, nullptr)
+                                                            partial, nullptr)
   if (vis_dtype == CIP_POL4I) {
     REDUCE(Pol4, WK_POL4I);
   } else if (vis_dtype == CIP_C64) {
@@ -674,15 +662,14 @@ hipError_t launch_prep_reduce(const RowMap& m, const void* vis, int vis_dtype, c
 hipError_t launch_plan_place(const double* uvw, const double* fx, const RowMap& m,
                              const void* vis, int vis_dtype, const void* wgt, int wgt_dtype, const GridGeometry& g,
                              unsigned* err_flag, uint8_t* vis_class, int64_t* blk_cnt, uint32_t* park_key,
-                             uint64_t* park_run, uint64_t* park_geo, double* partial, int64_t* hist0,
-                             hipStream_t s) {
+                             uint64_t* park_run, double* partial, int64_t* hist0, hipStream_t s) {
   const dim3 gd(plan_blocks(m.nvis));
   const bool rows64 = place_rows64() && m.nchan > 0 && m.nvis / m.nchan < ((int64_t)1 << 31) && m.nvis < ((int64_t)1 << 37);
   const int rm = m.delta != nullptr ? 2 : (m.nchan % 64 == 0 ? (rows64 ? (g.do_wstacking ? 4 : 3) : 1) : 0);
 #define PLACE_RM(VT, WKV, RMV)                                                                                      \
   plan_place_kernel<VT, WKV, true, RMV><<<gd, dim3(256), 0, s>>>(uvw, fx, m, (const VT*)vis, wgt, g, err_flag,     \
-                                                                 vis_class, blk_cnt, park_key, park_run, park_geo,  \
-                                                                 partial, hist0)
+                                                                 vis_class, blk_cnt, park_key, park_run, partial,   \
+                                                                 hist0)
 #define PLACE(VT, WKV)            \
   do {                            \
     if (rm == 4) {                \
@@ -829,8 +816,7 @@ __global__ void radix_group_hist_kernel(const int64_t* __restrict__ hist0, int64
 __global__ __launch_bounds__(kRadixThreads) void radix_scatter_kernel(
     const uint32_t* __restrict__ keys, const uint64_t* __restrict__ vals, int64_t n,
     const int64_t* __restrict__ blk_cnt, int64_t nsub, int G, int shift, int64_t ngroups,
-    const int64_t* __restrict__ hist, uint32_t* __restrict__ keys_out, uint64_t* __restrict__ vals_out,
-    const uint64_t* __restrict__ geo, uint64_t* __restrict__ geo_out) {
+    const int64_t* __restrict__ hist, uint32_t* __restrict__ keys_out, uint64_t* __restrict__ vals_out) {
   __shared__ unsigned wcnt[4][256];  // per-wave running digit counts
   __shared__ int64_t dnext[256];     // the group's next position per digit
   __shared__ int64_t woff[4][256];   // global position of each wave's first item per digit
@@ -891,24 +877,13 @@ __global__ __launch_bounds__(kRadixThreads) void radix_scatter_kernel(
       dnext[d] = o;
     }
     __syncthreads();
-    int64_t pos[kRadixPer];
 #pragma unroll
     for (int k = 0; k < kRadixPer; ++k)
       if (k < steps && i0 + k * 64 < lim) {
-        pos[k] = woff[wave][(key[k] >> shift) & 255u] + rank[k];
-        keys_out[pos[k]] = key[k];
-        vals_out[pos[k]] = val[k];
+        const int64_t pos = woff[wave][(key[k] >> shift) & 255u] + rank[k];
+        keys_out[pos] = key[k];
+        vals_out[pos] = val[k];
       }
-    // the runs' geometry words (RowMap-independent payload of the order pass),
-    // moved after the records so they hold no registers across the ranking
-    if (geo) {
-      uint64_t gv[kRadixPer];
-#pragma unroll
-      for (int k = 0; k < kRadixPer; ++k) gv[k] = (k < steps && i0 + k * 64 < lim) ? geo[i0 + k * 64] : 0ull;
-#pragma unroll
-      for (int k = 0; k < kRadixPer; ++k)
-        if (k < steps && i0 + k * 64 < lim) geo_out[pos[k]] = gv[k];
-    }
     __syncthreads();  // wcnt / woff are reused by the next sub-block
   }
 }
@@ -948,11 +923,11 @@ hipError_t launch_radix_group_hist(const int64_t* hist0, int64_t nsub, int G, in
 
 hipError_t launch_radix_scatter(const uint32_t* keys, const uint64_t* vals, int64_t n, const int64_t* blk_cnt,
                                 int64_t nsub, int G, int shift, const int64_t* hist, uint32_t* keys_out,
-                                uint64_t* vals_out, hipStream_t s, const uint64_t* geo, uint64_t* geo_out) {
+                                uint64_t* vals_out, hipStream_t s) {
   if (nsub == 0) return hipSuccess;
   const int64_t ngroups = (nsub + G - 1) / G;
   radix_scatter_kernel<<<dim3((unsigned)ngroups), dim3(kRadixThreads), 0, s>>>(
-      keys, vals, n, blk_cnt, nsub, G, shift, ngroups, hist, keys_out, vals_out, geo, geo_out);
+      keys, vals, n, blk_cnt, nsub, G, shift, ngroups, hist, keys_out, vals_out);
   return hipGetLastError();
 }
 
