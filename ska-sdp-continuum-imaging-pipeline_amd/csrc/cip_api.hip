@@ -592,6 +592,16 @@ static bool ragged_pack() {
   return !(e && e[0] == '0');
 }
 
+// CIP_ROW_PHASES=0: the order pass assigns no row phases (cip_grid.hip
+// order_kernel; A/B experiments and the phase test)
+static bool row_phases() {
+  static const bool on = [] {
+    const char* e = getenv("CIP_ROW_PHASES");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 // sub-blocks per radix workgroup: pass 0 (place blocks of ~500 runs) and the
 // dense passes (4096 runs)
 static int radix_group(int pass) { return pass ? 1 : 8; }
@@ -750,7 +760,7 @@ static int make_plan(Workspace* ws, const double* uvw, const double* fx, const R
     CIP_HIP_CHECK(launch_chunk_emit(tile_vis_off, tile_vis, win_off, run_goff, tile_runs, ntiles, kOrderWindow, 0, nwin,
                                     windows, s));
     CIP_ALLOC(perm, uint32_t, "perm", ragged ? 2 * nvis : nvis)
-    CIP_HIP_CHECK(launch_order(vis_class, mp, runs, run_goff, windows, nwin, perm, s));
+    CIP_HIP_CHECK(launch_order(vis_class, mp, runs, run_goff, windows, nwin, perm, s, row_phases() ? g.support : 0));
     pr->perm = perm;
   }
   return CIP_OK;

@@ -105,13 +105,27 @@ static_assert(kOrderBatch == kOrderWindow, "one order block per window");
 // classes here instead - from a uvw gather, or from fp32 (u, v) carried with
 // each run through the radix sort - measured slower in rounds 2-5: the
 // gathered class byte costs fewer lines than either.)
-template <int WIDE>
+//
+// Row phases (round 6, PH = dense entries of < 2^31 visibilities, W <= 16):
+// a visibility of phase 1 adds its footprint rows in the order 1, 2, ..,
+// W - 1, 0 instead of 0 .. W - 1 (cip_scatter.h), so at every tap its LDS bank
+// pair is its class + dP (dP = P mod 32 = W - 1; + dP - W P on the last row)
+// - it behaves as class c + dP. The windows' class counts are skewed (the
+// largest ~1.6x the mean), which leaves the level-major order's top levels
+// with repeated classes in a 32-lane group; moving the excess of each class
+// to its neighbour c + dP along the 32-cycle c -> c + dP (one carry walk from
+// the largest class, twice round, by wave 0 in scalar registers) evens the
+// effective counts: 2.02 -> 1.65 LDS cycles per 32-lane tap in a host
+// simulation of C3's windows (tools/sim_row_phase.py). The phase rides in
+// bit 31 of the entry.
+template <int WIDE, bool PH, int NC = 16>
 __global__ __launch_bounds__(kOrderThreads, 8) void order_kernel(const uint8_t* __restrict__ vis_class, RowMap m,
                                                                  const uint64_t* __restrict__ runs,
                                                                  const int64_t* __restrict__ run_goff,
                                                                  const Chunk* __restrict__ windows,
-                                                                 void* __restrict__ perm) {
+                                                                 void* __restrict__ perm, int dP) {
   __shared__ __attribute__((aligned(16))) unsigned s_cnt[32];
+  __shared__ unsigned s_keep[PH ? NC : 1], s_eff[PH ? NC : 1];  // PH: phase-0 items / effective count per class
   // the staged slices are dead once every position has its class: the level
   // tables reuse their space
   __shared__ union {
@@ -152,7 +166,7 @@ __global__ __launch_bounds__(kOrderThreads, 8) void order_kernel(const uint8_t* 
     }
     if constexpr (WIDE == 1) sh.a.delta[k] = m.delta[(int64_t)(rec >> 32)];
   }
-  if (threadIdx.x < 32) s_cnt[threadIdx.x] = 0u;
+  if (threadIdx.x < NC) s_cnt[threadIdx.x] = 0u;
   __syncthreads();
   // expand: every position learns its slice (slices are <= 64 positions long)
   for (int k = threadIdx.x; k < nst; k += kOrderThreads) {
@@ -196,20 +210,73 @@ __global__ __launch_bounds__(kOrderThreads, 8) void order_kernel(const uint8_t* 
     if (threadIdx.x + k * kOrderThreads < nsb)
       cls[k] = vis_class[WIDE == 2   ? (int64_t)((uint64_t)packed[k] >> pk_shift)
                          : WIDE == 1 ? sh.a.delta[slice[k]] + chan[k]
-                                     : (int64_t)packed[k]];
+                                     : (int64_t)packed[k]] &
+               (unsigned)(NC - 1);
   }
 #pragma unroll
   for (int k = 0; k < kOrderPer; ++k)
     if (cls[k] < 32u) rk[k] = atomicAdd(&s_cnt[cls[k]], 1u);
   __syncthreads();
+  const unsigned* cnt_of = s_cnt;  // the counts the level tables follow
+  if constexpr (PH) {
+    if (threadIdx.x < 64) {
+      // wave 0: k_c = items of class c moved to c + dP, one carry walk along
+      // the cycle from the class after the largest, twice round; lane c holds
+      // class c's count and (written lane by lane) its k_c
+      const int lane = threadIdx.x;
+      const unsigned nc = lane < NC ? s_cnt[lane] : 0u;
+      unsigned tot = nc, best = nc;
+      int start = lane;
+      for (int d = 32; d > 0; d >>= 1) {
+        tot += __shfl_xor(tot, d, 64);
+        const unsigned ob = __shfl_xor(best, d, 64);
+        const int os = __shfl_xor(start, d, 64);
+        if (ob > best || (ob == best && os < start)) {
+          best = ob;
+          start = os;
+        }
+      }
+      const unsigned mean = (tot + (unsigned)NC - 1u) / (unsigned)NC;
+      int kreg = 0;
+      unsigned kc = 0u;  // the walk's last k (scalar)
+      int cc = __builtin_amdgcn_readfirstlane(start);
+      for (int s2 = 0; s2 < 2 * NC; ++s2) {
+        cc = (cc + dP) & (NC - 1);
+        const unsigned n = (unsigned)__builtin_amdgcn_readlane((int)nc, cc);
+        const unsigned e = n + kc;  // its own items and the carry from cc - dP
+        kc = e > mean ? (e - mean < n ? e - mean : n) : 0u;
+        kreg = lane == cc ? (int)kc : kreg;
+      }
+      const unsigned kin = (unsigned)__shfl(kreg, (lane - dP) & (NC - 1), 64);
+      if (lane < NC) {
+        s_keep[lane] = nc - (unsigned)kreg;
+        s_eff[lane] = nc - (unsigned)kreg + kin;
+      }
+    }
+    __syncthreads();
+    // each item's effective class and rank: the last k_c items of class c go
+    // to c + dP after that class's own kept items
+#pragma unroll
+    for (int k = 0; k < kOrderPer; ++k)
+      if (cls[k] < 32u) {
+        const unsigned keep = s_keep[cls[k]];
+        if (rk[k] >= keep) {
+          const unsigned e = (cls[k] + (unsigned)dP) & (unsigned)(NC - 1);
+          rk[k] = s_keep[e] + (rk[k] - keep);
+          cls[k] = e;
+          packed[k] = (Entry)((uint32_t)packed[k] | 0x80000000u);
+        }
+      }
+    cnt_of = s_eff;
+  }
   unsigned maxcnt = 0;
 #pragma unroll
-  for (int i = 0; i < 32; ++i) maxcnt = s_cnt[i] > maxcnt ? s_cnt[i] : maxcnt;  // LDS broadcast reads
+  for (int i = 0; i < NC; ++i) maxcnt = cnt_of[i] > maxcnt ? cnt_of[i] : maxcnt;  // LDS broadcast reads
   for (unsigned r = threadIdx.x; r < maxcnt; r += kOrderThreads) {
     unsigned S = 0, M = 0;
 #pragma unroll
-    for (int c2 = 0; c2 < 32; ++c2) {
-      const unsigned cnt = s_cnt[c2];
+    for (int c2 = 0; c2 < NC; ++c2) {
+      const unsigned cnt = cnt_of[c2];
       S += cnt < r ? cnt : r;
       M |= (cnt > r ? 1u : 0u) << c2;
     }
@@ -222,18 +289,44 @@ __global__ __launch_bounds__(kOrderThreads, 8) void order_kernel(const uint8_t* 
     if (cls[k] < 32u) ((Entry*)perm)[sb + s_S[rk[k]] + __popc(s_M[rk[k]] & ((1u << cls[k]) - 1u))] = packed[k];
 }
 
+// CIP_ORDER_CLASSES=32: bank classes mod 32 (rounds 1-6) instead of mod 16 (A/B)
+static bool order_classes32() {
+  static const bool on = [] {
+    const char* e = getenv("CIP_ORDER_CLASSES");
+    return e && e[0] == '3';
+  }();
+  return on;
+}
+
 hipError_t launch_order(const uint8_t* vis_class, const RowMap& m, const uint64_t* runs, const int64_t* run_goff,
-                        const Chunk* windows, int64_t nwindows, void* perm, hipStream_t s) {
+                        const Chunk* windows, int64_t nwindows, void* perm, hipStream_t s, int phase_support) {
   if (nwindows <= 0) return hipSuccess;
   if (!vis_class) return hipErrorInvalidValue;
-#define ORDER(WI)                                                                                            \
-  order_kernel<WI><<<dim3((unsigned)nwindows), dim3(kOrderThreads), 0, s>>>(vis_class, m, runs, run_goff,   \
-                                                                           windows, perm)
+#define ORDER(WI, PHV, NCV)                                                                                    \
+  order_kernel<WI, PHV, NCV><<<dim3((unsigned)nwindows), dim3(kOrderThreads), 0, s>>>(vis_class, m, runs,     \
+                                                                                      run_goff, windows, perm, dP)
   // ragged row slices: u64 entries (2: packed (index, row, channel))
   const int wide = m.delta == nullptr ? 0 : (m.pk_cbits ? 2 : 1);
-  if (wide == 2) ORDER(2);
-  else if (wide) ORDER(1);
-  else ORDER(0);
+  // 8-byte LDS atomics are banked like ds_write_b64 (MI355X_MICROARCH.md, LDS:
+  // four 16-lane groups, bank pair = element mod 16), so the classes are the
+  // footprint origin's element mod 16 (mod 32 before round 6)
+  const bool c32 = order_classes32();
+  const int nc = c32 ? 32 : 16;
+  // row phases: dense entries with bit 31 free, a lane scatter whose support
+  // gives a full cycle (dP = (T + W - 1) mod NC odd)
+  const int dP = (kTile + phase_support - 1) & (nc - 1);
+  const bool ph = wide == 0 && phase_support >= 2 && phase_support <= 16 && (dP & 1) && m.nvis < ((int64_t)1 << 31);
+  if (c32) {
+    if (wide == 2) ORDER(2, false, 32);
+    else if (wide) ORDER(1, false, 32);
+    else if (ph) ORDER(0, true, 32);
+    else ORDER(0, false, 32);
+  } else {
+    if (wide == 2) ORDER(2, false, 16);
+    else if (wide) ORDER(1, false, 16);
+    else if (ph) ORDER(0, true, 16);
+    else ORDER(0, false, 16);
+  }
 #undef ORDER
   return hipGetLastError();
 }

@@ -142,8 +142,11 @@ hipError_t launch_scatter(int support, int vis_dtype, int wgt_dtype, bool packed
 // row * nchan + channel, bank-class sorted within each window (the tiles split
 // into <= kOrderWindow pieces by chunk_emit with cv = kOrderWindow)
 // vis_class: the place pass's class byte per visibility (required)
+// phase_support: the support W of the lane scatter that reads perm, which then
+// carries row phases (bit 31 of dense entries, cip_grid.hip order_kernel);
+// 0: no phases
 hipError_t launch_order(const uint8_t* vis_class, const RowMap& m, const uint64_t* runs, const int64_t* run_goff,
-                        const Chunk* windows, int64_t nwindows, void* perm, hipStream_t s);
+                        const Chunk* windows, int64_t nwindows, void* perm, hipStream_t s, int phase_support = 0);
 hipError_t launch_crop_correct_2d(const double* grid, const GridGeometry& g, int64_t npix_x, int64_t npix_y,
                                   const double* cx, const double* cy, double* dirty, hipStream_t s);
 hipError_t launch_wplane_accumulate(const double* grid, const GridGeometry& g, int64_t npix_x, int64_t npix_y,

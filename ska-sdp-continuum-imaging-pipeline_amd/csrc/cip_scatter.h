@@ -37,6 +37,7 @@ constexpr int kRunBatch = 256;
 // the global-memory latency overlaps the previous visibility's taps.
 struct VisFetch {
   double u, v, w, fx, vr, vi, wt;
+  uint32_t h;  // row phase (order_kernel): 1 = footprint rows in the order 1 .. W - 1, 0
 };
 
 // last staged run starting at or before flattened visibility q
@@ -67,6 +68,7 @@ __device__ __forceinline__ void fetch_vis(int64_t q, const int64_t* s_voff, cons
   f.fx = fx[c];
   load_vis(vis, idx, f.vr, f.vi);
   f.wt = load_weight<WK>(wgt, m, idx);
+  f.h = 0u;
 }
 
 // The same, as loaded (complex64 / float32 kept in their own types): the
@@ -80,6 +82,7 @@ struct RawFetch {
   double u, v, w, fx;
   VisT vis;
   WT wt;
+  uint32_t h;
 };
 template <>
 struct RawFetch<Pol4, WK_POL4I> {
@@ -87,6 +90,7 @@ struct RawFetch<Pol4, WK_POL4I> {
   float2 a, d;
   float wa, wb;
   uint32_t fw;
+  uint32_t h;
 };
 
 // Branch-free loads of the visibility of ordered-stream entry e (callers pass
@@ -100,6 +104,12 @@ __device__ __forceinline__ void fetch_raw(uint64_t e, const double* __restrict__
                                           bool unit_vis, const void* __restrict__ wgt, const RowMap& m,
                                           RawFetch<VisT, WK>& f) {
   int64_t il, r, c;
+  f.h = 0u;
+  if constexpr (WIDE == 0) {
+    // dense entries: the row phase in bit 31 (order_kernel<0, true>)
+    f.h = (uint32_t)(e >> 31) & 1u;
+    e &= 0x7fffffffull;
+  }
   if constexpr (WIDE < 0) perm_decode(e, m, &il, &r, &c);
   else perm_decode_t<WIDE == 1>(e, m, &il, &r, &c);
   f.u = uvw[3 * r];
@@ -128,6 +138,7 @@ __device__ __forceinline__ VisFetch from_raw(const RawFetch<VisT, WK>& r, bool u
   f.v = r.v;
   f.w = r.w;
   f.fx = r.fx;
+  f.h = r.h;
   if constexpr (WK == WK_POL4I) {
     const float2 s = stokes_i_vis(r.a, r.d);
     f.vr = unit_vis ? 1.0 : (double)s.x;
@@ -156,6 +167,26 @@ constexpr unsigned long long kMagicPair = ((unsigned long long)kMagicFBits << 32
 __device__ __forceinline__ unsigned long long packed_tap(float ku, f32x2 k_ir) {
   const f32x2 q = __builtin_elementwise_fma(f32x2{ku, ku}, k_ir, f32x2{kMagicF, kMagicF});
   return __builtin_bit_cast(unsigned long long, q) - kMagicPair;
+}
+
+// A visibility of row phase h (order_kernel) adds its footprint rows in the
+// order h, h + 1, .., (W - 1 + h) mod W: its kernel values rotated by h here,
+// and the rows' LDS addresses rotated in row_ptr - the same taps into the same
+// cells, but at each tap instruction its bank pair is shifted by P (the order
+// pass balances the bank classes with it).
+template <int W, typename T>
+__device__ __forceinline__ void rotate_rows(T* k, uint32_t h) {
+  const T k0 = k[0];
+#pragma unroll
+  for (int i = 0; i < W - 1; ++i) k[i] = h ? k[i + 1] : k[i];
+  k[W - 1] = h ? k0 : k[W - 1];
+}
+// the LDS address of tap (i, 0) of a footprint at base, rows rotated by h:
+// rows i < W - 1 from base + h P (one register), the last from base + (1 - h)
+// (W - 1) P
+template <int W, int P>
+__device__ __forceinline__ unsigned long long* row_ptr(unsigned long long* b0, unsigned long long* bl, int i) {
+  return i < W - 1 ? b0 + i * P : bl;
 }
 
 // The packed class's visibility: fp32 kernel values and tap products (the
@@ -187,15 +218,18 @@ __device__ __forceinline__ void grid_fetched_packed(const VisFetch& f, const Gri
     }
   }
   unsigned long long* base = sub + (lx * P + ly);
+  rotate_rows<W>(ku, f.h);
   auto taps = [&](unsigned long long* bk, float vr, float vi) {
     f32x2 k_ir[W];  // (kv vi, kv vr): the low / high word of each tap
     const f32x2 v_ir{vi, vr};
 #pragma unroll
     for (int j = 0; j < W; ++j) k_ir[j] = f32x2{kv[j], kv[j]} * v_ir;
+    unsigned long long* b0 = bk + (f.h ? P : 0);
+    unsigned long long* bl = bk + (f.h ? 0 : (W - 1) * P);
 #pragma unroll
     for (int i = 0; i < W; ++i)
 #pragma unroll
-      for (int j = 0; j < W; ++j) atomicAdd(bk + (i * P + j), packed_tap(ku[i], k_ir[j]));
+      for (int j = 0; j < W; ++j) atomicAdd(row_ptr<W, P>(b0, bl, i) + j, packed_tap(ku[i], k_ir[j]));
   };
   if constexpr (!WSTACK) {
     taps(base, vr0, vi0);
@@ -239,6 +273,7 @@ __device__ __forceinline__ void grid_fetched(const VisFetch& f, const GridGeomet
     eval_kernel<W>(yw, kwv);
     eval_kernel<W>(yu, ku);
     eval_kernel<W>(yv, kv);
+    rotate_rows<W>(ku, f.h);
     const double sc0 = f.wt * fixed_scale;
     unsigned long long* base = sub + (lx * P + ly);
 #pragma unroll
@@ -258,8 +293,11 @@ __device__ __forceinline__ void grid_fetched(const VisFetch& f, const GridGeomet
         ki[j] = kv[j] * vi;
       }
       unsigned long long* bk = base + k * S;
+      unsigned long long* b0 = bk + (f.h ? P : 0);
+      unsigned long long* bl = bk + (f.h ? 0 : (W - 1) * P);
 #pragma unroll
       for (int i = 0; i < W; ++i) {
+        unsigned long long* bi0 = row_ptr<W, P>(b0, bl, i);
 #pragma unroll
         for (int j = 0; j < W; ++j) {
           const double qr = fma(ku[i], kr[j], kMagic);
@@ -270,10 +308,10 @@ __device__ __forceinline__ void grid_fetched(const VisFetch& f, const GridGeomet
             unsigned hi;
             asm("v_add3_u32 %0, %1, %2, %3" : "=v"(hi) : "v"((unsigned)br), "v"((unsigned)(bi >> 32)),
                 "s"(0u - kMagicHi));
-            atomicAdd(bk + (i * P + j), __builtin_bit_cast(unsigned long long, make_uint2((unsigned)bi, hi)));
+            atomicAdd(bi0 + j, __builtin_bit_cast(unsigned long long, make_uint2((unsigned)bi, hi)));
           } else {
-            atomicAdd(bk + (i * P + j), br - kTapBias);
-            atomicAdd(bk + P * P + (i * P + j), bi - kTapBias);
+            atomicAdd(bi0 + j, br - kTapBias);
+            atomicAdd(bi0 + P * P + j, bi - kTapBias);
           }
         }
       }
@@ -295,6 +333,7 @@ __device__ __forceinline__ void grid_fetched(const VisFetch& f, const GridGeomet
   double ku[W], kv[W];
   eval_kernel<W>(yu, ku);
   eval_kernel<W>(yv, kv);
+  rotate_rows<W>(ku, f.h);
   double kr[W], ki[W];
 #pragma unroll
   for (int j = 0; j < W; ++j) {
@@ -305,8 +344,11 @@ __device__ __forceinline__ void grid_fetched(const VisFetch& f, const GridGeomet
   // LDS banks, so 8-byte cells spread a wave over twice the bank pairs that
   // interleaved 16-byte (re, im) cells would
   unsigned long long* base = sub + (lx * P + ly);
+  unsigned long long* b0 = base + (f.h ? P : 0);
+  unsigned long long* bl = base + (f.h ? 0 : (W - 1) * P);
 #pragma unroll
   for (int i = 0; i < W; ++i) {
+    unsigned long long* bi0 = row_ptr<W, P>(b0, bl, i);
 #pragma unroll
     for (int j = 0; j < W; ++j) {
       const double qr = fma(ku[i], kr[j], kMagic);
@@ -319,10 +361,10 @@ __device__ __forceinline__ void grid_fetched(const VisFetch& f, const GridGeomet
         unsigned hi;  // one v_add3_u32 (the compiler otherwise widens it to 64-bit adds)
         asm("v_add3_u32 %0, %1, %2, %3" : "=v"(hi) : "v"((unsigned)br), "v"((unsigned)(bi >> 32)),
             "s"(0u - kMagicHi));
-        atomicAdd(base + (i * P + j), __builtin_bit_cast(unsigned long long, make_uint2((unsigned)bi, hi)));
+        atomicAdd(bi0 + j, __builtin_bit_cast(unsigned long long, make_uint2((unsigned)bi, hi)));
       } else {
-        atomicAdd(base + (i * P + j), br - kTapBias);
-        atomicAdd(base + P * P + (i * P + j), bi - kTapBias);
+        atomicAdd(bi0 + j, br - kTapBias);
+        atomicAdd(bi0 + P * P + j, bi - kTapBias);
       }
     }
   }
