@@ -106,18 +106,22 @@ static_assert(kOrderBatch == kOrderWindow, "one order block per window");
 // each run through the radix sort - measured slower in rounds 2-5: the
 // gathered class byte costs fewer lines than either.)
 //
-// Row phases (round 6, PH = dense entries of < 2^31 visibilities, W <= 16):
-// a visibility of phase 1 adds its footprint rows in the order 1, 2, ..,
-// W - 1, 0 instead of 0 .. W - 1 (cip_scatter.h), so at every tap its LDS bank
-// pair is its class + dP (dP = P mod 32 = W - 1; + dP - W P on the last row)
-// - it behaves as class c + dP. The windows' class counts are skewed (the
-// largest ~1.6x the mean), which leaves the level-major order's top levels
-// with repeated classes in a 32-lane group; moving the excess of each class
-// to its neighbour c + dP along the 32-cycle c -> c + dP (one carry walk from
-// the largest class, twice round, by wave 0 in scalar registers) evens the
-// effective counts: 2.02 -> 1.65 LDS cycles per 32-lane tap in a host
-// simulation of C3's windows (tools/sim_row_phase.py). The phase rides in
-// bit 31 of the entry.
+// Bank classes (round 6): 8-byte LDS atomics are banked like ds_write_b64 -
+// four 16-lane groups, bank pair = element mod 16 (MI355X_MICROARCH.md, LDS) -
+// so a class is the footprint origin's sub-grid element mod NC = 16 (32 in
+// rounds 1-5; CIP_ORDER_CLASSES=32 for A/B).
+// Row phases (PH: dense entries of < 2^31 visibilities, W <= 16): a
+// visibility of phase 1 adds its footprint rows in the order 1, 2, .., W - 1,
+// 0 instead of 0 .. W - 1 (cip_scatter.h rotate_rows / row_ptr), so at every
+// tap but the last row's its bank pair is its class + dP (dP = P mod 16) - it
+// behaves as class c + dP. The windows' class counts are skewed (the largest
+// ~1.6x the mean), which leaves the level-major order's top levels with
+// repeated classes in a 16-lane group; moving the excess of each class to its
+// neighbour c + dP along the cycle c -> c + dP (a carry walk from the class
+// after the largest, twice round, by wave 0 with a scalar carry) evens the
+// effective counts. Host simulation of C3's windows under the 16-lane model
+// (tools/sim_bank16.py): 1.74 LDS cycles per 16-lane tap for mod-32 classes,
+// 1.58 mod 16, 1.27 mod 16 with phases. The phase rides in bit 31 of the entry.
 template <int WIDE, bool PH, int NC = 16>
 __global__ __launch_bounds__(kOrderThreads, 8) void order_kernel(const uint8_t* __restrict__ vis_class, RowMap m,
                                                                  const uint64_t* __restrict__ runs,
@@ -237,20 +241,25 @@ __global__ __launch_bounds__(kOrderThreads, 8) void order_kernel(const uint8_t* 
         }
       }
       const unsigned mean = (tot + (unsigned)NC - 1u) / (unsigned)NC;
-      int kreg = 0;
-      unsigned kc = 0u;  // the walk's last k (scalar)
-      int cc = __builtin_amdgcn_readfirstlane(start);
+      // lane j < NC: the j-th class of the walk (from the class after the
+      // largest along c -> c + dP) and its count
+      const int st = __builtin_amdgcn_readfirstlane(start);
+      const int cw = (st + (lane + 1) * dP) & (NC - 1);
+      const unsigned nw = (unsigned)__shfl((int)nc, cw, 64);
+      // the walk, unrolled over constant lanes (scalar carry; lap 2 final)
+      unsigned kc = 0u, kw = 0u;
+#pragma unroll
       for (int s2 = 0; s2 < 2 * NC; ++s2) {
-        cc = (cc + dP) & (NC - 1);
-        const unsigned n = (unsigned)__builtin_amdgcn_readlane((int)nc, cc);
-        const unsigned e = n + kc;  // its own items and the carry from cc - dP
+        const unsigned n = (unsigned)__builtin_amdgcn_readlane((int)nw, s2 & (NC - 1));
+        const unsigned e = n + kc;  // its own items and the carry from the class before
         kc = e > mean ? (e - mean < n ? e - mean : n) : 0u;
-        kreg = lane == cc ? (int)kc : kreg;
+        if (s2 >= NC) kw = lane == (s2 & (NC - 1)) ? kc : kw;
       }
-      const unsigned kin = (unsigned)__shfl(kreg, (lane - dP) & (NC - 1), 64);
+      // the carry into walk position j is position j - 1's
+      const unsigned kin = (unsigned)__shfl((int)kw, (lane - 1) & (NC - 1), 64);
       if (lane < NC) {
-        s_keep[lane] = nc - (unsigned)kreg;
-        s_eff[lane] = nc - (unsigned)kreg + kin;
+        s_keep[cw] = nw - kw;
+        s_eff[cw] = nw - kw + kin;
       }
     }
     __syncthreads();
@@ -264,7 +273,9 @@ __global__ __launch_bounds__(kOrderThreads, 8) void order_kernel(const uint8_t* 
           const unsigned e = (cls[k] + (unsigned)dP) & (unsigned)(NC - 1);
           rk[k] = s_keep[e] + (rk[k] - keep);
           cls[k] = e;
-          packed[k] = (Entry)((uint32_t)packed[k] | 0x80000000u);
+          // the phase: bit 31 of a dense entry, bit 63 of a ragged one
+          if constexpr (WIDE == 0) packed[k] = (Entry)((uint32_t)packed[k] | 0x80000000u);
+          else packed[k] = (Entry)((uint64_t)packed[k] | 0x8000000000000000ull);
         }
       }
     cnt_of = s_eff;
@@ -315,14 +326,27 @@ hipError_t launch_order(const uint8_t* vis_class, const RowMap& m, const uint64_
   // row phases: dense entries with bit 31 free, a lane scatter whose support
   // gives a full cycle (dP = (T + W - 1) mod NC odd)
   const int dP = (kTile + phase_support - 1) & (nc - 1);
-  const bool ph = wide == 0 && phase_support >= 2 && phase_support <= 16 && (dP & 1) && m.nvis < ((int64_t)1 << 31);
+  // (a bit to spare: bit 31 of dense entries, bit 63 of ragged ones - the
+  // packed (index, row, channel) form must leave it free)
+  auto bits = [](int64_t n) {
+    int b = 1;
+    while (b < 62 && ((int64_t)1 << b) < n) ++b;
+    return b;
+  };
+  const bool spare = wide == 0 ? m.nvis < ((int64_t)1 << 31)
+                               : (wide == 1 || m.pk_cbits + m.pk_rbits + bits(m.nvis) <= 63);
+  const bool ph = phase_support >= 2 && phase_support <= 16 && (dP & 1) && spare;
   if (c32) {
-    if (wide == 2) ORDER(2, false, 32);
+    if (wide == 2 && ph) ORDER(2, true, 32);
+    else if (wide == 2) ORDER(2, false, 32);
+    else if (wide && ph) ORDER(1, true, 32);
     else if (wide) ORDER(1, false, 32);
     else if (ph) ORDER(0, true, 32);
     else ORDER(0, false, 32);
   } else {
-    if (wide == 2) ORDER(2, false, 16);
+    if (wide == 2 && ph) ORDER(2, true, 16);
+    else if (wide == 2) ORDER(2, false, 16);
+    else if (wide && ph) ORDER(1, true, 16);
     else if (wide) ORDER(1, false, 16);
     else if (ph) ORDER(0, true, 16);
     else ORDER(0, false, 16);
