@@ -117,8 +117,8 @@ static_assert(kOrderBatch == kOrderWindow, "one order block per window");
 // behaves as class c + dP. The windows' class counts are skewed (the largest
 // ~1.6x the mean), which leaves the level-major order's top levels with
 // repeated classes in a 16-lane group; moving the excess of each class to its
-// neighbour c + dP along the cycle c -> c + dP (a carry walk from the class
-// after the largest, twice round, by wave 0 with a scalar carry) evens the
+// neighbour c + dP along the cycle c -> c + dP (a carry walk twice round, by
+// wave 0 with a scalar carry) evens the
 // effective counts. Host simulation of C3's windows under the 16-lane model
 // (tools/sim_bank16.py): 1.74 LDS cycles per 16-lane tap for mod-32 classes,
 // 1.58 mod 16, 1.27 mod 16 with phases. The phase rides in bit 31 of the entry.
@@ -225,27 +225,14 @@ __global__ __launch_bounds__(kOrderThreads, 8) void order_kernel(const uint8_t* 
   if constexpr (PH) {
     if (threadIdx.x < 64) {
       // wave 0: k_c = items of class c moved to c + dP, one carry walk along
-      // the cycle from the class after the largest, twice round; lane c holds
-      // class c's count and (written lane by lane) its k_c
+      // the cycle c -> c + dP from class dP, twice round (where the walk
+      // starts does not matter after two laps - host simulation), against the
+      // mean count ceil(positions / NC); lane j < NC holds the j-th class of
+      // the walk and its count
       const int lane = threadIdx.x;
-      const unsigned nc = lane < NC ? s_cnt[lane] : 0u;
-      unsigned tot = nc, best = nc;
-      int start = lane;
-      for (int d = 32; d > 0; d >>= 1) {
-        tot += __shfl_xor(tot, d, 64);
-        const unsigned ob = __shfl_xor(best, d, 64);
-        const int os = __shfl_xor(start, d, 64);
-        if (ob > best || (ob == best && os < start)) {
-          best = ob;
-          start = os;
-        }
-      }
-      const unsigned mean = (tot + (unsigned)NC - 1u) / (unsigned)NC;
-      // lane j < NC: the j-th class of the walk (from the class after the
-      // largest along c -> c + dP) and its count
-      const int st = __builtin_amdgcn_readfirstlane(start);
-      const int cw = (st + (lane + 1) * dP) & (NC - 1);
-      const unsigned nw = (unsigned)__shfl((int)nc, cw, 64);
+      const unsigned mean = ((unsigned)nsb + (unsigned)NC - 1u) / (unsigned)NC;
+      const int cw = ((lane + 1) * dP) & (NC - 1);
+      const unsigned nw = lane < NC ? s_cnt[cw] : 0u;
       // the walk, unrolled over constant lanes (scalar carry; lap 2 final)
       unsigned kc = 0u, kw = 0u;
 #pragma unroll
