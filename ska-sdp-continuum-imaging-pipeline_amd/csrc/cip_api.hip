@@ -292,6 +292,7 @@ struct PlanResult {
   int64_t* tile_run_off = nullptr;
   Chunk* chunks = nullptr;
   void* perm = nullptr;  // bank-class ordered visibility stream (perm_encode entries), or NULL
+  bool phases = false;   // perm's entries carry row phases (RowMap::row_phase for the scatter)
   uint32_t* dmask = nullptr;  // grid tiles the scatter writes, per plane (bit-packed, ntx / 32 words per tile row)
 };
 
@@ -614,6 +615,7 @@ static int make_plan(Workspace* ws, const double* uvw, const double* fx, const R
                      int group = 1) {
   const int64_t ntiles = g.ntx * g.nty * g.ntw;
   pr->ntiles = ntiles;
+  pr->phases = false;
   CIP_ALLOC(tile_runs, int64_t, "tile_runs", ntiles + 1)
   CIP_ALLOC(tile_vis, int64_t, "tile_vis", ntiles + 1)
   CIP_ALLOC(tile_vis_off, int64_t, "tile_vis_off", ntiles + 1)
@@ -760,7 +762,9 @@ static int make_plan(Workspace* ws, const double* uvw, const double* fx, const R
     CIP_HIP_CHECK(launch_chunk_emit(tile_vis_off, tile_vis, win_off, run_goff, tile_runs, ntiles, kOrderWindow, 0, nwin,
                                     windows, s));
     CIP_ALLOC(perm, uint32_t, "perm", ragged ? 2 * nvis : nvis)
-    CIP_HIP_CHECK(launch_order(vis_class, mp, runs, run_goff, windows, nwin, perm, s, row_phases() ? g.support : 0));
+    const bool ph = row_phases() && order_phases_ok(mp, g.support);
+    CIP_HIP_CHECK(launch_order(vis_class, mp, runs, run_goff, windows, nwin, perm, s, ph ? g.support : 0));
+    pr->phases = ph;
     pr->perm = perm;
   }
   return CIP_OK;
@@ -1077,8 +1081,10 @@ static int scatter_plane(const Prepared& pp, int64_t q, const double* uvw, const
   const int64_t cb = pp.plan.plane_chunk_off[k], ce = pp.plan.plane_chunk_off[k + 1];
   if (wgt == nullptr) wgt_dtype = CIP_NONE;
   hipEvent_t a = g_prof.mark(s);
+  RowMap ms = pp.m;
+  ms.row_phase = pp.plan.phases ? 1 : 0;
   CIP_HIP_CHECK(launch_scatter(g.support, vis_dtype, wgt_dtype, pp.packed, G, share_cus,
-                               !accumulate && flush_store_enabled(g), uvw, pp.fx, vis, wgt, pp.m,
+                               !accumulate && flush_store_enabled(g), uvw, pp.fx, vis, wgt, ms,
                                pp.plan.runs, pp.plan.run_goff, pp.plan.tile_run_off, pp.plan.perm, pp.plan.chunks, cb,
                                ce - cb, g, p0, pp.fixed_scale, grid, s));
   g_prof.span(2, a, g_prof.mark(s));

@@ -463,6 +463,10 @@ struct RowMap {
   // 2^(cbits + rbits))) and its length - 1 rides in bits 26-31 of its sort key,
   // above the radix digits - so the order pass needs no delta[row] gather
   int pk_runs = 0;
+  // the plan's ordered-stream entries carry row phases (cip_grid.hip
+  // order_kernel: bit 31 of dense entries, bit 63 of ragged ones), which the
+  // scatter strips and applies (cip_scatter.h fetch_raw)
+  int row_phase = 0;
 };
 
 constexpr int kRunLenShift = 26;  // RowMap::pk_runs: run length - 1 in sort-key bits 26-31

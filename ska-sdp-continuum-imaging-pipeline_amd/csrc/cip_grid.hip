@@ -296,6 +296,24 @@ static bool order_classes32() {
   return on;
 }
 
+// Row phases apply when the entries have a bit to spare (bit 31 of dense
+// entries, bit 63 of ragged ones - the packed (index, row, channel) form must
+// leave it free) and the lane scatter's support gives a full cycle (dP = (T +
+// W - 1) mod 16 odd)
+bool order_phases_ok(const RowMap& m, int support) {
+  auto bits = [](int64_t n) {
+    int b = 1;
+    while (b < 62 && ((int64_t)1 << b) < n) ++b;
+    return b;
+  };
+  const int wide = m.delta == nullptr ? 0 : (m.pk_cbits ? 2 : 1);
+  const bool spare = wide == 0 ? m.nvis < ((int64_t)1 << 31)
+                               : (wide == 1 || m.pk_cbits + m.pk_rbits + bits(m.nvis) <= 63);
+  const int nc = order_classes32() ? 32 : 16;
+  const int dP = (kTile + support - 1) & (nc - 1);
+  return spare && support >= 2 && support <= 16 && (dP & 1);
+}
+
 hipError_t launch_order(const uint8_t* vis_class, const RowMap& m, const uint64_t* runs, const int64_t* run_goff,
                         const Chunk* windows, int64_t nwindows, void* perm, hipStream_t s, int phase_support) {
   if (nwindows <= 0) return hipSuccess;
@@ -310,19 +328,8 @@ hipError_t launch_order(const uint8_t* vis_class, const RowMap& m, const uint64_
   // footprint origin's element mod 16 (mod 32 before round 6)
   const bool c32 = order_classes32();
   const int nc = c32 ? 32 : 16;
-  // row phases: dense entries with bit 31 free, a lane scatter whose support
-  // gives a full cycle (dP = (T + W - 1) mod NC odd)
   const int dP = (kTile + phase_support - 1) & (nc - 1);
-  // (a bit to spare: bit 31 of dense entries, bit 63 of ragged ones - the
-  // packed (index, row, channel) form must leave it free)
-  auto bits = [](int64_t n) {
-    int b = 1;
-    while (b < 62 && ((int64_t)1 << b) < n) ++b;
-    return b;
-  };
-  const bool spare = wide == 0 ? m.nvis < ((int64_t)1 << 31)
-                               : (wide == 1 || m.pk_cbits + m.pk_rbits + bits(m.nvis) <= 63);
-  const bool ph = phase_support >= 2 && phase_support <= 16 && (dP & 1) && spare;
+  const bool ph = phase_support > 0 && order_phases_ok(m, phase_support);
   if (c32) {
     if (wide == 2 && ph) ORDER(2, true, 32);
     else if (wide == 2) ORDER(2, false, 32);

@@ -145,8 +145,10 @@ hipError_t launch_scatter(int support, int vis_dtype, int wgt_dtype, bool packed
 // phase_support: the support W of the lane scatter that reads perm, which then
 // carries row phases (bit 31 of dense entries, cip_grid.hip order_kernel);
 // 0: no phases
+// (phases only where order_phases_ok; the scatter then needs RowMap::row_phase)
 hipError_t launch_order(const uint8_t* vis_class, const RowMap& m, const uint64_t* runs, const int64_t* run_goff,
                         const Chunk* windows, int64_t nwindows, void* perm, hipStream_t s, int phase_support = 0);
+bool order_phases_ok(const RowMap& m, int support);
 hipError_t launch_crop_correct_2d(const double* grid, const GridGeometry& g, int64_t npix_x, int64_t npix_y,
                                   const double* cx, const double* cy, double* dirty, hipStream_t s);
 hipError_t launch_wplane_accumulate(const double* grid, const GridGeometry& g, int64_t npix_x, int64_t npix_y,

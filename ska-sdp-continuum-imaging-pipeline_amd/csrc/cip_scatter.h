@@ -105,14 +105,16 @@ __device__ __forceinline__ void fetch_raw(uint64_t e, const double* __restrict__
                                           RawFetch<VisT, WK>& f) {
   int64_t il, r, c;
   f.h = 0u;
-  if constexpr (WIDE == 0) {
-    // dense entries: the row phase in bit 31 (order_kernel<0, true>)
-    f.h = (uint32_t)(e >> 31) & 1u;
-    e &= 0x7fffffffull;
-  } else if constexpr (WIDE == 1) {
-    // ragged entries: bit 63 (order_kernel<1 / 2, true>)
-    f.h = (uint32_t)(e >> 63);
-    e &= 0x7fffffffffffffffull;
+  if (m.row_phase) {  // (uniform)
+    if constexpr (WIDE == 0) {
+      // dense entries: the row phase in bit 31 (order_kernel<0, true>)
+      f.h = (uint32_t)(e >> 31) & 1u;
+      e &= 0x7fffffffull;
+    } else if constexpr (WIDE == 1) {
+      // ragged entries: bit 63 (order_kernel<1 / 2, true>)
+      f.h = (uint32_t)(e >> 63);
+      e &= 0x7fffffffffffffffull;
+    }
   }
   if constexpr (WIDE < 0) perm_decode(e, m, &il, &r, &c);
   else perm_decode_t<WIDE == 1>(e, m, &il, &r, &c);
